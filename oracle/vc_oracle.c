@@ -1,0 +1,917 @@
+/*
+ * vc_oracle.c -- CPU restatement of vproxy's classification hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see vc_oracle.h).  Plain C, linear scans exactly
+ * as the Java reference does them; no tries, no hashing.  Each function
+ * cites the reference file:line it restates (paths under /root/reference).
+ */
+#define _GNU_SOURCE
+#include "vc_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Java String helpers over ASCII bytes                                     */
+/* ------------------------------------------------------------------------ */
+
+static int j_index_of(const char *s, int n, const char *e, int en, int from)
+{
+    if (from < 0) from = 0;
+    for (int i = from; i + en <= n; ++i)
+        if (memcmp(s + i, e, (size_t)en) == 0) return i;
+    return -1;
+}
+
+static int j_index_of_ch(const char *s, int n, char c)
+{
+    for (int i = 0; i < n; ++i)
+        if (s[i] == c) return i;
+    return -1;
+}
+
+static int j_last_index_of_ch(const char *s, int n, char c, int from)
+{
+    if (from >= n) from = n - 1;
+    for (int i = from; i >= 0; --i)
+        if (s[i] == c) return i;
+    return -1;
+}
+
+static int j_starts_with(const char *s, int n, const char *p, int pn)
+{
+    return n >= pn && memcmp(s, p, (size_t)pn) == 0;
+}
+
+static int j_ends_with(const char *s, int n, const char *p, int pn)
+{
+    return n >= pn && memcmp(s + n - pn, p, (size_t)pn) == 0;
+}
+
+static int j_equals(const char *a, int an, const char *b, int bn)
+{
+    return an == bn && memcmp(a, b, (size_t)an) == 0;
+}
+
+/* Utils.split (base/src/main/java/vproxybase/util/Utils.java:162-177):
+ * splits on the literal e, keeping every empty piece.  Writes piece offsets
+ * and lengths; returns the piece count (<= n + 1). */
+static int j_split(const char *s, int n, const char *e, int en, int *off, int *len)
+{
+    int cnt = 0;
+    int idx = -en;
+    int last = 0;
+    for (;;) {
+        idx = j_index_of(s, n, e, en, idx + en);
+        if (idx == -1) {
+            off[cnt] = last;
+            len[cnt] = n - last;
+            ++cnt;
+            break;
+        }
+        off[cnt] = last;
+        len[cnt] = idx - last;
+        ++cnt;
+        last = idx + en;
+    }
+    return cnt;
+}
+
+static int hexval(char c)
+{
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    return c - 'A' + 10;
+}
+
+/* ------------------------------------------------------------------------ */
+/* IP.java parsers                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* IP.parseIpv4String(String, byte[], int) -- IP.java:129-155 */
+static int parse_ipv4_into(const char *s, int n, uint8_t *bytes, int cap, int from_idx)
+{
+    int off[64], len[64];
+    /* more than 63 dots can never be 4 pieces; bail before overflow */
+    int dots = 0;
+    for (int i = 0; i < n; ++i) dots += (s[i] == '.');
+    if (dots != 3) return -1;
+    int cnt = j_split(s, n, ".", 1, off, len);
+    if (cnt != 4) return -1;
+    for (int i = 0; i < cnt; ++i) {
+        int idx = from_idx + i;
+        if (idx >= cap) return -1;
+        const char *p = s + off[i];
+        int l = len[i];
+        if (l > 3 || l == 0) return -1;
+        for (int k = 0; k < l; ++k)
+            if (p[k] < '0' || p[k] > '9') return -1;
+        if (p[0] == '0' && l > 1) return -1;
+        int num = 0;
+        for (int k = 0; k < l; ++k) num = num * 10 + (p[k] - '0');
+        if (num > 255) return -1;
+        bytes[idx] = (uint8_t)num;
+    }
+    return cnt;
+}
+
+int vo_parse_ipv4(const char *s, int len, uint8_t out[4])
+{
+    uint8_t b[4] = {0, 0, 0, 0};
+    if (parse_ipv4_into(s, len, b, 4, 0) == -1) return -1;
+    memcpy(out, b, 4);
+    return 4;
+}
+
+/* IP.parseIpv6ColonPart -- IP.java:200-248 (s == NULL is Java null) */
+static int parse_ipv6_colon_part(const char *s, int n, uint8_t *bytes, int from_idx)
+{
+    if (s == NULL || n == 0) return 0;
+    if (from_idx < 0) return -1;
+    int *off = (int *)malloc(sizeof(int) * (size_t)(n + 1));
+    int *len = (int *)malloc(sizeof(int) * (size_t)(n + 1));
+    int cnt = j_split(s, n, ":", 1, off, len);
+    int ret = cnt * 2;
+    for (int i = 0; i < cnt; ++i) {
+        int base = from_idx + 2 * i;
+        if (base >= 16) { ret = -1; break; }
+        const char *f = s + off[i];
+        int l = len[i];
+        if (l > 4 || l == 0) { ret = -1; break; }
+        int bad = 0;
+        for (int k = 0; k < l; ++k) {
+            char c = f[k];
+            if ((c < 'A' || c > 'F') && (c < 'a' || c > 'f') && (c < '0' || c > '9')) bad = 1;
+        }
+        if (bad) { ret = -1; break; }
+        switch (l) {
+        case 1: bytes[base + 1] = (uint8_t)hexval(f[0]); break;
+        case 2: bytes[base + 1] = (uint8_t)(hexval(f[0]) * 16 + hexval(f[1])); break;
+        case 3:
+            bytes[base] = (uint8_t)hexval(f[0]);
+            bytes[base + 1] = (uint8_t)(hexval(f[1]) * 16 + hexval(f[2]));
+            break;
+        case 4:
+            bytes[base] = (uint8_t)(hexval(f[0]) * 16 + hexval(f[1]));
+            bytes[base + 1] = (uint8_t)(hexval(f[2]) * 16 + hexval(f[3]));
+            break;
+        }
+    }
+    free(off);
+    free(len);
+    return ret;
+}
+
+static int count_pieces(const char *s, int n, char c)
+{
+    int k = 1;
+    for (int i = 0; i < n; ++i) k += (s[i] == c);
+    return k;
+}
+
+/* IP.parseIpv6LastBits -- IP.java:251-269.  NB the `4 + colonPart` sum at
+ * :264 turns a failed colon part (-1) into 3, which the caller accepts when a
+ * "::" is present; restated verbatim. */
+static int parse_ipv6_last_bits(const char *s, int n, uint8_t *bytes)
+{
+    int dot = j_index_of_ch(s, n, '.');
+    if (dot != -1) {
+        int idx = j_last_index_of_ch(s, n, ':', dot);
+        if (idx == -1) {
+            return parse_ipv4_into(s, n, bytes, 16, 12);
+        } else {
+            const char *colon = s;
+            int colon_n = idx;
+            const char *dotp = s + idx + 1;
+            int dot_n = n - idx - 1;
+            int r = parse_ipv4_into(dotp, dot_n, bytes, 16, 12);
+            if (r == -1) return -1;
+            return 4 + parse_ipv6_colon_part(colon, colon_n, bytes,
+                                             16 - 4 - count_pieces(colon, colon_n, ':') * 2);
+        }
+    } else {
+        return parse_ipv6_colon_part(s, n, bytes, 16 - count_pieces(s, n, ':') * 2);
+    }
+}
+
+/* IP.parseIpv6String -- IP.java:158-197 */
+int vo_parse_ipv6(const char *s, int n, uint8_t out[16])
+{
+    if (j_starts_with(s, n, "[", 1) && j_ends_with(s, n, "]", 1) && n >= 1) {
+        /* Java substring(1, len-1) on "[" alone would throw; "[" does not end
+         * with "]" unless n >= 2, except the one-char string "]"... which does
+         * not start with "[".  So n >= 2 here. */
+        s = s + 1;
+        n = n - 2;
+    }
+    {
+        /* count of "::" pieces - 1 */
+        int pieces = 1;
+        int idx = -2;
+        for (;;) {
+            idx = j_index_of(s, n, "::", 2, idx + 2);
+            if (idx == -1) break;
+            ++pieces;
+        }
+        if (pieces - 1 > 1) return -1;
+    }
+    int has_dbl;
+    const char *colon_only;
+    int colon_only_n;
+    const char *colon_and_dot;
+    int colon_and_dot_n;
+    int idx = j_index_of(s, n, "::", 2, 0);
+    if (idx == -1) {
+        has_dbl = 0;
+        colon_only = NULL;
+        colon_only_n = 0;
+        colon_and_dot = s;
+        colon_and_dot_n = n;
+    } else {
+        has_dbl = 1;
+        colon_only = s;
+        colon_only_n = idx;
+        colon_and_dot = s + idx + 2;
+        colon_and_dot_n = n - idx - 2;
+    }
+    uint8_t b[16];
+    memset(b, 0, sizeof b);
+    int consumed = parse_ipv6_colon_part(colon_only, colon_only_n, b, 0);
+    if (consumed == -1) return -1;
+    int consumed2 = parse_ipv6_last_bits(colon_and_dot, colon_and_dot_n, b);
+    if (consumed2 == -1) return -1;
+    if (has_dbl) {
+        if (consumed + consumed2 >= 16) return -1;
+    } else {
+        if (consumed + consumed2 != 16) return -1;
+    }
+    memcpy(out, b, 16);
+    return 16;
+}
+
+/* IP.parseIpString -- IP.java:112-117 */
+int vo_parse_ip(const char *s, int n, uint8_t out[16])
+{
+    if (j_index_of_ch(s, n, ':') != -1) return vo_parse_ipv6(s, n, out);
+    return vo_parse_ipv4(s, n, out);
+}
+
+int vo_is_ipv6(const char *s, int n)
+{
+    uint8_t b[16];
+    return vo_parse_ipv6(s, n, b) != -1;
+}
+
+/* IP.isIpLiteral = isIpv4 || isIpv6 (IP.java:271-300).  isIpv4 goes through
+ * parseIpv4StringConsiderV6Compatible: a parseable v6 string answers there
+ * (null or not), but then isIpv6 is true anyway, so the disjunction reduces
+ * to v6-parses || v4-parses. */
+int vo_is_ip_literal(const char *s, int n)
+{
+    uint8_t b[16];
+    if (vo_parse_ipv6(s, n, b) != -1) return 1;
+    return vo_parse_ipv4(s, n, b) != -1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Network.java                                                             */
+/* ------------------------------------------------------------------------ */
+
+/* Utils.getByte -- Utils.java:137-160 */
+static uint8_t get_byte(int ones)
+{
+    switch (ones) {
+    case 8: return 0xFF;
+    case 7: return 0xFE;
+    case 6: return 0xFC;
+    case 5: return 0xF8;
+    case 4: return 0xF0;
+    case 3: return 0xE0;
+    case 2: return 0xC0;
+    case 1: return 0x80;
+    default: return 0;
+    }
+}
+
+/* Utils.zeros -- Utils.java:94-104 (trailing zero bits of a byte, 8 for 0) */
+static int zeros(uint8_t b)
+{
+    for (int k = 0; k < 8; ++k)
+        if (b & (1u << k)) return k;
+    return 8;
+}
+
+/* Network.parseMask + getMask -- Network.java:101-133 */
+int vo_parse_mask(int m, uint8_t out[16])
+{
+    if (m > 128) return -1;
+    int len = m > 32 ? 16 : 4;
+    for (int i = 0; i < len; ++i) {
+        out[i] = get_byte(m > 8 ? 8 : m);
+        m -= 8;
+    }
+    return len;
+}
+
+/* Network.maskInt -- Network.java:135-145 */
+int vo_mask_int(const uint8_t *mask, int mlen)
+{
+    int m = 0;
+    for (int i = mlen - 1; i >= 0; --i) {
+        int cnt = zeros(mask[i]);
+        if (cnt == 0) break;
+        m += cnt;
+    }
+    return mlen * 8 - m;
+}
+
+/* Network.validNetwork -- Network.java:163-181 */
+int vo_valid_network(const uint8_t *a, int alen, const uint8_t *m, int mlen)
+{
+    if (alen < mlen) return 0;
+    for (int i = 0; i < mlen; ++i) {
+        int ab = (int8_t)a[i], mb = (int8_t)m[i];
+        if ((ab & mb) != ab) return 0;
+    }
+    for (int i = mlen; i < alen; ++i)
+        if (a[i] != 0) return 0;
+    return 1;
+}
+
+/* Utils.lowBitsV6V4 -- Utils.java:122-133 */
+static int low_bits_v6v4(const uint8_t *ip, int last, int second)
+{
+    for (int i = 0; i < second; ++i)
+        if (ip[i] != 0) return 0;
+    if (ip[last] == 0) return ip[second] == 0;
+    if (ip[last] == 0xFF) return ip[second] == 0xFF;
+    return 0;
+}
+
+static int byte_ne(uint8_t in, uint8_t mask, uint8_t rule)
+{
+    /* Java: (inputB & maskB) != ruleB over sign-extended ints */
+    return (((int)(int8_t)in) & ((int)(int8_t)mask)) != (int)(int8_t)rule;
+}
+
+/* Network.maskMatch -- Network.java:183-278 (five length cases) */
+int vo_mask_match(const uint8_t *in, int inlen, const uint8_t *rule, int rlen,
+                  const uint8_t *mask, int mlen)
+{
+    if (inlen == rlen && rlen > mlen) {                      /* case 1 */
+        for (int i = 0; i < mlen; ++i)
+            if (byte_ne(in[i], mask[i], rule[i])) return 0;
+        return 1;
+    } else if (inlen < rlen && rlen > mlen) {                /* case 2 */
+        return 0;
+    } else if (inlen < rlen && rlen == mlen) {               /* case 3 */
+        int last = rlen - inlen - 1;
+        int second = last - 1;
+        for (int i = 0; i < inlen; ++i)
+            if (byte_ne(in[i], mask[i + rlen - inlen], rule[i + rlen - inlen])) return 0;
+        return low_bits_v6v4(rule, last, second);
+    }
+    int min_len = inlen;                                     /* cases 4, 5 */
+    if (rlen < min_len) min_len = rlen;
+    if (mlen < min_len) min_len = mlen;
+    for (int i = 0; i < min_len; ++i)
+        if (byte_ne(in[inlen - i - 1], mask[mlen - i - 1], rule[rlen - i - 1])) return 0;
+    if (inlen > rlen) {
+        int last = inlen - rlen - 1;
+        int second = last - 1;
+        return low_bits_v6v4(in, last, second);
+    }
+    return 1;
+}
+
+/* Network(String) -- Network.java:16-25 via validNetworkStr :73-99 */
+int vo_net_from_str(const char *s, int n, vo_net *out)
+{
+    int slash = j_index_of_ch(s, n, '/');
+    if (slash == -1) return -1;
+    /* net.split("/") must give exactly 2 pieces: one '/', non-empty tail */
+    int slashes = 0;
+    for (int i = 0; i < n; ++i) slashes += s[i] == '/';
+    if (slashes != 1 || slash == n - 1 || slash == 0) return -1;
+    const char *ms = s + slash + 1;
+    int mn = n - slash - 1;
+    /* Integer.parseInt: optional sign then digits */
+    int k = 0, neg = 0;
+    if (ms[0] == '-' || ms[0] == '+') { neg = ms[0] == '-'; k = 1; }
+    if (k >= mn) return -1;
+    long v = 0;
+    for (; k < mn; ++k) {
+        if (ms[k] < '0' || ms[k] > '9') return -1;
+        v = v * 10 + (ms[k] - '0');
+        if (v > 2147483648L) return -1;
+    }
+    if (neg) v = -v;
+    if (v > 2147483647L) return -1;
+    memset(out, 0, sizeof *out);
+    int iplen = vo_parse_ip(s, slash, out->ip);
+    if (iplen == -1) return -1;
+    int mlen = vo_parse_mask((int)v, out->mask);
+    if (mlen == -1) return -1;
+    if (!vo_valid_network(out->ip, iplen, out->mask, mlen)) return -1;
+    out->ip_len = iplen;
+    out->mask_len = mlen;
+    return 0;
+}
+
+int vo_net_contains_ip(const vo_net *n, const uint8_t *ip, int iplen)
+{
+    return vo_mask_match(ip, iplen, n->ip, n->ip_len, n->mask, n->mask_len);
+}
+
+/* Network.contains(Network) -- Network.java:31-36 */
+int vo_net_contains_net(const vo_net *a, const vo_net *b)
+{
+    if (!vo_net_contains_ip(a, b->ip, b->ip_len)) return 0;
+    return vo_mask_int(a->mask, a->mask_len) < vo_mask_int(b->mask, b->mask_len);
+}
+
+int vo_net_equals(const vo_net *a, const vo_net *b)
+{
+    return a->ip_len == b->ip_len && a->mask_len == b->mask_len &&
+           memcmp(a->ip, b->ip, (size_t)a->ip_len) == 0 &&
+           memcmp(a->mask, b->mask, (size_t)a->mask_len) == 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SecurityGroup.allow -- SecurityGroup.java:30-45, SecurityGroupRule:27-29  */
+/* ------------------------------------------------------------------------ */
+
+int vo_sg_allow(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                int default_allow, int proto, const uint8_t *ip, int iplen, int port,
+                int *verdict)
+{
+    const vo_sg_rule *rules = proto == 6 ? tcp : udp;
+    int n = proto == 6 ? ntcp : nudp;
+    if (n == 0) {
+        if (verdict) *verdict = default_allow;
+        return -1;
+    }
+    for (int i = 0; i < n; ++i) {
+        const vo_sg_rule *r = &rules[i];
+        if (vo_net_contains_ip(&r->net, ip, iplen) && r->min_port <= port && port <= r->max_port) {
+            if (verdict) *verdict = r->allow;
+            return i;
+        }
+    }
+    if (verdict) *verdict = default_allow;
+    return -1;
+}
+
+/* ---- pthread partition helper ---- */
+typedef void (*range_fn)(void *ctx, int64_t lo, int64_t hi);
+typedef struct { range_fn fn; void *ctx; int64_t lo, hi; } range_job;
+
+static void *range_thread(void *p)
+{
+    range_job *j = (range_job *)p;
+    j->fn(j->ctx, j->lo, j->hi);
+    return NULL;
+}
+
+static void parallel_for(int64_t n, int nthreads, range_fn fn, void *ctx)
+{
+    if (nthreads <= 1 || n < 2) {
+        fn(ctx, 0, n);
+        return;
+    }
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    range_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].fn = fn;
+        jobs[t].ctx = ctx;
+        jobs[t].lo = n * t / nthreads;
+        jobs[t].hi = n * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, range_thread, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    const vo_sg_rule *tcp; int ntcp; const vo_sg_rule *udp; int nudp; int dflt;
+    const uint8_t *proto; const uint32_t *src4; const uint8_t *src6; const uint16_t *port;
+    int32_t *out; uint8_t *verdict;
+} sg_batch_ctx;
+
+static void sg_v4_range(void *p, int64_t lo, int64_t hi)
+{
+    sg_batch_ctx *c = (sg_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        uint32_t a = c->src4[i];
+        uint8_t ip[4] = {(uint8_t)(a >> 24), (uint8_t)(a >> 16), (uint8_t)(a >> 8), (uint8_t)a};
+        int v;
+        c->out[i] = vo_sg_allow(c->tcp, c->ntcp, c->udp, c->nudp, c->dflt, c->proto[i], ip, 4,
+                                c->port[i], &v);
+        if (c->verdict) c->verdict[i] = (uint8_t)v;
+    }
+}
+
+static void sg_v6_range(void *p, int64_t lo, int64_t hi)
+{
+    sg_batch_ctx *c = (sg_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        int v;
+        c->out[i] = vo_sg_allow(c->tcp, c->ntcp, c->udp, c->nudp, c->dflt, c->proto[i],
+                                c->src6 + 16 * i, 16, c->port[i], &v);
+        if (c->verdict) c->verdict[i] = (uint8_t)v;
+    }
+}
+
+void vo_sg_allow_batch_v4(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                          int default_allow, const uint8_t *proto, const uint32_t *src4,
+                          const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_verdict,
+                          int nthreads)
+{
+    sg_batch_ctx c = {tcp, ntcp, udp, nudp, default_allow, proto, src4, NULL, port, out_idx, out_verdict};
+    parallel_for(n, nthreads, sg_v4_range, &c);
+}
+
+void vo_sg_allow_batch_v6(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                          int default_allow, const uint8_t *proto, const uint8_t *src6,
+                          const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_verdict,
+                          int nthreads)
+{
+    sg_batch_ctx c = {tcp, ntcp, udp, nudp, default_allow, proto, NULL, src6, port, out_idx, out_verdict};
+    parallel_for(n, nthreads, sg_v6_range, &c);
+}
+
+/* ------------------------------------------------------------------------ */
+/* RouteTable -- core/src/main/java/vswitch/RouteTable.java                 */
+/* ------------------------------------------------------------------------ */
+
+void vo_rt_init(vo_route_table *t) { memset(t, 0, sizeof *t); }
+
+void vo_rt_free(vo_route_table *t)
+{
+    free(t->v4);
+    free(t->v6);
+    memset(t, 0, sizeof *t);
+}
+
+/* RouteTable.addRule(RouteRule, List) -- RouteTable.java:110-154 */
+static void rt_insert(vo_net **list, int *n, int *cap, const vo_net *r)
+{
+    int similar = -1;
+    for (int i = 0; i < *n; ++i) {
+        const vo_net *ri = &(*list)[i];
+        if (vo_net_contains_net(ri, r) || vo_net_contains_net(r, ri)) {
+            similar = i;
+            break;
+        }
+    }
+    int insert_index;
+    if (similar == -1) {
+        insert_index = *n;
+    } else {
+        insert_index = 0;
+        for (int i = similar; i < *n; ++i) {
+            const vo_net *curr = &(*list)[i];
+            const vo_net *next = (i + 1) < *n ? &(*list)[i + 1] : NULL;
+            if (vo_net_contains_net(curr, r)) {
+                insert_index = i;
+                break;
+            }
+            if (vo_net_contains_net(r, curr)) {
+                if (next == NULL) {
+                    insert_index = i + 1;
+                    break;
+                }
+                if (vo_net_contains_net(r, next)) continue;
+                if (vo_net_contains_net(next, r)) {
+                    insert_index = i + 1;
+                    break;
+                }
+            }
+            insert_index = i + 1;
+            break;
+        }
+    }
+    if (*n == *cap) {
+        *cap = *cap ? *cap * 2 : 16;
+        *list = (vo_net *)realloc(*list, sizeof(vo_net) * (size_t)*cap);
+    }
+    memmove(&(*list)[insert_index + 1], &(*list)[insert_index],
+            sizeof(vo_net) * (size_t)(*n - insert_index));
+    (*list)[insert_index] = *r;
+    ++*n;
+}
+
+/* RouteTable.addRule(RouteRule) -- RouteTable.java:68-108 (network part) */
+int vo_rt_add(vo_route_table *t, const vo_net *r)
+{
+    for (int i = 0; i < t->n4; ++i)
+        if (vo_net_equals(&t->v4[i], r)) return -1;
+    for (int i = 0; i < t->n6; ++i)
+        if (vo_net_equals(&t->v6[i], r)) return -1;
+    if (r->ip_len == 4) rt_insert(&t->v4, &t->n4, &t->cap4, r);
+    else rt_insert(&t->v6, &t->n6, &t->cap6, r);
+    return 0;
+}
+
+int vo_rt_lookup_list(const vo_net *list, int n, const uint8_t *ip, int iplen)
+{
+    for (int i = 0; i < n; ++i)
+        if (vo_net_contains_ip(&list[i], ip, iplen)) return i;
+    return -1;
+}
+
+/* RouteTable.lookup -- RouteTable.java:44-59 */
+int vo_rt_lookup(const vo_route_table *t, const uint8_t *ip, int iplen)
+{
+    if (iplen == 4) return vo_rt_lookup_list(t->v4, t->n4, ip, iplen);
+    return vo_rt_lookup_list(t->v6, t->n6, ip, iplen);
+}
+
+typedef struct {
+    const vo_net *list; int nl; const uint32_t *d4; const uint8_t *d6; int32_t *out;
+} rt_batch_ctx;
+
+static void rt_v4_range(void *p, int64_t lo, int64_t hi)
+{
+    rt_batch_ctx *c = (rt_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        uint32_t a = c->d4[i];
+        uint8_t ip[4] = {(uint8_t)(a >> 24), (uint8_t)(a >> 16), (uint8_t)(a >> 8), (uint8_t)a};
+        c->out[i] = vo_rt_lookup_list(c->list, c->nl, ip, 4);
+    }
+}
+
+static void rt_v6_range(void *p, int64_t lo, int64_t hi)
+{
+    rt_batch_ctx *c = (rt_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i)
+        c->out[i] = vo_rt_lookup_list(c->list, c->nl, c->d6 + 16 * i, 16);
+}
+
+void vo_rt_lookup_batch_v4(const vo_net *v4, int n4, const uint32_t *dst4, int64_t n,
+                           int32_t *out, int nthreads)
+{
+    rt_batch_ctx c = {v4, n4, dst4, NULL, out};
+    parallel_for(n, nthreads, rt_v4_range, &c);
+}
+
+void vo_rt_lookup_batch_v6(const vo_net *v6, int n6, const uint8_t *dst6, int64_t n,
+                           int32_t *out, int nthreads)
+{
+    rt_batch_ctx c = {v6, n6, NULL, dst6, out};
+    parallel_for(n, nthreads, rt_v6_range, &c);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Hint -- base/src/main/java/vproxybase/processor/Hint.java                */
+/* ------------------------------------------------------------------------ */
+
+/* Hint.formatHost -- Hint.java:57-73 */
+int vo_format_host(const char *s, int len, int *off, int *olen)
+{
+    if (s == NULL) return 0;
+    int colon = j_index_of_ch(s, len, ':');
+    if (vo_is_ipv6(s, len) || colon == -1) {
+        *off = 0;
+        *olen = len;
+        return 1;
+    }
+    int o = 0, l = colon;
+    if (j_starts_with(s, l, "www.", 4)) {
+        o = 4;
+        l -= 4;
+    }
+    if (l == 0) return 0;
+    *off = o;
+    *olen = l;
+    return 1;
+}
+
+/* Hint.formatUri -- Hint.java:75-90 */
+int vo_format_uri(const char *s, int len, int *off, int *olen)
+{
+    if (s == NULL) return 0;
+    int q = j_index_of_ch(s, len, '?');
+    if (q != -1) len = q;
+    *off = 0;
+    if (len == 1 && s[0] == '/') {
+        *olen = 1;
+        return 1;
+    }
+    if (len > 0 && s[len - 1] == '/') len -= 1;
+    *olen = len;
+    return 1;
+}
+
+/* Hint.ofHostPortUri and friends -- Hint.java:17-55 */
+vo_hint vo_hint_of(const char *host, int host_len, int port, const char *uri, int uri_len)
+{
+    vo_hint h;
+    int off, l;
+    if (vo_format_host(host, host_len, &off, &l)) {
+        h.host = host + off;
+        h.host_len = l;
+    } else {
+        h.host = NULL;
+        h.host_len = 0;
+    }
+    h.port = port;
+    if (vo_format_uri(uri, uri_len, &off, &l)) {
+        h.uri = uri + off;
+        h.uri_len = l;
+    } else {
+        h.uri = NULL;
+        h.uri_len = 0;
+    }
+    return h;
+}
+
+/* Hint.matchLevel -- Hint.java:100-160 */
+int vo_match_level(const vo_hint *h, const vo_annos *a, int na)
+{
+    const char *ah = NULL; int ahn = 0;
+    int ap = 0;
+    const char *au = NULL; int aun = 0;
+    for (int i = 0; i < na; ++i) {
+        if (ah == NULL) { ah = a[i].host; ahn = a[i].host_len; }
+        if (ap == 0) ap = a[i].port;
+        if (au == NULL) { au = a[i].uri; aun = a[i].uri_len; }
+    }
+    if (ah == NULL && ap == 0 && au == NULL) return 0;
+    if (h->port != 0 && ap != 0 && h->port != ap) return 0;
+    int level = 0;
+    int host_level = 0;
+    if (ah != NULL && h->host != NULL) {
+        if (j_equals(h->host, h->host_len, ah, ahn)) {
+            host_level = 3;
+        } else if (h->host_len >= ahn + 1 && h->host[h->host_len - ahn - 1] == '.' &&
+                   memcmp(h->host + h->host_len - ahn, ah, (size_t)ahn) == 0) {
+            host_level = 2;  /* host.endsWith("." + annoHost) */
+        } else if (j_equals(ah, ahn, "*", 1)) {
+            host_level = 1;
+        }
+    }
+    level += host_level << 10;
+    int uri_level = 0;
+    if (au != NULL && h->uri != NULL) {
+        if (j_equals(h->uri, h->uri_len, au, aun)) {
+            uri_level = h->uri_len + 1;
+        } else if (j_starts_with(h->uri, h->uri_len, au, aun)) {
+            uri_level = aun + 1;
+        } else if (j_equals(au, aun, "*", 1)) {
+            uri_level = 1;
+        }
+    }
+    if (uri_level > 1023) uri_level = 1023;
+    level += uri_level;
+    return level;
+}
+
+/* Upstream.searchForGroup -- Upstream.java:187-198 */
+int vo_search_for_group(const vo_group *g, int ng, const vo_hint *h)
+{
+    int level = 0;
+    int last_max = -1;
+    for (int i = 0; i < ng; ++i) {
+        vo_annos a[2] = {g[i].handle, g[i].group};
+        int l = vo_match_level(h, a, 2);
+        if (l > level) {
+            level = l;
+            last_max = i;
+        }
+    }
+    return last_max;
+}
+
+/* ------------------------------------------------------------------------ */
+/* DNSServer.handleRequest classification -- DNSServer.java:116-166         */
+/* ------------------------------------------------------------------------ */
+
+static int hosts_get(const vo_hosts *hs, const char *k, int kn)
+{
+    if (hs == NULL) return -1;
+    for (int i = 0; i < hs->n; ++i)
+        if (j_equals(hs->keys[i], hs->key_lens[i], k, kn)) return hs->values[i];
+    return -1;
+}
+
+int vo_dns_classify(const vo_hosts *hosts, const vo_group *g, int ng,
+                    const char *qname, int qlen, int32_t *value)
+{
+    int hv = hosts_get(hosts, qname, qlen);                  /* :127 */
+    if (hv >= 0) {
+        *value = hv;
+        return VO_DNS_HOSTS;
+    }
+    int dlen = qlen;
+    if (dlen > 0 && qname[dlen - 1] == '.') dlen -= 1;        /* :133-135 */
+    vo_hint h = vo_hint_of(qname, dlen, 0, NULL, 0);          /* :136 Hint.ofHost */
+    int gi = vo_search_for_group(g, ng, &h);
+    if (gi >= 0) {
+        *value = gi;
+        return VO_DNS_GROUP;
+    }
+    if (vo_is_ip_literal(qname, dlen)) {                      /* :140-149 */
+        *value = j_index_of_ch(qname, dlen, ':') != -1 ? 6 : 4;
+        return VO_DNS_IP_LITERAL;
+    }
+    if (j_ends_with(qname, dlen, ".vproxy.local", 13)) {      /* :150-157 */
+        *value = 0;
+        return VO_DNS_INTERNAL;
+    }
+    *value = 0;                                               /* :164 */
+    return VO_DNS_RECURSIVE;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Resolver.getHosts -- base/src/main/java/vproxybase/dns/Resolver.java:62-153 */
+/* ------------------------------------------------------------------------ */
+
+static int java_ws(char c)  /* Character.isWhitespace over ASCII */
+{
+    return c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r' ||
+           (c >= 0x1C && c <= 0x1F);
+}
+
+int vo_hosts_parse(const char *text, int len,
+                   char *keybuf, int keybuf_cap, int32_t *key_off, int32_t *key_len,
+                   int32_t *value, int cap,
+                   uint8_t *line_ip, int32_t *line_iplen, int line_cap)
+{
+    int nkeys = 0, kb = 0, nlines = 0;
+    int pos = 0;
+    while (pos < len) {
+        /* BufferedReader.readLine: \n, \r or \r\n terminate a line */
+        int end = pos;
+        while (end < len && text[end] != '\n' && text[end] != '\r') ++end;
+        int next = end + 1;
+        if (end < len && text[end] == '\r' && next < len && text[next] == '\n') ++next;
+        const char *line = text + pos;
+        int ln = end - pos;
+        pos = next;
+
+        int hash = j_index_of_ch(line, ln, '#');                  /* :100-102 */
+        if (hash != -1) ln = hash;
+        int blank = 1;                                            /* :103-105 */
+        for (int i = 0; i < ln; ++i)
+            if (!java_ws(line[i])) { blank = 0; break; }
+        if (blank) continue;
+        while (ln > 0 && (unsigned char)line[0] <= ' ') { ++line; --ln; }      /* trim */
+        while (ln > 0 && (unsigned char)line[ln - 1] <= ' ') --ln;
+        /* split("[ \t]") then trim + drop empties */
+        int toff[512], tlen[512], nt = 0;
+        int s = 0;
+        for (int i = 0; i <= ln; ++i) {
+            if (i == ln || line[i] == ' ' || line[i] == '\t') {
+                int a = s, b = i;
+                while (a < b && (unsigned char)line[a] <= ' ') ++a;
+                while (b > a && (unsigned char)line[b - 1] <= ' ') --b;
+                if (b > a && nt < 512) {
+                    toff[nt] = a;
+                    tlen[nt] = b - a;
+                    ++nt;
+                }
+                s = i + 1;
+            }
+        }
+        if (nt < 2) continue;                                     /* :108-113 */
+        uint8_t ip[16];
+        int iplen = vo_parse_ip(line + toff[0], tlen[0], ip);     /* :114-120 */
+        if (iplen == -1) continue;
+        if (nlines >= line_cap) return -1;
+        int entry = nlines++;
+        memcpy(line_ip + 16 * entry, ip, (size_t)iplen);
+        line_iplen[entry] = iplen;
+        for (int i = 1; i < nt; ++i) {                            /* :122-141 */
+            const char *d1 = line + toff[i];
+            int d1n = tlen[i];
+            char d2[1024];
+            int d2n;
+            if (d1n >= 1023) continue;
+            if (d1[d1n - 1] == '.') {
+                memcpy(d2, d1, (size_t)(d1n - 1));
+                d2n = d1n - 1;
+            } else {
+                memcpy(d2, d1, (size_t)d1n);
+                d2[d1n] = '.';
+                d2n = d1n + 1;
+            }
+            int present = 0;
+            for (int k = 0; k < nkeys; ++k) {
+                if (j_equals(keybuf + key_off[k], key_len[k], d1, d1n) ||
+                    j_equals(keybuf + key_off[k], key_len[k], d2, d2n)) {
+                    present = 1;
+                    break;
+                }
+            }
+            if (present) continue;
+            if (nkeys + 2 > cap || kb + d1n + d2n > keybuf_cap) return -1;
+            memcpy(keybuf + kb, d1, (size_t)d1n);
+            key_off[nkeys] = kb; key_len[nkeys] = d1n; value[nkeys] = entry; ++nkeys; kb += d1n;
+            memcpy(keybuf + kb, d2, (size_t)d2n);
+            key_off[nkeys] = kb; key_len[nkeys] = d2n; value[nkeys] = entry; ++nkeys; kb += d2n;
+        }
+    }
+    return nkeys;
+}

@@ -1,0 +1,148 @@
+/*
+ * vc_oracle.h -- CPU restatement of vproxy's classification hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the
+ * MI355X classifier (libvclassify).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path never links,
+ * loads or calls it.
+ *
+ * Every function restates one Java method of nintha/vproxy (paths relative to
+ * /root/reference) with Java semantics: signed bytes, list order, strict '>'
+ * tie-breaks, String.equals/endsWith/startsWith over ASCII bytes.  Strings are
+ * (pointer, length) pairs; a NULL pointer is Java `null`.
+ *
+ * Pinned by: tests/golden/ fixtures (vectors transcribed from the reference's
+ * own JUnit tests TestNetMask, TestRouteTable, TestIpParser, the behavioural
+ * tests TestSocks5/TestProtocols/CI, and SURVEY.md Appendix B quirk KATs).
+ */
+#ifndef VC_ORACLE_H
+#define VC_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- IP parsing: base/src/main/java/vfd/IP.java ---- */
+int vo_parse_ipv4(const char *s, int len, uint8_t out[4]);   /* IP.java:120-127; 4 or -1 */
+int vo_parse_ipv6(const char *s, int len, uint8_t out[16]);  /* IP.java:158-197; 16 or -1 */
+int vo_parse_ip(const char *s, int len, uint8_t out[16]);    /* IP.java:112-117; 4/16/-1 */
+int vo_is_ipv6(const char *s, int len);                      /* IP.java:294-296 */
+int vo_is_ip_literal(const char *s, int len);                /* IP.java:271-300 */
+
+/* ---- Network: base/src/main/java/vproxybase/util/Network.java ---- */
+int vo_parse_mask(int m, uint8_t out[16]);                   /* :101-115; len or -1 (throws) */
+int vo_mask_int(const uint8_t *mask, int mlen);              /* :135-145 */
+int vo_valid_network(const uint8_t *a, int alen, const uint8_t *m, int mlen); /* :163-181 */
+int vo_mask_match(const uint8_t *in, int inlen, const uint8_t *rule, int rlen,
+                  const uint8_t *mask, int mlen);            /* :183-278 */
+
+typedef struct {
+    uint8_t ip[16];
+    uint8_t mask[16];
+    int32_t ip_len;    /* 4 or 16 */
+    int32_t mask_len;  /* 4 or 16 */
+} vo_net;
+
+int vo_net_from_str(const char *s, int len, vo_net *out);     /* Network(String) :16-25; 0 ok, -1 invalid */
+int vo_net_contains_ip(const vo_net *n, const uint8_t *ip, int iplen); /* :27-29 */
+int vo_net_contains_net(const vo_net *a, const vo_net *b);    /* :31-36 */
+int vo_net_equals(const vo_net *a, const vo_net *b);          /* :50-57 */
+
+/* ---- SecurityGroup: core/.../component/secure/SecurityGroup{,Rule}.java ---- */
+typedef struct {
+    vo_net net;
+    int32_t min_port, max_port;
+    int32_t allow;
+} vo_sg_rule;
+
+/* SecurityGroup.allow (SecurityGroup.java:30-45) with the matched index
+ * exposed: returns index into the protocol's list, or -1 for defaultAllow.
+ * *verdict receives the boolean allow() would return. proto==6 -> tcp list,
+ * anything else -> udp list (Java's else-branch). */
+int vo_sg_allow(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                int default_allow, int proto, const uint8_t *ip, int iplen, int port,
+                int *verdict);
+
+/* batched, pthread-partitioned restatement (CPU baseline). src4 = big-endian
+ * int (IP.ipv4Bytes2Int); out_idx per item; verdict optional. */
+void vo_sg_allow_batch_v4(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                          int default_allow, const uint8_t *proto, const uint32_t *src4,
+                          const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_verdict,
+                          int nthreads);
+void vo_sg_allow_batch_v6(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                          int default_allow, const uint8_t *proto, const uint8_t *src6,
+                          const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_verdict,
+                          int nthreads);
+
+/* ---- RouteTable: core/src/main/java/vswitch/RouteTable.java ---- */
+typedef struct {
+    vo_net *v4; int n4, cap4;
+    vo_net *v6; int n6, cap6;
+} vo_route_table;
+
+void vo_rt_init(vo_route_table *t);
+void vo_rt_free(vo_route_table *t);
+/* RouteTable.addRule(RouteRule) ordering part (:68-154): duplicate network ->
+ * returns -1 (AlreadyExistException), else 0.  Alias/ip checks are host-side. */
+int vo_rt_add(vo_route_table *t, const vo_net *n);
+/* RouteTable.lookup (:44-59): family list index or -1 (null). */
+int vo_rt_lookup(const vo_route_table *t, const uint8_t *ip, int iplen);
+int vo_rt_lookup_list(const vo_net *list, int n, const uint8_t *ip, int iplen);
+void vo_rt_lookup_batch_v4(const vo_net *v4, int n4, const uint32_t *dst4, int64_t n,
+                           int32_t *out, int nthreads);
+void vo_rt_lookup_batch_v6(const vo_net *v6, int n6, const uint8_t *dst6, int64_t n,
+                           int32_t *out, int nthreads);
+
+/* ---- Hint / Upstream: base/.../processor/Hint.java, core/.../svrgroup/Upstream.java ---- */
+typedef struct {
+    const char *host; int32_t host_len;   /* NULL = absent */
+    int32_t port;                         /* 0 = absent */
+    const char *uri; int32_t uri_len;     /* NULL = absent */
+} vo_annos;
+
+typedef struct {
+    vo_annos handle;   /* ServerGroupHandle.annotations */
+    vo_annos group;    /* ServerGroup.getAnnotations()  */
+} vo_group;
+
+typedef struct {
+    const char *host; int32_t host_len;
+    int32_t port;
+    const char *uri; int32_t uri_len;
+} vo_hint;
+
+/* Hint.formatHost (:57-73): writes [*off,*len) sub-range of s; returns 1 if
+ * non-null, 0 if the result is null. */
+int vo_format_host(const char *s, int len, int *off, int *olen);
+/* Hint.formatUri (:75-90): same convention. */
+int vo_format_uri(const char *s, int len, int *off, int *olen);
+/* Hint.of{Host,HostPort,HostUri,HostPortUri,Uri} (:17-55). host/uri may be NULL. */
+vo_hint vo_hint_of(const char *host, int host_len, int port, const char *uri, int uri_len);
+int vo_match_level(const vo_hint *h, const vo_annos *a, int na);   /* :100-160 */
+int vo_search_for_group(const vo_group *g, int ng, const vo_hint *h); /* Upstream.java:187-198 */
+
+/* ---- DNSServer classification: core/src/main/java/vproxy/dns/DNSServer.java:116-166 ---- */
+enum { VO_DNS_HOSTS = 1, VO_DNS_GROUP = 2, VO_DNS_IP_LITERAL = 3, VO_DNS_INTERNAL = 4, VO_DNS_RECURSIVE = 5 };
+typedef struct {
+    const char *const *keys; const int32_t *key_lens; const int32_t *values; int n;
+} vo_hosts;  /* exact map, linear lookup; first key wins */
+/* returns kind; *value = hosts value / group index / 4|6 for literal / 0 */
+int vo_dns_classify(const vo_hosts *hosts, const vo_group *g, int ng,
+                    const char *qname, int qlen, int32_t *value);
+
+/* Resolver.getHosts (base/.../dns/Resolver.java:62-153) over the text of a
+ * hosts file.  Emits map entries (key -> value) in insertion order: keys are
+ * copied into keybuf (key_off/key_len), value = index of the accepted host
+ * line (its IP bytes in line_ip[16*value], length line_iplen[value]).
+ * Returns the entry count, or -1 if a capacity is exceeded. */
+int vo_hosts_parse(const char *text, int len,
+                   char *keybuf, int keybuf_cap, int32_t *key_off, int32_t *key_len,
+                   int32_t *value, int cap,
+                   uint8_t *line_ip, int32_t *line_iplen, int line_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

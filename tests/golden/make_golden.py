@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Writes the golden fixtures under tests/golden/.
+
+The expected values here are NOT produced by our oracle.  They are
+transcribed from the reference's own JUnit assertions (file:line cited per
+fixture, paths under /root/reference), from SURVEY.md Appendix B (quirk KATs
+hand-derived from the Java source), or -- for IPv6 literals that TestIpParser
+checks against the JDK's InetAddress -- from Python's `ipaddress`, which
+implements the same RFC 4291 text form the JDK parses.
+
+The reference is Java and cannot run in this container (no JDK), so nothing
+here executes reference code.  Re-run this script to regenerate the JSON.
+"""
+import ipaddress
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+        f.write("\n")
+
+
+# ---------------------------------------------------------------------------
+# TestNetMask (test/src/test/java/vproxy/test/cases/TestNetMask.java)
+# ---------------------------------------------------------------------------
+def netmask():
+    # mask(): TestNetMask.java:15-47 -- m ones then zeros to 32 (m<=32) or 128
+    masks = []
+    for m in range(0, 129):
+        width = 32 if m <= 32 else 128
+        bits = "1" * m + "0" * (width - m)
+        masks.append({"m": m, "bits": bits})
+    # validNetwork(): TestNetMask.java:49-70
+    valid = [
+        [False, "10.144.0.0", 11],
+        [True, "10.144.0.0", 12],
+        [True, "10.144.0.0", 13],
+        [False, "[0000:0010:0000:0000:0000:0000:0000:0000]", 27],
+        [True, "[0000:0010:0000:0000:0000:0000:0000:0000]", 28],
+        [True, "[0000:0010:0000:0000:0000:0000:0000:0000]", 29],
+        [False, "[0000:0010:0000:0000:1000:0000:0000:0000]", 67],
+        [True, "[0000:0010:0000:0000:1000:0000:0000:0000]", 68],
+        [True, "[0000:0010:0000:0000:1000:0000:0000:0000]", 69],
+    ]
+    # ipNetMask(): TestNetMask.java:72-113 (14 maskMatch vectors)
+    match = [
+        [True, "10.144.0.1", "10.144.0.0/12"],
+        [True, "10.144.0.1", "10.144.0.0/13"],
+        [True, "10.152.0.1", "10.144.0.0/12"],
+        [True, "127.0.0.1", "[0000:0000:0000:0000:0000:0000:7F00:0000]/112"],
+        [True, "127.0.0.1", "[0000:0000:0000:0000:0000:ffff:7F00:0000]/112"],
+        [True, "[0000:0000:0000:0000:0000:0000:7F00:0001]", "127.0.0.1/32"],
+        [True, "[0000:0000:0000:0000:0000:FFFF:7F00:0001]", "127.0.0.1/32"],
+        [False, "10.152.0.1", "10.144.0.0/13"],
+        [False, "255.255.255.255", "[0000:0010:0000:0000:0000:0000:0000:0000]/28"],
+        [False, "127.0.0.1", "[0000:0010:0000:0000:0000:0000:0000:0000]/28"],
+        [False, "128.0.0.1", "[0000:0000:0000:0000:0000:0000:7F00:0000]/112"],
+        [False, "128.0.0.1", "[0000:0000:0000:0000:0000:ffff:7F00:0000]/112"],
+        [False, "[0000:0000:0000:0000:0000:1234:7F00:0001]", "127.0.0.1/32"],
+        [False, "[0000:0000:0000:0000:0000:FFFF:7F00:0002]", "127.0.0.1/32"],
+    ]
+    dump("netmask.json", {
+        "source": "test/src/test/java/vproxy/test/cases/TestNetMask.java:15-113",
+        "mask": masks,
+        "valid_network": [{"expect": e, "addr": a, "mask": m} for e, a, m in valid],
+        "mask_match": [{"expect": e, "input": i, "net": n} for e, i, n in match],
+    })
+
+
+# ---------------------------------------------------------------------------
+# TestIpParser (test/src/test/java/vproxy/test/cases/TestIpParser.java)
+# ---------------------------------------------------------------------------
+def v6_bytes(s):
+    s2 = s[1:-1] if s.startswith("[") and s.endswith("]") else s
+    return list(ipaddress.IPv6Address(s2).packed)
+
+
+def ip_parser():
+    v4_ok = [["192.168.12.34", [192, 168, 12, 34]], ["192.168.0.0", [192, 168, 0, 0]]]  # :12-38
+    v4_fail = ["1", "a.b.c.d", "1.2.3.", "...", "1.2..", "..3.4", "1...4", "256.1.1.1",
+               "1.256.1.1"]  # :40-51
+    v6_ok = [  # :83-111, each also checked bracketed (:73-80)
+        "ABCD:EF01:2345:6789:ABCD:EF01:2345:6789", "2001:DB8:0:0:8:800:200C:417A",
+        "FF01:0:0:0:0:0:0:101", "0:0:0:0:0:0:0:1", "0:0:0:0:0:0:0:0",
+        "2001:DB8::8:800:200C:417A", "FF01::101", "::1", "::", "0:0:0:0:0:0:13.1.68.3",
+        "0:0:0:0:0:FFFF:129.144.52.38", "::13.1.68.3", "::FFFF:129.144.52.38", "1::",
+        "1a2b::3c4d", "22::", "333::", "4444::", "2001:db8:c000:221::",
+        "2001:db8:1c0:2:21::", "2001:db8:122:c000:2:2100::", "2001:db8:122:3c0:0:221::",
+        "2001:db8:122:344:c0:2:2100::", "2001:db8:122:344::192.0.2.33",
+    ]
+    v6 = []
+    for s in v6_ok:
+        v6.append({"s": s, "bytes": v6_bytes(s)})
+        v6.append({"s": "[" + s + "]", "bytes": v6_bytes(s)})
+    bogus = [  # :117-182 (guava InetAddressesTest bogus inputs) -> parseIpString == null
+        "", "016.016.016.016", "016.016.016", "016.016", "016", "000.000.000.000", "000",
+        "0x0a.0x0a.0x0a.0x0a", "0x0a.0x0a.0x0a", "0x0a.0x0a", "0x0a", "42.42.42.42.42",
+        "42.42.42", "42.42", "42", "42..42.42", "42..42.42.42", "42.42.42.42.",
+        "42.42.42.42...", ".42.42.42.42", "...42.42.42.42", "42.42.42.-0", "42.42.42.+0", ".",
+        "...", "bogus", "bogus.com", "192.168.0.1.com", "12345.67899.-54321.-98765",
+        "257.0.0.0", "42.42.42.-42", "3ffe::1.net", "3ffe::1::1", "1::2::3::4:5",
+        "::7:6:5:4:3:2:", ":6:5:4:3:2:1::", "2001::db:::1", "FEDC:9878", "+1.+2.+3.4",
+        "1.2.3.4e0", "::7:6:5:4:3:2:1:0", "7:6:5:4:3:2:1:0::", "9:8:7:6:5:4:3::2:1",
+        "0:1:2:3::4:5:6:7", "3ffe:0:0:0:0:0:0:0:1", "3ffe::10000", "3ffe::goog", "3ffe::-0",
+        "3ffe::+0", "3ffe::-1", ":", ":::", "::1.2.3", "::1.2.3.4.5", "::1.2.3.4:", "1.2.3.4::",
+        "2001:db8::1:", ":2001:db8::1", ":1:2:3:4:5:6:7", "1:2:3:4:5:6:7:", ":1:2:3:4:5:6:",
+    ]
+    dump("ip_parser.json", {
+        "source": "test/src/test/java/vproxy/test/cases/TestIpParser.java:12-191",
+        "v4_ok": [{"s": s, "bytes": b} for s, b in v4_ok],
+        "v4_fail": v4_fail,
+        "v6_ok": v6,
+        "bogus": bogus,
+    })
+
+
+# ---------------------------------------------------------------------------
+# TestRouteTable (+ Appendix B F3 example)
+# ---------------------------------------------------------------------------
+def route_table():
+    expect = ["192.168.3.0/24", "192.168.0.0/16", "0.0.0.0/0"]
+    cases = [
+        {"source": "TestRouteTable.java:28-35 ordering",
+         "add": ["192.168.0.0/16", "192.168.3.0/24", "0.0.0.0/0"], "expect": expect,
+         "lookups": []},
+        {"source": "TestRouteTable.java:37-46 ordering2",
+         "add": ["192.168.0.0/16", "0.0.0.0/0", "192.168.3.0/24"], "expect": expect,
+         "lookups": []},
+        {"source": "SURVEY.md Appendix B (RouteTable.java:110-154, not LPM)",
+         "add": ["10.1.0.0/16", "192.168.0.0/16", "10.2.0.0/16", "10.0.0.0/8"],
+         "expect": ["10.1.0.0/16", "10.0.0.0/8", "192.168.0.0/16", "10.2.0.0/16"],
+         "lookups": [["10.2.0.1", 1], ["10.1.2.3", 0], ["192.168.1.1", 2], ["11.0.0.1", -1]]},
+    ]
+    dump("route_table.json", {"cases": cases})
+
+
+# ---------------------------------------------------------------------------
+# Appendix B quirk KATs + behavioural scenarios transcribed from integration tests
+# ---------------------------------------------------------------------------
+def kats():
+    mask_match = [  # SURVEY.md Appendix B (Network.java:183-278)
+        [False, "1.2.3.4", "::/0"], [True, "1.2.3.4", "::/80"], [True, "1.2.3.4", "::/33"],
+        [True, "1.2.3.4", "::ffff:0:0/96"], [True, "::ffff:1.2.3.4", "0.0.0.0/0"],
+        [True, "::1", "0.0.0.0/0"], [False, "2001:db8::1", "0.0.0.0/0"],
+        [True, "2001:db8::1", "::/0"],
+    ]
+    # Upstream.searchForGroup scenarios: groups are [handle annos, group annos]
+    # with annos = {"host":..., "port":..., "uri":...}; hint = Hint.of* args.
+    hints = [
+        {"source": "SURVEY.md Appendix B tie-break (Upstream.java:190-196 strict >)",
+         "groups": [[{}, {"host": "com"}], [{}, {"host": "example.com"}]],
+         "queries": [[{"host": "a.example.com"}, 0]]},
+        {"source": "SURVEY.md Appendix B www. (Hint.java:57-73)",
+         "groups": [[{}, {"host": "example.com"}], [{}, {"host": "www.example.com"}]],
+         "queries": [[{"host": "www.example.com"}, 1], [{"host": "www.example.com:8080"}, 0],
+                     [{"host": "www.example.com", "port": 80}, 1]]},
+        {"source": "SURVEY.md Appendix B port filter (Hint.java:120-128)",
+         "groups": [[{}, {"port": 80}], [{}, {"host": "a.com", "port": 8080}],
+                    [{}, {"host": "a.com"}]],
+         "queries": [[{"host": "a.com", "port": 80}, 2], [{"host": "a.com", "port": 8080}, 1],
+                     [{"host": "a.com"}, 1], [{"host": "b.com", "port": 80}, -1]]},
+        {"source": "TestSocks5.java:62-88,129-148 proxyDomain (Socks5Server.java:62-66 ofHostPort)",
+         "groups": [[{}, {}], [{}, {"host": "domain.com", "port": "80"}]],
+         "queries": [[{"host": "domain.com", "port": 80}, 1], [{"host": "domain.com", "port": 81}, -1]]},
+        {"source": "TestProtocols.java:67-93,226-260 host/uri routing (HttpContext.java:55-71)",
+         "groups": [[{}, {"host": "s1.test.com", "uri": "/a"}],
+                    [{}, {"host": "s2.test.com", "uri": "/b"}]],
+         "queries": [[{"host": "s1.test.com", "uri": "/"}, 0], [{"host": "s2.test.com", "uri": "/"}, 1],
+                     [{"uri": "/a"}, 0], [{"uri": "/b"}, 1], [{"host": "s1.test.com"}, 0],
+                     [{"host": "127.0.0.1", "uri": "/a"}, 0], [{"host": "127.0.0.1", "uri": "/b"}, 1]]},
+        {"source": "CI.java:563-630 simpleSocks5 (hint-host + hint-port 8080)",
+         "groups": [[{}, {"host": "myexample.com", "port": "8080"}],
+                    [{}, {"host": "myexample2.com", "port": "8080"}]],
+         "queries": [[{"host": "myexample.com", "port": 8080}, 0],
+                     [{"host": "myexample2.com", "port": 8080}, 1]]},
+        {"source": "Hint.java:144-157 uri levels (length+1, prefix, wildcard, cap 1023)",
+         "groups": [[{}, {"uri": "*"}], [{}, {"uri": "/a"}], [{}, {"uri": "/a/b"}],
+                    [{"host": "x.com"}, {"host": "y.com", "uri": "/a"}]],
+         "queries": [[{"uri": "/a/b/c"}, 2], [{"uri": "/a/"}, 1], [{"uri": "/z"}, 0],
+                     [{"host": "x.com", "uri": "/a"}, 3], [{"host": "y.com", "uri": "/a"}, 1],
+                     [{"uri": "/a?q=1"}, 1]]},
+    ]
+    dns = [  # CI.java:632-697 dnsServer + SURVEY.md Appendix B DNS flow (DNSServer.java:116-166)
+        {"source": "CI.java:632-697 dnsServer; Appendix B DNS",
+         "groups": [[{}, {"host": "example.com"}], [{}, {"host": "test.com"}]],
+         "hosts": [["localhost", 0], ["localhost.", 0], ["example.com", 1], ["example.com.", 1]],
+         "queries": [["example.com.", 1, 1],      # hosts hit on raw qname (kind HOSTS)
+                     ["test.com.", 2, 1],          # hint-host group
+                     ["a.test.com.", 2, 1],
+                     ["1.2.3.4.", 3, 4],           # IP literal v4
+                     ["::1.", 3, 6],
+                     ["x.vproxy.local.", 4, 0],
+                     ["nothing.org.", 5, 0]]},
+    ]
+    # SecurityGroup scenarios: a list of steps (TestTcpLB.java:640-674, CI.java:1071-1197)
+    lb, s5 = 7005, 7006
+    sg = [
+        {"source": "TestTcpLB.java:640-674 forbidOnRunning (lbPort 18080)",
+         "steps": [
+             ["default", True],
+             ["add", "secgr0", "127.0.0.1/32", "TCP", 18080, 18080, False],
+             ["check", "TCP", "127.0.0.1", 18080, False], ["check", "TCP", "127.0.0.1", 18081, True],
+             ["remove", "secgr0"],
+             ["check", "TCP", "127.0.0.1", 18080, True]]},
+        {"source": "CI.java:1071-1197 security-group flips (lbPort 7005, socks5Port 7006)",
+         "steps": [
+             ["default", True], ["check", "TCP", "127.0.0.1", lb, True],
+             ["check", "TCP", "127.0.0.1", s5, True],
+             ["default", False], ["check", "TCP", "127.0.0.1", lb, False],
+             ["check", "TCP", "127.0.0.1", s5, False],
+             ["add", "lb", "127.0.0.1/32", "TCP", lb, lb, True],
+             ["check", "TCP", "127.0.0.1", lb, True], ["check", "TCP", "127.0.0.1", s5, False],
+             ["add", "s5", "127.0.0.1/32", "TCP", s5, s5, True],
+             ["check", "TCP", "127.0.0.1", lb, True], ["check", "TCP", "127.0.0.1", s5, True],
+             ["remove", "lb"],
+             ["check", "TCP", "127.0.0.1", lb, False], ["check", "TCP", "127.0.0.1", s5, True],
+             ["remove", "s5"],
+             ["check", "TCP", "127.0.0.1", lb, False], ["check", "TCP", "127.0.0.1", s5, False],
+             ["default", True], ["add", "lb", "127.0.0.1/32", "TCP", lb, lb, False],
+             ["check", "TCP", "127.0.0.1", lb, False], ["check", "TCP", "127.0.0.1", s5, True]]},
+        {"source": "SURVEY.md Appendix B: empty TCP list -> defaultAllow regardless of UDP rules",
+         "steps": [
+             ["default", False], ["add", "u", "0.0.0.0/0", "UDP", 0, 65535, True],
+             ["check", "TCP", "1.2.3.4", 80, False], ["check", "UDP", "1.2.3.4", 80, True]]},
+    ]
+    dump("kats.json", {"mask_match": [{"expect": e, "input": i, "net": n}
+                                      for e, i, n in mask_match],
+                       "hints": hints, "dns": dns, "security_group": sg})
+
+
+if __name__ == "__main__":
+    netmask()
+    ip_parser()
+    route_table()
+    kats()

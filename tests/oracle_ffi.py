@@ -1,0 +1,356 @@
+"""ctypes bindings for the CPU oracle (oracle/vc_oracle.c).
+
+Test infrastructure only: the oracle is the parity checker.  Product code in
+vproxy_amd/ never imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "build", "libvc_oracle.so")
+
+_lib = None
+
+
+class VoNet(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 16), ("mask", C.c_uint8 * 16),
+                ("ip_len", C.c_int32), ("mask_len", C.c_int32)]
+
+
+class VoSgRule(C.Structure):
+    _fields_ = [("net", VoNet), ("min_port", C.c_int32), ("max_port", C.c_int32),
+                ("allow", C.c_int32)]
+
+
+class VoAnnos(C.Structure):
+    _fields_ = [("host", C.c_char_p), ("host_len", C.c_int32), ("port", C.c_int32),
+                ("uri", C.c_char_p), ("uri_len", C.c_int32)]
+
+
+class VoGroup(C.Structure):
+    _fields_ = [("handle", VoAnnos), ("group", VoAnnos)]
+
+
+class VoHint(C.Structure):
+    _fields_ = [("host", C.c_void_p), ("host_len", C.c_int32), ("port", C.c_int32),
+                ("uri", C.c_void_p), ("uri_len", C.c_int32)]
+
+
+class VoRouteTable(C.Structure):
+    _fields_ = [("v4", C.POINTER(VoNet)), ("n4", C.c_int), ("cap4", C.c_int),
+                ("v6", C.POINTER(VoNet)), ("n6", C.c_int), ("cap6", C.c_int)]
+
+
+class VoHosts(C.Structure):
+    _fields_ = [("keys", C.POINTER(C.c_char_p)), ("key_lens", C.POINTER(C.c_int32)),
+                ("values", C.POINTER(C.c_int32)), ("n", C.c_int)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ROOT, "oracle", "vc_oracle.c")
+        if (not os.path.exists(LIB_PATH) or
+                os.path.getmtime(LIB_PATH) < os.path.getmtime(src)):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        u8p, i32p = P(C.c_uint8), P(C.c_int32)
+        L.vo_parse_ipv4.argtypes = [C.c_char_p, C.c_int, u8p]
+        L.vo_parse_ipv6.argtypes = [C.c_char_p, C.c_int, u8p]
+        L.vo_parse_ip.argtypes = [C.c_char_p, C.c_int, u8p]
+        L.vo_is_ipv6.argtypes = [C.c_char_p, C.c_int]
+        L.vo_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
+        L.vo_parse_mask.argtypes = [C.c_int, u8p]
+        L.vo_mask_int.argtypes = [u8p, C.c_int]
+        L.vo_valid_network.argtypes = [u8p, C.c_int, u8p, C.c_int]
+        L.vo_mask_match.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, C.c_int]
+        L.vo_net_from_str.argtypes = [C.c_char_p, C.c_int, P(VoNet)]
+        L.vo_net_contains_ip.argtypes = [P(VoNet), u8p, C.c_int]
+        L.vo_net_contains_net.argtypes = [P(VoNet), P(VoNet)]
+        L.vo_sg_allow.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int, C.c_int,
+                                  u8p, C.c_int, C.c_int, P(C.c_int)]
+        L.vo_sg_allow_batch_v4.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                           C.c_void_p, C.c_void_p, C.c_int]
+        L.vo_sg_allow_batch_v6.argtypes = L.vo_sg_allow_batch_v4.argtypes
+        L.vo_rt_init.argtypes = [P(VoRouteTable)]
+        L.vo_rt_free.argtypes = [P(VoRouteTable)]
+        L.vo_rt_add.argtypes = [P(VoRouteTable), P(VoNet)]
+        L.vo_rt_lookup.argtypes = [P(VoRouteTable), u8p, C.c_int]
+        L.vo_rt_lookup_list.argtypes = [P(VoNet), C.c_int, u8p, C.c_int]
+        L.vo_rt_lookup_batch_v4.argtypes = [P(VoNet), C.c_int, C.c_void_p, C.c_int64,
+                                            C.c_void_p, C.c_int]
+        L.vo_rt_lookup_batch_v6.argtypes = L.vo_rt_lookup_batch_v4.argtypes
+        L.vo_hint_of.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.vo_hint_of.restype = VoHint
+        L.vo_match_level.argtypes = [P(VoHint), P(VoAnnos), C.c_int]
+        L.vo_search_for_group.argtypes = [P(VoGroup), C.c_int, P(VoHint)]
+        L.vo_dns_classify.argtypes = [P(VoHosts), P(VoGroup), C.c_int, C.c_char_p, C.c_int,
+                                      P(C.c_int32)]
+        L.vo_hosts_parse.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p,
+                                     C.c_int, u8p, i32p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else s
+
+
+def parse_ip(s):
+    b = (C.c_uint8 * 16)()
+    s = _b(s)
+    n = lib().vo_parse_ip(s, len(s), b)
+    return None if n < 0 else bytes(b[:n])
+
+
+def parse_ipv4(s):
+    b = (C.c_uint8 * 16)()
+    s = _b(s)
+    n = lib().vo_parse_ipv4(s, len(s), b)
+    return None if n < 0 else bytes(b[:n])
+
+
+def parse_ipv6(s):
+    b = (C.c_uint8 * 16)()
+    s = _b(s)
+    n = lib().vo_parse_ipv6(s, len(s), b)
+    return None if n < 0 else bytes(b[:n])
+
+
+def is_ip_literal(s):
+    s = _b(s)
+    return bool(lib().vo_is_ip_literal(s, len(s)))
+
+
+def parse_mask(m):
+    b = (C.c_uint8 * 16)()
+    n = lib().vo_parse_mask(m, b)
+    if n < 0:
+        raise ValueError("unknown mask %d" % m)
+    return bytes(b[:n])
+
+
+def _u8(b):
+    return (C.c_uint8 * max(1, len(b))).from_buffer_copy(b if b else b"\0")
+
+
+def valid_network(addr, mask):
+    return bool(lib().vo_valid_network(_u8(addr), len(addr), _u8(mask), len(mask)))
+
+
+def mask_match(inp, rule, mask):
+    return bool(lib().vo_mask_match(_u8(inp), len(inp), _u8(rule), len(rule), _u8(mask), len(mask)))
+
+
+def net(s):
+    n = VoNet()
+    s = _b(s)
+    if lib().vo_net_from_str(s, len(s), C.byref(n)) != 0:
+        raise ValueError("invalid network %r" % s)
+    return n
+
+
+def net_str(n):
+    """Network.toString (Network.java:66-69) -- canonical text for comparisons."""
+    ip = bytes(n.ip[:n.ip_len])
+    mi = lib().vo_mask_int((C.c_uint8 * 16)(*n.mask), n.mask_len)
+    if n.ip_len == 4:
+        s = ".".join(str(x) for x in ip)
+    else:
+        import ipaddress
+        s = str(ipaddress.IPv6Address(ip))
+    return "%s/%d" % (s, mi)
+
+
+def sg_rule(netstr, min_port, max_port, allow):
+    r = VoSgRule()
+    r.net = net(netstr)
+    r.min_port, r.max_port, r.allow = min_port, max_port, 1 if allow else 0
+    return r
+
+
+def sg_rule_arr(rules):
+    arr = (VoSgRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i] = r
+    return arr
+
+
+def sg_allow(tcp, udp, default_allow, proto, ip_bytes, port):
+    v = C.c_int()
+    idx = lib().vo_sg_allow(sg_rule_arr(tcp), len(tcp), sg_rule_arr(udp), len(udp),
+                            1 if default_allow else 0, proto, _u8(ip_bytes), len(ip_bytes), port,
+                            C.byref(v))
+    return idx, bool(v.value)
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def sg_allow_batch_v4(tcp, udp, default_allow, proto, src4, port, nthreads=1):
+    n = len(src4)
+    out = np.empty(n, np.int32)
+    ver = np.empty(n, np.uint8)
+    ta, ua = sg_rule_arr(tcp), sg_rule_arr(udp)
+    lib().vo_sg_allow_batch_v4(ta, len(tcp), ua, len(udp), 1 if default_allow else 0,
+                               _ptr(proto), _ptr(src4), _ptr(port), n, _ptr(out), _ptr(ver),
+                               nthreads)
+    return out, ver
+
+
+def sg_allow_batch_v6(tcp, udp, default_allow, proto, src6, port, nthreads=1):
+    n = len(port)
+    out = np.empty(n, np.int32)
+    ver = np.empty(n, np.uint8)
+    ta, ua = sg_rule_arr(tcp), sg_rule_arr(udp)
+    lib().vo_sg_allow_batch_v6(ta, len(tcp), ua, len(udp), 1 if default_allow else 0,
+                               _ptr(proto), _ptr(src6), _ptr(port), n, _ptr(out), _ptr(ver),
+                               nthreads)
+    return out, ver
+
+
+class RouteTable:
+    """Oracle RouteTable: RouteTable.addRule ordering + linear lookup."""
+
+    def __init__(self):
+        self.t = VoRouteTable()
+        lib().vo_rt_init(C.byref(self.t))
+
+    def __del__(self):
+        try:
+            lib().vo_rt_free(C.byref(self.t))
+        except Exception:
+            pass
+
+    def add(self, netstr):
+        n = net(netstr) if isinstance(netstr, (str, bytes)) else netstr
+        return lib().vo_rt_add(C.byref(self.t), C.byref(n)) == 0
+
+    def rules(self):
+        return ([net_str(self.t.v4[i]) for i in range(self.t.n4)] +
+                [net_str(self.t.v6[i]) for i in range(self.t.n6)])
+
+    def lookup(self, ip_bytes):
+        return lib().vo_rt_lookup(C.byref(self.t), _u8(ip_bytes), len(ip_bytes))
+
+
+def net_list(nets):
+    arr = (VoNet * max(1, len(nets)))()
+    for i, n in enumerate(nets):
+        arr[i] = n
+    return arr
+
+
+def rt_lookup_batch_v4(v4_nets_arr, n4, dst4, nthreads=1):
+    out = np.empty(len(dst4), np.int32)
+    lib().vo_rt_lookup_batch_v4(v4_nets_arr, n4, _ptr(dst4), len(dst4), _ptr(out), nthreads)
+    return out
+
+
+def rt_lookup_batch_v6(v6_nets_arr, n6, dst6, nthreads=1):
+    n = dst6.shape[0]
+    out = np.empty(n, np.int32)
+    lib().vo_rt_lookup_batch_v6(v6_nets_arr, n6, _ptr(dst6), n, _ptr(out), nthreads)
+    return out
+
+
+def parse_java_int(s):
+    """Integer.parseInt with Annotations' failure -> 0 (Annotations.java:45-58)."""
+    if isinstance(s, int):
+        return s
+    try:
+        if s is None or not s or s.strip() != s:
+            raise ValueError
+        v = int(s, 10)
+        if v < -2**31 or v > 2**31 - 1 or "_" in s:
+            raise ValueError
+        return v
+    except ValueError:
+        return 0
+
+
+class Groups:
+    """Keeps the byte buffers alive for a vo_group array."""
+
+    def __init__(self, groups):
+        self.keep = []
+        self.arr = (VoGroup * max(1, len(groups)))()
+        self.n = len(groups)
+        for i, (ha, ga) in enumerate(groups):
+            self.arr[i].handle = self._annos(ha)
+            self.arr[i].group = self._annos(ga)
+
+    def _annos(self, a):
+        x = VoAnnos()
+        h, u = a.get("host"), a.get("uri")
+        if h is not None:
+            hb = _b(h)
+            self.keep.append(hb)
+            x.host, x.host_len = hb, len(hb)
+        x.port = parse_java_int(a.get("port", 0))
+        if u is not None:
+            ub = _b(u)
+            self.keep.append(ub)
+            x.uri, x.uri_len = ub, len(ub)
+        return x
+
+
+def hint_of(host=None, port=0, uri=None):
+    hb = _b(host) if host is not None else None
+    ub = _b(uri) if uri is not None else None
+    hbuf = C.create_string_buffer(hb, len(hb)) if hb is not None else None
+    ubuf = C.create_string_buffer(ub, len(ub)) if ub is not None else None
+    h = lib().vo_hint_of(C.cast(hbuf, C.c_void_p) if hbuf is not None else None,
+                         len(hb) if hb is not None else 0, port,
+                         C.cast(ubuf, C.c_void_p) if ubuf is not None else None,
+                         len(ub) if ub is not None else 0)
+    return h, (hbuf, ubuf)
+
+
+def search_for_group(groups, host=None, port=0, uri=None):
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    h, keep = hint_of(host, port, uri)
+    return lib().vo_search_for_group(g.arr, g.n, C.byref(h))
+
+
+class Hosts:
+    def __init__(self, pairs):
+        self.keys = [_b(k) for k, _ in pairs]
+        n = len(pairs)
+        self.karr = (C.c_char_p * max(1, n))(*self.keys)
+        self.larr = (C.c_int32 * max(1, n))(*[len(k) for k in self.keys])
+        self.varr = (C.c_int32 * max(1, n))(*[v for _, v in pairs])
+        self.h = VoHosts(self.karr, self.larr, self.varr, n)
+
+
+def dns_classify(hosts, groups, qname):
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    h = hosts if isinstance(hosts, Hosts) else Hosts(hosts)
+    q = _b(qname)
+    v = C.c_int32()
+    kind = lib().vo_dns_classify(C.byref(h.h), g.arr, g.n, q, len(q), C.byref(v))
+    return kind, v.value
+
+
+def hosts_parse(text):
+    t = _b(text)
+    cap = 4 * len(t) + 16
+    keybuf = C.create_string_buffer(cap * 2)
+    ko = (C.c_int32 * cap)()
+    kl = (C.c_int32 * cap)()
+    kv = (C.c_int32 * cap)()
+    lip = (C.c_uint8 * (16 * cap))()
+    lil = (C.c_int32 * cap)()
+    n = lib().vo_hosts_parse(t, len(t), keybuf, cap * 2, ko, kl, kv, cap, lip, lil, cap)
+    assert n >= 0
+    raw = keybuf.raw
+    pairs = [(raw[ko[i]:ko[i] + kl[i]].decode(), kv[i]) for i in range(n)]
+    nlines = (max(kv[i] for i in range(n)) + 1) if n else 0
+    ips = [bytes(lip[16 * j:16 * j + lil[j]]) for j in range(nlines)]
+    return pairs, ips
