@@ -1,0 +1,249 @@
+/*
+ * vclassify.h -- C ABI of libvclassify, the MI355X-native batched classifier
+ * behind vproxy's classification API.
+ *
+ * Each batched entry point replaces one Java hot-path method (paths relative
+ * to the nintha/vproxy tree).  The JNI shim a maintainer would add on the Java
+ * side is shown in INTEGRATION.md; it maps 1:1 onto these functions in the
+ * style of base/src/main/c/vfd_posix_GeneralPosix.c (jlong handles, direct
+ * ByteBuffers, status codes mapped to IOException/UnsupportedOperationException).
+ *
+ * Conventions
+ *  - Plain C types only.  Every function returns an int status (VC_OK = 0,
+ *    negative VC_E* on error); the message is available from vc_last_error().
+ *  - Results are indices into the *live Java lists* in list order, -1 for
+ *    null / "no rule" (the caller maps index -> SecurityGroupRule / RouteRule
+ *    / ServerGroupHandle exactly as the Java code would have returned it).
+ *  - *_dev functions take DEVICE pointers and a hipStream_t (passed as void*,
+ *    NULL = the context's stream); they are asynchronous.  The plain variants
+ *    take HOST pointers and are synchronous (H2D + kernel + D2H).
+ *  - IPv4 addresses are uint32 in IP.ipv4Bytes2Int order (big-endian value,
+ *    vfd/IP.java:476-478); IPv6 addresses are 16 raw bytes per item.
+ *  - Strings are packed in a byte blob with uint32 offsets (n+1 entries, item
+ *    i = blob[off[i], off[i+1])); an optional uint8 `null` array marks Java
+ *    null items (NULL pointer = no null items).
+ *  - Rule tables are compiled into immutable snapshots and published
+ *    atomically; concurrent classify calls keep using the snapshot they
+ *    started with (threads: SURVEY.md §8(b) "Threading").
+ */
+#ifndef VCLASSIFY_H
+#define VCLASSIFY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VC_OK         0
+#define VC_EINVAL    -1   /* IllegalArgumentException (bad network, mask, size) */
+#define VC_EEXIST    -2   /* AlreadyExistException */
+#define VC_ENOTFOUND -3   /* NotFoundException */
+#define VC_EXEXC     -4   /* XException (RouteTable validation) */
+#define VC_EDEVICE   -5   /* HIP runtime / device error */
+#define VC_ENOMEM    -6
+#define VC_ESTATE    -7   /* nothing compiled yet for this classifier */
+
+#define VC_PROTO_TCP  6   /* vproxybase.connection.Protocol.TCP */
+#define VC_PROTO_UDP 17   /* Protocol.UDP (any non-6 value selects the UDP list) */
+
+typedef struct vc_ctx vc_ctx;
+
+const char *vc_version(void);
+/* Thread-local message of the last failing call on this thread. */
+const char *vc_last_error(void);
+
+/* One classifier instance on one GPU (device ordinal).  Fails with
+ * VC_EDEVICE when no MI355X (gfx950) device is usable: there is no CPU path. */
+int vc_create(int device, vc_ctx **out);
+void vc_destroy(vc_ctx *ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Network value: base/src/main/java/vproxybase/util/Network.java            */
+/* ------------------------------------------------------------------------ */
+typedef struct vc_net {
+    uint8_t ip[16];     /* Network.ip, first ip_len bytes used */
+    uint8_t mask[16];   /* Network.mask = parseMask(m): 4 bytes if m <= 32 else 16 */
+    int32_t ip_len;     /* 4 or 16 */
+    int32_t mask_len;   /* 4 or 16 */
+} vc_net;
+
+/* new Network(String) (Network.java:16-25): "a.b.c.d/m" or "v6/m";
+ * VC_EINVAL when validNetworkStr fails. */
+int vc_net_parse(const char *s, vc_net *out);
+/* new Network(ip, Network.parseMask(prefix)) with validNetwork enforced
+ * (NetworkHandle.get, app/.../param/NetworkHandle.java:21-30). */
+int vc_net_from_prefix(const uint8_t *ip, int ip_len, int prefix, vc_net *out);
+/* Network.contains(IP) -> Network.maskMatch (Network.java:27-29,183-278). */
+int vc_net_contains_ip(const vc_net *net, const uint8_t *ip, int ip_len);
+/* IP.parseIpString (vfd/IP.java:112-117): returns 4, 16 or VC_EINVAL. */
+int vc_ip_parse(const char *s, uint8_t out[16]);
+
+/* ------------------------------------------------------------------------ */
+/* SecurityGroup: core/src/main/java/vproxy/component/secure/SecurityGroup.java */
+/* ------------------------------------------------------------------------ */
+typedef struct vc_acl_rule {
+    vc_net net;          /* SecurityGroupRule.network */
+    int32_t min_port;    /* SecurityGroupRule.minPort */
+    int32_t max_port;    /* SecurityGroupRule.maxPort */
+    int32_t allow;       /* SecurityGroupRule.allow */
+} vc_acl_rule;
+
+/* Compile SecurityGroup{tcpRules, udpRules, defaultAllow} (list order =
+ * priority) into the GPU ACL image and publish it. */
+int vc_compile_acl(vc_ctx *ctx, const vc_acl_rule *tcp, int n_tcp,
+                   const vc_acl_rule *udp, int n_udp, int default_allow);
+
+/* Batched SecurityGroup.allow(Protocol, IP, int) (SecurityGroup.java:30-45).
+ * out_idx[i] = index of the first matching rule in the protocol's list, or
+ * -1 when defaultAllow decided; out_allow[i] (optional) = the boolean allow()
+ * returns.  proto: VC_PROTO_TCP selects tcpRules, anything else udpRules. */
+int vc_acl_classify_v4_dev(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
+                           const uint16_t *port, int64_t n, int32_t *out_idx,
+                           uint8_t *out_allow, void *stream);
+int vc_acl_classify_v6_dev(vc_ctx *ctx, const uint8_t *proto, const uint8_t *src6,
+                           const uint16_t *port, int64_t n, int32_t *out_idx,
+                           uint8_t *out_allow, void *stream);
+int vc_acl_classify_v4(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
+                       const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_allow);
+int vc_acl_classify_v6(vc_ctx *ctx, const uint8_t *proto, const uint8_t *src6,
+                       const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_allow);
+
+/* ------------------------------------------------------------------------ */
+/* RouteTable: core/src/main/java/vswitch/RouteTable.java                    */
+/* ------------------------------------------------------------------------ */
+/* Compile rulesV4 / rulesV6 (list order = priority: lookup returns the first
+ * matching rule, RouteTable.java:44-59) into stride tries and publish. */
+int vc_compile_routes(vc_ctx *ctx, const vc_net *v4, int n4, const vc_net *v6, int n6);
+/* Batched RouteTable.lookup(IP): out[i] = index in rulesV4 (v4 call) or
+ * rulesV6 (v6 call), -1 for null. */
+int vc_route_lookup_v4_dev(vc_ctx *ctx, const uint32_t *dst4, int64_t n, int32_t *out,
+                           void *stream);
+int vc_route_lookup_v6_dev(vc_ctx *ctx, const uint8_t *dst6, int64_t n, int32_t *out,
+                           void *stream);
+int vc_route_lookup_v4(vc_ctx *ctx, const uint32_t *dst4, int64_t n, int32_t *out);
+int vc_route_lookup_v6(vc_ctx *ctx, const uint8_t *dst6, int64_t n, int32_t *out);
+
+/* ------------------------------------------------------------------------ */
+/* Upstream hint matching: core/.../svrgroup/Upstream.java + Hint.java       */
+/* ------------------------------------------------------------------------ */
+typedef struct vc_annos {      /* vproxybase.util.Annotations hint fields */
+    const char *host; int32_t host_len;   /* vproxy/hint-host, NULL = absent */
+    int32_t port;                         /* vproxy/hint-port, 0 = absent */
+    const char *uri; int32_t uri_len;     /* vproxy/hint-uri, NULL = absent */
+} vc_annos;
+
+typedef struct vc_group_annos {  /* one ServerGroupHandle, in Upstream list order */
+    vc_annos handle;             /* ServerGroupHandle.getAnnotations() */
+    vc_annos group;              /* handle.group.getAnnotations() */
+} vc_group_annos;
+
+/* Compile Upstream.serverGroupHandles (list order) for searchForGroup. */
+int vc_compile_upstream(vc_ctx *ctx, const vc_group_annos *groups, int n);
+
+/* Batched Upstream.searchForGroup(Hint.ofHostPortUri(host, port, uri))
+ * (Upstream.java:187-198, Hint.java:17-160): raw host/uri strings are
+ * formatted on the device exactly as Hint.formatHost/formatUri do.
+ * host_null / uri_blob / uri_off / uri_null may be NULL.  out_group[i] =
+ * handle index or -1 (null). */
+int vc_hint_search_dev(vc_ctx *ctx, const uint8_t *host_blob, const uint32_t *host_off,
+                       const uint8_t *host_null, const uint16_t *port,
+                       const uint8_t *uri_blob, const uint32_t *uri_off, const uint8_t *uri_null,
+                       int64_t n, int32_t *out_group, void *stream);
+int vc_hint_search(vc_ctx *ctx, const uint8_t *host_blob, const uint32_t *host_off,
+                   const uint8_t *host_null, const uint16_t *port,
+                   const uint8_t *uri_blob, const uint32_t *uri_off, const uint8_t *uri_null,
+                   int64_t n, int32_t *out_group);
+
+/* ------------------------------------------------------------------------ */
+/* DNSServer classification: core/src/main/java/vproxy/dns/DNSServer.java:116-166 */
+/* ------------------------------------------------------------------------ */
+#define VC_DNS_HOSTS       1  /* hosts.get(qname) hit: value = hosts value */
+#define VC_DNS_GROUP       2  /* rrsets.searchForGroup(Hint.ofHost(domain)): value = handle index */
+#define VC_DNS_IP_LITERAL  3  /* IP.isIpLiteral(domain): value = 4 or 6 (IP.from type) */
+#define VC_DNS_INTERNAL    4  /* domain.endsWith(".vproxy.local") */
+#define VC_DNS_RECURSIVE   5  /* falls through to runRecursive */
+
+/* The hosts map (Resolver.getHosts result, exact keys incl. trailing-dot
+ * variants).  The rrsets Upstream is the one given to vc_compile_upstream. */
+int vc_compile_hosts(vc_ctx *ctx, const char *const *keys, const int32_t *key_lens,
+                     const int32_t *values, int n);
+/* Resolver.getHosts over hosts-file text (Resolver.java:62-153), then
+ * vc_compile_hosts; value = index of the accepted host line. */
+int vc_compile_hosts_text(vc_ctx *ctx, const char *text, int64_t len);
+int vc_dns_classify_dev(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int64_t n,
+                        uint8_t *out_kind, int32_t *out_value, void *stream);
+int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int64_t n,
+                    uint8_t *out_kind, int32_t *out_value);
+
+/* ------------------------------------------------------------------------ */
+/* Combined per-packet pipeline: ACL -> route -> host      */
+/* ------------------------------------------------------------------------ */
+/* For each IPv4 packet: out_acl = SecurityGroup.allow index on (proto, src,
+ * dport), out_route = RouteTable.lookup(dst) index, out_group =
+ * pool_group[host_id] (the per-pass classified hostname pool from
+ * vc_hint_search_dev; host_id == 0xFFFFFFFF -> -1).  out_allow optional. */
+int vc_pipeline_v4_dev(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
+                       const uint32_t *dst4, const uint16_t *dport, const uint32_t *host_id,
+                       const int32_t *pool_group, int64_t n, int32_t *out_acl,
+                       int32_t *out_route, int32_t *out_group, uint8_t *out_allow, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Per-rule hit counters (no reference counterpart)          */
+/* ------------------------------------------------------------------------ */
+#define VC_COUNTERS_ACL    0  /* [tcp rules][udp rules][tcp default][udp default] */
+#define VC_COUNTERS_ROUTE  1  /* [v4 rules][v6 rules][v4 null][v6 null] */
+#define VC_COUNTERS_GROUP  2  /* [handles][null] */
+/* When enabled, every classify call adds its hits into device-resident uint64
+ * counters of the current snapshot (reset when a table is recompiled). */
+int vc_counters_enable(vc_ctx *ctx, int on);
+/* Device pointer + length of a counter array (for an RCCL all-reduce). */
+int vc_counters_device(vc_ctx *ctx, int kind, uint64_t **dev_ptr, int64_t *n);
+int vc_counters_read(vc_ctx *ctx, int kind, uint64_t *host, int64_t n);
+int vc_counters_reset(vc_ctx *ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Control-plane mirrors (host only, no GPU): the reference's list-ordering  */
+/* and validation rules, so a caller can keep the exact Java list order.    */
+/* ------------------------------------------------------------------------ */
+typedef struct vc_secgroup vc_secgroup;
+/* new SecurityGroup(alias, defaultAllow) (SecurityGroup.java:21-24) */
+int vc_secgroup_new(const char *alias, int default_allow, vc_secgroup **out);
+void vc_secgroup_free(vc_secgroup *sg);
+int vc_secgroup_set_default(vc_secgroup *sg, int default_allow);
+/* SecurityGroup.addRule (SecurityGroup.java:56-83): VC_EEXIST on duplicate
+ * alias or duplicate (network, protocol, minPort, maxPort). */
+int vc_secgroup_add_rule(vc_secgroup *sg, const char *alias, const vc_net *net, int proto,
+                         int min_port, int max_port, int allow);
+/* SecurityGroup.removeRule (SecurityGroup.java:85-103): VC_ENOTFOUND. */
+int vc_secgroup_remove_rule(vc_secgroup *sg, const char *alias);
+/* Rule counts and list export in list order (proto = VC_PROTO_TCP / UDP). */
+int vc_secgroup_rules(const vc_secgroup *sg, int proto, vc_acl_rule *out, int cap);
+int vc_secgroup_compile(vc_ctx *ctx, const vc_secgroup *sg);
+
+typedef struct vc_routetable vc_routetable;
+/* new RouteTable() (RouteTable.java:25-28) when v4net == NULL, else
+ * new RouteTable(Table) seeding "default"/"default-v6" (RouteTable.java:30-42). */
+int vc_routetable_new(const vc_net *v4net, const vc_net *v6net, int vni, vc_routetable **out);
+void vc_routetable_free(vc_routetable *rt);
+/* RouteTable.addRule (RouteTable.java:68-154) incl. the insertion-order
+ * heuristic.  via_ip NULL -> RouteRule(alias, net, toVni); else
+ * RouteRule(alias, net, ip) (via_len 4/16).  VC_EEXIST / VC_EXEXC as Java. */
+int vc_routetable_add_rule(vc_routetable *rt, const char *alias, const vc_net *net, int to_vni,
+                           const uint8_t *via_ip, int via_len);
+/* Bulk insert of vni rules in the given order.  Exact same final lists as
+ * repeated vc_routetable_add_rule; O(n log n) when every insert is no
+ * shorter than the rules already present, otherwise
+ * falls back to the per-rule heuristic. Aliases are "<prefix><i>". */
+int vc_routetable_add_rules(vc_routetable *rt, const char *alias_prefix, const vc_net *nets,
+                            int n, int to_vni);
+/* RouteTable.delRule (RouteTable.java:156-172) */
+int vc_routetable_del_rule(vc_routetable *rt, const char *alias);
+/* family 4 -> rulesV4, 6 -> rulesV6; returns count (writes up to cap). */
+int vc_routetable_rules(const vc_routetable *rt, int family, vc_net *out, int cap);
+int vc_routetable_compile(vc_ctx *ctx, const vc_routetable *rt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VCLASSIFY_H */

@@ -1,0 +1,121 @@
+"""Shared edge-case generators for the CPU (image) and GPU parity tests."""
+import numpy as np
+
+import oracle_ffi as O
+from vproxy_amd import workloads as W
+
+
+def rule_row(netstr, lo, hi, allow):
+    r = np.zeros(1, W.RULE_DT)
+    r["net"] = np.frombuffer(bytes(O.net(netstr)), W.NET_DT)
+    r["min_port"], r["max_port"], r["allow"] = lo, hi, 1 if allow else 0
+    return r
+
+
+def acl_edge_rules():
+    """Rule lists exercising Network.maskMatch's cross-family cases
+     and port-range edges."""
+    tcp_specs = [
+        ("10.0.0.0/8", 80, 80, False),
+        ("::ffff:0:0/96", 0, 1000, True),       # every IPv4 input (case 3)
+        ("::/80", 443, 443, False),             # every IPv4 input (case 3, m-96 < 0)
+        ("::/33", 22, 22, True),
+        ("2001:db8::/32", 0, 65535, False),     # 4-byte mask: first 4 bytes (case 1)
+        ("[0000:0010:0000:0000:0000:0000:0000:0000]/28", 100, 200, True),
+        ("127.0.0.1/32", 0, 65535, True),       # matches ::7f00:1 and ::ffff:7f00:1 (case 4)
+        ("1.2.3.0/24", 500, 400, True),         # min > max: never matches
+        ("::ffff:7f00:0/104", 5000, 6000, False),
+        ("::7f00:0/104", 6000, 7000, True),
+        ("0.0.0.0/0", 1024, 2048, True),
+        ("2001:db8:1::/48", 53, 53, True),
+        ("::/0", 0, 65535, True),               # never matches IPv4 input (case 2)
+        ("0.0.0.0/0", 0, 65535, False),         # catch-all
+        ("192.168.0.0/16", 0, 65535, True),     # shadowed by the catch-all
+    ]
+    udp_specs = [
+        ("0.0.0.0/0", 53, 53, True),
+        ("::1/128", 0, 65535, True),
+        ("::/0", 0, 0, False),
+        ("8.8.0.0/16", 0, 65535, False),
+        ("::ffff:8.8.8.0/120", 0, 65535, True),
+        ("8.8.8.8/32", 65535, 65535, True),
+        ("::8.8.8.0/120", 100, 65535, True),
+    ]
+    tcp = np.concatenate([rule_row(*s) for s in tcp_specs])
+    udp = np.concatenate([rule_row(*s) for s in udp_specs])
+    return tcp, udp
+
+
+def v6_edge_inputs(rng, n):
+    """IPv6 sources: mapped / compat IPv4, near-misses on bytes 10-11,
+    2001:db8 space, ::1, zero, random; edge ports."""
+    src = rng.integers(0, 256, (n, 16), dtype=np.int64).astype(np.uint8)
+    kind = rng.integers(0, 8, n)
+    v4 = rng.choice(np.array([[127, 0, 0, 1], [8, 8, 8, 8], [10, 1, 2, 3], [1, 2, 3, 4],
+                              [192, 168, 1, 1], [8, 8, 8, 200]], dtype=np.uint8), n)
+    rand4 = rng.integers(0, 256, (n, 4), dtype=np.int64).astype(np.uint8)
+    v4 = np.where((rng.random(n) < 0.5)[:, None], v4, rand4)
+    for k, (b10, b11) in enumerate([(0, 0), (0xFF, 0xFF), (0, 0xFF), (0xFF, 0)]):
+        sel = kind == k
+        src[sel, :10] = 0
+        src[sel, 10] = b10
+        src[sel, 11] = b11
+        src[sel, 12:] = v4[sel]
+    sel = kind == 4
+    src[sel, :4] = [0x20, 0x01, 0x0D, 0xB8]
+    src[sel & (rng.random(n) < 0.5), 4:6] = [0, 1]
+    sel = kind == 5
+    src[sel] = 0
+    src[sel & (rng.random(n) < 0.5), 15] = 1
+    sel = kind == 6
+    src[sel, 0] = 0
+    src[sel, 1] = rng.integers(0, 0x20, sel.sum())
+    proto = rng.choice(np.array([6, 17, 1], dtype=np.uint8), n)
+    port = rng.choice(np.array([0, 22, 53, 80, 100, 443, 999, 1000, 1024, 2048, 5000, 6000, 65535],
+                               dtype=np.uint16), n)
+    rp = rng.random(n) < 0.3
+    port[rp] = rng.integers(0, 65536, rp.sum())
+    return src, proto, port
+
+
+_HOSTS = ["com", "a.com", "b.a.com", "www.a.com", "x.net", "y.x.net", "*", "example.com",
+          "s1.test.com", "s2.test.com", "test.com", "", "a.b.c.d.e.f", "127.0.0.1", "::1",
+          "[::1]", "com.", "*.com"]
+_URIS = [None, None, None, "/", "/a", "/a/b", "*", "", "/b", "/a/b/c/d"]
+
+
+def hint_cases_random(rng, ng, nq):
+    """Groups with overlapping hint-hosts (long member lists, suffix chains),
+    handle/group annotation merging, hint-ports and hint-uris; queries with
+    ports, ':port' host forms, www., IPv6 literals, nulls and URI variants."""
+    groups = []
+    for _ in range(ng):
+        def annos():
+            a = {}
+            if rng.random() < 0.7:
+                a["host"] = _HOSTS[int(rng.integers(0, len(_HOSTS)))]
+            if rng.random() < 0.2:
+                a["port"] = int(rng.choice([80, 8080, 443]))
+            if rng.random() < 0.3:
+                u = _URIS[int(rng.integers(0, len(_URIS)))]
+                if u is not None:
+                    a["uri"] = u
+            return a
+        groups.append((annos() if rng.random() < 0.3 else {}, annos()))
+    prefixes = ["", "www.", "m.", "q.w."]
+    queries = []
+    for _ in range(nq):
+        r = rng.random()
+        if r < 0.05:
+            host = None
+        else:
+            host = prefixes[int(rng.integers(0, 4))] + _HOSTS[int(rng.integers(0, len(_HOSTS)))]
+            if rng.random() < 0.2:
+                host += ":%d" % int(rng.choice([80, 8080, 1]))
+            if rng.random() < 0.03:
+                host = "[::1]:80"
+        port = int(rng.choice([0, 0, 80, 8080, 443]))
+        uri = ["/a/b/c", "/a/", "/a?x=1", "/", "/b/", "*", "/z", None, None, "/a/b"][
+            int(rng.integers(0, 10))]
+        queries.append((host, port, uri))
+    return groups, _HOSTS, queries

@@ -1,0 +1,81 @@
+"""ctypes binding of the test-only image harness (tests/native/imgcheck.hip).
+
+It walks the compiled table images on the host with the kernels' own probe
+functions, so the compilers are checked against the oracle on CPU.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "native", "build", "libvc_imgcheck.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
+        L = C.CDLL(LIB)
+        vp = C.c_void_p
+        L.ic_acl.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp,
+                             vp, vp]
+        L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp]
+        L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
+        L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
+        L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def P(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return C.c_void_p(a.ctypes.data)
+    return C.cast(a, C.c_void_p)
+
+
+def acl(tcp, udp, dflt, family, proto, src, port):
+    n = len(port)
+    out = np.empty(n, np.int32)
+    allow = np.empty(n, np.uint8)
+    stats = np.zeros(8, np.int32)
+    rc = lib().ic_acl(P(tcp), len(tcp), P(udp), len(udp), 1 if dflt else 0, family, P(proto),
+                      P(src), P(port), n, P(out), P(allow), P(stats))
+    assert rc == 0, rc
+    return out, allow, stats
+
+
+def route(rules, family, keys):
+    n = len(keys)
+    out = np.empty(n, np.int32)
+    stats = np.zeros(2, np.int32)
+    rc = lib().ic_route(P(rules), len(rules), family, P(keys), n, P(out), P(stats))
+    assert rc == 0, rc
+    return out, stats
+
+
+def hint(group_arr, ng, hosts, ports, uris):
+    hb, ho, hn = hosts
+    n = len(ho) - 1
+    ub = uo = un = None
+    if uris is not None:
+        ub, uo, un = uris
+    out = np.empty(n, np.int32)
+    rc = lib().ic_hint(P(group_arr), ng, P(hb), P(ho), P(hn), P(ports), P(ub), P(uo), P(un), n,
+                       P(out))
+    assert rc == 0, rc
+    return out
+
+
+def is_ipv6(s):
+    b = s.encode() if isinstance(s, str) else s
+    return bool(lib().ic_is_ipv6(b, len(b)))
+
+
+def is_ip_literal(s):
+    b = s.encode() if isinstance(s, str) else s
+    return bool(lib().ic_is_ip_literal(b, len(b)))

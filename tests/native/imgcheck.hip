@@ -1,0 +1,118 @@
+// imgcheck.hip -- TEST HARNESS ONLY (not part of libvclassify).
+//
+// Builds the same table images as the product compiler and walks them on the
+// host with the kernels' own __host__ __device__ probe functions, so compile
+// bugs show up in the CPU test tier before any GPU run.  The product library
+// never contains or calls this code.
+#include <vector>
+
+#include "../../vproxy_amd/csrc/compile/compile.hpp"
+#include "../../vproxy_amd/csrc/device/acl_dev.h"
+#include "../../vproxy_amd/csrc/device/hint_dev.h"
+#include "../../vproxy_amd/csrc/device/route_dev.h"
+
+using namespace vcd;
+
+namespace {
+AclFamilyImage fam_img(const vc::AclFamilyBuilt& b) {
+    AclFamilyImage f{};
+    f.bounds4 = b.bounds4.data();
+    f.bounds6 = b.bounds6.data();
+    f.desc = b.desc.data();
+    f.pieces = b.pieces.data();
+    f.nb = b.nb;
+    f.np = int32_t(b.pieces.size() / 2);
+    return f;
+}
+
+HintImage hint_img(const vc::HintBuilt& b) {
+    HintImage h{};
+    h.blob = b.blob.data();
+    h.host_slots = reinterpret_cast<const KeySlot*>(b.host_slots.data());
+    h.uri_slots = reinterpret_cast<const KeySlot*>(b.uri_slots.data());
+    h.lists = b.lists.data();
+    h.port_mins = reinterpret_cast<const PortMin*>(b.port_mins.data());
+    h.port_min_off = b.port_min_off.data();
+    h.groups = reinterpret_cast<const GroupRec*>(b.groups.data());
+    h.host_mask = uint32_t(b.host_slots.size() - 1);
+    h.uri_mask = uint32_t(b.uri_slots.size() - 1);
+    h.n_groups = b.n_groups;
+    h.wildcard_slot = b.wildcard_slot;
+    h.uri_star_slot = b.uri_star_slot;
+    h.has_uri_keys = b.has_uri_keys;
+    return h;
+}
+}  // namespace
+
+extern "C" {
+
+int ic_acl(const vc_acl_rule* tcp, int nt, const vc_acl_rule* udp, int nu, int dflt, int family,
+           const uint8_t* proto, const void* src, const uint16_t* port, int64_t n, int32_t* out,
+           uint8_t* allow, int32_t* stats) {
+    vc::AclBuilt b;
+    int rc = vc::build_acl(tcp, nt, udp, nu, dflt, &b);
+    if (rc) return rc;
+    for (int l = 0; l < 2; ++l)
+        for (int f = 0; f < 2; ++f) {
+            stats[(l * 2 + f) * 2] = b.fam[l][f].nb;
+            stats[(l * 2 + f) * 2 + 1] = int32_t(b.fam[l][f].pieces.size() / 2);
+        }
+    for (int64_t i = 0; i < n; ++i) {
+        const int l = proto[i] == VC_PROTO_TCP ? 0 : 1;
+        AclFamilyImage f = fam_img(b.fam[l][family == 4 ? 0 : 1]);
+        int j;
+        if (family == 4) {
+            j = bsearch_u32(f.bounds4, f.nb, static_cast<const uint32_t*>(src)[i]);
+        } else {
+            uint64_t hi, lo;
+            v6_key(static_cast<const uint4*>(src)[i], &hi, &lo);
+            j = bsearch_u128(f.bounds6, f.nb, hi, lo);
+        }
+        uint32_t v = port_lookup(f.pieces, load_desc(f.desc, j), port[i]);
+        out[i] = out_index(v);
+        allow[i] = v == VC_NONE ? uint8_t(b.default_allow) : b.allow[(l ? b.n_tcp : 0) + v];
+    }
+    return 0;
+}
+
+int ic_route(const vc_net* rules, int nr, int family, const void* keys, int64_t n, int32_t* out,
+             int32_t* stats) {
+    vc::TrieBuilt t;
+    int rc = vc::build_trie(rules, nr, family == 4 ? 0 : 1, &t);
+    if (rc) return rc;
+    stats[0] = t.root_bits;
+    stats[1] = int32_t((t.nodes.size() - (size_t(1) << t.root_bits)) / 256);
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t e;
+        if (family == 4) {
+            e = trie_v4(t.nodes.data(), t.root_bits, static_cast<const uint32_t*>(keys)[i]);
+        } else {
+            uint64_t hi, lo;
+            v6_key(static_cast<const uint4*>(keys)[i], &hi, &lo);
+            e = trie_v6(t.nodes.data(), t.root_bits, hi, lo);
+        }
+        out[i] = out_index(e);
+    }
+    return 0;
+}
+
+int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* ho,
+            const uint8_t* hn, const uint16_t* port, const uint8_t* ub, const uint32_t* uo,
+            const uint8_t* un, int64_t n, int32_t* out) {
+    vc::HintBuilt b;
+    int rc = vc::build_hints(g, ng, &b);
+    if (rc) return rc;
+    HintImage img = hint_img(b);
+    for (int64_t i = 0; i < n; ++i) {
+        DStr h{nullptr, -1}, u{nullptr, -1};
+        if (hb && !(hn && hn[i])) h = DStr{hb + ho[i], int(ho[i + 1] - ho[i])};
+        if (ub && !(un && un[i])) u = DStr{ub + uo[i], int(uo[i + 1] - uo[i])};
+        out[i] = search_for_group(img, format_host(h), port ? port[i] : 0, format_uri(u));
+    }
+    return 0;
+}
+
+int ic_is_ipv6(const uint8_t* s, int n) { return d_is_ipv6(s, n) ? 1 : 0; }
+int ic_is_ip_literal(const uint8_t* s, int n) { return d_is_ip_literal(s, n) ? 1 : 0; }
+
+}  // extern "C"

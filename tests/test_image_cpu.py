@@ -1,0 +1,165 @@
+"""CPU tier: the product's table compilers + the kernels' own probe code
+(walked on the host by the test harness) against the oracle.
+
+The GPU tier (test_gpu_*.py) repeats these comparisons with the real HIP
+kernels; this tier catches compile/image bugs without a GPU.
+"""
+import numpy as np
+import pytest
+
+import imgcheck_ffi as IC
+import oracle_ffi as O
+from vproxy_amd import workloads as W
+from vproxy_amd.classifier import group_array, pack_strings
+
+from cases import acl_edge_rules, v6_edge_inputs, hint_cases_random
+
+
+@pytest.mark.parametrize("n_rules,p_range,weighted,seed", [
+    (64, 0.5, False, 1),        # C1 shape
+    (2000, 0.3, True, 2),       # C2 generator, reduced
+    (300, 0.9, True, 3),        # wide port ranges -> multi-piece port functions
+])
+def test_acl_v4_random(n_rules, p_range, weighted, seed):
+    tcp, udp = W.gen_sg_rules(n_rules, seed, p_range=p_range, weighted=weighted)
+    proto, src, port = W.gen_acl_queries(tcp, udp, 40000, seed + 100)
+    for dflt in (False, True):
+        got, allow, _ = IC.acl(tcp, udp, dflt, 4, proto, src, port)
+        want, wv = O.sg_batch_v4_np(tcp, udp, dflt, proto, src, port, nthreads=4)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(allow, wv)
+
+
+def test_acl_edges_v4_v6():
+    tcp, udp = acl_edge_rules()
+    rng = np.random.default_rng(7)
+    src6, proto6, port6 = v6_edge_inputs(rng, 20000)
+    src4 = src6[:, 12:].copy().view(">u4").reshape(-1).astype(np.uint32)
+    for dflt in (False, True):
+        got, allow, _ = IC.acl(tcp, udp, dflt, 6, proto6, src6, port6)
+        want, wv = O.sg_batch_v6_np(tcp, udp, dflt, proto6, src6, port6)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(allow, wv)
+        got, allow, _ = IC.acl(tcp, udp, dflt, 4, proto6, src4, port6)
+        want, wv = O.sg_batch_v4_np(tcp, udp, dflt, proto6, src4, port6)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(allow, wv)
+
+
+def test_acl_empty_lists():
+    tcp, udp = W.gen_sg_rules(20, 5)
+    empty = tcp[:0]
+    proto, src, port = W.gen_acl_queries(tcp, udp, 5000, 6)
+    for t, u in ((empty, udp), (tcp, empty), (empty, empty)):
+        for dflt in (False, True):
+            got, allow, _ = IC.acl(t, u, dflt, 4, proto, src, port)
+            want, wv = O.sg_batch_v4_np(t, u, dflt, proto, src, port)
+            np.testing.assert_array_equal(got, want)
+            np.testing.assert_array_equal(allow, wv)
+
+
+def _c1_route_table(seed):
+    """RouteTable(Table{10.0.0.0/8}) + 255 CIDRs /8-/30 in random order,
+    through the oracle's exact addRule heuristic."""
+    rng = np.random.default_rng(seed)
+    plen = rng.integers(8, 31, 400)
+    net = rng.integers(0, 2**32, 400, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    t = O.RouteTable()
+    t.add("10.0.0.0/8")
+    nets = W.v4_nets(net, plen)
+    added = 0
+    for i in range(len(nets)):
+        if added == 255:
+            break
+        n = O.VoNet.from_buffer_copy(nets[i].tobytes())
+        if O.lib().vo_rt_add(O.C.byref(t.t), O.C.byref(n)) == 0:
+            added += 1
+    return t
+
+
+def test_route_c1_random_order():
+    t = _c1_route_table(11)
+    v4, _ = O.rt_table_np(t)
+    q = W.v4_lookups(v4["ip"][:, :4].copy().view(">u4").reshape(-1).astype(np.uint32),
+                     np.array([O.lib().vo_mask_int((O.C.c_uint8 * 16)(*r["mask"]), 4) for r in v4]),
+                     50000, 12)
+    got, stats = IC.route(v4, 4, q)
+    want = O.rt_batch_v4_np(v4, q, nthreads=4)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_route_v4_deep_and_long():
+    """prefixes longer than the root stride (/25-/32) and nested chains."""
+    rng = np.random.default_rng(21)
+    plen = rng.integers(0, 33, 6000)
+    net = rng.integers(0, 2**32, 6000, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    net[:200] = net[200] & W._mask32(plen[:200])   # nested chain around one address
+    key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
+    _, first = np.unique(key, return_index=True)
+    first = np.sort(first)
+    nets = W.v4_nets(net[first], plen[first])
+    rng.shuffle(nets)     # arbitrary list order: priority = index, not length
+    q = W.v4_lookups(net[first], plen[first], 40000, 22)
+    for nr in (len(nets), 1000):   # 24-bit and 16-bit roots
+        got, stats = IC.route(nets[:nr], 4, q)
+        want = O.rt_batch_v4_np(nets[:nr], q, nthreads=4)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_route_v6():
+    hi, lo, plen = W.gen_v6_prefixes(3000, 31)
+    nets = W.v6_nets(hi, lo, plen)
+    nets = np.concatenate([nets, W.v6_nets([0], [0], [0])])   # ::/0 last
+    q = W.v6_lookups(hi, lo, plen, 30000, 32)
+    got, _ = IC.route(nets, 6, q)
+    want = O.rt_batch_v6_np(nets, q, nthreads=4)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_hint_random():
+    groups, hosts, queries = hint_cases_random(np.random.default_rng(41), 800, 20000)
+    arr, ng, keep = group_array(groups)
+    h = pack_strings([q[0] for q in queries])
+    ports = np.array([q[1] for q in queries], np.uint16)
+    u = pack_strings([q[2] for q in queries])
+    got = IC.hint(arr, ng, h, ports, u)
+    og = O.Groups(groups)
+    want = np.array([O.search_for_group(og, q[0], q[1], q[2]) for q in queries], np.int32)
+    np.testing.assert_array_equal(got, want)
+    # host-only batch (uri null everywhere) exercises the summary fast path
+    got2 = IC.hint(arr, ng, h, ports, None)
+    want2 = np.array([O.search_for_group(og, q[0], q[1], None) for q in queries], np.int32)
+    np.testing.assert_array_equal(got2, want2)
+
+
+def test_hint_kats_on_image():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "kats.json")) as f:
+        kats = json.load(f)
+    for case in kats["hints"]:
+        arr, ng, keep = group_array(case["groups"])
+        qs = case["queries"]
+        h = pack_strings([q.get("host") for q, _ in qs])
+        u = pack_strings([q.get("uri") for q, _ in qs])
+        p = np.array([q.get("port", 0) for q, _ in qs], np.uint16)
+        got = IC.hint(arr, ng, h, p, u)
+        assert list(got) == [w for _, w in qs], case["source"]
+
+
+def test_device_ip_literal_parser():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ip_parser.json")) as f:
+        d = json.load(f)
+    strs = [v["s"] for v in d["v6_ok"]] + d["bogus"] + [v["s"] for v in d["v4_ok"]] + d["v4_fail"]
+    strs += ["::x:1.2.3.4", "::hello:1.2.3.4", "1:2:3:4:5:6:7:1.2.3.4", "::1:2:3:4:5:6:7:1.2.3.4",
+             "[::1]", "[", "]", "[]", "::", ":::", "1::2:", "::ffff:1.2.3.4", "a.b:80",
+             "www.example.com:8080", "fe80::1%eth0", "1.2.3.04", "0.0.0.0", "255.255.255.255"]
+    rng = np.random.default_rng(3)
+    alpha = list("0123456789abcdefABCDEF:.[]xg")
+    for _ in range(4000):
+        strs.append("".join(rng.choice(alpha, int(rng.integers(0, 20)))))
+    for s in strs:
+        assert IC.is_ipv6(s) == (O.parse_ipv6(s) is not None), s
+        assert IC.is_ip_literal(s) == O.is_ip_literal(s), s

@@ -1,0 +1,14 @@
+"""vproxy_amd -- MI355X-native batched classifier for vproxy's hot path.
+
+SecurityGroup first-match ACL, vswitch RouteTable lookup, Upstream Host/SNI
+hint matching and DNSServer record classification, evaluated by hand-written
+HIP kernels for gfx950 behind the C ABI in include/vclassify.h.
+"""
+from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,  # noqa: F401
+                   NotFoundException, StateError, VcError, XException, lib,
+                   COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP, PROTO_TCP, PROTO_UDP,
+                   DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE)
+from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
+                         acl_rule_array, group_array, net_array, pack_strings, parse_ip)
+
+__all__ = ["Classifier", "Network", "SecurityGroup", "RouteTable", "Annotations", "parse_ip"]

@@ -1,0 +1,145 @@
+"""ctypes binding of libvclassify.so (include/vclassify.h).
+
+The library is built in-tree by `make -C vproxy_amd/csrc` (or
+__graft_entry__.build()).  There is no fallback: if the shared library is
+missing, importing the classifier raises.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvclassify.so")
+
+VC_OK, VC_EINVAL, VC_EEXIST, VC_ENOTFOUND, VC_EXEXC, VC_EDEVICE, VC_ENOMEM, VC_ESTATE = \
+    0, -1, -2, -3, -4, -5, -6, -7
+PROTO_TCP, PROTO_UDP = 6, 17
+DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE = 1, 2, 3, 4, 5
+COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP = 0, 1, 2
+
+
+class VcNet(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 16), ("mask", C.c_uint8 * 16),
+                ("ip_len", C.c_int32), ("mask_len", C.c_int32)]
+
+
+class VcAclRule(C.Structure):
+    _fields_ = [("net", VcNet), ("min_port", C.c_int32), ("max_port", C.c_int32),
+                ("allow", C.c_int32)]
+
+
+class VcAnnos(C.Structure):
+    _fields_ = [("host", C.c_char_p), ("host_len", C.c_int32), ("port", C.c_int32),
+                ("uri", C.c_char_p), ("uri_len", C.c_int32)]
+
+
+class VcGroupAnnos(C.Structure):
+    _fields_ = [("handle", VcAnnos), ("group", VcAnnos)]
+
+
+# ---- exceptions mirroring the reference's (vproxybase.util.exception.*) ----
+class VcError(Exception):
+    code = None
+
+
+class IllegalArgumentException(VcError, ValueError):
+    code = VC_EINVAL
+
+
+class AlreadyExistException(VcError):
+    code = VC_EEXIST
+
+
+class NotFoundException(VcError):
+    code = VC_ENOTFOUND
+
+
+class XException(VcError):
+    code = VC_EXEXC
+
+
+class DeviceError(VcError, RuntimeError):
+    code = VC_EDEVICE
+
+
+class StateError(VcError, RuntimeError):
+    code = VC_ESTATE
+
+
+_EXC = {c.code: c for c in (IllegalArgumentException, AlreadyExistException, NotFoundException,
+                            XException, DeviceError, StateError)}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libvclassify.so not built (run `make -C vproxy_amd/csrc` or "
+                              "__graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
+        L.vc_version.restype = C.c_char_p
+        L.vc_last_error.restype = C.c_char_p
+        L.vc_create.argtypes = [i32, P(vp)]
+        L.vc_destroy.argtypes = [vp]
+        L.vc_net_parse.argtypes = [C.c_char_p, P(VcNet)]
+        L.vc_net_from_prefix.argtypes = [vp, i32, i32, P(VcNet)]
+        L.vc_net_contains_ip.argtypes = [P(VcNet), vp, i32]
+        L.vc_ip_parse.argtypes = [C.c_char_p, vp]
+        L.vc_compile_acl.argtypes = [vp, P(VcAclRule), i32, P(VcAclRule), i32, i32]
+        for f in ("vc_acl_classify_v4_dev", "vc_acl_classify_v6_dev"):
+            getattr(L, f).argtypes = [vp, vp, vp, vp, i64, vp, vp, vp]
+        for f in ("vc_acl_classify_v4", "vc_acl_classify_v6"):
+            getattr(L, f).argtypes = [vp, vp, vp, vp, i64, vp, vp]
+        L.vc_compile_routes.argtypes = [vp, P(VcNet), i32, P(VcNet), i32]
+        for f in ("vc_route_lookup_v4_dev", "vc_route_lookup_v6_dev"):
+            getattr(L, f).argtypes = [vp, vp, i64, vp, vp]
+        for f in ("vc_route_lookup_v4", "vc_route_lookup_v6"):
+            getattr(L, f).argtypes = [vp, vp, i64, vp]
+        L.vc_compile_upstream.argtypes = [vp, P(VcGroupAnnos), i32]
+        L.vc_hint_search_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp]
+        L.vc_hint_search.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]
+        L.vc_compile_hosts.argtypes = [vp, P(C.c_char_p), vp, vp, i32]
+        L.vc_compile_hosts_text.argtypes = [vp, C.c_char_p, i64]
+        L.vc_dns_classify_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp]
+        L.vc_dns_classify.argtypes = [vp, vp, vp, i64, vp, vp]
+        L.vc_pipeline_v4_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+        L.vc_counters_enable.argtypes = [vp, i32]
+        L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
+        L.vc_counters_read.argtypes = [vp, i32, vp, i64]
+        L.vc_counters_reset.argtypes = [vp]
+        L.vc_secgroup_new.argtypes = [C.c_char_p, i32, P(vp)]
+        L.vc_secgroup_free.argtypes = [vp]
+        L.vc_secgroup_set_default.argtypes = [vp, i32]
+        L.vc_secgroup_add_rule.argtypes = [vp, C.c_char_p, P(VcNet), i32, i32, i32, i32]
+        L.vc_secgroup_remove_rule.argtypes = [vp, C.c_char_p]
+        L.vc_secgroup_rules.argtypes = [vp, i32, P(VcAclRule), i32]
+        L.vc_secgroup_compile.argtypes = [vp, vp]
+        L.vc_routetable_new.argtypes = [P(VcNet), P(VcNet), i32, P(vp)]
+        L.vc_routetable_free.argtypes = [vp]
+        L.vc_routetable_add_rule.argtypes = [vp, C.c_char_p, P(VcNet), i32, vp, i32]
+        L.vc_routetable_add_rules.argtypes = [vp, C.c_char_p, P(VcNet), i32, i32]
+        L.vc_routetable_del_rule.argtypes = [vp, C.c_char_p]
+        L.vc_routetable_rules.argtypes = [vp, i32, P(VcNet), i32]
+        L.vc_routetable_compile.argtypes = [vp, vp]
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    """Raise the reference-style exception for a negative status."""
+    if rc is not None and rc < 0:
+        msg = lib().vc_last_error().decode(errors="replace")
+        raise _EXC.get(rc, VcError)(msg)
+    return rc
+
+
+# every symbol include/vclassify.h declares (checked by tests/test_capi_symbols.py)
+def header_symbols(header=None):
+    import re
+    header = header or os.path.join(os.path.dirname(HERE), "include", "vclassify.h")
+    with open(header) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(vc_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,496 @@
+"""Python face of the MI355X classifier, named after the reference's classes.
+
+    Network         base/src/main/java/vproxybase/util/Network.java
+    SecurityGroup   core/src/main/java/vproxy/component/secure/SecurityGroup.java
+    RouteTable      core/src/main/java/vswitch/RouteTable.java
+    Upstream hints  core/src/main/java/vproxy/component/svrgroup/Upstream.java + Hint.java
+    DNS             core/src/main/java/vproxy/dns/DNSServer.java:116-166
+
+Everything here is plumbing over the C ABI in include/vclassify.h: rule
+containers live in C++ (vproxy_amd/csrc/host), classification runs in the
+HIP kernels.  Batches may be numpy arrays (host memory; synchronous, PCIe
+included) or torch CUDA tensors (device memory; asynchronous on torch's
+current stream).
+"""
+import ctypes as C
+import ipaddress
+
+import numpy as np
+
+from . import _lib
+from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, check, lib)
+
+HINT_HOST = "vproxy/hint-host"   # AnnotationKeys.ServerGroup_HintHost
+HINT_PORT = "vproxy/hint-port"   # AnnotationKeys.ServerGroup_HintPort
+HINT_URI = "vproxy/hint-uri"     # AnnotationKeys.ServerGroup_HintUri
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def parse_ip(s):
+    """IP.parseIpString: bytes (4 or 16) or None."""
+    out = (C.c_uint8 * 16)()
+    n = lib().vc_ip_parse(_b(s), out)
+    return None if n < 0 else bytes(out[:n])
+
+
+class Network:
+    """vproxybase.util.Network (ip bytes + parseMask bytes)."""
+
+    def __init__(self, spec=None, *, ip=None, prefix=None, raw=None):
+        self.c = VcNet()
+        if raw is not None:
+            C.memmove(C.byref(self.c), C.byref(raw), C.sizeof(VcNet))
+        elif spec is not None:
+            check(lib().vc_net_parse(_b(spec), C.byref(self.c)))
+        else:
+            ipb = _b(ip) if not isinstance(ip, (bytes, bytearray)) else bytes(ip)
+            if isinstance(ip, str):
+                ipb = parse_ip(ip)
+                if ipb is None:
+                    raise _lib.IllegalArgumentException("not an ip: %s" % ip)
+            buf = (C.c_uint8 * 16).from_buffer_copy(ipb.ljust(16, b"\0"))
+            check(lib().vc_net_from_prefix(buf, len(ipb), int(prefix), C.byref(self.c)))
+
+    @property
+    def ip(self):
+        return bytes(self.c.ip[:self.c.ip_len])
+
+    @property
+    def mask(self):
+        return bytes(self.c.mask[:self.c.mask_len])
+
+    @property
+    def prefix(self):
+        """Network.getMask -> maskInt (Network.java:135-145)."""
+        zeros = 0
+        for b in reversed(self.mask):
+            cnt = 8 if b == 0 else (b & -b).bit_length() - 1
+            if cnt == 0:
+                break
+            zeros += cnt
+        return len(self.mask) * 8 - zeros
+
+    def contains(self, ip):
+        ipb = parse_ip(ip) if isinstance(ip, str) else bytes(ip)
+        buf = (C.c_uint8 * 16).from_buffer_copy(ipb.ljust(16, b"\0"))
+        return bool(check(lib().vc_net_contains_ip(C.byref(self.c), buf, len(ipb))))
+
+    def __str__(self):
+        """Network.toString (Network.java:66-69)."""
+        ip = self.ip
+        s = ".".join(map(str, ip)) if len(ip) == 4 else str(ipaddress.IPv6Address(ip))
+        return "%s/%d" % (s, self.prefix)
+
+    __repr__ = __str__
+
+    def __eq__(self, o):
+        return isinstance(o, Network) and self.ip == o.ip and self.mask == o.mask
+
+    def __hash__(self):
+        return hash((self.ip, self.mask))
+
+
+def _proto(p):
+    if isinstance(p, str):
+        if p in ("TCP", "tcp"):          # ProtocolHandle.get (ProtocolHandle.java:20-31)
+            return PROTO_TCP
+        if p in ("UDP", "udp"):
+            return PROTO_UDP
+        raise _lib.IllegalArgumentException("unknown protocol %s" % p)
+    return int(p)
+
+
+class SecurityGroup:
+    """Mirror of SecurityGroup (list order, duplicate checks) in C++."""
+
+    def __init__(self, alias, default_allow):
+        self.h = C.c_void_p()
+        check(lib().vc_secgroup_new(_b(alias), 1 if default_allow else 0, C.byref(self.h)))
+        self.alias = alias
+        self._default = bool(default_allow)
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().vc_secgroup_free(self.h)
+
+    @property
+    def default_allow(self):
+        return self._default
+
+    @default_allow.setter
+    def default_allow(self, v):
+        check(lib().vc_secgroup_set_default(self.h, 1 if v else 0))
+        self._default = bool(v)
+
+    def add_rule(self, alias, network, protocol, min_port, max_port, allow):
+        net = network if isinstance(network, Network) else Network(network)
+        check(lib().vc_secgroup_add_rule(self.h, _b(alias), C.byref(net.c), _proto(protocol),
+                                         int(min_port), int(max_port), 1 if allow else 0))
+
+    def remove_rule(self, alias):
+        check(lib().vc_secgroup_remove_rule(self.h, _b(alias)))
+
+    def rules(self, protocol):
+        n = check(lib().vc_secgroup_rules(self.h, _proto(protocol), None, 0))
+        arr = (VcAclRule * max(1, n))()
+        lib().vc_secgroup_rules(self.h, _proto(protocol), arr, n)
+        return [arr[i] for i in range(n)]
+
+
+class RouteTable:
+    """Mirror of vswitch.RouteTable (insertion-order heuristic) in C++."""
+
+    def __init__(self, v4network=None, v6network=None, vni=0):
+        self.h = C.c_void_p()
+        a = Network(v4network) if isinstance(v4network, str) else v4network
+        b = Network(v6network) if isinstance(v6network, str) else v6network
+        check(lib().vc_routetable_new(C.byref(a.c) if a else None, C.byref(b.c) if b else None,
+                                      int(vni), C.byref(self.h)))
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().vc_routetable_free(self.h)
+
+    def add_rule(self, alias, network, to_vni=0, via=None):
+        net = network if isinstance(network, Network) else Network(network)
+        ipb = None
+        if via is not None:
+            ipb = parse_ip(via) if isinstance(via, str) else bytes(via)
+        buf = (C.c_uint8 * 16).from_buffer_copy(ipb.ljust(16, b"\0")) if ipb else None
+        check(lib().vc_routetable_add_rule(self.h, _b(alias), C.byref(net.c), int(to_vni), buf,
+                                           len(ipb) if ipb else 0))
+
+    def add_rules(self, alias_prefix, networks, to_vni=0, n=None):
+        """Bulk addRule in the given order (exact same lists as one by one).
+        networks: list of Network/str, or a VcNet ctypes array with count n."""
+        if isinstance(networks, C.Array):
+            arr, n = networks, (len(networks) if n is None else n)
+        else:
+            arr, n = net_array(networks), len(networks)
+        check(lib().vc_routetable_add_rules(self.h, _b(alias_prefix), arr, n, int(to_vni)))
+
+    def del_rule(self, alias):
+        check(lib().vc_routetable_del_rule(self.h, _b(alias)))
+
+    def rules_raw(self, family):
+        n = check(lib().vc_routetable_rules(self.h, family, None, 0))
+        arr = (VcNet * max(1, n))()
+        lib().vc_routetable_rules(self.h, family, arr, n)
+        return arr, n
+
+    def rules(self, family):
+        arr, n = self.rules_raw(family)
+        return [Network(raw=arr[i]) for i in range(n)]
+
+    def get_rules(self):
+        """RouteTable.getRules(): v4 list then v6 list."""
+        return self.rules(4) + self.rules(6)
+
+
+def net_array(nets):
+    arr = (VcNet * max(1, len(nets)))()
+    for i, n in enumerate(nets):
+        n = n if isinstance(n, Network) else Network(n)
+        C.memmove(C.byref(arr[i]), C.byref(n.c), C.sizeof(VcNet))
+    return arr
+
+
+def acl_rule_array(rules):
+    """rules: iterable of (network, min_port, max_port, allow) or VcAclRule."""
+    rules = list(rules)
+    arr = (VcAclRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        if isinstance(r, VcAclRule):
+            arr[i] = r
+            continue
+        net, lo, hi, allow = r
+        net = net if isinstance(net, Network) else Network(net)
+        C.memmove(C.byref(arr[i].net), C.byref(net.c), C.sizeof(VcNet))
+        arr[i].min_port, arr[i].max_port, arr[i].allow = int(lo), int(hi), 1 if allow else 0
+    return arr, len(rules)
+
+
+def java_parse_int(s):
+    """Integer.parseInt, Annotations' failure -> 0 (Annotations.java:45-58)."""
+    if s is None:
+        return 0
+    if isinstance(s, int):
+        return s
+    t = s[1:] if s[:1] in ("+", "-") else s
+    if not t or not all("0" <= ch <= "9" for ch in t):
+        return 0
+    v = int(s)
+    return v if -2**31 <= v < 2**31 else 0
+
+
+class Annotations:
+    """The hint fields of vproxybase.util.Annotations."""
+
+    def __init__(self, m=None, *, host=None, port=0, uri=None):
+        if m is not None:
+            host = m.get(HINT_HOST, m.get("host"))
+            port = java_parse_int(m.get(HINT_PORT, m.get("port")))
+            uri = m.get(HINT_URI, m.get("uri"))
+        self.host, self.port, self.uri = host, int(port or 0), uri
+
+
+class _Keep:
+    def __init__(self):
+        self.items = []
+
+    def s(self, v):
+        if v is None:
+            return None, 0
+        b = _b(v)
+        self.items.append(b)
+        return b, len(b)
+
+
+def group_array(groups):
+    """groups: list of (handle annotations, group annotations); each an
+    Annotations or a dict with hint keys."""
+    keep = _Keep()
+    arr = (VcGroupAnnos * max(1, len(groups)))()
+    for i, (ha, ga) in enumerate(groups):
+        for slot, a in (("handle", ha), ("group", ga)):
+            a = a if isinstance(a, Annotations) else Annotations(a or {})
+            x = getattr(arr[i], slot)
+            x.host, x.host_len = keep.s(a.host)
+            x.port = a.port
+            x.uri, x.uri_len = keep.s(a.uri)
+    return arr, len(groups), keep
+
+
+def pack_strings(items):
+    """list of str/bytes/None -> (blob uint8, off uint32[n+1], null uint8 or None)."""
+    bs = [None if x is None else _b(x) for x in items]
+    lens = np.fromiter((0 if b is None else len(b) for b in bs), dtype=np.int64, count=len(bs))
+    off = np.zeros(len(bs) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    if off[-1] >= 2**32:
+        raise _lib.IllegalArgumentException("string blob exceeds 4 GiB")
+    blob = np.frombuffer(b"".join(b for b in bs if b is not None) or b"\0", dtype=np.uint8)
+    null = None
+    if any(b is None for b in bs):
+        null = np.fromiter((b is None for b in bs), dtype=np.uint8, count=len(bs))
+    return blob.copy(), off.astype(np.uint32), null
+
+
+def _is_dev(x):
+    return x is not None and hasattr(x, "is_cuda") and x.is_cuda
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        return C.c_void_p(x.data_ptr())
+    return C.c_void_p(x.ctypes.data)
+
+
+def _stream():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Classifier:
+    """One libvclassify context on one GPU.  Raises DeviceError without a
+    usable gfx950 device: there is no CPU path."""
+
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        check(lib().vc_create(int(device), C.byref(self.h)))
+        self.device = device
+
+    def close(self):
+        if self.h and self.h.value:
+            lib().vc_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------- compile ----------------
+    def compile_acl(self, tcp_rules, udp_rules, default_allow):
+        t, nt = acl_rule_array(tcp_rules)
+        u, nu = acl_rule_array(udp_rules)
+        check(lib().vc_compile_acl(self.h, t, nt, u, nu, 1 if default_allow else 0))
+
+    def compile_security_group(self, sg):
+        check(lib().vc_secgroup_compile(self.h, sg.h))
+
+    def compile_routes(self, v4, v6=()):
+        a = v4 if isinstance(v4, C.Array) else net_array(v4)
+        b = v6 if isinstance(v6, C.Array) else net_array(v6)
+        na = len(v4) if not isinstance(v4, C.Array) else len(a)
+        nb = len(v6) if not isinstance(v6, C.Array) else len(b)
+        check(lib().vc_compile_routes(self.h, a, na, b, nb))
+
+    def compile_routes_raw(self, v4arr, n4, v6arr, n6):
+        check(lib().vc_compile_routes(self.h, v4arr, n4, v6arr, n6))
+
+    def compile_route_table(self, rt):
+        check(lib().vc_routetable_compile(self.h, rt.h))
+
+    def compile_upstream(self, groups):
+        arr, n, keep = group_array(groups)
+        check(lib().vc_compile_upstream(self.h, arr, n))
+
+    def compile_hosts(self, pairs):
+        keys = [_b(k) for k, _ in pairs]
+        karr = (C.c_char_p * max(1, len(keys)))(*keys)
+        lens = np.array([len(k) for k in keys] or [0], dtype=np.int32)
+        vals = np.array([v for _, v in pairs] or [0], dtype=np.int32)
+        check(lib().vc_compile_hosts(self.h, karr, _ptr(lens), _ptr(vals), len(keys)))
+
+    def compile_hosts_text(self, text):
+        t = _b(text)
+        check(lib().vc_compile_hosts_text(self.h, t, len(t)))
+
+    # ---------------- classify ----------------
+    def acl_v4(self, proto, src4, port, out_idx=None, out_allow=None, want_allow=True):
+        """Batched SecurityGroup.allow over IPv4 sources -> (idx, allow)."""
+        n = len(src4)
+        if _is_dev(src4):
+            import torch
+            out_idx = out_idx if out_idx is not None else torch.empty(n, dtype=torch.int32,
+                                                                      device=src4.device)
+            if want_allow and out_allow is None:
+                out_allow = torch.empty(n, dtype=torch.uint8, device=src4.device)
+            check(lib().vc_acl_classify_v4_dev(self.h, _ptr(proto), _ptr(src4), _ptr(port), n,
+                                               _ptr(out_idx), _ptr(out_allow), _stream()))
+        else:
+            proto, src4, port = (np.ascontiguousarray(proto, np.uint8),
+                                 np.ascontiguousarray(src4, np.uint32),
+                                 np.ascontiguousarray(port, np.uint16))
+            out_idx = np.empty(n, np.int32)
+            out_allow = np.empty(n, np.uint8) if want_allow else None
+            check(lib().vc_acl_classify_v4(self.h, _ptr(proto), _ptr(src4), _ptr(port), n,
+                                           _ptr(out_idx), _ptr(out_allow)))
+        return out_idx, out_allow
+
+    def acl_v6(self, proto, src6, port, want_allow=True):
+        n = len(port)
+        if _is_dev(src6):
+            import torch
+            out_idx = torch.empty(n, dtype=torch.int32, device=src6.device)
+            out_allow = torch.empty(n, dtype=torch.uint8, device=src6.device) if want_allow else None
+            check(lib().vc_acl_classify_v6_dev(self.h, _ptr(proto), _ptr(src6), _ptr(port), n,
+                                               _ptr(out_idx), _ptr(out_allow), _stream()))
+        else:
+            proto, src6, port = (np.ascontiguousarray(proto, np.uint8),
+                                 np.ascontiguousarray(src6, np.uint8),
+                                 np.ascontiguousarray(port, np.uint16))
+            out_idx = np.empty(n, np.int32)
+            out_allow = np.empty(n, np.uint8) if want_allow else None
+            check(lib().vc_acl_classify_v6(self.h, _ptr(proto), _ptr(src6), _ptr(port), n,
+                                           _ptr(out_idx), _ptr(out_allow)))
+        return out_idx, out_allow
+
+    def route_v4(self, dst4, out=None):
+        n = len(dst4)
+        if _is_dev(dst4):
+            import torch
+            out = out if out is not None else torch.empty(n, dtype=torch.int32, device=dst4.device)
+            check(lib().vc_route_lookup_v4_dev(self.h, _ptr(dst4), n, _ptr(out), _stream()))
+        else:
+            dst4 = np.ascontiguousarray(dst4, np.uint32)
+            out = np.empty(n, np.int32)
+            check(lib().vc_route_lookup_v4(self.h, _ptr(dst4), n, _ptr(out)))
+        return out
+
+    def route_v6(self, dst6, out=None):
+        n = len(dst6)
+        if _is_dev(dst6):
+            import torch
+            out = out if out is not None else torch.empty(n, dtype=torch.int32, device=dst6.device)
+            check(lib().vc_route_lookup_v6_dev(self.h, _ptr(dst6), n, _ptr(out), _stream()))
+        else:
+            dst6 = np.ascontiguousarray(dst6, np.uint8)
+            out = np.empty(n, np.int32)
+            check(lib().vc_route_lookup_v6(self.h, _ptr(dst6), n, _ptr(out)))
+        return out
+
+    def hint_search(self, hosts, ports=None, uris=None):
+        """Batched Upstream.searchForGroup(Hint.ofHostPortUri(host, port, uri)).
+        hosts/uris: lists of str/None (host path) or packed (blob, off, null)
+        tuples of torch CUDA tensors (device path)."""
+        if isinstance(hosts, tuple) and _is_dev(hosts[0]):
+            import torch
+            hb, ho, hn = hosts
+            n = len(ho) - 1
+            ub, uo, un = uris if uris is not None else (None, None, None)
+            out = torch.empty(n, dtype=torch.int32, device=hb.device)
+            check(lib().vc_hint_search_dev(self.h, _ptr(hb), _ptr(ho), _ptr(hn), _ptr(ports),
+                                           _ptr(ub), _ptr(uo), _ptr(un), n, _ptr(out), _stream()))
+            return out
+        n = len(hosts)
+        hb, ho, hn = pack_strings(hosts)
+        ub = uo = un = None
+        if uris is not None:
+            ub, uo, un = pack_strings(uris)
+        p = np.ascontiguousarray(ports if ports is not None else np.zeros(n), np.uint16)
+        out = np.empty(n, np.int32)
+        check(lib().vc_hint_search(self.h, _ptr(hb), _ptr(ho), _ptr(hn), _ptr(p), _ptr(ub),
+                                   _ptr(uo), _ptr(un), n, _ptr(out)))
+        return out
+
+    def dns_classify(self, qnames):
+        """Batched DNSServer.handleRequest classification -> (kind, value)."""
+        if isinstance(qnames, tuple) and _is_dev(qnames[0]):
+            import torch
+            qb, qo = qnames[0], qnames[1]
+            n = len(qo) - 1
+            kind = torch.empty(n, dtype=torch.uint8, device=qb.device)
+            val = torch.empty(n, dtype=torch.int32, device=qb.device)
+            check(lib().vc_dns_classify_dev(self.h, _ptr(qb), _ptr(qo), n, _ptr(kind), _ptr(val),
+                                            _stream()))
+            return kind, val
+        n = len(qnames)
+        qb, qo, _ = pack_strings(qnames)
+        kind = np.empty(n, np.uint8)
+        val = np.empty(n, np.int32)
+        check(lib().vc_dns_classify(self.h, _ptr(qb), _ptr(qo), n, _ptr(kind), _ptr(val)))
+        return kind, val
+
+    def pipeline_v4(self, proto, src4, dst4, dport, host_id, pool_group, outs=None,
+                    want_allow=False):
+        """Combined ACL -> route -> host pipeline on device tensors."""
+        import torch
+        n = len(src4)
+        if outs is None:
+            dev = src4.device
+            outs = (torch.empty(n, dtype=torch.int32, device=dev),
+                    torch.empty(n, dtype=torch.int32, device=dev),
+                    torch.empty(n, dtype=torch.int32, device=dev),
+                    torch.empty(n, dtype=torch.uint8, device=dev) if want_allow else None)
+        a, r, g, al = outs
+        check(lib().vc_pipeline_v4_dev(self.h, _ptr(proto), _ptr(src4), _ptr(dst4), _ptr(dport),
+                                       _ptr(host_id), _ptr(pool_group), n, _ptr(a), _ptr(r),
+                                       _ptr(g), _ptr(al), _stream()))
+        return outs
+
+    # ---------------- counters ----------------
+    def counters_enable(self, on=True):
+        check(lib().vc_counters_enable(self.h, 1 if on else 0))
+
+    def counters_device(self, kind):
+        p = C.c_void_p()
+        n = C.c_int64()
+        check(lib().vc_counters_device(self.h, kind, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def counters_read(self, kind):
+        _, n = self.counters_device(kind)
+        out = np.zeros(max(1, n), np.uint64)
+        check(lib().vc_counters_read(self.h, kind, _ptr(out), n))
+        return out[:n]
+
+    def counters_reset(self):
+        check(lib().vc_counters_reset(self.h))

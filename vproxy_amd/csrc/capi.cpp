@@ -1,0 +1,746 @@
+// capi.cpp -- the C ABI (include/vclassify.h): contexts, snapshot
+// publication, uploads, and the host-side control-plane mirrors.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common/images.h"
+#include "compile/compile.hpp"
+#include "device/launch.h"
+#include "host/mirror.hpp"
+#include "host/net.hpp"
+#include "vclassify.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(VC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Device allocation owned by a snapshot.
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        // hipFree synchronises with in-flight work on the device, so a
+        // snapshot released while a batch still reads it is freed after it.
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Snapshot {
+    std::vector<std::unique_ptr<DevBuf>> bufs;
+    unsigned long long* counters = nullptr;
+    int64_t n_counters = 0;
+
+    template <class T>
+    const T* upload(const std::vector<T>& v, hipError_t* err) {
+        auto b = std::make_unique<DevBuf>();
+        size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+        hipError_t e = hipMalloc(&b->p, bytes);
+        if (e == hipSuccess && !v.empty()) e = hipMemcpy(b->p, v.data(), v.size() * sizeof(T),
+                                                         hipMemcpyHostToDevice);
+        if (e != hipSuccess) *err = e;
+        const T* p = static_cast<const T*>(b->p);
+        bufs.push_back(std::move(b));
+        return p;
+    }
+    hipError_t alloc_counters(int64_t n) {
+        auto b = std::make_unique<DevBuf>();
+        hipError_t e = hipMalloc(&b->p, size_t(std::max<int64_t>(n, 1)) * 8);
+        if (e == hipSuccess) e = hipMemset(b->p, 0, size_t(std::max<int64_t>(n, 1)) * 8);
+        counters = static_cast<unsigned long long*>(b->p);
+        n_counters = n;
+        bufs.push_back(std::move(b));
+        return e;
+    }
+};
+
+struct AclSnap : Snapshot {
+    AclImage img{};
+};
+struct RouteSnap : Snapshot {
+    RouteImage img{};
+    int32_t n4 = 0, n6 = 0;
+};
+struct HintSnap : Snapshot {
+    HintImage img{};
+};
+struct HostsSnap : Snapshot {
+    HostsImage img{};
+};
+
+}  // namespace
+
+struct vc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 256;
+    std::atomic<bool> counters_on{false};
+    std::mutex compile_mu;   // serialises compiles; classify never takes it
+    std::shared_ptr<const AclSnap> acl;
+    std::shared_ptr<const RouteSnap> route;
+    std::shared_ptr<const HintSnap> hint;
+    std::shared_ptr<const HostsSnap> hosts;
+
+    template <class S>
+    std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
+        return std::atomic_load(&p);
+    }
+    template <class S>
+    void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
+        std::atomic_store(&slot, std::move(v));
+    }
+    vc::LaunchCfg cfg(void* s) const {
+        vc::LaunchCfg c;
+        c.num_cus = num_cus;
+        c.stream = s ? static_cast<hipStream_t>(s) : stream;
+        return c;
+    }
+};
+
+namespace {
+
+int set_dev(vc_ctx* ctx) {
+    if (!ctx) return fail(VC_EINVAL, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hipSetDevice");
+}
+
+// Synchronous host-pointer staging for the plain (non _dev) entry points.
+struct Staging {
+    std::vector<std::unique_ptr<DevBuf>> bufs;
+    hipError_t err = hipSuccess;
+    void* in(const void* h, size_t bytes, hipStream_t s) {
+        if (!h) return nullptr;
+        auto b = std::make_unique<DevBuf>();
+        if (err == hipSuccess) err = hipMalloc(&b->p, std::max<size_t>(bytes, 16));
+        if (err == hipSuccess && bytes) err = hipMemcpyAsync(b->p, h, bytes, hipMemcpyHostToDevice, s);
+        void* p = b->p;
+        bufs.push_back(std::move(b));
+        return p;
+    }
+    void* out(const void* h, size_t bytes) {
+        if (!h) return nullptr;
+        auto b = std::make_unique<DevBuf>();
+        if (err == hipSuccess) err = hipMalloc(&b->p, std::max<size_t>(bytes, 16));
+        void* p = b->p;
+        bufs.push_back(std::move(b));
+        return p;
+    }
+    void back(void* h, const void* d, size_t bytes, hipStream_t s) {
+        if (h && d && bytes && err == hipSuccess)
+            err = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* vc_version(void) { return "vclassify 0.1 (gfx950)"; }
+
+const char* vc_last_error(void) { return g_err.c_str(); }
+
+int vc_create(int device, vc_ctx** out) {
+    if (!out) return fail(VC_EINVAL, "null out");
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) return fail(VC_EDEVICE, "no HIP device available");
+    if (device < 0 || device >= count) return fail(VC_EINVAL, "bad device ordinal");
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(VC_EDEVICE, std::string("libvclassify is built for gfx950, device is ") +
+                                    prop.gcnArchName);
+    auto* c = new vc_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    if ((e = hipSetDevice(device)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete c;
+        return hip_fail(e, "stream create");
+    }
+    *out = c;
+    return VC_OK;
+}
+
+void vc_destroy(vc_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->acl.reset();
+    ctx->route.reset();
+    ctx->hint.reset();
+    ctx->hosts.reset();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// ---------------------------------------------------------------------------
+// Network helpers
+// ---------------------------------------------------------------------------
+int vc_net_parse(const char* s, vc_net* out) {
+    if (!s || !out) return fail(VC_EINVAL, "null argument");
+    if (!vc::net_parse(s, out)) return fail(VC_EINVAL, std::string("invalid network ") + s);
+    return VC_OK;
+}
+
+int vc_net_from_prefix(const uint8_t* ip, int ip_len, int prefix, vc_net* out) {
+    if (!ip || !out) return fail(VC_EINVAL, "null argument");
+    if (!vc::net_from_prefix(ip, ip_len, prefix, out)) return fail(VC_EINVAL, "invalid network");
+    return VC_OK;
+}
+
+int vc_net_contains_ip(const vc_net* net, const uint8_t* ip, int ip_len) {
+    if (!net || !ip || (ip_len != 4 && ip_len != 16)) return fail(VC_EINVAL, "bad argument");
+    return vc::net_contains_ip(*net, ip, ip_len) ? 1 : 0;
+}
+
+int vc_ip_parse(const char* s, uint8_t out[16]) {
+    if (!s || !out) return fail(VC_EINVAL, "null argument");
+    auto ip = vc::parse_ip(s);
+    if (!ip) return fail(VC_EINVAL, std::string("not an ip literal: ") + s);
+    std::memcpy(out, ip->b.data(), ip->len);
+    return ip->len;
+}
+
+// ---------------------------------------------------------------------------
+// ACL
+// ---------------------------------------------------------------------------
+int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp,
+                   int n_udp, int default_allow) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if ((n_tcp && !tcp) || (n_udp && !udp)) return fail(VC_EINVAL, "null rule array");
+    vc::AclBuilt b;
+    rc = vc::build_acl(tcp, n_tcp, udp, n_udp, default_allow, &b);
+    if (rc) return fail(rc, "invalid SecurityGroup rule (network must be a valid Network)");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<AclSnap>();
+    hipError_t e = hipSuccess;
+    for (int l = 0; l < 2; ++l)
+        for (int f = 0; f < 2; ++f) {
+            const vc::AclFamilyBuilt& fb = b.fam[l][f];
+            AclFamilyImage& fi = s->img.fam[l][f];
+            fi.bounds4 = f == 0 ? s->upload(fb.bounds4, &e) : nullptr;
+            fi.bounds6 = f == 1 ? s->upload(fb.bounds6, &e) : nullptr;
+            fi.desc = s->upload(fb.desc, &e);
+            fi.pieces = s->upload(fb.pieces, &e);
+            fi.nb = fb.nb;
+            fi.np = static_cast<int32_t>(fb.pieces.size() / 2);
+        }
+    s->img.allow = s->upload(b.allow, &e);
+    s->img.n_tcp = b.n_tcp;
+    s->img.n_udp = b.n_udp;
+    s->img.default_allow = b.default_allow;
+    if (e == hipSuccess) e = s->alloc_counters(int64_t(n_tcp) + n_udp + 2);
+    if (e != hipSuccess) return hip_fail(e, "ACL upload");
+    ctx->publish(ctx->acl, std::shared_ptr<const AclSnap>(std::move(s)));
+    return VC_OK;
+}
+
+static int acl_dev(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
+                   const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow,
+                   void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!proto || !src || !port || !out_idx)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto s = ctx->get(ctx->acl);
+    if (!s) return fail(VC_ESTATE, "no SecurityGroup compiled");
+    unsigned long long* cnt = ctx->counters_on ? s->counters : nullptr;
+    hipError_t e = fam == 4
+        ? vc::launch_acl_v4(ctx->cfg(stream), s->img, proto, static_cast<const uint32_t*>(src),
+                            port, n, out_idx, out_allow, cnt)
+        : vc::launch_acl_v6(ctx->cfg(stream), s->img, proto, static_cast<const uint8_t*>(src),
+                            port, n, out_idx, out_allow, cnt);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "ACL launch");
+}
+
+int vc_acl_classify_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
+                           const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow,
+                           void* stream) {
+    return acl_dev(ctx, 4, proto, src4, port, n, out_idx, out_allow, stream);
+}
+
+int vc_acl_classify_v6_dev(vc_ctx* ctx, const uint8_t* proto, const uint8_t* src6,
+                           const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow,
+                           void* stream) {
+    return acl_dev(ctx, 6, proto, src6, port, n, out_idx, out_allow, stream);
+}
+
+static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
+                    const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    auto* dp = static_cast<uint8_t*>(st.in(proto, size_t(n), s));
+    auto* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), s);
+    auto* dq = static_cast<uint16_t*>(st.in(port, size_t(n) * 2, s));
+    auto* di = static_cast<int32_t*>(st.out(out_idx, size_t(n) * 4));
+    auto* da = static_cast<uint8_t*>(st.out(out_allow, size_t(n)));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = acl_dev(ctx, fam, dp, ds, dq, n, di, da, s);
+    if (rc) return rc;
+    st.back(out_idx, di, size_t(n) * 4, s);
+    st.back(out_allow, da, size_t(n), s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "ACL classify");
+}
+
+int vc_acl_classify_v4(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
+                       const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow) {
+    return acl_host(ctx, 4, proto, src4, port, n, out_idx, out_allow);
+}
+
+int vc_acl_classify_v6(vc_ctx* ctx, const uint8_t* proto, const uint8_t* src6,
+                       const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow) {
+    return acl_host(ctx, 6, proto, src6, port, n, out_idx, out_allow);
+}
+
+// ---------------------------------------------------------------------------
+// Routes
+// ---------------------------------------------------------------------------
+int vc_compile_routes(vc_ctx* ctx, const vc_net* v4, int n4, const vc_net* v6, int n6) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if ((n4 && !v4) || (n6 && !v6) || n4 < 0 || n6 < 0) return fail(VC_EINVAL, "bad rule arrays");
+    vc::TrieBuilt t4, t6;
+    if ((rc = vc::build_trie(v4, n4, 0, &t4)) != VC_OK) return fail(rc, "invalid IPv4 route rule");
+    if ((rc = vc::build_trie(v6, n6, 1, &t6)) != VC_OK) return fail(rc, "invalid IPv6 route rule");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<RouteSnap>();
+    hipError_t e = hipSuccess;
+    vc::TrieBuilt* tb[2] = {&t4, &t6};
+    for (int f = 0; f < 2; ++f) {
+        s->img.fam[f].nodes = s->upload(tb[f]->nodes, &e);
+        s->img.fam[f].root_bits = tb[f]->root_bits;
+        s->img.fam[f].key_bits = tb[f]->key_bits;
+        s->img.fam[f].n_rules = tb[f]->n_rules;
+    }
+    s->n4 = n4;
+    s->n6 = n6;
+    if (e == hipSuccess) e = s->alloc_counters(int64_t(n4) + n6 + 2);
+    if (e != hipSuccess) return hip_fail(e, "route upload");
+    ctx->publish(ctx->route, std::shared_ptr<const RouteSnap>(std::move(s)));
+    return VC_OK;
+}
+
+static int route_dev(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t* out, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!dst || !out))) return fail(VC_EINVAL, "bad batch arguments");
+    auto s = ctx->get(ctx->route);
+    if (!s) return fail(VC_ESTATE, "no RouteTable compiled");
+    unsigned long long* cnt = ctx->counters_on ? s->counters : nullptr;
+    const int64_t nn = int64_t(s->n4) + s->n6;
+    hipError_t e = fam == 4
+        ? vc::launch_route_v4(ctx->cfg(stream), s->img.fam[0], static_cast<const uint32_t*>(dst),
+                              n, out, cnt, 0, nn)
+        : vc::launch_route_v6(ctx->cfg(stream), s->img.fam[1], static_cast<const uint8_t*>(dst),
+                              n, out, cnt, s->n4, nn + 1);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "route launch");
+}
+
+int vc_route_lookup_v4_dev(vc_ctx* ctx, const uint32_t* dst4, int64_t n, int32_t* out,
+                           void* stream) {
+    return route_dev(ctx, 4, dst4, n, out, stream);
+}
+
+int vc_route_lookup_v6_dev(vc_ctx* ctx, const uint8_t* dst6, int64_t n, int32_t* out,
+                           void* stream) {
+    return route_dev(ctx, 6, dst6, n, out, stream);
+}
+
+static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    void* dd = st.in(dst, size_t(n) * (fam == 4 ? 4 : 16), s);
+    auto* dout = static_cast<int32_t*>(st.out(out, size_t(n) * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = route_dev(ctx, fam, dd, n, dout, s);
+    if (rc) return rc;
+    st.back(out, dout, size_t(n) * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "route lookup");
+}
+
+int vc_route_lookup_v4(vc_ctx* ctx, const uint32_t* dst4, int64_t n, int32_t* out) {
+    return route_host(ctx, 4, dst4, n, out);
+}
+
+int vc_route_lookup_v6(vc_ctx* ctx, const uint8_t* dst6, int64_t n, int32_t* out) {
+    return route_host(ctx, 6, dst6, n, out);
+}
+
+// ---------------------------------------------------------------------------
+// Upstream hints + DNS
+// ---------------------------------------------------------------------------
+int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n && !groups)) return fail(VC_EINVAL, "bad group array");
+    vc::HintBuilt b;
+    if ((rc = vc::build_hints(groups, n, &b)) != VC_OK) return fail(rc, "invalid annotations");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<HintSnap>();
+    hipError_t e = hipSuccess;
+    static_assert(sizeof(KeySlot) == sizeof(vc::KeySlotH), "slot layout");
+    s->img.blob = s->upload(b.blob, &e);
+    s->img.host_slots = reinterpret_cast<const KeySlot*>(s->upload(b.host_slots, &e));
+    s->img.uri_slots = reinterpret_cast<const KeySlot*>(s->upload(b.uri_slots, &e));
+    s->img.lists = s->upload(b.lists, &e);
+    s->img.port_mins = reinterpret_cast<const PortMin*>(s->upload(b.port_mins, &e));
+    s->img.port_min_off = s->upload(b.port_min_off, &e);
+    s->img.groups = reinterpret_cast<const GroupRec*>(s->upload(b.groups, &e));
+    s->img.host_mask = static_cast<uint32_t>(b.host_slots.size() - 1);
+    s->img.uri_mask = static_cast<uint32_t>(b.uri_slots.size() - 1);
+    s->img.n_groups = n;
+    s->img.wildcard_slot = b.wildcard_slot;
+    s->img.uri_star_slot = b.uri_star_slot;
+    s->img.has_uri_keys = b.has_uri_keys;
+    if (e == hipSuccess) e = s->alloc_counters(int64_t(n) + 1);
+    if (e != hipSuccess) return hip_fail(e, "hint upload");
+    ctx->publish(ctx->hint, std::shared_ptr<const HintSnap>(std::move(s)));
+    return VC_OK;
+}
+
+int vc_hint_search_dev(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_off,
+                       const uint8_t* host_null, const uint16_t* port, const uint8_t* uri_blob,
+                       const uint32_t* uri_off, const uint8_t* uri_null, int64_t n,
+                       int32_t* out_group, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && !out_group) || (host_blob && !host_off) || (uri_blob && !uri_off))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto s = ctx->get(ctx->hint);
+    if (!s) return fail(VC_ESTATE, "no Upstream compiled");
+    hipError_t e = vc::launch_hint(ctx->cfg(stream), s->img, host_blob, host_off, host_null, port,
+                                   uri_blob, uri_off, uri_null, n, out_group,
+                                   ctx->counters_on ? s->counters : nullptr);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hint launch");
+}
+
+int vc_hint_search(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_off,
+                   const uint8_t* host_null, const uint16_t* port, const uint8_t* uri_blob,
+                   const uint32_t* uri_off, const uint8_t* uri_null, int64_t n,
+                   int32_t* out_group) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    size_t hb = host_blob ? host_off[n] : 0, ub = uri_blob ? uri_off[n] : 0;
+    auto* dhb = static_cast<uint8_t*>(host_blob ? st.in(host_blob, hb, s) : nullptr);
+    auto* dho = static_cast<uint32_t*>(host_blob ? st.in(host_off, size_t(n + 1) * 4, s) : nullptr);
+    auto* dhn = static_cast<uint8_t*>(st.in(host_null, size_t(n), s));
+    auto* dp = static_cast<uint16_t*>(st.in(port, size_t(n) * 2, s));
+    auto* dub = static_cast<uint8_t*>(uri_blob ? st.in(uri_blob, ub, s) : nullptr);
+    auto* duo = static_cast<uint32_t*>(uri_blob ? st.in(uri_off, size_t(n + 1) * 4, s) : nullptr);
+    auto* dun = static_cast<uint8_t*>(st.in(uri_null, size_t(n), s));
+    auto* dout = static_cast<int32_t*>(st.out(out_group, size_t(n) * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_hint_search_dev(ctx, dhb, dho, dhn, dp, dub, duo, dun, n, dout, s);
+    if (rc) return rc;
+    st.back(out_group, dout, size_t(n) * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hint search");
+}
+
+int vc_compile_hosts(vc_ctx* ctx, const char* const* keys, const int32_t* key_lens,
+                     const int32_t* values, int n) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n && (!keys || !key_lens || !values))) return fail(VC_EINVAL, "bad hosts arrays");
+    vc::HostsBuilt b;
+    if ((rc = vc::build_hosts(keys, key_lens, values, n, &b)) != VC_OK)
+        return fail(rc, "invalid hosts entry");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<HostsSnap>();
+    hipError_t e = hipSuccess;
+    s->img.blob = s->upload(b.blob, &e);
+    s->img.slots = reinterpret_cast<const KeySlot*>(s->upload(b.slots, &e));
+    s->img.mask = static_cast<uint32_t>(b.slots.size() - 1);
+    s->img.n = b.n;
+    if (e != hipSuccess) return hip_fail(e, "hosts upload");
+    ctx->publish(ctx->hosts, std::shared_ptr<const HostsSnap>(std::move(s)));
+    return VC_OK;
+}
+
+int vc_compile_hosts_text(vc_ctx* ctx, const char* text, int64_t len) {
+    if (!text && len) return fail(VC_EINVAL, "null text");
+    auto entries = vc::parse_hosts_text(std::string_view(text ? text : "", size_t(len)));
+    std::vector<const char*> k;
+    std::vector<int32_t> kl, v;
+    for (auto& e : entries) {
+        k.push_back(e.key.data());
+        kl.push_back(static_cast<int32_t>(e.key.size()));
+        v.push_back(e.value);
+    }
+    return vc_compile_hosts(ctx, k.data(), kl.data(), v.data(), static_cast<int>(k.size()));
+}
+
+int vc_dns_classify_dev(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int64_t n,
+                        uint8_t* out_kind, int32_t* out_value, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!qblob || !qoff || !out_kind || !out_value)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto h = ctx->get(ctx->hint);
+    if (!h) return fail(VC_ESTATE, "no Upstream (rrsets) compiled");
+    auto ho = ctx->get(ctx->hosts);
+    HostsImage hi{};
+    if (ho) hi = ho->img;
+    hipError_t e = vc::launch_dns(ctx->cfg(stream), hi, h->img, qblob, qoff, n, out_kind, out_value,
+                                  ctx->counters_on ? h->counters : nullptr);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "dns launch");
+}
+
+int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int64_t n,
+                    uint8_t* out_kind, int32_t* out_value) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    auto* db = static_cast<uint8_t*>(st.in(qblob, qoff[n], s));
+    auto* dof = static_cast<uint32_t*>(st.in(qoff, size_t(n + 1) * 4, s));
+    auto* dk = static_cast<uint8_t*>(st.out(out_kind, size_t(n)));
+    auto* dv = static_cast<int32_t*>(st.out(out_value, size_t(n) * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_dns_classify_dev(ctx, db, dof, n, dk, dv, s);
+    if (rc) return rc;
+    st.back(out_kind, dk, size_t(n), s);
+    st.back(out_value, dv, size_t(n) * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "dns classify");
+}
+
+// ---------------------------------------------------------------------------
+// Pipeline
+// ---------------------------------------------------------------------------
+int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
+                       const uint32_t* dst4, const uint16_t* dport, const uint32_t* host_id,
+                       const int32_t* pool_group, int64_t n, int32_t* out_acl, int32_t* out_route,
+                       int32_t* out_group, uint8_t* out_allow, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!proto || !src4 || !dst4 || !dport || !host_id || !pool_group ||
+                            !out_acl || !out_route || !out_group)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto a = ctx->get(ctx->acl);
+    auto r = ctx->get(ctx->route);
+    auto h = ctx->get(ctx->hint);
+    if (!a || !r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
+    const bool on = ctx->counters_on;
+    const int32_t ng = h ? h->img.n_groups : 0;
+    hipError_t e = vc::launch_pipeline_v4(
+        ctx->cfg(stream), a->img, r->img.fam[0], proto, src4, dst4, dport, host_id, pool_group, n,
+        out_acl, out_route, out_group, out_allow, on ? a->counters : nullptr,
+        on ? r->counters : nullptr, int64_t(r->n4) + r->n6, on && h ? h->counters : nullptr, ng);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");
+}
+
+// ---------------------------------------------------------------------------
+// Counters
+// ---------------------------------------------------------------------------
+int vc_counters_enable(vc_ctx* ctx, int on) {
+    if (!ctx) return fail(VC_EINVAL, "null context");
+    ctx->counters_on = on != 0;
+    return VC_OK;
+}
+
+static const Snapshot* counter_snap(vc_ctx* ctx, int kind, std::shared_ptr<const void>* keep) {
+    switch (kind) {
+    case VC_COUNTERS_ACL: { auto s = ctx->get(ctx->acl); *keep = s; return s.get(); }
+    case VC_COUNTERS_ROUTE: { auto s = ctx->get(ctx->route); *keep = s; return s.get(); }
+    case VC_COUNTERS_GROUP: { auto s = ctx->get(ctx->hint); *keep = s; return s.get(); }
+    default: return nullptr;
+    }
+}
+
+int vc_counters_device(vc_ctx* ctx, int kind, uint64_t** dev_ptr, int64_t* n) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    std::shared_ptr<const void> keep;
+    const Snapshot* s = counter_snap(ctx, kind, &keep);
+    if (!s) return fail(VC_ESTATE, "no table compiled for this counter kind");
+    if (dev_ptr) *dev_ptr = reinterpret_cast<uint64_t*>(s->counters);
+    if (n) *n = s->n_counters;
+    return VC_OK;
+}
+
+int vc_counters_read(vc_ctx* ctx, int kind, uint64_t* host, int64_t n) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    std::shared_ptr<const void> keep;
+    const Snapshot* s = counter_snap(ctx, kind, &keep);
+    if (!s) return fail(VC_ESTATE, "no table compiled for this counter kind");
+    if (!host || n < s->n_counters) return fail(VC_EINVAL, "host buffer too small");
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess)
+        e = hipMemcpy(host, s->counters, size_t(s->n_counters) * 8, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "counter read");
+}
+
+int vc_counters_reset(vc_ctx* ctx) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) {
+        std::shared_ptr<const void> keep;
+        const Snapshot* s = counter_snap(ctx, k, &keep);
+        if (!s) continue;
+        hipError_t e = hipMemsetAsync(s->counters, 0, size_t(std::max<int64_t>(s->n_counters, 1)) * 8,
+                                      ctx->stream);
+        if (e != hipSuccess) return hip_fail(e, "counter reset");
+    }
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "counter reset");
+}
+
+// ---------------------------------------------------------------------------
+// Control-plane mirrors
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+struct vc_secgroup {
+    vc::SecurityGroup sg;
+};
+struct vc_routetable {
+    vc::RouteTable rt;
+};
+
+extern "C" {
+
+int vc_secgroup_new(const char* alias, int default_allow, vc_secgroup** out) {
+    if (!alias || !out) return fail(VC_EINVAL, "null argument");
+    *out = new vc_secgroup{vc::SecurityGroup(alias, default_allow != 0)};
+    return VC_OK;
+}
+
+void vc_secgroup_free(vc_secgroup* sg) { delete sg; }
+
+int vc_secgroup_set_default(vc_secgroup* sg, int default_allow) {
+    if (!sg) return fail(VC_EINVAL, "null argument");
+    sg->sg.set_default_allow(default_allow != 0);
+    return VC_OK;
+}
+
+int vc_secgroup_add_rule(vc_secgroup* sg, const char* alias, const vc_net* net, int proto,
+                         int min_port, int max_port, int allow) {
+    if (!sg || !alias || !net) return fail(VC_EINVAL, "null argument");
+    vc::SecurityGroupRule r{alias, *net, proto == VC_PROTO_TCP ? VC_PROTO_TCP : VC_PROTO_UDP,
+                            min_port, max_port, allow != 0};
+    int rc = sg->sg.add_rule(std::move(r));
+    return rc ? fail(rc, std::string("security-group-rule already exists: ") + alias) : VC_OK;
+}
+
+int vc_secgroup_remove_rule(vc_secgroup* sg, const char* alias) {
+    if (!sg || !alias) return fail(VC_EINVAL, "null argument");
+    int rc = sg->sg.remove_rule(alias);
+    return rc ? fail(rc, std::string("security-group-rule not found: ") + alias) : VC_OK;
+}
+
+int vc_secgroup_rules(const vc_secgroup* sg, int proto, vc_acl_rule* out, int cap) {
+    if (!sg) return fail(VC_EINVAL, "null argument");
+    const auto& l = proto == VC_PROTO_TCP ? sg->sg.tcp() : sg->sg.udp();
+    for (int i = 0; i < cap && i < static_cast<int>(l.size()); ++i)
+        out[i] = vc_acl_rule{l[i].network, l[i].min_port, l[i].max_port, l[i].allow ? 1 : 0};
+    return static_cast<int>(l.size());
+}
+
+int vc_secgroup_compile(vc_ctx* ctx, const vc_secgroup* sg) {
+    if (!sg) return fail(VC_EINVAL, "null argument");
+    std::vector<vc_acl_rule> t(sg->sg.tcp().size()), u(sg->sg.udp().size());
+    vc_secgroup_rules(sg, VC_PROTO_TCP, t.data(), static_cast<int>(t.size()));
+    vc_secgroup_rules(sg, VC_PROTO_UDP, u.data(), static_cast<int>(u.size()));
+    return vc_compile_acl(ctx, t.data(), static_cast<int>(t.size()), u.data(),
+                          static_cast<int>(u.size()), sg->sg.default_allow() ? 1 : 0);
+}
+
+int vc_routetable_new(const vc_net* v4net, const vc_net* v6net, int vni, vc_routetable** out) {
+    if (!out) return fail(VC_EINVAL, "null argument");
+    if (!v4net && v6net) return fail(VC_EINVAL, "v6 network needs a v4 network");
+    *out = v4net ? new vc_routetable{vc::RouteTable(*v4net, v6net, vni)} : new vc_routetable{};
+    return VC_OK;
+}
+
+void vc_routetable_free(vc_routetable* rt) { delete rt; }
+
+int vc_routetable_add_rule(vc_routetable* rt, const char* alias, const vc_net* net, int to_vni,
+                           const uint8_t* via_ip, int via_len) {
+    if (!rt || !alias || !net) return fail(VC_EINVAL, "null argument");
+    vc::RouteRule r;
+    r.alias = alias;
+    r.rule = *net;
+    if (via_ip) {
+        if (via_len != 4 && via_len != 16) return fail(VC_EINVAL, "bad via ip");
+        r.has_ip = true;
+        std::memcpy(r.ip, via_ip, via_len);
+        r.ip_len = via_len;
+    } else {
+        r.to_vni = to_vni;
+    }
+    int rc = rt->rt.add_rule(r);
+    return rc ? fail(rc, std::string("cannot add route ") + alias) : VC_OK;
+}
+
+int vc_routetable_add_rules(vc_routetable* rt, const char* alias_prefix, const vc_net* nets, int n,
+                            int to_vni) {
+    if (!rt || !alias_prefix || (n && !nets) || n < 0) return fail(VC_EINVAL, "bad arguments");
+    std::vector<vc::RouteRule> v(n);
+    for (int i = 0; i < n; ++i) {
+        v[i].alias = std::string(alias_prefix) + std::to_string(i);
+        v[i].rule = nets[i];
+        v[i].to_vni = to_vni;
+    }
+    int rc = rt->rt.add_rules_bulk(std::move(v));
+    return rc ? fail(rc, "cannot add routes") : VC_OK;
+}
+
+int vc_routetable_del_rule(vc_routetable* rt, const char* alias) {
+    if (!rt || !alias) return fail(VC_EINVAL, "null argument");
+    int rc = rt->rt.del_rule(alias);
+    return rc ? fail(rc, std::string("route not found: ") + alias) : VC_OK;
+}
+
+int vc_routetable_rules(const vc_routetable* rt, int family, vc_net* out, int cap) {
+    if (!rt) return fail(VC_EINVAL, "null argument");
+    const auto& l = family == 4 ? rt->rt.v4() : rt->rt.v6();
+    for (int i = 0; i < cap && i < static_cast<int>(l.size()); ++i) out[i] = l[i].rule;
+    return static_cast<int>(l.size());
+}
+
+int vc_routetable_compile(vc_ctx* ctx, const vc_routetable* rt) {
+    if (!rt) return fail(VC_EINVAL, "null argument");
+    std::vector<vc_net> a(rt->rt.v4().size()), b(rt->rt.v6().size());
+    vc_routetable_rules(rt, 4, a.data(), static_cast<int>(a.size()));
+    vc_routetable_rules(rt, 6, b.data(), static_cast<int>(b.size()));
+    return vc_compile_routes(ctx, a.data(), static_cast<int>(a.size()), b.data(),
+                             static_cast<int>(b.size()));
+}
+
+}  // extern "C"

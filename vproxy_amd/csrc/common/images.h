@@ -1,0 +1,116 @@
+// images.h -- the device-resident table images the HIP kernels read.
+//
+// Built on the host by csrc/compile/*.cpp, copied to HBM once per compile
+// (snapshot), read-only afterwards.  Layouts are flat arrays of 4/8/16-byte
+// words so every probe is one aligned load.
+#pragma once
+
+#include <stdint.h>
+
+#define VC_NONE 0x7FFFFFFFu       // "no rule" in a value slot (-> -1 on output)
+#define VC_PTR  0x80000000u       // trie entry: child node pointer flag
+
+// ---------------------------------------------------------------------------
+// ACL (SecurityGroup): one image per (protocol list, input family).
+//
+// The input key space (32-bit for IPv4 inputs, 128-bit for IPv6 inputs) is
+// cut into elementary intervals at every rule-projection edge.  Interval j
+// = [bounds[j], bounds[j+1]).  desc[j] describes the port -> first-rule
+// function on that interval:
+//   desc.y == 0 : constant, desc.x = rule index or VC_NONE
+//   desc.y  > 0 : desc.y pieces at pieces[desc.x ...], each (port_start,
+//                 value), port_start ascending, first port_start == 0.
+// Identical port functions share one piece run.
+// ---------------------------------------------------------------------------
+struct AclFamilyImage {
+    const uint32_t* bounds4;      // v4: nb boundaries (bounds4[0] == 0)
+    const uint64_t* bounds6;      // v6: nb boundaries as (hi, lo) pairs, 2*nb words
+    const uint32_t* desc;         // 2*nb words: (x, y) per interval
+    const uint32_t* pieces;       // 2*np words: (port_start, value)
+    int32_t nb;
+    int32_t np;
+};
+
+struct AclImage {
+    AclFamilyImage fam[2][2];     // [0 = tcp list, 1 = udp list][0 = v4 input, 1 = v6 input]
+    const uint8_t* allow;         // rule allow bits: tcp rules then udp rules
+    int32_t n_tcp, n_udp;
+    int32_t default_allow;
+};
+
+// ---------------------------------------------------------------------------
+// RouteTable: one multibit stride trie per family (DIR-24-8 for IPv4).
+// Root = 2^root_bits entries, every deeper node 256 entries (8-bit stride).
+// Entry: VC_PTR | node_id  -> child at nodes[(1<<root_bits) + node_id*256]
+//        otherwise value   -> min list index of the prefixes covering this
+//                             entry's address range (VC_NONE if none).
+// "min list index" is RouteTable.lookup's first-match (list order), not LPM.
+// ---------------------------------------------------------------------------
+struct TrieImage {
+    const uint32_t* nodes;
+    int32_t root_bits;
+    int32_t key_bits;             // 32 (v4) or 128 (v6)
+    int32_t n_rules;
+};
+
+struct RouteImage {
+    TrieImage fam[2];             // 0 = rulesV4, 1 = rulesV6
+};
+
+// ---------------------------------------------------------------------------
+// Upstream hint matching + DNS hosts.
+//
+// Keys are hashed with 64-bit FNV-1a.  Host keys (merged hint-host H) hash
+// the string right-to-left, so one right-to-left scan of a query host yields
+// the hash of every dot-suffix incrementally (a reversed-suffix index).  URI
+// keys (merged hint-uri U) and hosts-map keys hash left-to-right, so one scan
+// of a URI yields the hash of every prefix.  Open addressing,
+// power-of-two capacity, linear probing; an empty slot has key_len == -1.
+// Every hash hit is confirmed by a full byte compare.
+// ---------------------------------------------------------------------------
+struct KeySlot {                   // 32 bytes
+    uint64_t hash;
+    int32_t key_len;               // -1 = empty slot
+    uint32_t key_off;              // into HintImage.blob
+    int32_t a;                     // host table: min handle index (any port); hosts: value
+    int32_t b;                     // host table: min handle index with no hint-port
+    uint32_t list_off;             // member list (handle indices ascending) in lists[]
+    uint32_t list_cnt;
+};
+
+struct PortMin {                   // per host key: min index per distinct hint-port
+    int32_t port;
+    int32_t idx;
+};
+
+struct GroupRec {                  // merged annotations of one ServerGroupHandle
+    int32_t host_len;              // -1 = null
+    uint32_t host_off;
+    int32_t uri_len;               // -1 = null
+    uint32_t uri_off;
+    int32_t port;                  // 0 = absent
+    int32_t any;                   // 0 when H, P and U are all absent (level is always 0)
+};
+
+struct HintImage {
+    const uint8_t* blob;           // key / annotation bytes
+    const KeySlot* host_slots;     // keyed by H (reverse hash)
+    const KeySlot* uri_slots;      // keyed by U (forward hash)
+    const uint32_t* lists;         // member lists
+    const PortMin* port_mins;      // per host key: distinct nonzero hint-ports
+    const uint32_t* port_min_off;  // 2 words per host slot: (off, cnt) into port_mins
+    const GroupRec* groups;
+    uint32_t host_mask;            // capacity - 1
+    uint32_t uri_mask;
+    int32_t n_groups;
+    int32_t wildcard_slot;         // host slot of "*" or -1
+    int32_t uri_star_slot;         // uri slot of "*" or -1
+    int32_t has_uri_keys;          // any group with a hint-uri
+};
+
+struct HostsImage {
+    const uint8_t* blob;
+    const KeySlot* slots;          // keyed by the exact qname (forward hash); value in .a
+    uint32_t mask;
+    int32_t n;
+};

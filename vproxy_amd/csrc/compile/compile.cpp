@@ -1,0 +1,472 @@
+// compile.cpp -- rule lists -> device table images (see common/images.h).
+#include "compile.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+
+#include "../common/images.h"
+#include "../host/net.hpp"
+
+namespace vc {
+
+using u128 = unsigned __int128;
+
+namespace {
+
+u128 key128(const uint8_t* b, int len) {   // big-endian bytes -> integer
+    u128 k = 0;
+    for (int i = 0; i < len; ++i) k = (k << 8) | b[i];
+    return k;
+}
+
+// A network must be what Network(String)/NetworkHandle produce: a standard
+// mask (parseMask(m) bytes) and validNetwork(ip, mask).
+bool standard_net(const vc_net& n) {
+    if (n.ip_len != 4 && n.ip_len != 16) return false;
+    if (n.mask_len != 4 && n.mask_len != 16) return false;
+    int m = mask_int(n.mask, n.mask_len);
+    uint8_t ref[16];
+    int ml = parse_mask(m, ref);
+    if (ml != n.mask_len || std::memcmp(ref, n.mask, ml) != 0) return false;
+    return valid_network(n.ip, n.ip_len, n.mask, n.mask_len);
+}
+
+u128 low_ones(int bits) {   // 2^bits - 1 (bits in 0..128)
+    if (bits <= 0) return 0;
+    if (bits >= 128) return ~(u128)0;
+    return (((u128)1) << bits) - 1;
+}
+
+struct Iv {
+    u128 lo, hi;   // inclusive
+    int rule;
+};
+
+// Projection of one SecurityGroupRule network onto an input family, exactly
+// as Network.maskMatch (Network.java:183-278) decides membership
+// (SURVEY.md Appendix A.1).  Appends 0, 1 or 2 intervals.
+void project(const vc_net& n, int family, int rule, std::vector<Iv>* out) {
+    int m = mask_int(n.mask, n.mask_len);
+    if (family == 0) {                       // IPv4 input (4 bytes)
+        if (n.ip_len == 4) {                 // case 5: plain v4 prefix
+            u128 lo = key128(n.ip, 4);
+            out->push_back({lo, lo | low_ones(32 - m), rule});
+        } else if (n.mask_len == 16) {       // case 3: low 32 bits + lowBitsV6V4(rule)
+            const uint8_t* r = n.ip;
+            for (int i = 0; i < 10; ++i)
+                if (r[i] != 0) return;
+            if (!((r[10] == 0 && r[11] == 0) || (r[10] == 0xFF && r[11] == 0xFF))) return;
+            int m4 = m > 96 ? m - 96 : 0;
+            u128 lo = key128(r + 12, 4);
+            out->push_back({lo, lo | low_ones(32 - m4), rule});
+        }
+        // v6 rule with a 4-byte mask: case 2, never matches IPv4 input
+    } else {                                 // IPv6 input (16 bytes)
+        if (n.ip_len == 4) {                 // case 4: tail compare + lowBitsV6V4(input)
+            u128 lo = key128(n.ip, 4);
+            u128 span = low_ones(32 - m);
+            out->push_back({lo, lo | span, rule});                      // ::a.b.c.d
+            u128 mapped = ((u128)0xFFFF) << 32;
+            out->push_back({mapped | lo, mapped | lo | span, rule});     // ::ffff:a.b.c.d
+        } else {                             // cases 1 and 5: plain v6 prefix
+            u128 lo = key128(n.ip, 16);
+            out->push_back({lo, lo | low_ones(128 - m), rule});
+        }
+    }
+}
+
+struct PortRule {
+    int rule, plo, phi;
+};
+
+// port -> min rule index over `act` (ascending rule order, truncated at the
+// first full-range rule).  Emits (port_start, value) pairs.
+void port_function(const std::vector<PortRule>& act, std::vector<uint32_t>* fn) {
+    fn->clear();
+    if (act.empty()) return;
+    std::vector<std::pair<int, int>> ev;   // (port, +rule+1 / -(rule+1))
+    ev.reserve(act.size() * 2);
+    for (auto& p : act) {
+        ev.push_back({p.plo, p.rule + 1});
+        if (p.phi < 65535) ev.push_back({p.phi + 1, -(p.rule + 1)});
+    }
+    std::sort(ev.begin(), ev.end());
+    std::set<int> live;
+    uint32_t cur = 0xFFFFFFFFu;
+    size_t k = 0;
+    if (ev[0].first != 0) {
+        fn->push_back(0);
+        fn->push_back(VC_NONE);
+        cur = VC_NONE;
+    }
+    while (k < ev.size()) {
+        int port = ev[k].first;
+        for (; k < ev.size() && ev[k].first == port; ++k) {
+            if (ev[k].second > 0) live.insert(ev[k].second - 1);
+            else live.erase(-ev[k].second - 1);
+        }
+        uint32_t v = live.empty() ? VC_NONE : static_cast<uint32_t>(*live.begin());
+        if (v != cur) {
+            fn->push_back(static_cast<uint32_t>(port));
+            fn->push_back(v);
+            cur = v;
+        }
+    }
+}
+
+void build_acl_family(const vc_acl_rule* rules, int n, int family, AclFamilyBuilt* out) {
+    std::vector<Iv> ivs;
+    std::vector<PortRule> pr(n);
+    for (int i = 0; i < n; ++i) {
+        int plo = std::max(rules[i].min_port, 0);
+        int phi = std::min(rules[i].max_port, 65535);
+        pr[i] = {i, plo, phi};
+        if (plo > phi) continue;             // the port test can never pass
+        project(rules[i].net, family, i, &ivs);
+    }
+    const u128 kmax = family == 0 ? low_ones(32) : ~(u128)0;
+    std::vector<u128> pts;
+    pts.reserve(ivs.size() * 2 + 1);
+    pts.push_back(0);
+    for (auto& iv : ivs) {
+        pts.push_back(iv.lo);
+        if (iv.hi != kmax) pts.push_back(iv.hi + 1);
+    }
+    std::sort(pts.begin(), pts.end());
+    pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+    const size_t K = pts.size();
+    // events per elementary interval index
+    std::vector<std::pair<uint32_t, int>> ev;   // (index, +rule+1 / -(rule+1))
+    ev.reserve(ivs.size() * 2);
+    for (auto& iv : ivs) {
+        uint32_t s = static_cast<uint32_t>(std::lower_bound(pts.begin(), pts.end(), iv.lo) - pts.begin());
+        ev.push_back({s, iv.rule + 1});
+        if (iv.hi != kmax) {
+            uint32_t e = static_cast<uint32_t>(
+                std::lower_bound(pts.begin(), pts.end(), iv.hi + 1) - pts.begin());
+            ev.push_back({e, -(iv.rule + 1)});
+        }
+    }
+    std::sort(ev.begin(), ev.end());
+    std::set<int> active;
+    std::map<std::vector<uint32_t>, uint32_t> memo;
+    std::vector<PortRule> act;
+    std::vector<uint32_t> fn;
+    size_t k = 0;
+    uint32_t px = 0xFFFFFFFFu, py = 0xFFFFFFFFu;
+    for (size_t j = 0; j < K; ++j) {
+        for (; k < ev.size() && ev[k].first == j; ++k) {
+            if (ev[k].second > 0) active.insert(ev[k].second - 1);
+            else active.erase(-ev[k].second - 1);
+        }
+        act.clear();
+        for (int r : active) {
+            act.push_back(pr[r]);
+            if (pr[r].plo == 0 && pr[r].phi == 65535) break;
+        }
+        uint32_t x, y;
+        if (act.empty()) {
+            x = VC_NONE;
+            y = 0;
+        } else if (act[0].plo == 0 && act[0].phi == 65535) {
+            x = static_cast<uint32_t>(act[0].rule);
+            y = 0;
+        } else {
+            port_function(act, &fn);
+            if (fn.size() == 2) {
+                x = fn[1];
+                y = 0;
+            } else {
+                auto it = memo.find(fn);
+                if (it == memo.end()) {
+                    uint32_t off = static_cast<uint32_t>(out->pieces.size() / 2);
+                    out->pieces.insert(out->pieces.end(), fn.begin(), fn.end());
+                    it = memo.emplace(fn, off).first;
+                }
+                x = it->second;
+                y = static_cast<uint32_t>(fn.size() / 2);
+            }
+        }
+        if (x == px && y == py) continue;    // merge with the previous interval
+        px = x;
+        py = y;
+        if (family == 0) {
+            out->bounds4.push_back(static_cast<uint32_t>(pts[j]));
+        } else {
+            out->bounds6.push_back(static_cast<uint64_t>(pts[j] >> 64));
+            out->bounds6.push_back(static_cast<uint64_t>(pts[j]));
+        }
+        out->desc.push_back(x);
+        out->desc.push_back(y);
+    }
+    out->nb = static_cast<int32_t>(out->desc.size() / 2);
+}
+
+}  // namespace
+
+int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_udp,
+              int default_allow, AclBuilt* out) {
+    if (n_tcp < 0 || n_udp < 0) return VC_EINVAL;
+    for (int i = 0; i < n_tcp; ++i)
+        if (!standard_net(tcp[i].net)) return VC_EINVAL;
+    for (int i = 0; i < n_udp; ++i)
+        if (!standard_net(udp[i].net)) return VC_EINVAL;
+    *out = AclBuilt{};
+    out->n_tcp = n_tcp;
+    out->n_udp = n_udp;
+    out->default_allow = default_allow ? 1 : 0;
+    for (int i = 0; i < n_tcp; ++i) out->allow.push_back(tcp[i].allow ? 1 : 0);
+    for (int i = 0; i < n_udp; ++i) out->allow.push_back(udp[i].allow ? 1 : 0);
+    if (out->allow.empty()) out->allow.push_back(0);
+    // four independent images: build them concurrently
+    std::thread th[4];
+    for (int l = 0; l < 2; ++l)
+        for (int f = 0; f < 2; ++f)
+            th[l * 2 + f] = std::thread(build_acl_family, l == 0 ? tcp : udp, l == 0 ? n_tcp : n_udp,
+                                        f, &out->fam[l][f]);
+    for (auto& t : th) t.join();
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Route trie
+// ---------------------------------------------------------------------------
+int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
+    *out = TrieBuilt{};
+    out->key_bits = family == 0 ? 32 : 128;
+    out->n_rules = n;
+    out->root_bits = n > 4096 ? 24 : 16;
+    const int rb = out->root_bits;
+    struct P {
+        u128 key;   // left-aligned in 128 bits
+        int len;
+        uint32_t idx;
+    };
+    std::vector<P> ps;
+    ps.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        const vc_net& r = rules[i];
+        if (!standard_net(r)) return VC_EINVAL;
+        if ((family == 0) != (r.ip_len == 4)) return VC_EINVAL;
+        int len = mask_int(r.mask, r.mask_len);
+        u128 k = key128(r.ip, r.ip_len);
+        if (family == 0) k <<= 96;
+        ps.push_back({k, len, static_cast<uint32_t>(i)});
+    }
+    std::stable_sort(ps.begin(), ps.end(), [](const P& a, const P& b) { return a.len < b.len; });
+    const size_t root = size_t(1) << rb;
+    out->nodes.assign(root, VC_NONE);
+    size_t split = 0;
+    while (split < ps.size() && ps[split].len <= rb) ++split;
+    // 1) prefixes no longer than the root stride: paint root ranges with min,
+    //    the root split into slices painted concurrently.
+    {
+        unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (split < 64) T = 1;
+        std::vector<std::thread> th;
+        uint32_t* nodes = out->nodes.data();
+        for (unsigned t = 0; t < T; ++t) {
+            size_t s0 = root * t / T, s1 = root * (t + 1) / T;
+            th.emplace_back([&, s0, s1]() {
+                for (size_t i = 0; i < split; ++i) {
+                    size_t a = static_cast<size_t>(ps[i].key >> (128 - rb));
+                    size_t b = a + (size_t(1) << (rb - ps[i].len));
+                    a = std::max(a, s0);
+                    b = std::min(b, s1);
+                    const uint32_t v = ps[i].idx;
+                    for (size_t e = a; e < b; ++e)
+                        if (v < nodes[e]) nodes[e] = v;
+                }
+            });
+        }
+        for (auto& t : th) t.join();
+    }
+    // 2) longer prefixes in ascending length: walk/create 8-bit nodes; a new
+    //    node inherits its parent entry's value (leaf pushing).
+    uint32_t n_children = 0;
+    for (size_t i = split; i < ps.size(); ++i) {
+        const P& p = ps[i];
+        size_t entry = static_cast<size_t>(p.key >> (128 - rb));
+        int bits = rb;
+        for (;;) {
+            uint32_t v = out->nodes[entry];
+            uint32_t child;
+            if (v & VC_PTR) {
+                child = v & ~VC_PTR;
+            } else {
+                child = n_children++;
+                if (child >= VC_PTR) return VC_ENOMEM;
+                out->nodes.resize(out->nodes.size() + 256, v);
+                out->nodes[entry] = VC_PTR | child;
+            }
+            size_t base = root + size_t(child) * 256;
+            int nb = bits + 8;
+            uint32_t sub = static_cast<uint32_t>(p.key >> (128 - nb)) & 255u;
+            if (p.len <= nb) {
+                uint32_t cnt = 1u << (nb - p.len);
+                for (uint32_t e = sub; e < sub + cnt; ++e)
+                    if (p.idx < out->nodes[base + e]) out->nodes[base + e] = p.idx;
+                break;
+            }
+            entry = base + sub;
+            bits = nb;
+        }
+    }
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Upstream hints
+// ---------------------------------------------------------------------------
+namespace {
+
+uint32_t pow2_cap(size_t n) {
+    uint32_t c = 16;
+    while (c < n * 2) c <<= 1;
+    return c;
+}
+
+uint32_t append_blob(std::vector<uint8_t>* blob, const char* s, int len) {
+    uint32_t off = static_cast<uint32_t>(blob->size());
+    blob->insert(blob->end(), s, s + len);
+    return off;
+}
+
+// insert into an open-addressing table; returns the slot index
+uint32_t table_insert(std::vector<KeySlotH>* t, uint64_t h, const KeySlotH& v) {
+    uint32_t mask = static_cast<uint32_t>(t->size() - 1);
+    uint32_t s = static_cast<uint32_t>(h) & mask;
+    while ((*t)[s].key_len != -1) s = (s + 1) & mask;
+    (*t)[s] = v;
+    return s;
+}
+
+}  // namespace
+
+int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
+    *out = HintBuilt{};
+    out->n_groups = n;
+    struct KeyAcc {
+        std::vector<uint32_t> members;
+        std::map<int32_t, int32_t> port_min;   // distinct nonzero hint-port -> min index
+        int32_t a = -1, b = -1;
+    };
+    std::map<std::string, KeyAcc> hostk, urik;
+    std::vector<std::string> host_order, uri_order;
+    out->groups.reserve(size_t(n) * 6);
+    for (int g = 0; g < n; ++g) {
+        // Hint.matchLevel merge (Hint.java:108-118): first non-null host,
+        // first non-zero port, first non-null uri over [handle, group].
+        const vc_annos* as[2] = {&groups[g].handle, &groups[g].group};
+        const char* H = nullptr; int Hn = 0; int P = 0; const char* U = nullptr; int Un = 0;
+        for (const vc_annos* a : as) {
+            if (!H && a->host) { H = a->host; Hn = a->host_len; }
+            if (P == 0) P = a->port;
+            if (!U && a->uri) { U = a->uri; Un = a->uri_len; }
+        }
+        if ((H && Hn < 0) || (U && Un < 0)) return VC_EINVAL;
+        int32_t rec[6] = {-1, 0, -1, 0, P, (H || P != 0 || U) ? 1 : 0};
+        if (H) { rec[0] = Hn; rec[1] = static_cast<int32_t>(append_blob(&out->blob, H, Hn)); }
+        if (U) { rec[2] = Un; rec[3] = static_cast<int32_t>(append_blob(&out->blob, U, Un)); }
+        out->groups.insert(out->groups.end(), rec, rec + 6);
+        if (H) {
+            std::string k(H, Hn);
+            auto it = hostk.find(k);
+            if (it == hostk.end()) {
+                host_order.push_back(k);
+                it = hostk.emplace(k, KeyAcc{}).first;
+            }
+            KeyAcc& acc = it->second;
+            acc.members.push_back(static_cast<uint32_t>(g));
+            if (acc.a < 0) acc.a = g;
+            if (P == 0 && acc.b < 0) acc.b = g;
+            if (P != 0 && !acc.port_min.count(P)) acc.port_min[P] = g;
+        }
+        if (U) {
+            out->has_uri_keys = 1;
+            std::string k(U, Un);
+            auto it = urik.find(k);
+            if (it == urik.end()) {
+                uri_order.push_back(k);
+                it = urik.emplace(k, KeyAcc{}).first;
+            }
+            it->second.members.push_back(static_cast<uint32_t>(g));
+        }
+    }
+    KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
+    out->host_slots.assign(pow2_cap(host_order.size()), empty);
+    out->uri_slots.assign(pow2_cap(uri_order.size()), empty);
+    out->port_min_off.assign(out->host_slots.size() * 2, 0);
+    for (auto& k : host_order) {
+        KeyAcc& acc = hostk[k];
+        KeySlotH s{};
+        s.hash = fnv_rev(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        s.key_len = static_cast<int32_t>(k.size());
+        s.key_off = append_blob(&out->blob, k.data(), static_cast<int>(k.size()));
+        s.a = acc.a;
+        s.b = acc.b < 0 ? static_cast<int32_t>(VC_NONE) : acc.b;
+        s.list_off = static_cast<uint32_t>(out->lists.size());
+        s.list_cnt = static_cast<uint32_t>(acc.members.size());
+        out->lists.insert(out->lists.end(), acc.members.begin(), acc.members.end());
+        uint32_t slot = table_insert(&out->host_slots, s.hash, s);
+        out->port_min_off[2 * slot] = static_cast<uint32_t>(out->port_mins.size() / 2);
+        out->port_min_off[2 * slot + 1] = static_cast<uint32_t>(acc.port_min.size());
+        for (auto& pm : acc.port_min) {
+            out->port_mins.push_back(pm.first);
+            out->port_mins.push_back(pm.second);
+        }
+        if (k == "*") out->wildcard_slot = static_cast<int32_t>(slot);
+    }
+    for (auto& k : uri_order) {
+        KeyAcc& acc = urik[k];
+        KeySlotH s{};
+        s.hash = fnv_fwd(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        s.key_len = static_cast<int32_t>(k.size());
+        s.key_off = append_blob(&out->blob, k.data(), static_cast<int>(k.size()));
+        s.a = acc.members.empty() ? -1 : static_cast<int32_t>(acc.members[0]);
+        s.b = -1;
+        s.list_off = static_cast<uint32_t>(out->lists.size());
+        s.list_cnt = static_cast<uint32_t>(acc.members.size());
+        out->lists.insert(out->lists.end(), acc.members.begin(), acc.members.end());
+        uint32_t slot = table_insert(&out->uri_slots, s.hash, s);
+        if (k == "*") out->uri_star_slot = static_cast<int32_t>(slot);
+    }
+    if (out->blob.empty()) out->blob.push_back(0);
+    if (out->lists.empty()) out->lists.push_back(0);
+    if (out->port_mins.empty()) { out->port_mins.push_back(0); out->port_mins.push_back(0); }
+    if (out->groups.empty()) out->groups.assign(6, 0);
+    return VC_OK;
+}
+
+int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
+                HostsBuilt* out) {
+    *out = HostsBuilt{};
+    KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
+    out->slots.assign(pow2_cap(static_cast<size_t>(n)), empty);
+    std::unordered_map<std::string, int> seen;
+    for (int i = 0; i < n; ++i) {
+        if (key_lens[i] < 0 || (!keys[i] && key_lens[i] > 0)) return VC_EINVAL;
+        std::string k(keys[i] ? keys[i] : "", key_lens[i]);
+        if (seen.count(k)) continue;     // first key wins
+        seen.emplace(k, i);
+        KeySlotH s{};
+        s.hash = fnv_fwd(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+        s.key_len = key_lens[i];
+        s.key_off = append_blob(&out->blob, k.data(), key_lens[i]);
+        s.a = values[i];
+        s.b = 0;
+        s.list_off = 0;
+        s.list_cnt = 0;
+        table_insert(&out->slots, s.hash, s);
+        ++out->n;
+    }
+    if (out->blob.empty()) out->blob.push_back(0);
+    return VC_OK;
+}
+
+}  // namespace vc

@@ -1,0 +1,83 @@
+// compile.hpp -- host-side table compilers: reference rule lists -> the flat
+// images of common/images.h (still in host memory; capi.cpp uploads them).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "vclassify.h"
+
+namespace vc {
+
+struct AclFamilyBuilt {
+    std::vector<uint32_t> bounds4;
+    std::vector<uint64_t> bounds6;   // (hi, lo) pairs
+    std::vector<uint32_t> desc;      // (x, y) pairs
+    std::vector<uint32_t> pieces;    // (port_start, value) pairs
+    int32_t nb = 0;
+};
+
+struct AclBuilt {
+    AclFamilyBuilt fam[2][2];        // [tcp/udp][v4/v6]
+    std::vector<uint8_t> allow;
+    int32_t n_tcp = 0, n_udp = 0, default_allow = 0;
+};
+
+// SecurityGroup lists -> ACL image.  Returns VC_OK or VC_EINVAL (bad rule).
+int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_udp,
+              int default_allow, AclBuilt* out);
+
+struct TrieBuilt {
+    std::vector<uint32_t> nodes;
+    int32_t root_bits = 16;
+    int32_t key_bits = 32;
+    int32_t n_rules = 0;
+};
+
+// One RouteTable family list (list order = priority) -> stride trie.
+int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out);
+
+struct KeySlotH {                    // host mirror of KeySlot
+    uint64_t hash;
+    int32_t key_len;
+    uint32_t key_off;
+    int32_t a, b;
+    uint32_t list_off, list_cnt;
+};
+
+struct HintBuilt {
+    std::vector<uint8_t> blob;
+    std::vector<KeySlotH> host_slots, uri_slots;
+    std::vector<uint32_t> lists;
+    std::vector<int32_t> port_mins;      // (port, idx) pairs
+    std::vector<uint32_t> port_min_off;  // (off, cnt) per host slot
+    std::vector<int32_t> groups;         // 6 words per GroupRec
+    int32_t n_groups = 0;
+    int32_t wildcard_slot = -1, uri_star_slot = -1, has_uri_keys = 0;
+};
+
+int build_hints(const vc_group_annos* groups, int n, HintBuilt* out);
+
+struct HostsBuilt {
+    std::vector<uint8_t> blob;
+    std::vector<KeySlotH> slots;
+    int32_t n = 0;
+};
+
+int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
+                HostsBuilt* out);
+
+// FNV-1a 64 over bytes, forwards and right-to-left (must match device code).
+inline uint64_t fnv_fwd(const uint8_t* p, size_t n) {
+    uint64_t h = 14695981039346656037ull;
+    for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+    return h;
+}
+inline uint64_t fnv_rev(const uint8_t* p, size_t n) {
+    uint64_t h = 14695981039346656037ull;
+    for (size_t i = n; i-- > 0;) { h ^= p[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+}  // namespace vc

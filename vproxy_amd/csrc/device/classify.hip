@@ -1,0 +1,361 @@
+// classify.hip -- ACL, route and combined-pipeline kernels for gfx950.
+//
+// One lane per header.  Inputs are SoA arrays streamed from HBM with 4
+// items per lane per step (16-byte address loads, 4-byte proto loads, 8-byte
+// port loads, 16-byte index stores); the ACL interval boundaries are staged
+// in LDS once per workgroup of a grid-stride (persistent-style) launch.
+#include "acl_dev.h"
+#include "launch.h"
+#include "route_dev.h"
+
+namespace vcd {
+
+constexpr int kBlock = 512;
+
+// ---------------------------------------------------------------------------
+// ACL (SecurityGroup.allow) on IPv4 sources
+// ---------------------------------------------------------------------------
+struct AclV4Ctx {
+    const uint32_t* b[2];
+    const uint32_t* desc[2];
+    const uint32_t* pieces[2];
+    int nb[2];
+};
+
+__device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint32_t key,
+                                               uint32_t port) {
+    const int l = tcp ? 0 : 1;
+    const int j = bsearch_u32(a.b[l], a.nb[l], key);
+    const uint2 d = load_desc(a.desc[l], j);
+    return port_lookup(a.pieces[l], d, port);
+}
+
+__device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t v,
+                                         uint8_t* allow_out, int32_t* idx_out,
+                                         unsigned long long* cnt) {
+    *idx_out = out_index(v);
+    if (allow_out) {
+        *allow_out = v == VC_NONE ? uint8_t(img.default_allow)
+                                  : img.allow[(tcp ? 0 : img.n_tcp) + v];
+    }
+    if (cnt) {
+        int64_t at = v == VC_NONE ? int64_t(img.n_tcp) + img.n_udp + (tcp ? 0 : 1)
+                                  : (tcp ? int64_t(v) : int64_t(img.n_tcp) + v);
+        atomicAdd(cnt + at, 1ull);
+    }
+}
+
+__device__ __forceinline__ AclV4Ctx acl_v4_ctx(const AclImage& img, const uint32_t* lds) {
+    AclV4Ctx a;
+    a.nb[0] = img.fam[0][0].nb;
+    a.nb[1] = img.fam[1][0].nb;
+    a.b[0] = lds ? lds : img.fam[0][0].bounds4;
+    a.b[1] = lds ? lds + a.nb[0] : img.fam[1][0].bounds4;
+    a.desc[0] = img.fam[0][0].desc;
+    a.desc[1] = img.fam[1][0].desc;
+    a.pieces[0] = img.fam[0][0].pieces;
+    a.pieces[1] = img.fam[1][0].pieces;
+    return a;
+}
+
+__device__ __forceinline__ void stage_bounds(const AclImage& img, uint32_t* lds) {
+    const int nb0 = img.fam[0][0].nb, nb1 = img.fam[1][0].nb;
+    const uint32_t* b0 = img.fam[0][0].bounds4;
+    const uint32_t* b1 = img.fam[1][0].bounds4;
+    for (int k = threadIdx.x; k < nb0; k += blockDim.x) lds[k] = b0[k];
+    for (int k = threadIdx.x; k < nb1; k += blockDim.x) lds[nb0 + k] = b1[k];
+    __syncthreads();
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void acl_v4_kernel(
+    AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
+    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
+    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (kLds) stage_bounds(img, lds);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    const int64_t n4 = n >> 2;
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
+        const uint4 s = reinterpret_cast<const uint4*>(src)[g];
+        const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
+        const uint2 pt = reinterpret_cast<const uint2*>(port)[g];
+        const uint32_t key[4] = {s.x, s.y, s.z, s.w};
+        const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
+        uint32_t v[4];
+        bool tcp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+            v[k] = acl_v4_one(a, tcp[k], key[k], po[k]);
+        }
+        int4 o;
+        uint32_t al = 0;
+        int32_t* op = reinterpret_cast<int32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint8_t b = 0;
+            acl_emit(img, tcp[k], v[k], allow ? &b : nullptr, op + k, cnt);
+            al |= uint32_t(b) << (8 * k);
+        }
+        reinterpret_cast<int4*>(out)[g] = o;
+        if (allow) reinterpret_cast<uint32_t*>(allow)[g] = al;
+    }
+    // tail (n % 4 items), handled by the first threads of block 0
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const int64_t i = (n4 << 2) + threadIdx.x;
+        const bool t = proto[i] == VC_PROTO_TCP;
+        const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+    }
+}
+
+// Unaligned-pointer variant: one item per lane.
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
+    AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
+    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
+    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (kLds) stage_bounds(img, lds);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const bool t = proto[i] == VC_PROTO_TCP;
+        const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ACL on IPv6 sources (128-bit interval search in global memory)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void acl_v6_kernel(
+    AclImage img, const uint8_t* __restrict__ proto, const uint8_t* __restrict__ src6,
+    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
+    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const bool t = proto[i] == VC_PROTO_TCP;
+        const AclFamilyImage& f = t ? img.fam[0][1] : img.fam[1][1];
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(src6)[i], &hi, &lo);
+        const int j = bsearch_u128(f.bounds6, f.nb, hi, lo);
+        const uint32_t v = port_lookup(f.pieces, load_desc(f.desc, j), port[i]);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// RouteTable.lookup
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void route_emit(uint32_t e, int32_t* o, unsigned long long* cnt,
+                                           int64_t rule_base, int64_t none_at) {
+    *o = out_index(e);
+    if (cnt) atomicAdd(cnt + (e == VC_NONE ? none_at : rule_base + e), 1ull);
+}
+
+__global__ __launch_bounds__(kBlock) void route_v4_kernel(
+    const uint32_t* __restrict__ nodes, int rb, const uint32_t* __restrict__ dst, int64_t n,
+    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
+    int64_t none_at) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    const int64_t n4 = n >> 2;
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
+        const uint4 d = reinterpret_cast<const uint4*>(dst)[g];
+        const uint32_t key[4] = {d.x, d.y, d.z, d.w};
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = nodes[key[k] >> (32 - rb)];   // 4 probes in flight
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int shift = 32 - rb;
+            while (e[k] & VC_PTR) {
+                shift -= 8;
+                e[k] = nodes[(1u << rb) + (e[k] & ~VC_PTR) * 256u + ((key[k] >> shift) & 255u)];
+            }
+        }
+        int4 o;
+        int32_t* op = reinterpret_cast<int32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) route_emit(e[k], op + k, cnt, rule_base, none_at);
+        reinterpret_cast<int4*>(out)[g] = o;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const int64_t i = (n4 << 2) + threadIdx.x;
+        route_emit(trie_v4(nodes, rb, dst[i]), out + i, cnt, rule_base, none_at);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void route_v4_kernel_scalar(
+    const uint32_t* __restrict__ nodes, int rb, const uint32_t* __restrict__ dst, int64_t n,
+    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
+    int64_t none_at) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        route_emit(trie_v4(nodes, rb, dst[i]), out + i, cnt, rule_base, none_at);
+}
+
+__global__ __launch_bounds__(kBlock) void route_v6_kernel(
+    const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
+    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
+    int64_t none_at) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(dst6)[i], &hi, &lo);
+        route_emit(trie_v6(nodes, rb, hi, lo), out + i, cnt, rule_base, none_at);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Combined pipeline (C5): ACL(src, dport) -> route(dst) -> pool group gather
+// ---------------------------------------------------------------------------
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
+    AclImage img, const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ proto,
+    const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+    const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
+    const int32_t* __restrict__ pool_group, int64_t n, int32_t* __restrict__ out_acl,
+    int32_t* __restrict__ out_route, int32_t* __restrict__ out_group,
+    uint8_t* __restrict__ out_allow, unsigned long long* __restrict__ acl_cnt,
+    unsigned long long* __restrict__ route_cnt, int64_t route_none_at,
+    unsigned long long* __restrict__ group_cnt, int32_t n_groups) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (kLds) stage_bounds(img, lds);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        // issue the independent global probes first (route root, pool gather)
+        const uint32_t d = dst[i];
+        uint32_t e = nodes[d >> (32 - rb)];
+        const uint32_t h = host_id[i];
+        const int32_t grp = h == 0xFFFFFFFFu ? -1 : pool_group[h];
+        const bool t = proto[i] == VC_PROTO_TCP;
+        const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
+        acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i, acl_cnt);
+        int shift = 32 - rb;
+        while (e & VC_PTR) {
+            shift -= 8;
+            e = nodes[(1u << rb) + (e & ~VC_PTR) * 256u + ((d >> shift) & 255u)];
+        }
+        route_emit(e, out_route + i, route_cnt, 0, route_none_at);
+        out_group[i] = grp;
+        if (group_cnt) atomicAdd(group_cnt + (grp < 0 ? n_groups : grp), 1ull);
+    }
+}
+
+}  // namespace vcd
+
+namespace vc {
+
+namespace {
+
+// LDS budget for the staged v4 ACL boundaries (words); above it the kernel
+// searches the boundaries in global memory (L2-resident).
+constexpr int kLdsWords = 30 * 1024;
+
+int grid_for(const LaunchCfg& c, int64_t work_items, int blocks_per_cu) {
+    int64_t want = (work_items + vcd::kBlock - 1) / vcd::kBlock;
+    int64_t cap = int64_t(c.num_cus) * blocks_per_cu;
+    if (want < 1) want = 1;
+    return int(want < cap ? want : cap);
+}
+
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+}  // namespace
+
+hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
+                         const uint32_t* src4, const uint16_t* port, int64_t n, int32_t* out,
+                         uint8_t* allow, unsigned long long* counters) {
+    if (n <= 0) return hipSuccess;
+    const int words = img.fam[0][0].nb + img.fam[1][0].nb;
+    const bool lds = words <= kLdsWords;
+    const size_t shmem = lds ? size_t(words) * 4 : 0;
+    const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(port, 8) &&
+                     aligned(out, 16) && (!allow || aligned(allow, 4));
+    const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
+    if (vec) {
+        const int grid = grid_for(c, (n + 3) / 4, per_cu);
+        if (lds)
+            hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
+                               c.stream, img, proto, src4, port, n, out, allow, counters);
+        else
+            hipLaunchKernelGGL(vcd::acl_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
+                               c.stream, img, proto, src4, port, n, out, allow, counters);
+    } else {
+        const int grid = grid_for(c, n, per_cu);
+        if (lds)
+            hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
+                               shmem, c.stream, img, proto, src4, port, n, out, allow, counters);
+        else
+            hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<false>, dim3(grid), dim3(vcd::kBlock), 0,
+                               c.stream, img, proto, src4, port, n, out, allow, counters);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_acl_v6(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
+                         const uint8_t* src6, const uint16_t* port, int64_t n, int32_t* out,
+                         uint8_t* allow, unsigned long long* counters) {
+    if (n <= 0) return hipSuccess;
+    if (!aligned(src6, 16)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vcd::acl_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
+                       c.stream, img, proto, src6, port, n, out, allow, counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_v4(const LaunchCfg& c, const TrieImage& t, const uint32_t* dst4, int64_t n,
+                           int32_t* out, unsigned long long* counters, int64_t rule_base,
+                           int64_t none_at) {
+    if (n <= 0) return hipSuccess;
+    if (aligned(dst4, 16) && aligned(out, 16))
+        hipLaunchKernelGGL(vcd::route_v4_kernel, dim3(grid_for(c, (n + 3) / 4, 8)),
+                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.root_bits, dst4, n, out,
+                           counters, rule_base, none_at);
+    else
+        hipLaunchKernelGGL(vcd::route_v4_kernel_scalar, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock),
+                           0, c.stream, t.nodes, t.root_bits, dst4, n, out, counters, rule_base,
+                           none_at);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t* dst6, int64_t n,
+                           int32_t* out, unsigned long long* counters, int64_t rule_base,
+                           int64_t none_at) {
+    if (n <= 0) return hipSuccess;
+    if (!aligned(dst6, 16)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vcd::route_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
+                       c.stream, t.nodes, t.root_bits, dst6, n, out, counters, rule_base, none_at);
+    return hipGetLastError();
+}
+
+hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
+                              const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
+                              const uint16_t* dport, const uint32_t* host_id,
+                              const int32_t* pool_group, int64_t n, int32_t* out_acl,
+                              int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
+                              unsigned long long* acl_cnt, unsigned long long* route_cnt,
+                              int64_t route_none_at, unsigned long long* group_cnt,
+                              int32_t n_groups) {
+    if (n <= 0) return hipSuccess;
+    const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
+    const bool lds = words <= kLdsWords;
+    const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
+    const int grid = grid_for(c, n, per_cu);
+    if (lds)
+        hipLaunchKernelGGL(vcd::pipeline_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock),
+                           size_t(words) * 4, c.stream, acl, r4.nodes, r4.root_bits, proto, src4,
+                           dst4, dport, host_id, pool_group, n, out_acl, out_route, out_group,
+                           out_allow, acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
+    else
+        hipLaunchKernelGGL(vcd::pipeline_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
+                           c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,
+                           host_id, pool_group, n, out_acl, out_route, out_group, out_allow,
+                           acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
+    return hipGetLastError();
+}
+
+}  // namespace vc

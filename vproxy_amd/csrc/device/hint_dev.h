@@ -1,0 +1,323 @@
+// hint_dev.h -- device side of Upstream.searchForGroup(Hint) and DNS
+// classification.  See hint.hip for the kernels.
+//
+//   Hint.formatHost / formatUri      base/.../processor/Hint.java:57-90
+//   Hint.matchLevel                  Hint.java:100-160
+//   Upstream.searchForGroup          core/.../svrgroup/Upstream.java:187-198
+//   IP.isIpv6 / isIpLiteral          base/src/main/java/vfd/IP.java:158-300
+//   DNSServer.handleRequest (class.) core/src/main/java/vproxy/dns/DNSServer.java:116-166
+//
+// One lane per hint.  The linear argmax over all groups becomes a handful of
+// hash probes: the query host is scanned right-to-left once, producing the
+// reversed-FNV hash of every dot-suffix ("." + annoHost candidates) and of
+// the whole host; each probe is confirmed by a byte compare.
+#pragma once
+
+#include "dev_common.h"
+
+#define VC_HDN __host__ __device__
+
+namespace vcd {
+
+
+struct DStr {
+    const uint8_t* p;
+    int n;        // -1 == Java null
+};
+
+VC_HD bool bytes_eq(const uint8_t* a, const uint8_t* b, int n) {
+    for (int i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// IP literal validity (IP.java).  Only validity is needed on the device.
+// ---------------------------------------------------------------------------
+
+// IP.parseIpv4String(s, bytes, from) with bytes.length == cap: 4 or -1
+VC_HDN int d_v4(const uint8_t* s, int n, int from, int cap) {
+    int pieces = 0, start = 0;
+    for (int i = 0; i <= n; ++i) {
+        if (i < n && s[i] != '.') continue;
+        int len = i - start;
+        if (pieces >= 4) return -1;                      // split length != 4
+        if (from + pieces >= cap) return -1;
+        if (len > 3 || len == 0) return -1;
+        int num = 0;
+        for (int k = start; k < i; ++k) {
+            uint8_t c = s[k];
+            if (c < '0' || c > '9') return -1;
+            num = num * 10 + (c - '0');
+        }
+        if (s[start] == '0' && len > 1) return -1;
+        if (num > 255) return -1;
+        ++pieces;
+        start = i + 1;
+    }
+    return pieces == 4 ? 4 : -1;
+}
+
+VC_HD bool d_hex(uint8_t c) {
+    return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+}
+
+// IP.parseIpv6ColonPart for a present (non-null) string
+VC_HDN int d_colon_part(const uint8_t* s, int n, int from) {
+    if (n == 0) return 0;
+    if (from < 0) return -1;
+    int fields = 0, start = 0;
+    for (int i = 0; i <= n; ++i) {
+        if (i < n && s[i] != ':') continue;
+        int len = i - start;
+        if (from + 2 * fields >= 16) return -1;
+        if (len > 4 || len == 0) return -1;
+        for (int k = start; k < i; ++k)
+            if (!d_hex(s[k])) return -1;
+        ++fields;
+        start = i + 1;
+    }
+    return fields * 2;
+}
+
+VC_HD int d_count(const uint8_t* s, int n, uint8_t c) {
+    int k = 0;
+    for (int i = 0; i < n; ++i) k += s[i] == c;
+    return k;
+}
+
+// IP.parseIpv6LastBits, including the `4 + colonPart` sum (IP.java:264)
+VC_HDN int d_last_bits(const uint8_t* s, int n) {
+    int dot = -1;
+    for (int i = 0; i < n; ++i)
+        if (s[i] == '.') { dot = i; break; }
+    if (dot >= 0) {
+        int colon = -1;
+        for (int i = dot - 1; i >= 0; --i)
+            if (s[i] == ':') { colon = i; break; }
+        if (colon < 0) return d_v4(s, n, 12, 16);
+        if (d_v4(s + colon + 1, n - colon - 1, 12, 16) == -1) return -1;
+        int pieces = 1 + d_count(s, colon, ':');
+        return 4 + d_colon_part(s, colon, 16 - 4 - pieces * 2);
+    }
+    int pieces = 1 + d_count(s, n, ':');
+    return d_colon_part(s, n, 16 - pieces * 2);
+}
+
+// IP.isIpv6 == parseIpv6String(s) != null (IP.java:158-197)
+VC_HDN bool d_is_ipv6(const uint8_t* s, int n) {
+    if (n >= 2 && s[0] == '[' && s[n - 1] == ']') {
+        s += 1;
+        n -= 2;
+    }
+    int dbl = 0, first = -1;
+    for (int i = 0; i + 1 < n;) {
+        if (s[i] == ':' && s[i + 1] == ':') {
+            if (first < 0) first = i;
+            ++dbl;
+            i += 2;
+        } else {
+            ++i;
+        }
+    }
+    if (dbl > 1) return false;
+    int c1 = first >= 0 ? d_colon_part(s, first, 0) : 0;
+    if (c1 == -1) return false;
+    int c2 = first >= 0 ? d_last_bits(s + first + 2, n - first - 2) : d_last_bits(s, n);
+    if (c2 == -1) return false;
+    return first >= 0 ? (c1 + c2 < 16) : (c1 + c2 == 16);
+}
+
+VC_HD bool d_is_ip_literal(const uint8_t* s, int n) {
+    return d_is_ipv6(s, n) || d_v4(s, n, 0, 4) == 4;
+}
+
+// ---------------------------------------------------------------------------
+// Hint.formatHost / formatUri
+// ---------------------------------------------------------------------------
+VC_HDN DStr format_host(DStr s) {
+    if (s.n < 0) return s;
+    int colon = -1;
+    for (int i = 0; i < s.n; ++i)
+        if (s.p[i] == ':') { colon = i; break; }
+    if (colon < 0 || d_is_ipv6(s.p, s.n)) return s;
+    DStr r{s.p, colon};
+    if (r.n >= 4 && r.p[0] == 'w' && r.p[1] == 'w' && r.p[2] == 'w' && r.p[3] == '.') {
+        r.p += 4;
+        r.n -= 4;
+    }
+    if (r.n == 0) r.n = -1;
+    return r;
+}
+
+VC_HDN DStr format_uri(DStr s) {
+    if (s.n < 0) return s;
+    for (int i = 0; i < s.n; ++i)
+        if (s.p[i] == '?') { s.n = i; break; }
+    if (s.n == 1 && s.p[0] == '/') return s;
+    if (s.n > 0 && s.p[s.n - 1] == '/') s.n -= 1;
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// key tables
+// ---------------------------------------------------------------------------
+VC_HD KeySlot load_slot(const KeySlot* t, uint32_t s) {
+    const uint4* p = reinterpret_cast<const uint4*>(t + s);
+    uint4 a = p[0], b = p[1];
+    KeySlot k;
+    k.hash = (uint64_t(a.y) << 32) | a.x;
+    k.key_len = int32_t(a.z);
+    k.key_off = a.w;
+    k.a = int32_t(b.x);
+    k.b = int32_t(b.y);
+    k.list_off = b.z;
+    k.list_cnt = b.w;
+    return k;
+}
+
+// slot index of key (p, n) with hash h, or -1
+VC_HDN int probe(const KeySlot* t, uint32_t mask, const uint8_t* blob, uint64_t h,
+                     const uint8_t* p, int n, KeySlot* out) {
+    uint32_t s = uint32_t(h) & mask;
+    for (;;) {
+        KeySlot k = load_slot(t, s);
+        if (k.key_len < 0) return -1;
+        if (k.hash == h && k.key_len == n && bytes_eq(blob + k.key_off, p, n)) {
+            *out = k;
+            return int(s);
+        }
+        s = (s + 1) & mask;
+    }
+}
+
+// min handle index of a host key not excluded by the port filter
+// (Hint.java:124-128): port == 0 -> any; else hint-port 0 or equal.
+VC_HD uint32_t pick(const HintImage& img, int slot, const KeySlot& k, int port) {
+    if (port == 0) return uint32_t(k.a);
+    uint32_t v = uint32_t(k.b);
+    const uint32_t off = img.port_min_off[2 * slot], cnt = img.port_min_off[2 * slot + 1];
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const PortMin pm = img.port_mins[off + i];
+        if (pm.port == port) v = uint32_t(pm.idx) < v ? uint32_t(pm.idx) : v;
+    }
+    return v;
+}
+
+// searchForGroup for hints whose uri is null (or no group has a hint-uri):
+// level = hostLevel << 10, so exact (3) beats any suffix (2) beats "*" (1),
+// and within a level the lowest handle index wins (strict '>' scan).
+VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
+    if (host.n < 0) return -1;
+    uint64_t h = kFnvBasis;
+    uint32_t best_suffix = VC_NONE;
+    KeySlot k;
+    for (int j = host.n - 1; j >= 0; --j) {
+        const uint8_t c = host.p[j];
+        if (c == '.') {   // host.endsWith("." + H) with H = host[j+1..]
+            int s = probe(img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
+                          host.n - j - 1, &k);
+            if (s >= 0) { uint32_t c = pick(img, s, k, port); best_suffix = c < best_suffix ? c : best_suffix; }
+        }
+        h = fnv_step(h, c);
+    }
+    int s = probe(img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k);
+    if (s >= 0) {
+        uint32_t e = pick(img, s, k, port);
+        if (e != VC_NONE) return int32_t(e);
+    }
+    if (best_suffix != VC_NONE) return int32_t(best_suffix);
+    if (img.wildcard_slot >= 0) {
+        KeySlot w = load_slot(img.host_slots, uint32_t(img.wildcard_slot));
+        uint32_t v = pick(img, img.wildcard_slot, w, port);
+        if (v != VC_NONE) return int32_t(v);
+    }
+    return -1;
+}
+
+// Hint.matchLevel for one merged group (Hint.java:100-160)
+VC_HDN int match_level(const HintImage& img, uint32_t g, DStr host, int port, DStr uri) {
+    const int32_t* r = reinterpret_cast<const int32_t*>(img.groups) + 6 * g;
+    const int32_t Hn = r[0], Un = r[2], P = r[4];
+    if (!r[5]) return 0;
+    if (port != 0 && P != 0 && port != P) return 0;
+    const uint8_t* H = img.blob + uint32_t(r[1]);
+    const uint8_t* U = img.blob + uint32_t(r[3]);
+    int hl = 0;
+    if (Hn >= 0 && host.n >= 0) {
+        if (host.n == Hn && bytes_eq(host.p, H, Hn)) hl = 3;
+        else if (host.n >= Hn + 1 && host.p[host.n - Hn - 1] == '.' &&
+                 bytes_eq(host.p + host.n - Hn, H, Hn)) hl = 2;
+        else if (Hn == 1 && H[0] == '*') hl = 1;
+    }
+    int ul = 0;
+    if (Un >= 0 && uri.n >= 0) {
+        if (uri.n == Un && bytes_eq(uri.p, U, Un)) ul = uri.n + 1;
+        else if (uri.n >= Un && bytes_eq(uri.p, U, Un)) ul = Un + 1;
+        else if (Un == 1 && U[0] == '*') ul = 1;
+    }
+    if (ul > 1023) ul = 1023;
+    return (hl << 10) + ul;
+}
+
+struct Best {
+    int level = 0;
+    int32_t idx = -1;
+    VC_HDN void consider(int lvl, int32_t g) {
+        if (lvl > level || (lvl == level && lvl > 0 && g < idx)) {
+            level = lvl;
+            idx = g;
+        }
+    }
+};
+
+VC_HDN void consider_list(const HintImage& img, const KeySlot& k, DStr host, int port, DStr uri,
+                              Best* b) {
+    for (uint32_t i = 0; i < k.list_cnt; ++i) {
+        uint32_t g = img.lists[k.list_off + i];
+        b->consider(match_level(img, g, host, port, uri), int32_t(g));
+    }
+}
+
+// General searchForGroup: every group with a nonzero level has its hint-host
+// equal to / a dot-suffix of / "*" for the host, or its hint-uri a prefix
+// of / "*" for the uri; those candidate lists are scored exactly.
+VC_HDN int32_t hint_general(const HintImage& img, DStr host, int port, DStr uri) {
+    Best b;
+    KeySlot k;
+    if (host.n >= 0) {
+        uint64_t h = kFnvBasis;
+        for (int j = host.n - 1; j >= 0; --j) {
+            const uint8_t c = host.p[j];
+            if (c == '.' && probe(img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
+                                  host.n - j - 1, &k) >= 0)
+                consider_list(img, k, host, port, uri, &b);
+            h = fnv_step(h, c);
+        }
+        if (probe(img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k) >= 0)
+            consider_list(img, k, host, port, uri, &b);
+        if (img.wildcard_slot >= 0)
+            consider_list(img, load_slot(img.host_slots, uint32_t(img.wildcard_slot)), host, port,
+                          uri, &b);
+    }
+    if (uri.n >= 0) {
+        uint64_t h = kFnvBasis;
+        for (int j = 0; j <= uri.n; ++j) {
+            if (probe(img.uri_slots, img.uri_mask, img.blob, h, uri.p, j, &k) >= 0)
+                consider_list(img, k, host, port, uri, &b);
+            if (j < uri.n) h = fnv_step(h, uri.p[j]);
+        }
+        if (img.uri_star_slot >= 0)
+            consider_list(img, load_slot(img.uri_slots, uint32_t(img.uri_star_slot)), host, port,
+                          uri, &b);
+    }
+    return b.idx;
+}
+
+VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,
+                                                    DStr uri) {
+    if (uri.n < 0 || !img.has_uri_keys) return hint_host_only(img, host, port);
+    return hint_general(img, host, port, uri);
+}
+
+}  // namespace vcd

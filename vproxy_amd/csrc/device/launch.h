@@ -1,0 +1,45 @@
+// launch.h -- host-callable launchers for the classifier kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../common/images.h"
+
+namespace vc {
+
+struct LaunchCfg {
+    int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
+    hipStream_t stream = nullptr;
+};
+
+hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
+                         const uint32_t* src4, const uint16_t* port, int64_t n, int32_t* out,
+                         uint8_t* allow, unsigned long long* counters);
+hipError_t launch_acl_v6(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
+                         const uint8_t* src6, const uint16_t* port, int64_t n, int32_t* out,
+                         uint8_t* allow, unsigned long long* counters);
+// counters (optional): rule i -> counters[rule_base + i], null -> counters[none_at]
+hipError_t launch_route_v4(const LaunchCfg& c, const TrieImage& t, const uint32_t* dst4, int64_t n,
+                           int32_t* out, unsigned long long* counters, int64_t rule_base,
+                           int64_t none_at);
+hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t* dst6, int64_t n,
+                           int32_t* out, unsigned long long* counters, int64_t rule_base,
+                           int64_t none_at);
+hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* host_blob,
+                       const uint32_t* host_off, const uint8_t* host_null, const uint16_t* port,
+                       const uint8_t* uri_blob, const uint32_t* uri_off, const uint8_t* uri_null,
+                       int64_t n, int32_t* out, unsigned long long* counters);
+hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintImage& hints,
+                      const uint8_t* qblob, const uint32_t* qoff, int64_t n, uint8_t* kind,
+                      int32_t* value, unsigned long long* group_counters);
+hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
+                              const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
+                              const uint16_t* dport, const uint32_t* host_id,
+                              const int32_t* pool_group, int64_t n, int32_t* out_acl,
+                              int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
+                              unsigned long long* acl_cnt, unsigned long long* route_cnt,
+                              int64_t route_none_at, unsigned long long* group_cnt,
+                              int32_t n_groups);
+
+}  // namespace vc
