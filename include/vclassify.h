@@ -181,11 +181,12 @@ int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int
 /* ------------------------------------------------------------------------ */
 /* For each IPv4 packet: out_acl = SecurityGroup.allow index on (proto, src,
  * dport), out_route = RouteTable.lookup(dst) index, out_group =
- * pool_group[host_id] (the per-pass classified hostname pool from
- * vc_hint_search_dev; host_id == 0xFFFFFFFF -> -1).  out_allow optional. */
+ * pool_group[host_id] (the per-pass classified hostname pool of n_pool
+ * entries from vc_hint_search_dev; host_id >= n_pool, e.g. 0xFFFFFFFF for
+ * "no hostname", -> -1).  out_allow optional. */
 int vc_pipeline_v4_dev(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
                        const uint32_t *dst4, const uint16_t *dport, const uint32_t *host_id,
-                       const int32_t *pool_group, int64_t n, int32_t *out_acl,
+                       const int32_t *pool_group, int64_t n_pool, int64_t n, int32_t *out_acl,
                        int32_t *out_route, int32_t *out_group, uint8_t *out_allow, void *stream);
 
 /* ------------------------------------------------------------------------ */

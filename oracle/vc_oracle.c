@@ -784,6 +784,29 @@ int vo_search_for_group(const vo_group *g, int ng, const vo_hint *h)
     return last_max;
 }
 
+typedef struct {
+    const vo_group *g; int ng; const uint8_t *blob; const uint32_t *off; const uint16_t *port;
+    int32_t *out;
+} hint_batch_ctx;
+
+static void hint_range(void *p, int64_t lo, int64_t hi)
+{
+    hint_batch_ctx *c = (hint_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        const char *s = (const char *)c->blob + c->off[i];
+        int len = (int)(c->off[i + 1] - c->off[i]);
+        vo_hint h = vo_hint_of(s, len, c->port ? c->port[i] : 0, NULL, 0);
+        c->out[i] = vo_search_for_group(c->g, c->ng, &h);
+    }
+}
+
+void vo_hint_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off,
+                   const uint16_t *port, int64_t n, int32_t *out, int nthreads)
+{
+    hint_batch_ctx c = {g, ng, blob, off, port, out};
+    parallel_for(n, nthreads, hint_range, &c);
+}
+
 /* ------------------------------------------------------------------------ */
 /* DNSServer.handleRequest classification -- DNSServer.java:116-166         */
 /* ------------------------------------------------------------------------ */

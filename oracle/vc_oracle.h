@@ -123,6 +123,11 @@ vo_hint vo_hint_of(const char *host, int host_len, int port, const char *uri, in
 int vo_match_level(const vo_hint *h, const vo_annos *a, int na);   /* :100-160 */
 int vo_search_for_group(const vo_group *g, int ng, const vo_hint *h); /* Upstream.java:187-198 */
 
+/* batched, pthread-partitioned searchForGroup(Hint.ofHostPort(host, port))
+ * over a packed host blob (item i = blob[off[i], off[i+1])) -- CPU baseline. */
+void vo_hint_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off,
+                   const uint16_t *port, int64_t n, int32_t *out, int nthreads);
+
 /* ---- DNSServer classification: core/src/main/java/vproxy/dns/DNSServer.java:116-166 ---- */
 enum { VO_DNS_HOSTS = 1, VO_DNS_GROUP = 2, VO_DNS_IP_LITERAL = 3, VO_DNS_INTERNAL = 4, VO_DNS_RECURSIVE = 5 };
 typedef struct {

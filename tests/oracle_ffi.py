@@ -89,6 +89,8 @@ def lib():
         L.vo_hint_of.restype = VoHint
         L.vo_match_level.argtypes = [P(VoHint), P(VoAnnos), C.c_int]
         L.vo_search_for_group.argtypes = [P(VoGroup), C.c_int, P(VoHint)]
+        L.vo_hint_batch.argtypes = [P(VoGroup), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_int64, C.c_void_p, C.c_int]
         L.vo_dns_classify.argtypes = [P(VoHosts), P(VoGroup), C.c_int, C.c_char_p, C.c_int,
                                       P(C.c_int32)]
         L.vo_hosts_parse.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p,
@@ -423,3 +425,14 @@ def rt_add_np(table, nets):
     for i in range(len(nets)):
         n = VoNet.from_buffer_copy(nets[i].tobytes())
         lib().vo_rt_add(C.byref(table.t), C.byref(n))
+
+
+def hint_batch_np(groups, blob, off, port, nthreads=1):
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    n = len(off) - 1
+    out = np.empty(n, np.int32)
+    lib().vo_hint_batch(g.arr, g.n, _ptr(np.ascontiguousarray(blob, np.uint8)),
+                        _ptr(np.ascontiguousarray(off, np.uint32)),
+                        _ptr(np.ascontiguousarray(port, np.uint16)) if port is not None else None,
+                        n, _ptr(out), nthreads)
+    return out

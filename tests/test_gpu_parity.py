@@ -1,0 +1,379 @@
+"""GPU tier: the HIP kernels, called through the C ABI, against the oracle.
+
+Bit-exact comparisons on seeded inputs at oracle-friendly sizes, plus full
+BASELINE-size tables with oracle-checked samples and size-independent
+properties.  Everything here runs on the MI355X box (`-m gpu`).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import vproxy_amd as V
+from vproxy_amd import workloads as W
+from vproxy_amd.classifier import group_array, pack_strings
+
+from cases import acl_edge_rules, hint_cases_random, v6_edge_inputs
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def clf():
+    c = V.Classifier(0)
+    yield c
+    c.close()
+
+
+def _acl_rules(tcp, udp):
+    a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+    b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+    return (a, na, ka), (b, nb, kb)
+
+
+def compile_acl_np(clf, tcp, udp, dflt):
+    (a, na, _), (b, nb, _) = _acl_rules(tcp, udp)
+    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1 if dflt else 0))
+
+
+# ---------------------------------------------------------------------------
+# SecurityGroup ACL
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n_rules,p_range,weighted,nq,seed", [
+    (64, 0.5, False, 1 << 20, 1),      # C1: 64 rules over 1M 5-tuples (full)
+    (2000, 0.3, True, 200000, 2),
+    (300, 0.9, True, 100003, 3),       # odd n: vector tail
+])
+def test_acl_v4_vs_oracle(clf, n_rules, p_range, weighted, nq, seed):
+    tcp, udp = W.gen_sg_rules(n_rules, seed, p_range=p_range, weighted=weighted)
+    proto, src, port = W.gen_acl_queries(tcp, udp, nq, seed + 100)
+    for dflt in (False, True):
+        compile_acl_np(clf, tcp, udp, dflt)
+        got, allow = clf.acl_v4(proto, src, port)
+        want, wv = O.sg_batch_v4_np(tcp, udp, dflt, proto, src, port, nthreads=THREADS)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(allow, wv)
+
+
+def test_acl_c2_full_size(clf):
+    """C2: 10k-rule ACL, 64M IPv4 5-tuples resident in HBM; oracle-checked
+    sample + whole-batch properties."""
+    import torch
+    tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+    compile_acl_np(clf, tcp, udp, False)
+    n = 64 << 20
+    proto, src, port = W.gen_acl_queries(tcp, udp, n, W.SEED + 20)
+    d = [torch.from_numpy(x).cuda() for x in (proto, src, port)]
+    idx, allow = clf.acl_v4(*d)
+    torch.cuda.synchronize()
+    idx_h, allow_h = idx.cpu().numpy(), allow.cpu().numpy()
+    rng = np.random.default_rng(5)
+    s = rng.integers(0, n, 100000)
+    want, wv = O.sg_batch_v4_np(tcp, udp, False, proto[s], src[s], port[s], nthreads=THREADS)
+    np.testing.assert_array_equal(idx_h[s], want)
+    np.testing.assert_array_equal(allow_h[s], wv)
+    # properties over all 64M: the index names a rule of the item's protocol
+    # that really matches it, and allow == that rule's bit (default when -1)
+    tcp_n = len(tcp)
+    hit = idx_h >= 0
+    is_tcp = proto == 6
+    assert np.all(idx_h[is_tcp] < tcp_n) and np.all(idx_h[~is_tcp] < len(udp))
+    for lst, sel in ((tcp, is_tcp & hit), (udp, ~is_tcp & hit)):
+        ip, mk = W.rule_v4_fields(lst)
+        r = idx_h[sel]
+        assert np.all((src[sel] & mk[r]) == ip[r])
+        assert np.all((port[sel] >= lst["min_port"][r]) & (port[sel] <= lst["max_port"][r]))
+        assert np.all(allow_h[sel] == lst["allow"][r])
+    assert np.all(allow_h[~hit] == 0)
+
+
+def test_acl_edges_and_paths(clf):
+    import torch
+    tcp, udp = acl_edge_rules()
+    rng = np.random.default_rng(7)
+    src6, proto, port = v6_edge_inputs(rng, 50001)
+    src4 = src6[:, 12:].copy().view(">u4").reshape(-1).astype(np.uint32)
+    for dflt in (False, True):
+        compile_acl_np(clf, tcp, udp, dflt)
+        want6, wv6 = O.sg_batch_v6_np(tcp, udp, dflt, proto, src6, port)
+        got, allow = clf.acl_v6(proto, src6, port)
+        np.testing.assert_array_equal(got, want6)
+        np.testing.assert_array_equal(allow, wv6)
+        want4, wv4 = O.sg_batch_v4_np(tcp, udp, dflt, proto, src4, port)
+        got, allow = clf.acl_v4(proto, src4, port)
+        np.testing.assert_array_equal(got, want4)
+        np.testing.assert_array_equal(allow, wv4)
+        # device path, aligned (vector kernel) and misaligned (scalar kernel)
+        dp, ds, dq = (torch.from_numpy(x).cuda() for x in (proto, src4, port))
+        gi, ga = clf.acl_v4(dp, ds, dq)
+        np.testing.assert_array_equal(gi.cpu().numpy(), want4)
+        np.testing.assert_array_equal(ga.cpu().numpy(), wv4)
+        gi, ga = clf.acl_v4(dp[1:], ds[1:], dq[1:])
+        np.testing.assert_array_equal(gi.cpu().numpy(), want4[1:])
+        d6 = torch.from_numpy(src6).cuda()
+        gi, ga = clf.acl_v6(dp, d6, dq)
+        np.testing.assert_array_equal(gi.cpu().numpy(), want6)
+
+
+def test_acl_empty_and_tiny_batches(clf):
+    tcp, udp = W.gen_sg_rules(30, 5)
+    for t, u in ((tcp[:0], udp), (tcp, udp[:0]), (tcp[:0], udp[:0])):
+        compile_acl_np(clf, t, u, True)
+        for n in (0, 1, 2, 3, 4, 5, 1023):
+            proto, src, port = W.gen_acl_queries(tcp, udp, n, n + 9)
+            got, allow = clf.acl_v4(proto, src, port)
+            want, wv = O.sg_batch_v4_np(t, u, True, proto, src, port)
+            np.testing.assert_array_equal(got, want)
+            np.testing.assert_array_equal(allow, wv)
+
+
+def test_security_group_scenarios_on_gpu(clf):
+    """TestTcpLB/CI security-group flows through the C++ mirror + GPU."""
+    with open(os.path.join(G, "kats.json")) as f:
+        kats = json.load(f)
+    for case in kats["security_group"]:
+        sg = V.SecurityGroup("secg", True)
+        for st in case["steps"]:
+            if st[0] == "default":
+                sg.default_allow = st[1]
+            elif st[0] == "add":
+                _, alias, n, proto, lo, hi, allow = st
+                sg.add_rule(alias, n, proto, lo, hi, allow)
+            elif st[0] == "remove":
+                sg.remove_rule(st[1])
+            else:
+                _, proto, ip, port, want = st
+                clf.compile_security_group(sg)
+                ipb = V.parse_ip(ip)
+                src = np.frombuffer(ipb, ">u4").astype(np.uint32)
+                _, allow = clf.acl_v4(np.array([6 if proto == "TCP" else 17], np.uint8), src,
+                                      np.array([port], np.uint16))
+                assert bool(allow[0]) == want, (case["source"], st)
+
+
+# ---------------------------------------------------------------------------
+# RouteTable
+# ---------------------------------------------------------------------------
+def test_route_golden_and_f3(clf):
+    with open(os.path.join(G, "route_table.json")) as f:
+        cases = json.load(f)["cases"]
+    for case in cases:
+        rt = V.RouteTable()
+        for i, n in enumerate(case["add"]):
+            rt.add_rule("r%d" % i, n)
+        assert [str(x) for x in rt.get_rules()] == case["expect"]
+        clf.compile_route_table(rt)
+        if case["lookups"]:
+            ips = np.array([int.from_bytes(V.parse_ip(ip), "big") for ip, _ in case["lookups"]],
+                           np.uint32)
+            assert list(clf.route_v4(ips)) == [w for _, w in case["lookups"]]
+
+
+def test_route_c1_random_order(clf):
+    rng = np.random.default_rng(11)
+    rt = V.RouteTable("10.0.0.0/8", None, 1)
+    ot = O.RouteTable()
+    ot.add("10.0.0.0/8")
+    plen = rng.integers(8, 31, 600)
+    net = rng.integers(0, 2**32, 600, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    added = 0
+    for i in range(600):
+        s = "%d.%d.%d.%d/%d" % (net[i] >> 24, (net[i] >> 16) & 255, (net[i] >> 8) & 255,
+                                net[i] & 255, plen[i])
+        if ot.add(s):
+            rt.add_rule("r%d" % i, s)
+            added += 1
+        if added == 255:
+            break
+    assert [str(x) for x in rt.get_rules()] == ot.rules()
+    clf.compile_route_table(rt)
+    v4, _ = O.rt_table_np(ot)
+    q = W.v4_lookups(net, plen, 1 << 20, 12)
+    np.testing.assert_array_equal(clf.route_v4(q), O.rt_batch_v4_np(v4, q, nthreads=THREADS))
+
+
+def test_route_arbitrary_priority_and_v6(clf):
+    rng = np.random.default_rng(21)
+    plen = rng.integers(0, 33, 6000)
+    net = rng.integers(0, 2**32, 6000, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
+    _, first = np.unique(key, return_index=True)
+    nets4 = W.v4_nets(net[np.sort(first)], plen[np.sort(first)])
+    rng.shuffle(nets4)
+    hi, lo, p6 = W.gen_v6_prefixes(5000, 31)
+    nets6 = np.concatenate([W.v6_nets(hi, lo, p6), W.v6_nets([0], [0], [0])])
+    rng.shuffle(nets6)
+    a, na, ka = W.as_ctypes(nets4, V._lib.VcNet)
+    b, nb, kb = W.as_ctypes(nets6, V._lib.VcNet)
+    clf.compile_routes_raw(a, na, b, nb)
+    q4 = W.v4_lookups(net, plen, 300001, 22)
+    np.testing.assert_array_equal(clf.route_v4(q4), O.rt_batch_v4_np(nets4, q4, nthreads=THREADS))
+    q6 = W.v6_lookups(hi, lo, p6, 100000, 23)
+    np.testing.assert_array_equal(clf.route_v6(q6), O.rt_batch_v6_np(nets6, q6, nthreads=THREADS))
+
+
+def test_route_c3_full_size(clf):
+    """C3: ~1M IPv4 + 200k IPv6 prefixes inserted shortest-first through the
+    RouteTable mirror (first match == LPM there); 16M device-resident
+    lookups; oracle-checked sample and LPM properties."""
+    import torch
+    net, plen = W.gen_v4_prefixes(1000000, W.SEED + 3)
+    hi, lo, p6 = W.gen_v6_prefixes(200000, W.SEED + 4)
+    rt = V.RouteTable()
+    allnets = np.concatenate([W.v4_nets(net, plen), W.v6_nets(hi, lo, p6)])
+    arr, n, keep = W.as_ctypes(allnets, V._lib.VcNet)
+    rt.add_rules("bgp", arr, n=n)
+    clf.compile_route_table(rt)
+    a4, n4 = rt.rules_raw(4)
+    a6, n6 = rt.rules_raw(6)
+    v4 = np.frombuffer(bytes(a4)[:n4 * 40], W.NET_DT)
+    v6 = np.frombuffer(bytes(a6)[:n6 * 40], W.NET_DT)
+    q4 = W.v4_lookups(net, plen, 16 << 20, 41)
+    got4 = clf.route_v4(torch.from_numpy(q4).cuda()).cpu().numpy()
+    s = np.random.default_rng(1).integers(0, len(q4), 3000)
+    np.testing.assert_array_equal(got4[s], O.rt_batch_v4_np(v4, q4[s], nthreads=THREADS))
+    # every hit's prefix contains the address; 90% of lookups were drawn inside one
+    ip, mk = v4["ip"][:, :4].copy().view(">u4").reshape(-1), v4["mask"][:, :4].copy().view(
+        ">u4").reshape(-1)
+    h = got4 >= 0
+    assert np.all((q4[h] & mk[got4[h]]) == ip[got4[h]])
+    assert h.mean() > 0.9
+    q6 = W.v6_lookups(hi, lo, p6, 1 << 20, 42)
+    got6 = clf.route_v6(torch.from_numpy(q6).cuda()).cpu().numpy()
+    s = np.random.default_rng(2).integers(0, len(q6), 2000)
+    np.testing.assert_array_equal(got6[s], O.rt_batch_v6_np(v6, q6[s], nthreads=THREADS))
+
+
+# ---------------------------------------------------------------------------
+# Upstream hints / DNS
+# ---------------------------------------------------------------------------
+def test_hint_kats(clf):
+    with open(os.path.join(G, "kats.json")) as f:
+        kats = json.load(f)
+    for case in kats["hints"]:
+        clf.compile_upstream(case["groups"])
+        qs = case["queries"]
+        got = clf.hint_search([q.get("host") for q, _ in qs],
+                              np.array([q.get("port", 0) for q, _ in qs], np.uint16),
+                              [q.get("uri") for q, _ in qs])
+        assert list(got) == [w for _, w in qs], case["source"]
+
+
+def test_hint_random_vs_oracle(clf):
+    groups, hosts, queries = hint_cases_random(np.random.default_rng(41), 800, 50000)
+    clf.compile_upstream(groups)
+    og = O.Groups(groups)
+    hs = [q[0] for q in queries]
+    ps = np.array([q[1] for q in queries], np.uint16)
+    us = [q[2] for q in queries]
+    got = clf.hint_search(hs, ps, us)
+    want = np.array([O.search_for_group(og, q[0], q[1], q[2]) for q in queries], np.int32)
+    np.testing.assert_array_equal(got, want)
+    got = clf.hint_search(hs, ps, None)
+    want = np.array([O.search_for_group(og, q[0], q[1], None) for q in queries], np.int32)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_hint_c4_scale(clf):
+    """C4: 100k hint-host groups vs 1M hostnames (16M in the bench);
+    oracle-checked sample (each oracle query scans all 100k groups)."""
+    groups, ghosts = W.gen_groups(100000, W.SEED + 5)
+    clf.compile_upstream(groups)
+    names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, pool=1 << 18)
+    rng = np.random.default_rng(3)
+    ports = np.where(rng.random(len(names)) < 0.2, rng.integers(1, 65536, len(names)), 0)
+    ports = ports.astype(np.uint16)
+    got = clf.hint_search(names, ports)
+    og = O.Groups(groups)
+    s = rng.integers(0, len(names), 1500)
+    want = [O.search_for_group(og, names[i], int(ports[i]), None) for i in s]
+    np.testing.assert_array_equal(got[s], np.array(want, np.int32))
+    assert (got >= 0).mean() > 0.5
+
+
+def test_dns_kats_and_random(clf):
+    with open(os.path.join(G, "kats.json")) as f:
+        kats = json.load(f)
+    for case in kats["dns"]:
+        clf.compile_upstream(case["groups"])
+        clf.compile_hosts([tuple(x) for x in case["hosts"]])
+        kind, val = clf.dns_classify([q for q, _, _ in case["queries"]])
+        assert [(int(k), int(v)) for k, v in zip(kind, val)] == \
+            [(k, v) for _, k, v in case["queries"]], case["source"]
+    groups, ghosts = W.gen_groups(3000, 77)
+    clf.compile_upstream(groups)
+    pairs = [(h + ".", i) for i, h in enumerate(ghosts[:50])] + [("localhost.", 999)]
+    clf.compile_hosts(pairs)
+    names = W.gen_hostnames(ghosts, 30000, 78, dns=True)
+    names += [b"1.2.3.4.", b"::1.", b"[::1].", b"a.vproxy.local.", b".", b"", b"::ffff:1.2.3.4.",
+              b"::x:1.2.3.4.", b"www.x.com:80."]
+    kind, val = clf.dns_classify(names)
+    og = O.Groups(groups)
+    oh = O.Hosts(pairs)
+    want = [O.dns_classify(oh, og, q) for q in names]
+    assert [(int(k), int(v)) for k, v in zip(kind, val)] == want
+
+
+def test_hosts_text(clf):
+    clf.compile_upstream([({}, {"host": "example.com"})])
+    text = "127.0.0.1 localhost\n10.0.0.1 db.example.com. db # x\n::1 localhost ip6\n"
+    clf.compile_hosts_text(text)
+    pairs, _ = O.hosts_parse(text)
+    kind, val = clf.dns_classify(["localhost.", "db.example.com.", "db.", "ip6.", "example.com."])
+    oh = O.Hosts(pairs)
+    og = O.Groups([({}, {"host": "example.com"})])
+    want = [O.dns_classify(oh, og, q) for q in
+            ["localhost.", "db.example.com.", "db.", "ip6.", "example.com."]]
+    assert [(int(k), int(v)) for k, v in zip(kind, val)] == want
+
+
+# ---------------------------------------------------------------------------
+# Pipeline + counters
+# ---------------------------------------------------------------------------
+def test_pipeline_and_counters(clf):
+    import torch
+    tcp, udp = W.gen_sg_rules(1000, 51)
+    compile_acl_np(clf, tcp, udp, False)
+    net, plen = W.gen_v4_prefixes(20000, 52)
+    nets = W.v4_nets(net, plen)
+    a, na, ka = W.as_ctypes(nets, V._lib.VcNet)
+    clf.compile_routes_raw(a, na, (V._lib.VcNet * 1)(), 0)
+    groups, ghosts = W.gen_groups(5000, 53)
+    clf.compile_upstream(groups)
+    names = W.gen_hostnames(ghosts, 20000, 54)
+    pool = clf.hint_search(names)
+    n = 1000003
+    proto, src, port = W.gen_acl_queries(tcp, udp, n, 55)
+    dst = W.v4_lookups(net, plen, n, 56)
+    hid = np.random.default_rng(57).integers(0, len(names), n).astype(np.uint32)
+    hid[::97] = 0xFFFFFFFF
+    clf.counters_enable(True)
+    clf.counters_reset()
+    T = lambda x: torch.from_numpy(x).cuda()
+    out = clf.pipeline_v4(T(proto), T(src), T(dst), T(port), T(hid), T(pool), want_allow=True)
+    torch.cuda.synchronize()
+    acl, route, grp, allow = (o.cpu().numpy() for o in out)
+    want_acl, want_allow = O.sg_batch_v4_np(tcp, udp, False, proto, src, port, nthreads=THREADS)
+    np.testing.assert_array_equal(acl, want_acl)
+    np.testing.assert_array_equal(allow, want_allow)
+    s = np.random.default_rng(58).integers(0, n, 20000)
+    np.testing.assert_array_equal(route[s], O.rt_batch_v4_np(nets, dst[s], nthreads=THREADS))
+    np.testing.assert_array_equal(grp, np.where(hid == 0xFFFFFFFF, -1, pool[np.minimum(
+        hid, len(pool) - 1)]))
+    # counters: exact histograms of the outputs
+    ca = clf.counters_read(V.COUNTERS_ACL)
+    nt, nu = len(tcp), len(udp)
+    exp = np.zeros(nt + nu + 2, np.uint64)
+    is_t = proto == 6
+    np.add.at(exp, np.where(acl >= 0, np.where(is_t, acl, nt + acl), nt + nu + (~is_t)), 1)
+    np.testing.assert_array_equal(ca, exp)
+    cr = clf.counters_read(V.COUNTERS_ROUTE)
+    exp = np.bincount(np.where(route >= 0, route, len(nets)), minlength=len(nets) + 2)
+    np.testing.assert_array_equal(cr, exp.astype(np.uint64))
+    cg = clf.counters_read(V.COUNTERS_GROUP)
+    assert int(cg.sum()) == n
+    clf.counters_enable(False)

@@ -472,7 +472,8 @@ class Classifier:
                     torch.empty(n, dtype=torch.uint8, device=dev) if want_allow else None)
         a, r, g, al = outs
         check(lib().vc_pipeline_v4_dev(self.h, _ptr(proto), _ptr(src4), _ptr(dst4), _ptr(dport),
-                                       _ptr(host_id), _ptr(pool_group), n, _ptr(a), _ptr(r),
+                                       _ptr(host_id), _ptr(pool_group), len(pool_group), n,
+                                       _ptr(a), _ptr(r),
                                        _ptr(g), _ptr(al), _stream()))
         return outs
 

@@ -543,11 +543,13 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
 // ---------------------------------------------------------------------------
 int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
                        const uint32_t* dst4, const uint16_t* dport, const uint32_t* host_id,
-                       const int32_t* pool_group, int64_t n, int32_t* out_acl, int32_t* out_route,
+                       const int32_t* pool_group, int64_t n_pool, int64_t n, int32_t* out_acl,
+                       int32_t* out_route,
                        int32_t* out_group, uint8_t* out_allow, void* stream) {
     int rc = set_dev(ctx);
     if (rc) return rc;
-    if (n < 0 || (n > 0 && (!proto || !src4 || !dst4 || !dport || !host_id || !pool_group ||
+    if (n < 0 || n_pool < 0 || (n > 0 && (!proto || !src4 || !dst4 || !dport || !host_id ||
+                                          (n_pool > 0 && !pool_group) ||
                             !out_acl || !out_route || !out_group)))
         return fail(VC_EINVAL, "bad batch arguments");
     auto a = ctx->get(ctx->acl);
@@ -557,7 +559,8 @@ int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
     const bool on = ctx->counters_on;
     const int32_t ng = h ? h->img.n_groups : 0;
     hipError_t e = vc::launch_pipeline_v4(
-        ctx->cfg(stream), a->img, r->img.fam[0], proto, src4, dst4, dport, host_id, pool_group, n,
+        ctx->cfg(stream), a->img, r->img.fam[0], proto, src4, dst4, dport, host_id, pool_group,
+        n_pool, n,
         out_acl, out_route, out_group, out_allow, on ? a->counters : nullptr,
         on ? r->counters : nullptr, int64_t(r->n4) + r->n6, on && h ? h->counters : nullptr, ng);
     return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");

@@ -217,7 +217,8 @@ __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
     AclImage img, const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ proto,
     const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
     const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
-    const int32_t* __restrict__ pool_group, int64_t n, int32_t* __restrict__ out_acl,
+    const int32_t* __restrict__ pool_group, int64_t n_pool, int64_t n,
+    int32_t* __restrict__ out_acl,
     int32_t* __restrict__ out_route, int32_t* __restrict__ out_group,
     uint8_t* __restrict__ out_allow, unsigned long long* __restrict__ acl_cnt,
     unsigned long long* __restrict__ route_cnt, int64_t route_none_at,
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
         const uint32_t d = dst[i];
         uint32_t e = nodes[d >> (32 - rb)];
         const uint32_t h = host_id[i];
-        const int32_t grp = h == 0xFFFFFFFFu ? -1 : pool_group[h];
+        const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
         const bool t = proto[i] == VC_PROTO_TCP;
         const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
         acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i, acl_cnt);
@@ -265,6 +266,15 @@ int grid_for(const LaunchCfg& c, int64_t work_items, int blocks_per_cu) {
 
 bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
+// Dynamic LDS beyond 64 KiB must be opted into per kernel (once).
+template <class K>
+void allow_lds(K kernel) {
+    static const hipError_t once = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+        kLdsWords * 4);
+    (void)once;
+}
+
 }  // namespace
 
 hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
@@ -279,18 +289,21 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
     const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
     if (vec) {
         const int grid = grid_for(c, (n + 3) / 4, per_cu);
-        if (lds)
+        if (lds) {
+            allow_lds(vcd::acl_v4_kernel<true>);
             hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
                                c.stream, img, proto, src4, port, n, out, allow, counters);
-        else
+        } else {
             hipLaunchKernelGGL(vcd::acl_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
                                c.stream, img, proto, src4, port, n, out, allow, counters);
+        }
     } else {
         const int grid = grid_for(c, n, per_cu);
-        if (lds)
+        if (lds) {
+            allow_lds(vcd::acl_v4_kernel_scalar<true>);
             hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
                                shmem, c.stream, img, proto, src4, port, n, out, allow, counters);
-        else
+        } else
             hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<false>, dim3(grid), dim3(vcd::kBlock), 0,
                                c.stream, img, proto, src4, port, n, out, allow, counters);
     }
@@ -335,7 +348,8 @@ hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t
 hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
                               const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
                               const uint16_t* dport, const uint32_t* host_id,
-                              const int32_t* pool_group, int64_t n, int32_t* out_acl,
+                              const int32_t* pool_group, int64_t n_pool, int64_t n,
+                              int32_t* out_acl,
                               int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
                               unsigned long long* acl_cnt, unsigned long long* route_cnt,
                               int64_t route_none_at, unsigned long long* group_cnt,
@@ -345,15 +359,16 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
     const bool lds = words <= kLdsWords;
     const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
     const int grid = grid_for(c, n, per_cu);
-    if (lds)
+    if (lds) {
+        allow_lds(vcd::pipeline_v4_kernel<true>);
         hipLaunchKernelGGL(vcd::pipeline_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock),
                            size_t(words) * 4, c.stream, acl, r4.nodes, r4.root_bits, proto, src4,
-                           dst4, dport, host_id, pool_group, n, out_acl, out_route, out_group,
+                           dst4, dport, host_id, pool_group, n_pool, n, out_acl, out_route, out_group,
                            out_allow, acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
-    else
+    } else
         hipLaunchKernelGGL(vcd::pipeline_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
                            c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,
-                           host_id, pool_group, n, out_acl, out_route, out_group, out_allow,
+                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group, out_allow,
                            acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
     return hipGetLastError();
 }

@@ -36,7 +36,8 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
 hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
                               const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
                               const uint16_t* dport, const uint32_t* host_id,
-                              const int32_t* pool_group, int64_t n, int32_t* out_acl,
+                              const int32_t* pool_group, int64_t n_pool, int64_t n,
+                              int32_t* out_acl,
                               int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
                               unsigned long long* acl_cnt, unsigned long long* route_cnt,
                               int64_t route_none_at, unsigned long long* group_cnt,
