@@ -235,7 +235,8 @@ int vc_routetable_add_rule(vc_routetable *rt, const char *alias, const vc_net *n
 /* Bulk insert of vni rules in the given order.  Exact same final lists as
  * repeated vc_routetable_add_rule; O(n log n) when every insert is no
  * shorter than the rules already present, otherwise
- * falls back to the per-rule heuristic. Aliases are "<prefix><i>". */
+ * falls back to the per-rule heuristic. Aliases are "<prefix><i>".
+ * Returns 1 when the bulk path ran, 0 for the per-rule path, <0 on error. */
 int vc_routetable_add_rules(vc_routetable *rt, const char *alias_prefix, const vc_net *nets,
                             int n, int to_vni);
 /* RouteTable.delRule (RouteTable.java:156-172) */

@@ -226,7 +226,7 @@ def test_route_c3_full_size(clf):
     rt = V.RouteTable()
     allnets = np.concatenate([W.v4_nets(net, plen), W.v6_nets(hi, lo, p6)])
     arr, n, keep = W.as_ctypes(allnets, V._lib.VcNet)
-    rt.add_rules("bgp", arr, n=n)
+    assert rt.add_rules("bgp", arr, n=n)
     clf.compile_route_table(rt)
     a4, n4 = rt.rules_raw(4)
     a6, n6 = rt.rules_raw(6)

@@ -116,7 +116,7 @@ def test_route_table_bulk_shortest_first_vs_oracle():
     pt = V.RouteTable()
     allnets = np.concatenate([v4, v6])
     arr, n, keep = W.as_ctypes(allnets, V._lib.VcNet)
-    pt.add_rules("p", arr, n=n)
+    assert pt.add_rules("p", arr, n=n)          # the O(n log n) path ran
     a4, b6 = O.rt_table_np(ot)
     g4, n4 = pt.rules_raw(4)
     g6, n6 = pt.rules_raw(6)
@@ -134,7 +134,7 @@ def test_route_table_bulk_fallback_random_order():
         if ot.add(s):
             uniq.append(s)
     pt = V.RouteTable()
-    pt.add_rules("x", uniq)
+    assert not pt.add_rules("x", uniq)          # random order: per-rule heuristic
     assert [str(x) for x in pt.get_rules()] == ot.rules()
 
 

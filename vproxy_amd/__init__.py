@@ -5,7 +5,7 @@ hint matching and DNSServer record classification, evaluated by hand-written
 HIP kernels for gfx950 behind the C ABI in include/vclassify.h.
 """
 from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,  # noqa: F401
-                   NotFoundException, StateError, VcError, XException, lib,
+                   NotFoundException, StateError, VcError, XException, check, lib,
                    COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP, PROTO_TCP, PROTO_UDP,
                    DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401

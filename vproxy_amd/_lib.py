@@ -77,6 +77,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError("libvclassify.so not built (run `make -C vproxy_amd/csrc` or "
                               "__graft_entry__.build()); there is no CPU fallback")
+        # One HIP runtime per process.  PyTorch-ROCm ships its own
+        # libamdhip64.so.7; if libvclassify loaded the system copy first,
+        # torch would bring up a second runtime that sees no GPU.  Loading
+        # torch first makes the dynamic linker bind libvclassify's
+        # libamdhip64.so.7 dependency to the already-loaded runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         P = C.POINTER
         vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int

@@ -170,7 +170,8 @@ class RouteTable:
             arr, n = networks, (len(networks) if n is None else n)
         else:
             arr, n = net_array(networks), len(networks)
-        check(lib().vc_routetable_add_rules(self.h, _b(alias_prefix), arr, n, int(to_vni)))
+        return check(lib().vc_routetable_add_rules(self.h, _b(alias_prefix), arr, n,
+                                                    int(to_vni))) == 1
 
     def del_rule(self, alias):
         check(lib().vc_routetable_del_rule(self.h, _b(alias)))

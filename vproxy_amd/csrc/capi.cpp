@@ -721,7 +721,7 @@ int vc_routetable_add_rules(vc_routetable* rt, const char* alias_prefix, const v
         v[i].to_vni = to_vni;
     }
     int rc = rt->rt.add_rules_bulk(std::move(v));
-    return rc ? fail(rc, "cannot add routes") : VC_OK;
+    return rc < 0 ? fail(rc, "cannot add routes") : rc;
 }
 
 int vc_routetable_del_rule(vc_routetable* rt, const char* alias) {

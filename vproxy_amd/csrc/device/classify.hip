@@ -39,9 +39,11 @@ __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t
                                   : img.allow[(tcp ? 0 : img.n_tcp) + v];
     }
     if (cnt) {
-        int64_t at = v == VC_NONE ? int64_t(img.n_tcp) + img.n_udp + (tcp ? 0 : 1)
-                                  : (tcp ? int64_t(v) : int64_t(img.n_tcp) + v);
-        atomicAdd(cnt + at, 1ull);
+        const bool none = v == VC_NONE;
+        const int64_t dflt = int64_t(img.n_tcp) + img.n_udp;
+        count_hot(cnt + dflt, none && tcp);
+        count_hot(cnt + dflt + 1, none && !tcp);
+        if (!none) atomicAdd(cnt + (tcp ? int64_t(v) : int64_t(img.n_tcp) + v), 1ull);
     }
 }
 
@@ -153,7 +155,10 @@ __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
 __device__ __forceinline__ void route_emit(uint32_t e, int32_t* o, unsigned long long* cnt,
                                            int64_t rule_base, int64_t none_at) {
     *o = out_index(e);
-    if (cnt) atomicAdd(cnt + (e == VC_NONE ? none_at : rule_base + e), 1ull);
+    if (cnt) {
+        count_hot(cnt + none_at, e == VC_NONE);
+        if (e != VC_NONE) atomicAdd(cnt + rule_base + e, 1ull);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void route_v4_kernel(
@@ -243,7 +248,10 @@ __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
         }
         route_emit(e, out_route + i, route_cnt, 0, route_none_at);
         out_group[i] = grp;
-        if (group_cnt) atomicAdd(group_cnt + (grp < 0 ? n_groups : grp), 1ull);
+        if (group_cnt) {
+            count_hot(group_cnt + n_groups, grp < 0);
+            if (grp >= 0) atomicAdd(group_cnt + grp, 1ull);
+        }
     }
 }
 

@@ -37,7 +37,10 @@ __global__ __launch_bounds__(kHintBlock) void hint_kernel(
         const int p = port ? int(port[i]) : 0;
         const int32_t g = search_for_group(img, format_host(h), p, format_uri(u));
         out[i] = g;
-        if (cnt) atomicAdd(cnt + (g < 0 ? img.n_groups : g), 1ull);
+        if (cnt) {
+            count_hot(cnt + img.n_groups, g < 0);
+            if (g >= 0) atomicAdd(cnt + g, 1ull);
+        }
     }
 }
 

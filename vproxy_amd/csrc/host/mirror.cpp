@@ -127,11 +127,15 @@ namespace {
 struct PKey {
     uint64_t hi, lo;
     int len;
-    bool operator==(const PKey& o) const { return hi == o.hi && lo == o.lo && len == o.len; }
+    int fam;   // 4 or 16: Network.equals compares the ip byte arrays, so families never collide
+    bool operator==(const PKey& o) const {
+        return hi == o.hi && lo == o.lo && len == o.len && fam == o.fam;
+    }
 };
 struct PKeyHash {
     size_t operator()(const PKey& k) const {
-        uint64_t h = k.hi * 0x9E3779B97F4A7C15ull ^ (k.lo + 0x632BE59BD9B4E019ull + (uint64_t)k.len);
+        uint64_t h = k.hi * 0x9E3779B97F4A7C15ull ^
+                     (k.lo + 0x632BE59BD9B4E019ull + (uint64_t)k.len + ((uint64_t)k.fam << 8));
         h ^= h >> 29;
         h *= 0xBF58476D1CE4E5B9ull;
         return static_cast<size_t>(h ^ (h >> 32));
@@ -146,11 +150,11 @@ PKey key_of(const vc_net& n) {
     for (int i = 0; i < 8; ++i) hi = (hi << 8) | b[i];
     for (int i = 8; i < 16; ++i) lo = (lo << 8) | b[i];
     if (n.ip_len == 4) hi = (hi >> 32) << 32;   // v4 keys live in the top 32 bits
-    return PKey{hi, lo, mask_int(n.mask, n.mask_len)};
+    return PKey{hi, lo, mask_int(n.mask, n.mask_len), n.ip_len};
 }
 
 PKey truncate(const PKey& k, int len) {
-    PKey r{0, 0, len};
+    PKey r{0, 0, len, k.fam};
     if (len >= 64) {
         r.hi = k.hi;
         r.lo = len == 128 ? k.lo : (len == 64 ? 0 : (k.lo & ~(~0ull >> (len - 64))));
@@ -249,11 +253,12 @@ int RouteTable::add_rules_bulk(std::vector<RouteRule> rules) {
         }
         return VC_OK;
     }
+    // (the bulk path reports 1 so callers/tests can tell which path ran)
     std::vector<RouteRule> s4(v4_.begin(), v4_.end()), s6(v6_.begin(), v6_.end());
     for (auto& r : rules) (r.rule.ip_len == 4 ? s4 : s6).push_back(std::move(r));
     v4_ = postorder_build(std::move(s4));
     v6_ = postorder_build(std::move(s6));
-    return VC_OK;
+    return 1;
 }
 
 int RouteTable::del_rule(std::string_view alias) {
