@@ -15,7 +15,7 @@
  *    null / "no rule" (the caller maps index -> SecurityGroupRule / RouteRule
  *    / ServerGroupHandle exactly as the Java code would have returned it).
  *  - *_dev functions take DEVICE pointers and a hipStream_t (passed as void*,
- *    NULL = the context's stream); they are asynchronous.  The plain variants
+ *    NULL = HIP's null stream); they are asynchronous and ordered on it.  The plain variants
  *    take HOST pointers and are synchronous (H2D + kernel + D2H).
  *  - IPv4 addresses are uint32 in IP.ipv4Bytes2Int order (big-endian value,
  *    vfd/IP.java:476-478); IPv6 addresses are 16 raw bytes per item.

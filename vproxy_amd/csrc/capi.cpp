@@ -105,10 +105,12 @@ struct vc_ctx {
     void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
         std::atomic_store(&slot, std::move(v));
     }
+    // `s` is the caller's hipStream_t; NULL is HIP's null stream, as in
+    // every HIP API (torch's default stream reports itself as 0).
     vc::LaunchCfg cfg(void* s) const {
         vc::LaunchCfg c;
         c.num_cus = num_cus;
-        c.stream = s ? static_cast<hipStream_t>(s) : stream;
+        c.stream = static_cast<hipStream_t>(s);
         return c;
     }
 };
