@@ -178,6 +178,7 @@ def main():
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-counters", action="store_true", help="ablation: skip hit counters")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,7 +229,7 @@ def main():
     torch.cuda.synchronize()
     log("packets generated (%d per GPU), setup %.1fs" % (B, time.time() - t_setup))
 
-    clf.counters_enable(True)
+    clf.counters_enable(not args.no_counters)
     cnt = []
     for kind in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP):
         ptr, n = clf.counters_device(kind)

@@ -31,19 +31,11 @@ __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint
 }
 
 __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t v,
-                                         uint8_t* allow_out, int32_t* idx_out,
-                                         unsigned long long* cnt) {
+                                         uint8_t* allow_out, int32_t* idx_out) {
     *idx_out = out_index(v);
     if (allow_out) {
         *allow_out = v == VC_NONE ? uint8_t(img.default_allow)
                                   : img.allow[(tcp ? 0 : img.n_tcp) + v];
-    }
-    if (cnt) {
-        const bool none = v == VC_NONE;
-        const int64_t dflt = int64_t(img.n_tcp) + img.n_udp;
-        count_hot(cnt + dflt, none && tcp);
-        count_hot(cnt + dflt + 1, none && !tcp);
-        if (!none) atomicAdd(cnt + (tcp ? int64_t(v) : int64_t(img.n_tcp) + v), 1ull);
     }
 }
 
@@ -73,7 +65,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
     AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
-    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    uint8_t* __restrict__ allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (kLds) stage_bounds(img, lds);
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
@@ -98,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             uint8_t b = 0;
-            acl_emit(img, tcp[k], v[k], allow ? &b : nullptr, op + k, cnt);
+            acl_emit(img, tcp[k], v[k], allow ? &b : nullptr, op + k);
             al |= uint32_t(b) << (8 * k);
         }
         reinterpret_cast<int4*>(out)[g] = o;
@@ -109,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
         const int64_t i = (n4 << 2) + threadIdx.x;
         const bool t = proto[i] == VC_PROTO_TCP;
         const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
-        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
 
@@ -118,7 +110,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
     AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
-    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    uint8_t* __restrict__ allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (kLds) stage_bounds(img, lds);
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
@@ -126,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
         const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
-        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
 
@@ -136,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
 __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
     AclImage img, const uint8_t* __restrict__ proto, const uint8_t* __restrict__ src6,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
-    uint8_t* __restrict__ allow, unsigned long long* __restrict__ cnt) {
+    uint8_t* __restrict__ allow) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
@@ -145,26 +137,18 @@ __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
         v6_key(reinterpret_cast<const uint4*>(src6)[i], &hi, &lo);
         const int j = bsearch_u128(f.bounds6, f.nb, hi, lo);
         const uint32_t v = port_lookup(f.pieces, load_desc(f.desc, j), port[i]);
-        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i, cnt);
+        acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
 
 // ---------------------------------------------------------------------------
 // RouteTable.lookup
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void route_emit(uint32_t e, int32_t* o, unsigned long long* cnt,
-                                           int64_t rule_base, int64_t none_at) {
-    *o = out_index(e);
-    if (cnt) {
-        count_hot(cnt + none_at, e == VC_NONE);
-        if (e != VC_NONE) atomicAdd(cnt + rule_base + e, 1ull);
-    }
-}
+__device__ __forceinline__ void route_emit(uint32_t e, int32_t* o) { *o = out_index(e); }
 
 __global__ __launch_bounds__(kBlock) void route_v4_kernel(
     const uint32_t* __restrict__ nodes, int rb, const uint32_t* __restrict__ dst, int64_t n,
-    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
-    int64_t none_at) {
+    int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     const int64_t n4 = n >> 2;
     for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
@@ -184,33 +168,31 @@ __global__ __launch_bounds__(kBlock) void route_v4_kernel(
         int4 o;
         int32_t* op = reinterpret_cast<int32_t*>(&o);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) route_emit(e[k], op + k, cnt, rule_base, none_at);
+        for (int k = 0; k < 4; ++k) route_emit(e[k], op + k);
         reinterpret_cast<int4*>(out)[g] = o;
     }
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
         const int64_t i = (n4 << 2) + threadIdx.x;
-        route_emit(trie_v4(nodes, rb, dst[i]), out + i, cnt, rule_base, none_at);
+        route_emit(trie_v4(nodes, rb, dst[i]), out + i);
     }
 }
 
 __global__ __launch_bounds__(kBlock) void route_v4_kernel_scalar(
     const uint32_t* __restrict__ nodes, int rb, const uint32_t* __restrict__ dst, int64_t n,
-    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
-    int64_t none_at) {
+    int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-        route_emit(trie_v4(nodes, rb, dst[i]), out + i, cnt, rule_base, none_at);
+        route_emit(trie_v4(nodes, rb, dst[i]), out + i);
 }
 
 __global__ __launch_bounds__(kBlock) void route_v6_kernel(
     const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
-    int32_t* __restrict__ out, unsigned long long* __restrict__ cnt, int64_t rule_base,
-    int64_t none_at) {
+    int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(dst6)[i], &hi, &lo);
-        route_emit(trie_v6(nodes, rb, hi, lo), out + i, cnt, rule_base, none_at);
+        route_emit(trie_v6(nodes, rb, hi, lo), out + i);
     }
 }
 
@@ -225,9 +207,7 @@ __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
     const int32_t* __restrict__ pool_group, int64_t n_pool, int64_t n,
     int32_t* __restrict__ out_acl,
     int32_t* __restrict__ out_route, int32_t* __restrict__ out_group,
-    uint8_t* __restrict__ out_allow, unsigned long long* __restrict__ acl_cnt,
-    unsigned long long* __restrict__ route_cnt, int64_t route_none_at,
-    unsigned long long* __restrict__ group_cnt, int32_t n_groups) {
+    uint8_t* __restrict__ out_allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (kLds) stage_bounds(img, lds);
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
@@ -240,18 +220,14 @@ __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
         const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
         const bool t = proto[i] == VC_PROTO_TCP;
         const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
-        acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i, acl_cnt);
+        acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i);
         int shift = 32 - rb;
         while (e & VC_PTR) {
             shift -= 8;
             e = nodes[(1u << rb) + (e & ~VC_PTR) * 256u + ((d >> shift) & 255u)];
         }
-        route_emit(e, out_route + i, route_cnt, 0, route_none_at);
+        route_emit(e, out_route + i);
         out_group[i] = grp;
-        if (group_cnt) {
-            count_hot(group_cnt + n_groups, grp < 0);
-            if (grp >= 0) atomicAdd(group_cnt + grp, 1ull);
-        }
     }
 }
 
@@ -300,22 +276,25 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
         if (lds) {
             allow_lds(vcd::acl_v4_kernel<true>);
             hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
-                               c.stream, img, proto, src4, port, n, out, allow, counters);
+                               c.stream, img, proto, src4, port, n, out, allow);
         } else {
             hipLaunchKernelGGL(vcd::acl_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
-                               c.stream, img, proto, src4, port, n, out, allow, counters);
+                               c.stream, img, proto, src4, port, n, out, allow);
         }
     } else {
         const int grid = grid_for(c, n, per_cu);
         if (lds) {
             allow_lds(vcd::acl_v4_kernel_scalar<true>);
             hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
-                               shmem, c.stream, img, proto, src4, port, n, out, allow, counters);
+                               shmem, c.stream, img, proto, src4, port, n, out, allow);
         } else
             hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<false>, dim3(grid), dim3(vcd::kBlock), 0,
-                               c.stream, img, proto, src4, port, n, out, allow, counters);
+                               c.stream, img, proto, src4, port, n, out, allow);
     }
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !counters) return e;
+    return launch_hist(c, VC_HIST_ACL, out, proto, n, int64_t(img.n_tcp) + img.n_udp, 0,
+                       int64_t(img.n_tcp) + img.n_udp, img.n_tcp, counters);
 }
 
 hipError_t launch_acl_v6(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
@@ -324,8 +303,11 @@ hipError_t launch_acl_v6(const LaunchCfg& c, const AclImage& img, const uint8_t*
     if (n <= 0) return hipSuccess;
     if (!aligned(src6, 16)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(vcd::acl_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
-                       c.stream, img, proto, src6, port, n, out, allow, counters);
-    return hipGetLastError();
+                       c.stream, img, proto, src6, port, n, out, allow);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !counters) return e;
+    return launch_hist(c, VC_HIST_ACL, out, proto, n, int64_t(img.n_tcp) + img.n_udp, 0,
+                       int64_t(img.n_tcp) + img.n_udp, img.n_tcp, counters);
 }
 
 hipError_t launch_route_v4(const LaunchCfg& c, const TrieImage& t, const uint32_t* dst4, int64_t n,
@@ -334,13 +316,14 @@ hipError_t launch_route_v4(const LaunchCfg& c, const TrieImage& t, const uint32_
     if (n <= 0) return hipSuccess;
     if (aligned(dst4, 16) && aligned(out, 16))
         hipLaunchKernelGGL(vcd::route_v4_kernel, dim3(grid_for(c, (n + 3) / 4, 8)),
-                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.root_bits, dst4, n, out,
-                           counters, rule_base, none_at);
+                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.root_bits, dst4, n, out);
     else
         hipLaunchKernelGGL(vcd::route_v4_kernel_scalar, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock),
-                           0, c.stream, t.nodes, t.root_bits, dst4, n, out, counters, rule_base,
-                           none_at);
-    return hipGetLastError();
+                           0, c.stream, t.nodes, t.root_bits, dst4, n, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !counters) return e;
+    return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, t.n_rules, rule_base, none_at, 0,
+                       counters);
 }
 
 hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t* dst6, int64_t n,
@@ -349,8 +332,11 @@ hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t
     if (n <= 0) return hipSuccess;
     if (!aligned(dst6, 16)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(vcd::route_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
-                       c.stream, t.nodes, t.root_bits, dst6, n, out, counters, rule_base, none_at);
-    return hipGetLastError();
+                       c.stream, t.nodes, t.root_bits, dst6, n, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !counters) return e;
+    return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, t.n_rules, rule_base, none_at, 0,
+                       counters);
 }
 
 hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
@@ -372,13 +358,22 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
         hipLaunchKernelGGL(vcd::pipeline_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock),
                            size_t(words) * 4, c.stream, acl, r4.nodes, r4.root_bits, proto, src4,
                            dst4, dport, host_id, pool_group, n_pool, n, out_acl, out_route, out_group,
-                           out_allow, acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
+                           out_allow);
     } else
         hipLaunchKernelGGL(vcd::pipeline_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
                            c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,
-                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group, out_allow,
-                           acl_cnt, route_cnt, route_none_at, group_cnt, n_groups);
-    return hipGetLastError();
+                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group, out_allow);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && acl_cnt)
+        e = launch_hist(c, VC_HIST_ACL, out_acl, proto, n, int64_t(acl.n_tcp) + acl.n_udp, 0,
+                        int64_t(acl.n_tcp) + acl.n_udp, acl.n_tcp, acl_cnt);
+    if (e == hipSuccess && route_cnt)
+        e = launch_hist(c, VC_HIST_PLAIN, out_route, nullptr, n, r4.n_rules, 0, route_none_at, 0,
+                        route_cnt);
+    if (e == hipSuccess && group_cnt)
+        e = launch_hist(c, VC_HIST_PLAIN, out_group, nullptr, n, n_groups, 0, n_groups, 0,
+                        group_cnt);
+    return e;
 }
 
 }  // namespace vc

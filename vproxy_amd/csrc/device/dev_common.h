@@ -32,14 +32,4 @@ VC_HD int32_t out_index(uint32_t v) {
     return v == VC_NONE ? -1 : int32_t(v);
 }
 
-// Hit counter for a hot bin (default verdict, null route, no group): the
-// wave's lanes vote and one lane adds the count, so half a batch landing on
-// one counter costs one atomic per wave instead of one per lane.  Must be
-// reached by every active lane (pred may differ per lane).
-__device__ __forceinline__ void count_hot(unsigned long long* c, bool pred) {
-    const unsigned long long m = __ballot(pred);
-    if (m && pred && int(__lane_id()) == __ffsll(static_cast<long long>(m)) - 1)
-        atomicAdd(c, static_cast<unsigned long long>(__popcll(m)));
-}
-
 }  // namespace vcd

@@ -21,8 +21,7 @@ __global__ __launch_bounds__(kHintBlock) void hint_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
     const uint8_t* __restrict__ uri_blob, const uint32_t* __restrict__ uri_off,
-    const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out,
-    unsigned long long* __restrict__ cnt) {
+    const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         DStr h{nullptr, -1}, u{nullptr, -1};
@@ -37,17 +36,13 @@ __global__ __launch_bounds__(kHintBlock) void hint_kernel(
         const int p = port ? int(port[i]) : 0;
         const int32_t g = search_for_group(img, format_host(h), p, format_uri(u));
         out[i] = g;
-        if (cnt) {
-            count_hot(cnt + img.n_groups, g < 0);
-            if (g >= 0) atomicAdd(cnt + g, 1ull);
-        }
     }
 }
 
 __global__ __launch_bounds__(kHintBlock) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
-    int32_t* __restrict__ value, unsigned long long* __restrict__ cnt) {
+    int32_t* __restrict__ value) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t a = qoff[i], e = qoff[i + 1];
@@ -69,10 +64,8 @@ __global__ __launch_bounds__(kHintBlock) void dns_kernel(
         if (g >= 0) {
             kind[i] = VC_DNS_GROUP;
             value[i] = g;
-            if (cnt) atomicAdd(cnt + g, 1ull);
             continue;
         }
-        if (cnt) atomicAdd(cnt + img.n_groups, 1ull);
         // (4) IP literal, :140-149
         if (d_is_ip_literal(q, dn)) {
             kind[i] = VC_DNS_IP_LITERAL;
@@ -101,9 +94,11 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
     int64_t cap = int64_t(c.num_cus) * 16;
     int grid = int(want < cap ? want : cap);
     hipLaunchKernelGGL(vcd::hint_kernel, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream, img,
-                       host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null, n, out,
+                       host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null, n, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !counters) return e;
+    return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, img.n_groups, 0, img.n_groups, 0,
                        counters);
-    return hipGetLastError();
 }
 
 hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintImage& hints,
@@ -114,8 +109,11 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
     int64_t cap = int64_t(c.num_cus) * 16;
     int grid = int(want < cap ? want : cap);
     hipLaunchKernelGGL(vcd::dns_kernel, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream, hosts,
-                       hints, qblob, qoff, n, kind, value, group_counters);
-    return hipGetLastError();
+                       hints, qblob, qoff, n, kind, value);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !group_counters) return e;
+    return launch_hist(c, VC_HIST_DNS, value, kind, n, hints.n_groups, 0, hints.n_groups, 0,
+                       group_counters);
 }
 
 }  // namespace vc

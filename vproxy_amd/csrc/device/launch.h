@@ -8,6 +8,11 @@
 
 namespace vc {
 
+// hit-counter histogram modes (counters.hip)
+#define VC_HIST_PLAIN 0   // v >= 0 -> base + v, v < 0 -> null_bin
+#define VC_HIST_ACL 1     // aux = proto: tcp v -> v, udp v -> nt + v, -1 -> null_bin (+1 udp)
+#define VC_HIST_DNS 2     // aux = kind: counted only where kind == VC_DNS_GROUP
+
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
     hipStream_t stream = nullptr;
@@ -42,5 +47,11 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
                               unsigned long long* acl_cnt, unsigned long long* route_cnt,
                               int64_t route_none_at, unsigned long long* group_cnt,
                               int32_t n_groups);
+
+// Histogram a classify output array into uint64 hit counters.  Values in
+// [0, nval) land at counters[base + v]; nulls at counters[null_bin].
+hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const uint8_t* aux,
+                       int64_t n, int64_t nval, int64_t base, int64_t null_bin, int32_t nt,
+                       unsigned long long* counters);
 
 }  // namespace vc
