@@ -30,6 +30,8 @@ HintImage hint_img(const vc::HintBuilt& b) {
     h.blob = b.blob.data();
     h.host_slots = reinterpret_cast<const KeySlot*>(b.host_slots.data());
     h.uri_slots = reinterpret_cast<const KeySlot*>(b.uri_slots.data());
+    h.host_tags = b.host_tags.data();
+    h.uri_tags = b.uri_tags.data();
     h.lists = b.lists.data();
     h.port_mins = reinterpret_cast<const PortMin*>(b.port_mins.data());
     h.port_min_off = b.port_min_off.data();

@@ -413,6 +413,8 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     s->img.blob = s->upload(b.blob, &e);
     s->img.host_slots = reinterpret_cast<const KeySlot*>(s->upload(b.host_slots, &e));
     s->img.uri_slots = reinterpret_cast<const KeySlot*>(s->upload(b.uri_slots, &e));
+    s->img.host_tags = s->upload(b.host_tags, &e);
+    s->img.uri_tags = s->upload(b.uri_tags, &e);
     s->img.lists = s->upload(b.lists, &e);
     s->img.port_mins = reinterpret_cast<const PortMin*>(s->upload(b.port_mins, &e));
     s->img.port_min_off = s->upload(b.port_min_off, &e);
@@ -484,6 +486,7 @@ int vc_compile_hosts(vc_ctx* ctx, const char* const* keys, const int32_t* key_le
     hipError_t e = hipSuccess;
     s->img.blob = s->upload(b.blob, &e);
     s->img.slots = reinterpret_cast<const KeySlot*>(s->upload(b.slots, &e));
+    s->img.tags = s->upload(b.tags, &e);
     s->img.mask = static_cast<uint32_t>(b.slots.size() - 1);
     s->img.n = b.n;
     if (e != hipSuccess) return hip_fail(e, "hosts upload");

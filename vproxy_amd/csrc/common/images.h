@@ -60,16 +60,18 @@ struct RouteImage {
 // ---------------------------------------------------------------------------
 // Upstream hint matching + DNS hosts.
 //
-// Keys are hashed with 64-bit FNV-1a.  Host keys (merged hint-host H) hash
+// Keys are hashed with 32-bit FNV-1a.  Host keys (merged hint-host H) hash
 // the string right-to-left, so one right-to-left scan of a query host yields
 // the hash of every dot-suffix incrementally (a reversed-suffix index).  URI
 // keys (merged hint-uri U) and hosts-map keys hash left-to-right, so one scan
 // of a URI yields the hash of every prefix.  Open addressing,
-// power-of-two capacity, linear probing; an empty slot has key_len == -1.
-// Every hash hit is confirmed by a full byte compare.
+// power-of-two capacity, linear probing.  Probes walk a compact tag array
+// (4 B per slot, hash | 1, 0 = empty; L2-resident for 100k keys) and only
+// read the 32-byte slot on a tag hit; every tag hit is confirmed by a full
+// byte compare of the key.
 // ---------------------------------------------------------------------------
 struct KeySlot {                   // 32 bytes
-    uint64_t hash;
+    uint64_t hash;                 // 32-bit FNV-1a in the low word
     int32_t key_len;               // -1 = empty slot
     uint32_t key_off;              // into HintImage.blob
     int32_t a;                     // host table: min handle index (any port); hosts: value
@@ -96,6 +98,8 @@ struct HintImage {
     const uint8_t* blob;           // key / annotation bytes
     const KeySlot* host_slots;     // keyed by H (reverse hash)
     const KeySlot* uri_slots;      // keyed by U (forward hash)
+    const uint32_t* host_tags;     // hash | 1 per host slot, 0 = empty
+    const uint32_t* uri_tags;
     const uint32_t* lists;         // member lists
     const PortMin* port_mins;      // per host key: distinct nonzero hint-ports
     const uint32_t* port_min_off;  // 2 words per host slot: (off, cnt) into port_mins
@@ -111,6 +115,7 @@ struct HintImage {
 struct HostsImage {
     const uint8_t* blob;
     const KeySlot* slots;          // keyed by the exact qname (forward hash); value in .a
+    const uint32_t* tags;
     uint32_t mask;
     int32_t n;
 };

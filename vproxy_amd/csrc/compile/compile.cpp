@@ -337,12 +337,14 @@ uint32_t append_blob(std::vector<uint8_t>* blob, const char* s, int len) {
     return off;
 }
 
-// insert into an open-addressing table; returns the slot index
-uint32_t table_insert(std::vector<KeySlotH>* t, uint64_t h, const KeySlotH& v) {
+// insert into an open-addressing table (slots + tags); returns the slot index
+uint32_t table_insert(std::vector<KeySlotH>* t, std::vector<uint32_t>* tags, uint32_t h,
+                      const KeySlotH& v) {
     uint32_t mask = static_cast<uint32_t>(t->size() - 1);
-    uint32_t s = static_cast<uint32_t>(h) & mask;
+    uint32_t s = h & mask;
     while ((*t)[s].key_len != -1) s = (s + 1) & mask;
     (*t)[s] = v;
+    (*tags)[s] = h | 1u;
     return s;
 }
 
@@ -401,6 +403,8 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
     KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
     out->host_slots.assign(pow2_cap(host_order.size()), empty);
     out->uri_slots.assign(pow2_cap(uri_order.size()), empty);
+    out->host_tags.assign(out->host_slots.size(), 0);
+    out->uri_tags.assign(out->uri_slots.size(), 0);
     out->port_min_off.assign(out->host_slots.size() * 2, 0);
     for (auto& k : host_order) {
         KeyAcc& acc = hostk[k];
@@ -413,7 +417,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         s.list_off = static_cast<uint32_t>(out->lists.size());
         s.list_cnt = static_cast<uint32_t>(acc.members.size());
         out->lists.insert(out->lists.end(), acc.members.begin(), acc.members.end());
-        uint32_t slot = table_insert(&out->host_slots, s.hash, s);
+        uint32_t slot = table_insert(&out->host_slots, &out->host_tags, uint32_t(s.hash), s);
         out->port_min_off[2 * slot] = static_cast<uint32_t>(out->port_mins.size() / 2);
         out->port_min_off[2 * slot + 1] = static_cast<uint32_t>(acc.port_min.size());
         for (auto& pm : acc.port_min) {
@@ -433,7 +437,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         s.list_off = static_cast<uint32_t>(out->lists.size());
         s.list_cnt = static_cast<uint32_t>(acc.members.size());
         out->lists.insert(out->lists.end(), acc.members.begin(), acc.members.end());
-        uint32_t slot = table_insert(&out->uri_slots, s.hash, s);
+        uint32_t slot = table_insert(&out->uri_slots, &out->uri_tags, uint32_t(s.hash), s);
         if (k == "*") out->uri_star_slot = static_cast<int32_t>(slot);
     }
     if (out->blob.empty()) out->blob.push_back(0);
@@ -448,6 +452,7 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
     *out = HostsBuilt{};
     KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
     out->slots.assign(pow2_cap(static_cast<size_t>(n)), empty);
+    out->tags.assign(out->slots.size(), 0);
     std::unordered_map<std::string, int> seen;
     for (int i = 0; i < n; ++i) {
         if (key_lens[i] < 0 || (!keys[i] && key_lens[i] > 0)) return VC_EINVAL;
@@ -462,7 +467,7 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
         s.b = 0;
         s.list_off = 0;
         s.list_cnt = 0;
-        table_insert(&out->slots, s.hash, s);
+        table_insert(&out->slots, &out->tags, uint32_t(s.hash), s);
         ++out->n;
     }
     if (out->blob.empty()) out->blob.push_back(0);

@@ -49,6 +49,7 @@ struct KeySlotH {                    // host mirror of KeySlot
 struct HintBuilt {
     std::vector<uint8_t> blob;
     std::vector<KeySlotH> host_slots, uri_slots;
+    std::vector<uint32_t> host_tags, uri_tags;
     std::vector<uint32_t> lists;
     std::vector<int32_t> port_mins;      // (port, idx) pairs
     std::vector<uint32_t> port_min_off;  // (off, cnt) per host slot
@@ -62,21 +63,22 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out);
 struct HostsBuilt {
     std::vector<uint8_t> blob;
     std::vector<KeySlotH> slots;
+    std::vector<uint32_t> tags;
     int32_t n = 0;
 };
 
 int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
                 HostsBuilt* out);
 
-// FNV-1a 64 over bytes, forwards and right-to-left (must match device code).
-inline uint64_t fnv_fwd(const uint8_t* p, size_t n) {
-    uint64_t h = 14695981039346656037ull;
-    for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+// 32-bit FNV-1a over bytes, forwards and right-to-left (must match device code).
+inline uint32_t fnv_fwd(const uint8_t* p, size_t n) {
+    uint32_t h = 2166136261u;
+    for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 16777619u; }
     return h;
 }
-inline uint64_t fnv_rev(const uint8_t* p, size_t n) {
-    uint64_t h = 14695981039346656037ull;
-    for (size_t i = n; i-- > 0;) { h ^= p[i]; h *= 1099511628211ull; }
+inline uint32_t fnv_rev(const uint8_t* p, size_t n) {
+    uint32_t h = 2166136261u;
+    for (size_t i = n; i-- > 0;) { h ^= p[i]; h *= 16777619u; }
     return h;
 }
 

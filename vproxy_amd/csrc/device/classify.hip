@@ -199,36 +199,96 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel(
 // ---------------------------------------------------------------------------
 // Combined pipeline (C5): ACL(src, dport) -> route(dst) -> pool group gather
 // ---------------------------------------------------------------------------
-template <bool kLds>
+__device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, uint32_t e,
+                                                uint32_t d) {
+    int shift = 32 - rb;
+    while (e & VC_PTR) {
+        shift -= 8;
+        e = nodes[(1u << rb) + (e & ~VC_PTR) * 256u + ((d >> shift) & 255u)];
+    }
+    return e;
+}
+
+// One packet through ACL -> route -> pool group (scalar form, also the tail).
+__device__ __forceinline__ void pipeline_one(
+    const AclImage& img, const AclV4Ctx& a, const uint32_t* nodes, int rb, const uint8_t* proto,
+    const uint32_t* src, const uint32_t* dst, const uint16_t* dport, const uint32_t* host_id,
+    const int32_t* pool_group, int64_t n_pool, int64_t i, int32_t* out_acl, int32_t* out_route,
+    int32_t* out_group, uint8_t* out_allow) {
+    const uint32_t d = dst[i];
+    const uint32_t e = nodes[d >> (32 - rb)];
+    const uint32_t h = host_id[i];
+    const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
+    const bool t = proto[i] == VC_PROTO_TCP;
+    const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
+    acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i);
+    route_emit(route_chase(nodes, rb, e, d), out_route + i);
+    out_group[i] = grp;
+}
+
+// kVec: 4 packets per lane per step -- 16-byte SoA loads/stores and four
+// independent route-root and pool gathers in flight before the ACL search.
+template <bool kLds, bool kVec>
 __global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
     AclImage img, const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ proto,
     const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
     const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
     const int32_t* __restrict__ pool_group, int64_t n_pool, int64_t n,
-    int32_t* __restrict__ out_acl,
-    int32_t* __restrict__ out_route, int32_t* __restrict__ out_group,
-    uint8_t* __restrict__ out_allow) {
+    int32_t* __restrict__ out_acl, int32_t* __restrict__ out_route,
+    int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (kLds) stage_bounds(img, lds);
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-        // issue the independent global probes first (route root, pool gather)
-        const uint32_t d = dst[i];
-        uint32_t e = nodes[d >> (32 - rb)];
-        const uint32_t h = host_id[i];
-        const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
-        const bool t = proto[i] == VC_PROTO_TCP;
-        const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
-        acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i);
-        int shift = 32 - rb;
-        while (e & VC_PTR) {
-            shift -= 8;
-            e = nodes[(1u << rb) + (e & ~VC_PTR) * 256u + ((d >> shift) & 255u)];
-        }
-        route_emit(e, out_route + i);
-        out_group[i] = grp;
+    if (!kVec) {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+            pipeline_one(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group, n_pool, i,
+                         out_acl, out_route, out_group, out_allow);
+        return;
     }
+    const int64_t n4 = n >> 2;
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
+        const uint4 d4 = reinterpret_cast<const uint4*>(dst)[g];
+        const uint4 h4 = reinterpret_cast<const uint4*>(host_id)[g];
+        const uint4 s4 = reinterpret_cast<const uint4*>(src)[g];
+        const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
+        const uint2 pt = reinterpret_cast<const uint2*>(dport)[g];
+        const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
+        const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
+        const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
+        const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
+        uint32_t e[4];
+        int32_t grp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = nodes[d[k] >> (32 - rb)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) grp[k] = int64_t(h[k]) < n_pool ? pool_group[h[k]] : -1;
+        uint32_t v[4];
+        bool tcp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+            v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+        }
+        int4 oa, orr;
+        uint32_t al = 0;
+        int32_t* pa = reinterpret_cast<int32_t*>(&oa);
+        int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint8_t b = 0;
+            acl_emit(img, tcp[k], v[k], out_allow ? &b : nullptr, pa + k);
+            al |= uint32_t(b) << (8 * k);
+            pr_[k] = out_index(route_chase(nodes, rb, e[k], d[k]));
+        }
+        reinterpret_cast<int4*>(out_acl)[g] = oa;
+        reinterpret_cast<int4*>(out_route)[g] = orr;
+        reinterpret_cast<int4*>(out_group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+        if (out_allow) reinterpret_cast<uint32_t*>(out_allow)[g] = al;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3))
+        pipeline_one(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group, n_pool,
+                     (n4 << 2) + threadIdx.x, out_acl, out_route, out_group, out_allow);
 }
 
 }  // namespace vcd
@@ -352,17 +412,25 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
     const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
     const bool lds = words <= kLdsWords;
     const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
-    const int grid = grid_for(c, n, per_cu);
-    if (lds) {
-        allow_lds(vcd::pipeline_v4_kernel<true>);
-        hipLaunchKernelGGL(vcd::pipeline_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock),
-                           size_t(words) * 4, c.stream, acl, r4.nodes, r4.root_bits, proto, src4,
-                           dst4, dport, host_id, pool_group, n_pool, n, out_acl, out_route, out_group,
-                           out_allow);
-    } else
-        hipLaunchKernelGGL(vcd::pipeline_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
-                           c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,
-                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group, out_allow);
+    const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(dst4, 16) &&
+                     aligned(dport, 8) && aligned(host_id, 16) && aligned(out_acl, 16) &&
+                     aligned(out_route, 16) && aligned(out_group, 16) &&
+                     (!out_allow || aligned(out_allow, 4));
+    const int grid = grid_for(c, vec ? (n + 3) / 4 : n, per_cu);
+    const size_t shmem = lds ? size_t(words) * 4 : 0;
+#define VC_PIPE(L, V)                                                                              \
+    do {                                                                                           \
+        if (L) allow_lds(vcd::pipeline_v4_kernel<L, V>);                                           \
+        hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V>), dim3(grid), dim3(vcd::kBlock), shmem,  \
+                           c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,        \
+                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group,         \
+                           out_allow);                                                             \
+    } while (0)
+    if (lds && vec) VC_PIPE(true, true);
+    else if (lds) VC_PIPE(true, false);
+    else if (vec) VC_PIPE(false, true);
+    else VC_PIPE(false, false);
+#undef VC_PIPE
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && acl_cnt)
         e = launch_hist(c, VC_HIST_ACL, out_acl, proto, n, int64_t(acl.n_tcp) + acl.n_udp, 0,

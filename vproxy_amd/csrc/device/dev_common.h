@@ -13,10 +13,10 @@
 
 namespace vcd {
 
-constexpr uint64_t kFnvBasis = 14695981039346656037ull;
-constexpr uint64_t kFnvPrime = 1099511628211ull;
+constexpr uint32_t kFnvBasis = 2166136261u;   // 32-bit FNV-1a
+constexpr uint32_t kFnvPrime = 16777619u;
 
-VC_HD uint64_t fnv_step(uint64_t h, uint32_t c) {
+VC_HD uint32_t fnv_step(uint32_t h, uint32_t c) {
     return (h ^ c) * kFnvPrime;
 }
 

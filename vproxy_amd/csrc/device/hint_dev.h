@@ -176,16 +176,21 @@ VC_HD KeySlot load_slot(const KeySlot* t, uint32_t s) {
     return k;
 }
 
-// slot index of key (p, n) with hash h, or -1
-VC_HDN int probe(const KeySlot* t, uint32_t mask, const uint8_t* blob, uint64_t h,
-                     const uint8_t* p, int n, KeySlot* out) {
-    uint32_t s = uint32_t(h) & mask;
+// slot index of key (p, n) with hash h, or -1.  Walks the 4-byte tag array;
+// the 32-byte slot and the key bytes are read only on a tag hit.
+VC_HDN int probe(const uint32_t* tags, const KeySlot* t, uint32_t mask, const uint8_t* blob,
+                 uint32_t h, const uint8_t* p, int n, KeySlot* out) {
+    const uint32_t want = h | 1u;
+    uint32_t s = h & mask;
     for (;;) {
-        KeySlot k = load_slot(t, s);
-        if (k.key_len < 0) return -1;
-        if (k.hash == h && k.key_len == n && bytes_eq(blob + k.key_off, p, n)) {
-            *out = k;
-            return int(s);
+        const uint32_t tag = tags[s];
+        if (tag == 0) return -1;
+        if (tag == want) {
+            KeySlot k = load_slot(t, s);
+            if (k.key_len == n && bytes_eq(blob + k.key_off, p, n)) {
+                *out = k;
+                return int(s);
+            }
         }
         s = (s + 1) & mask;
     }
@@ -209,19 +214,19 @@ VC_HD uint32_t pick(const HintImage& img, int slot, const KeySlot& k, int port) 
 // and within a level the lowest handle index wins (strict '>' scan).
 VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
     if (host.n < 0) return -1;
-    uint64_t h = kFnvBasis;
+    uint32_t h = kFnvBasis;
     uint32_t best_suffix = VC_NONE;
     KeySlot k;
     for (int j = host.n - 1; j >= 0; --j) {
         const uint8_t c = host.p[j];
         if (c == '.') {   // host.endsWith("." + H) with H = host[j+1..]
-            int s = probe(img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
+            int s = probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
                           host.n - j - 1, &k);
             if (s >= 0) { uint32_t c = pick(img, s, k, port); best_suffix = c < best_suffix ? c : best_suffix; }
         }
         h = fnv_step(h, c);
     }
-    int s = probe(img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k);
+    int s = probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k);
     if (s >= 0) {
         uint32_t e = pick(img, s, k, port);
         if (e != VC_NONE) return int32_t(e);
@@ -286,24 +291,24 @@ VC_HDN int32_t hint_general(const HintImage& img, DStr host, int port, DStr uri)
     Best b;
     KeySlot k;
     if (host.n >= 0) {
-        uint64_t h = kFnvBasis;
+        uint32_t h = kFnvBasis;
         for (int j = host.n - 1; j >= 0; --j) {
             const uint8_t c = host.p[j];
-            if (c == '.' && probe(img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
+            if (c == '.' && probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
                                   host.n - j - 1, &k) >= 0)
                 consider_list(img, k, host, port, uri, &b);
             h = fnv_step(h, c);
         }
-        if (probe(img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k) >= 0)
+        if (probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k) >= 0)
             consider_list(img, k, host, port, uri, &b);
         if (img.wildcard_slot >= 0)
             consider_list(img, load_slot(img.host_slots, uint32_t(img.wildcard_slot)), host, port,
                           uri, &b);
     }
     if (uri.n >= 0) {
-        uint64_t h = kFnvBasis;
+        uint32_t h = kFnvBasis;
         for (int j = 0; j <= uri.n; ++j) {
-            if (probe(img.uri_slots, img.uri_mask, img.blob, h, uri.p, j, &k) >= 0)
+            if (probe(img.uri_tags, img.uri_slots, img.uri_mask, img.blob, h, uri.p, j, &k) >= 0)
                 consider_list(img, k, host, port, uri, &b);
             if (j < uri.n) h = fnv_step(h, uri.p[j]);
         }
