@@ -229,29 +229,39 @@ def main():
     torch.cuda.synchronize()
     log("packets generated (%d per GPU), setup %.1fs" % (B, time.time() - t_setup))
 
-    clf.counters_enable(not args.no_counters)
+    # Hit counters: the library's histogram pass over this batch's outputs,
+    # scheduled explicitly after the pipeline so each kernel is timed alone.
+    clf.counters_enable(False)
+    count = not args.no_counters
     cnt = []
     for kind in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP):
         ptr, n = clf.counters_device(kind)
         cnt.append((ptr, n, torch.zeros(n, dtype=torch.int64, device=dev)))
+    stream = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     ev = []
 
     def step(timed):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
         if timed:
             e[0].record()
         V.check(V.lib().vc_hint_search_dev(clf.h, C.c_void_p(pool_blob.data_ptr()),
                                            C.c_void_p(pool_off.data_ptr()), None, None, None,
                                            None, None, args.pool,
-                                           C.c_void_p(pool_out.data_ptr()),
-                                           C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+                                           C.c_void_p(pool_out.data_ptr()), stream()))
         if timed:
             e[1].record()
             e[2].record()
         clf.pipeline_v4(proto, src, dst, dport, hid, pool_out, outs=outs)
         if timed:
             e[3].record()
+            e[4].record()
+        if count:
+            clf.counters_add(V.COUNTERS_ACL, outs[0], aux=proto)
+            clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
+            clf.counters_add(V.COUNTERS_GROUP, outs[2])
+        if timed:
+            e[5].record()
             ev.append(e)
         if world > 1:
             import torch.distributed as dist
@@ -281,6 +291,7 @@ def main():
 
     hint_ms = float(np.mean([x[0].elapsed_time(x[1]) for x in ev]))
     pipe_ms = float(np.mean([x[2].elapsed_time(x[3]) for x in ev]))
+    count_ms = float(np.mean([x[4].elapsed_time(x[5]) for x in ev]))
     total = float(B) * world * args.steps
     value = total / elapsed / 1e6
     # roofline of the dominant kernel, algorithmic bytes only
@@ -296,7 +307,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic("c5"),
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
-                                "pipeline_v4_kernel": round(pipe_ms, 4)}}
+                                "pipeline_v4_kernel": round(pipe_ms, 4),
+                                "hit_counter_passes": round(count_ms, 4)}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)

@@ -202,6 +202,15 @@ int vc_counters_enable(vc_ctx *ctx, int on);
 int vc_counters_device(vc_ctx *ctx, int kind, uint64_t **dev_ptr, int64_t *n);
 int vc_counters_read(vc_ctx *ctx, int kind, uint64_t *host, int64_t n);
 int vc_counters_reset(vc_ctx *ctx);
+/* Add the hits of an already-computed output array to the counters of the
+ * current snapshot (what vc_counters_enable does automatically after each
+ * classify call; exposed so callers can schedule the counting pass):
+ *   VC_COUNTERS_ACL   out = out_idx,   aux = proto (required)
+ *   VC_COUNTERS_ROUTE out = route out, family = 4 or 6, aux = NULL
+ *   VC_COUNTERS_GROUP out = group out (hint / pipeline), aux = NULL; or
+ *                     out = DNS out_value with aux = DNS out_kind. */
+int vc_counters_add_dev(vc_ctx *ctx, int kind, const int32_t *out, const uint8_t *aux, int family,
+                        int64_t n, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Control-plane mirrors (host only, no GPU): the reference's list-ordering  */

@@ -233,7 +233,15 @@ def test_route_c3_full_size(clf):
     v4 = np.frombuffer(bytes(a4)[:n4 * 40], W.NET_DT)
     v6 = np.frombuffer(bytes(a6)[:n6 * 40], W.NET_DT)
     q4 = W.v4_lookups(net, plen, 16 << 20, 41)
+    clf.counters_enable(True)
+    clf.counters_reset()
     got4 = clf.route_v4(torch.from_numpy(q4).cuda()).cpu().numpy()
+    torch.cuda.synchronize()
+    # hit counters (bucketed histogram path: ~30 chunks of 32K rules)
+    cr = clf.counters_read(V.COUNTERS_ROUTE)
+    exp = np.bincount(np.where(got4 >= 0, got4, n4 + n6), minlength=n4 + n6 + 2)
+    np.testing.assert_array_equal(cr, exp.astype(np.uint64))
+    clf.counters_enable(False)
     s = np.random.default_rng(1).integers(0, len(q4), 3000)
     np.testing.assert_array_equal(got4[s], O.rt_batch_v4_np(v4, q4[s], nthreads=THREADS))
     # every hit's prefix contains the address; 90% of lookups were drawn inside one
@@ -287,7 +295,13 @@ def test_hint_c4_scale(clf):
     rng = np.random.default_rng(3)
     ports = np.where(rng.random(len(names)) < 0.2, rng.integers(1, 65536, len(names)), 0)
     ports = ports.astype(np.uint16)
+    clf.counters_enable(True)
+    clf.counters_reset()
     got = clf.hint_search(names, ports)
+    cg = clf.counters_read(V.COUNTERS_GROUP)
+    exp = np.bincount(np.where(got >= 0, got, len(groups)), minlength=len(groups) + 1)
+    np.testing.assert_array_equal(cg, exp.astype(np.uint64))
+    clf.counters_enable(False)
     og = O.Groups(groups)
     s = rng.integers(0, len(names), 1500)
     want = [O.search_for_group(og, names[i], int(ports[i]), None) for i in s]

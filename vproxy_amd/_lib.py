@@ -119,6 +119,7 @@ def lib():
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]
         L.vc_counters_reset.argtypes = [vp]
+        L.vc_counters_add_dev.argtypes = [vp, i32, vp, vp, i32, i64, vp]
         L.vc_secgroup_new.argtypes = [C.c_char_p, i32, P(vp)]
         L.vc_secgroup_free.argtypes = [vp]
         L.vc_secgroup_set_default.argtypes = [vp, i32]

@@ -496,3 +496,8 @@ class Classifier:
 
     def counters_reset(self):
         check(lib().vc_counters_reset(self.h))
+
+    def counters_add(self, kind, out, aux=None, family=4):
+        """Explicit counting pass over a device output array (torch tensor)."""
+        check(lib().vc_counters_add_dev(self.h, kind, _ptr(out), _ptr(aux), family, len(out),
+                                        _stream()))

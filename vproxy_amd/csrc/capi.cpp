@@ -629,6 +629,41 @@ int vc_counters_reset(vc_ctx* ctx) {
     return e == hipSuccess ? VC_OK : hip_fail(e, "counter reset");
 }
 
+int vc_counters_add_dev(vc_ctx* ctx, int kind, const int32_t* out, const uint8_t* aux, int family,
+                        int64_t n, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && !out)) return fail(VC_EINVAL, "bad batch arguments");
+    if (n == 0) return VC_OK;
+    hipError_t e = hipSuccess;
+    vc::LaunchCfg c = ctx->cfg(stream);
+    if (kind == VC_COUNTERS_ACL) {
+        auto s = ctx->get(ctx->acl);
+        if (!s) return fail(VC_ESTATE, "no SecurityGroup compiled");
+        if (!aux) return fail(VC_EINVAL, "ACL counters need the proto array");
+        const int64_t nr = int64_t(s->img.n_tcp) + s->img.n_udp;
+        e = vc::launch_hist(c, VC_HIST_ACL, out, aux, n, nr, 0, nr, s->img.n_tcp, s->counters);
+    } else if (kind == VC_COUNTERS_ROUTE) {
+        auto s = ctx->get(ctx->route);
+        if (!s) return fail(VC_ESTATE, "no RouteTable compiled");
+        if (family != 4 && family != 6) return fail(VC_EINVAL, "family must be 4 or 6");
+        const int64_t nn = int64_t(s->n4) + s->n6;
+        e = family == 4 ? vc::launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, s->n4, 0, nn, 0,
+                                          s->counters)
+                        : vc::launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, s->n6, s->n4, nn + 1,
+                                          0, s->counters);
+    } else if (kind == VC_COUNTERS_GROUP) {
+        auto s = ctx->get(ctx->hint);
+        if (!s) return fail(VC_ESTATE, "no Upstream compiled");
+        const int32_t ng = s->img.n_groups;
+        e = vc::launch_hist(c, aux ? VC_HIST_DNS : VC_HIST_PLAIN, out, aux, n, ng, 0, ng, 0,
+                            s->counters);
+    } else {
+        return fail(VC_EINVAL, "unknown counter kind");
+    }
+    return e == hipSuccess ? VC_OK : hip_fail(e, "counter pass");
+}
+
 // ---------------------------------------------------------------------------
 // Control-plane mirrors
 // ---------------------------------------------------------------------------
