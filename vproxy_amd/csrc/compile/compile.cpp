@@ -331,17 +331,23 @@ uint32_t pow2_cap(size_t n) {
     return c;
 }
 
+// Strings go into the blob 16-byte aligned and zero padded to a multiple of
+// 16, so the device compares keys one uint4 at a time (hint_dev.h key_eq).
 uint32_t append_blob(std::vector<uint8_t>* blob, const char* s, int len) {
+    blob->resize((blob->size() + 15) & ~size_t(15), 0);
     uint32_t off = static_cast<uint32_t>(blob->size());
     blob->insert(blob->end(), s, s + len);
+    blob->resize((blob->size() + 15) & ~size_t(15), 0);
     return off;
 }
 
-// insert into an open-addressing table (slots + tags); returns the slot index
+// insert into an open-addressing table (slots + tags); returns the slot index.
+// Linear probing that starts at the 4-slot group of the hash, so a lookup
+// reads one 16-byte tag group per step (hint_dev.h probe).
 uint32_t table_insert(std::vector<KeySlotH>* t, std::vector<uint32_t>* tags, uint32_t h,
                       const KeySlotH& v) {
     uint32_t mask = static_cast<uint32_t>(t->size() - 1);
-    uint32_t s = h & mask;
+    uint32_t s = h & mask & ~3u;
     while ((*t)[s].key_len != -1) s = (s + 1) & mask;
     (*t)[s] = v;
     (*tags)[s] = h | 1u;
@@ -440,7 +446,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         uint32_t slot = table_insert(&out->uri_slots, &out->uri_tags, uint32_t(s.hash), s);
         if (k == "*") out->uri_star_slot = static_cast<int32_t>(slot);
     }
-    if (out->blob.empty()) out->blob.push_back(0);
+    if (out->blob.empty()) out->blob.assign(16, 0);
     if (out->lists.empty()) out->lists.push_back(0);
     if (out->port_mins.empty()) { out->port_mins.push_back(0); out->port_mins.push_back(0); }
     if (out->groups.empty()) out->groups.assign(6, 0);
@@ -470,7 +476,7 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
         table_insert(&out->slots, &out->tags, uint32_t(s.hash), s);
         ++out->n;
     }
-    if (out->blob.empty()) out->blob.push_back(0);
+    if (out->blob.empty()) out->blob.assign(16, 0);
     return VC_OK;
 }
 

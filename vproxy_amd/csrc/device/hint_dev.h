@@ -176,23 +176,51 @@ VC_HD KeySlot load_slot(const KeySlot* t, uint32_t s) {
     return k;
 }
 
-// slot index of key (p, n) with hash h, or -1.  Walks the 4-byte tag array;
-// the 32-byte slot and the key bytes are read only on a tag hit.
+// key (16-byte aligned, zero padded in the blob) == query bytes p[0, n)?
+// One uint4 key load per 16 bytes and branch-free byte gathers of the query
+// (LDS when staged), instead of a byte-by-byte loop of dependent loads.
+VC_HD bool key_eq(const uint8_t* key, const uint8_t* q, int n) {
+    for (int base = 0; base < n; base += 16) {
+        const uint4 kw = *reinterpret_cast<const uint4*>(key + base);
+        const uint32_t k[4] = {kw.x, kw.y, kw.z, kw.w};
+        uint32_t diff = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            uint32_t qw = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int i = base + 4 * w + b;
+                qw |= uint32_t(i < n ? q[i] : 0) << (8 * b);
+            }
+            diff |= qw ^ k[w];
+        }
+        if (diff) return false;
+    }
+    return true;
+}
+
+// slot index of key (p, n) with hash h, or -1.  Linear probing from the
+// hash's 4-slot group: one 16-byte tag-group load per step; the 32-byte slot
+// and the key are read only on a tag hit.
 VC_HDN int probe(const uint32_t* tags, const KeySlot* t, uint32_t mask, const uint8_t* blob,
                  uint32_t h, const uint8_t* p, int n, KeySlot* out) {
     const uint32_t want = h | 1u;
-    uint32_t s = h & mask;
+    uint32_t s = h & mask & ~3u;
     for (;;) {
-        const uint32_t tag = tags[s];
-        if (tag == 0) return -1;
-        if (tag == want) {
-            KeySlot k = load_slot(t, s);
-            if (k.key_len == n && bytes_eq(blob + k.key_off, p, n)) {
-                *out = k;
-                return int(s);
+        const uint4 g = *reinterpret_cast<const uint4*>(tags + s);
+        const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (tg[k] == 0) return -1;
+            if (tg[k] == want) {
+                KeySlot ks = load_slot(t, s + k);
+                if (ks.key_len == n && key_eq(blob + ks.key_off, p, n)) {
+                    *out = ks;
+                    return int(s + k);
+                }
             }
         }
-        s = (s + 1) & mask;
+        s = (s + 4) & mask;
     }
 }
 
