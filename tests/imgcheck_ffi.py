@@ -24,6 +24,7 @@ def lib():
                              vp, vp]
         L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
+        L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
         L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
         _lib = L
@@ -79,3 +80,17 @@ def is_ipv6(s):
 def is_ip_literal(s):
     b = s.encode() if isinstance(s, str) else s
     return bool(lib().ic_is_ip_literal(b, len(b)))
+
+
+def dns(pairs, group_arr, ng, qblob, qoff):
+    keys = [k.encode() if isinstance(k, str) else k for k, _ in pairs]
+    karr = (C.c_char_p * max(1, len(keys)))(*keys)
+    kl = np.array([len(k) for k in keys] or [0], np.int32)
+    kv = np.array([v for _, v in pairs] or [0], np.int32)
+    n = len(qoff) - 1
+    kind = np.empty(n, np.uint8)
+    val = np.empty(n, np.int32)
+    rc = lib().ic_dns(karr, P(kl), P(kv), len(keys), P(group_arr), ng, P(qblob), P(qoff), n,
+                      P(kind), P(val))
+    assert rc == 0, rc
+    return kind, val

@@ -4,6 +4,7 @@
 // host with the kernels' own __host__ __device__ probe functions, so compile
 // bugs show up in the CPU test tier before any GPU run.  The product library
 // never contains or calls this code.
+#include <cstring>
 #include <vector>
 
 #include "../../vproxy_amd/csrc/compile/compile.hpp"
@@ -110,6 +111,39 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
         if (hb && !(hn && hn[i])) h = DStr{hb + ho[i], int(ho[i + 1] - ho[i])};
         if (ub && !(un && un[i])) u = DStr{ub + uo[i], int(uo[i + 1] - uo[i])};
         out[i] = search_for_group(img, format_host(h), port ? port[i] : 0, format_uri(u));
+    }
+    return 0;
+}
+
+int ic_dns(const char* const* keys, const int32_t* key_lens, const int32_t* values, int nk,
+           const vc_group_annos* g, int ng, const uint8_t* qb, const uint32_t* qo, int64_t n,
+           uint8_t* kind, int32_t* value) {
+    vc::HostsBuilt hb;
+    vc::HintBuilt b;
+    int rc = vc::build_hosts(keys, key_lens, values, nk, &hb);
+    if (rc == 0) rc = vc::build_hints(g, ng, &b);
+    if (rc) return rc;
+    HintImage img = hint_img(b);
+    HostsImage hosts{hb.blob.data(), reinterpret_cast<const KeySlot*>(hb.slots.data()),
+                     hb.tags.data(), uint32_t(hb.slots.size() - 1), hb.n};
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* q = qb + qo[i];
+        const int qn = int(qo[i + 1] - qo[i]);
+        uint32_t h = kFnvBasis;
+        for (int j = 0; j < qn; ++j) h = fnv_step(h, q[j]);
+        KeySlot k;
+        if (hosts.n > 0 && probe(hosts.tags, hosts.slots, hosts.mask, hosts.blob, h, q, qn, &k) >= 0) {
+            kind[i] = VC_DNS_HOSTS;
+            value[i] = k.a;
+            continue;
+        }
+        const int dn = (qn > 0 && q[qn - 1] == '.') ? qn - 1 : qn;
+        const int32_t gg = hint_host_only(img, format_host(DStr{q, dn}), 0);
+        if (gg >= 0) { kind[i] = VC_DNS_GROUP; value[i] = gg; continue; }
+        if (d_is_ip_literal(q, dn)) { kind[i] = VC_DNS_IP_LITERAL; value[i] = d_count(q, dn, ':') ? 6 : 4; continue; }
+        bool internal = dn >= 13 && std::memcmp(q + dn - 13, ".vproxy.local", 13) == 0;
+        kind[i] = internal ? VC_DNS_INTERNAL : VC_DNS_RECURSIVE;
+        value[i] = 0;
     }
     return 0;
 }

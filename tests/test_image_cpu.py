@@ -163,3 +163,33 @@ def test_device_ip_literal_parser():
     for s in strs:
         assert IC.is_ipv6(s) == (O.parse_ipv6(s) is not None), s
         assert IC.is_ip_literal(s) == O.is_ip_literal(s), s
+
+
+def test_hint_dense_table():
+    """~30k distinct hint-hosts in a 64K-slot table: full 4-slot tag groups,
+    so probes continue past the first group (the batched probe path)."""
+    groups, ghosts = W.gen_groups(30000, 61)
+    arr, ng, keep = group_array(groups)
+    names = W.gen_hostnames(ghosts, 4000, 62)
+    h = pack_strings(names)
+    ports = np.random.default_rng(63).choice(np.array([0, 0, 80, 8080], np.uint16), len(names))
+    got = IC.hint(arr, ng, h, ports, None)
+    og = O.Groups(groups)
+    blob, off = W.pack(names)
+    want = O.hint_batch_np(og, blob, off, ports, nthreads=8)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_dns_image():
+    groups, ghosts = W.gen_groups(20000, 71)
+    arr, ng, keep = group_array(groups)
+    pairs = [(h + ".", i) for i, h in enumerate(ghosts[:5000])] + [("localhost.", 999)]
+    names = W.gen_hostnames(ghosts, 3000, 72, dns=True)
+    names += [b"1.2.3.4.", b"::1.", b"[::1].", b"a.vproxy.local.", b".", b"", b"::ffff:1.2.3.4.",
+              b"::x:1.2.3.4.", b"www.x.com:80."]
+    qb, qo = W.pack(names)
+    kind, val = IC.dns(pairs, arr, ng, qb, qo)
+    og = O.Groups(groups)
+    oh = O.Hosts(pairs)
+    want = [O.dns_classify(oh, og, q) for q in names]
+    assert [(int(k), int(v)) for k, v in zip(kind, val)] == want

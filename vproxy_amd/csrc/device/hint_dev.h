@@ -237,11 +237,35 @@ VC_HD uint32_t pick(const HintImage& img, int slot, const KeySlot& k, int port) 
     return v;
 }
 
-// searchForGroup for hints whose uri is null (or no group has a hint-uri):
-// level = hostLevel << 10, so exact (3) beats any suffix (2) beats "*" (1),
-// and within a level the lowest handle index wins (strict '>' scan).
-VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
-    if (host.n < 0) return -1;
+// Continue a probe at group start `s` whose 16-byte tag group `g` is already
+// loaded (linear probing moves on only when that group is full of other keys).
+VC_HDN int probe_from(const uint32_t* tags, const KeySlot* t, uint32_t mask, const uint8_t* blob,
+                      uint32_t h, const uint8_t* p, int n, uint32_t s, uint4 g, KeySlot* out) {
+    const uint32_t want = h | 1u;
+    for (;;) {
+        const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (tg[k] == 0) return -1;
+            if (tg[k] == want) {
+                KeySlot ks = load_slot(t, s + k);
+                if (ks.key_len == n && key_eq(blob + ks.key_off, p, n)) {
+                    *out = ks;
+                    return int(s + k);
+                }
+            }
+        }
+        s = (s + 4) & mask;
+        g = *reinterpret_cast<const uint4*>(tags + s);
+    }
+}
+
+VC_HD uint4 tag_group(const uint32_t* tags, uint32_t mask, uint32_t h) {
+    return *reinterpret_cast<const uint4*>(tags + (h & mask & ~3u));
+}
+
+// Sequential form (any number of labels): scan right-to-left, probe at dots.
+VC_HDN int32_t hint_host_only_seq(const HintImage& img, DStr host, int port) {
     uint32_t h = kFnvBasis;
     uint32_t best_suffix = VC_NONE;
     KeySlot k;
@@ -250,7 +274,10 @@ VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
         if (c == '.') {   // host.endsWith("." + H) with H = host[j+1..]
             int s = probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
                           host.n - j - 1, &k);
-            if (s >= 0) { uint32_t c = pick(img, s, k, port); best_suffix = c < best_suffix ? c : best_suffix; }
+            if (s >= 0) {
+                uint32_t c2 = pick(img, s, k, port);
+                best_suffix = c2 < best_suffix ? c2 : best_suffix;
+            }
         }
         h = fnv_step(h, c);
     }
@@ -263,6 +290,127 @@ VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
     if (img.wildcard_slot >= 0) {
         KeySlot w = load_slot(img.host_slots, uint32_t(img.wildcard_slot));
         uint32_t v = pick(img, img.wildcard_slot, w, port);
+        if (v != VC_NONE) return int32_t(v);
+    }
+    return -1;
+}
+
+// Per-probe summary of a loaded 16-byte tag group: bits 0-3 = slots whose
+// tag matches, bit 4 = the group holds no empty slot (probing may continue).
+VC_HD uint32_t group_code(uint4 g, uint32_t h) {
+    const uint32_t want = h | 1u;
+    const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
+    uint32_t code = 0, open = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // slots past the first empty one are never part of this key's chain
+        const bool before_empty = open == 0;
+        if (tg[k] == 0) open = 1;
+        if (before_empty && tg[k] == want) code |= 1u << k;
+    }
+    if (!open) code |= 16u;
+    return code;
+}
+
+// Resolve one probe given its first-group summary (slot loads + key compare
+// only for tag hits); -1 when absent.  Kept out of line: it runs about once
+// per name, and inlining it per suffix multiplied the register footprint.
+// Returns pick(...) of the matching host key, or VC_NONE when the key is
+// absent (or every member is excluded by the port filter).
+// (Takes the image's arrays one by one: passing the HintImage by reference
+// to an out-of-line function put a copy of it on the scratch stack.)
+__host__ __device__ __noinline__ uint32_t resolve_pick(
+    const uint32_t* tags, const KeySlot* slots, uint32_t mask, const uint8_t* blob,
+    const uint32_t* pm_off, const PortMin* pms, uint32_t h, const uint8_t* p, int n,
+    uint32_t code, int port) {
+    const uint32_t s0 = h & mask & ~3u;
+    int s = -1;
+    KeySlot ks;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (s < 0 && (code & (1u << k))) {
+            const KeySlot c = load_slot(slots, s0 + k);
+            if (c.key_len == n && key_eq(blob + c.key_off, p, n)) {
+                s = int(s0 + k);
+                ks = c;
+            }
+        }
+    }
+    if (s < 0) {
+        if (!(code & 16u)) return VC_NONE;
+        // the first group was full of other keys: continue linear probing
+        const uint32_t s1 = (s0 + 4) & mask;
+        s = probe_from(tags, slots, mask, blob, h, p, n, s1,
+                       *reinterpret_cast<const uint4*>(tags + s1), &ks);
+        if (s < 0) return VC_NONE;
+    }
+    if (port == 0) return uint32_t(ks.a);            // pick() (Hint.java:124-128)
+    uint32_t v = uint32_t(ks.b);
+    const uint32_t off = pm_off[2 * s], cnt = pm_off[2 * s + 1];
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const PortMin pm = pms[off + i];
+        if (pm.port == port) v = uint32_t(pm.idx) < v ? uint32_t(pm.idx) : v;
+    }
+    return v;
+}
+
+// searchForGroup for hints whose uri is null (or no group has a hint-uri):
+// level = hostLevel << 10, so exact (3) beats any suffix (2) beats "*" (1),
+// and within a level the lowest handle index wins (strict '>' scan).
+// Batched form: one register-only scan hashes the whole host and every
+// dot-suffix, then all first tag groups are loaded together (independent
+// loads in flight) before any slot or key is touched.
+constexpr int kMaxSuffix = 6;
+
+VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
+    if (host.n < 0) return -1;
+    uint32_t hs[kMaxSuffix];
+    int st[kMaxSuffix];
+    int np = 0;
+    uint32_t h = kFnvBasis;
+    for (int j = host.n - 1; j >= 0; --j) {
+        const uint8_t c = host.p[j];
+        if (c == '.') {
+#pragma unroll
+            for (int k = 0; k < kMaxSuffix; ++k)
+                if (k == np) {
+                    hs[k] = h;
+                    st[k] = j + 1;
+                }
+            ++np;
+        }
+        h = fnv_step(h, c);
+    }
+    if (np > kMaxSuffix) return hint_host_only_seq(img, host, port);
+    uint4 g[kMaxSuffix + 1];
+    g[kMaxSuffix] = tag_group(img.host_tags, img.host_mask, h);
+#pragma unroll
+    for (int k = 0; k < kMaxSuffix; ++k)
+        if (k < np) g[k] = tag_group(img.host_tags, img.host_mask, hs[k]);
+    uint32_t code[kMaxSuffix + 1];
+    code[kMaxSuffix] = group_code(g[kMaxSuffix], h);
+#pragma unroll
+    for (int k = 0; k < kMaxSuffix; ++k) code[k] = k < np ? group_code(g[k], hs[k]) : 0u;
+    if (code[kMaxSuffix]) {
+        const uint32_t e = resolve_pick(img.host_tags, img.host_slots, img.host_mask, img.blob,
+                                        img.port_min_off, img.port_mins, h, host.p, host.n,
+                                        code[kMaxSuffix], port);
+        if (e != VC_NONE) return int32_t(e);
+    }
+    uint32_t best = VC_NONE;
+#pragma unroll
+    for (int k = 0; k < kMaxSuffix; ++k) {
+        if (code[k]) {
+            const uint32_t c = resolve_pick(img.host_tags, img.host_slots, img.host_mask,
+                                            img.blob, img.port_min_off, img.port_mins, hs[k],
+                                            host.p + st[k], host.n - st[k], code[k], port);
+            best = c < best ? c : best;
+        }
+    }
+    if (best != VC_NONE) return int32_t(best);
+    if (img.wildcard_slot >= 0) {
+        KeySlot w = load_slot(img.host_slots, uint32_t(img.wildcard_slot));
+        const uint32_t v = pick(img, img.wildcard_slot, w, port);
         if (v != VC_NONE) return int32_t(v);
     }
     return -1;
