@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 import vproxy_amd as V  # noqa: E402
 from vproxy_amd import workloads as W  # noqa: E402
+from vproxy_amd.dist import HitCounterBucket  # noqa: E402
 
 METRIC = "M classifications/sec (ACL+LPM+host) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -105,26 +106,6 @@ def gather_strings_dev(blob, off, idx, dev):
 
 
 # ---------------------------------------------------------------------------
-# hip helpers (counter copy for the RCCL all-reduce)
-# ---------------------------------------------------------------------------
-_hip = None
-
-
-def hip():
-    global _hip
-    if _hip is None:
-        _hip = C.CDLL("libamdhip64.so")
-        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
-    return _hip
-
-
-def copy_dev(dst_tensor, src_ptr, nbytes):
-    rc = hip().hipMemcpyAsync(C.c_void_p(dst_tensor.data_ptr()), C.c_void_p(src_ptr), nbytes, 3,
-                              C.c_void_p(torch.cuda.current_stream().cuda_stream))
-    assert rc == 0, rc
-
-
-# ---------------------------------------------------------------------------
 # CPU baseline (oracle, test-infrastructure C restatement of the Java scans)
 # ---------------------------------------------------------------------------
 def cpu_baseline_c5(tcp, udp, v4_list, groups, names_blob, names_off, seed, threads,
@@ -158,13 +139,16 @@ def cpu_baseline_c5(tcp, udp, v4_list, groups, names_blob, names_off, seed, thre
                       "them, %d threads, %.1f s" % (n, len(v4_list), len(groups), threads, t)}
 
 
-def load_traffic(workload):
+def load_traffic(workload, kernel):
+    """Per-launch HBM-side bytes of `kernel` from the committed PMC passes
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench)."""
     p = os.path.join(PROFILES, "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(workload)
-    except (OSError, ValueError):
+        return d[workload]["kernels"][kernel]["traffic_bytes"]
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -233,10 +217,8 @@ def main():
     # scheduled explicitly after the pipeline so each kernel is timed alone.
     clf.counters_enable(False)
     count = not args.no_counters
-    cnt = []
-    for kind in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP):
-        ptr, n = clf.counters_device(kind)
-        cnt.append((ptr, n, torch.zeros(n, dtype=torch.int64, device=dev)))
+    csrc = [clf.counters_device(k) for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
+    bucket = HitCounterBucket([n for _, n in csrc], dev) if world > 1 else None
     stream = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     ev = []
@@ -263,11 +245,10 @@ def main():
         if timed:
             e[5].record()
             ev.append(e)
-        if world > 1:
-            import torch.distributed as dist
-            for ptr, n, t in cnt:      # hit counters: one RCCL all-reduce per batch
-                copy_dev(t, ptr, n * 8)
-                dist.all_reduce(t)
+        if bucket is not None:     # hit counters: one RCCL all-reduce per batch
+            for i, cs in enumerate(csrc):
+                bucket.fill(i, cs)
+            bucket.reduce()
 
     for _ in range(args.warmup):
         step(False)
@@ -304,7 +285,7 @@ def main():
         unit_desc = "%.1f B/hostname (avg bytes + 4 offset + 4 out)" % per_unit
     achieved = per_unit * units / (ms / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic("c5"),
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic("c5", dom),
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
                                 "pipeline_v4_kernel": round(pipe_ms, 4),

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV outputs into profiles/ (run on this side, after
+gpurun merged gpurun_out/ back).
+
+    scripts/pmc_traffic.py STATS_DIR FETCH_DIR WRITE_DIR [--tag r01] [--workload c5]
+
+STATS_DIR: `rocprofv3 --kernel-trace --stats --output-format csv` output
+FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
+(separate passes, as MI355X_MICROARCH.md §rocprofv3 PMC slots requires).
+
+Per kernel it writes the average per-launch HBM-side bytes.  FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
+coalesced stream (MI355X_MICROARCH.md §HBM), so the read side is reported
+both raw and doubled, and `traffic` = 2 x FETCH + WRITE (the guide's
+correction; other access widths are uncalibrated there -- the gathers in
+these kernels are 4-16 B per lane, so `traffic` is an upper estimate of the
+read side and the raw value a lower one).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kname(s):
+    """'void vcd::pipeline_v4_kernel<true, true>(AclImage, ...)' -> 'pipeline_v4_kernel'"""
+    s = s.split("(")[0]
+    if s.startswith("void "):
+        s = s[5:]
+    return s.split("<")[0].split("::")[-1].strip()
+
+
+def _find(d, pattern):
+    hits = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    if not hits:
+        raise SystemExit("no %s under %s" % (pattern, d))
+    return hits[0]
+
+
+def counter_avg(d, name):
+    """kernel -> (launches, mean counter value per launch)."""
+    path = _find(d, "*counter_collection.csv")
+    per = defaultdict(lambda: defaultdict(float))
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != name:
+                continue
+            k = kname(row["Kernel_Name"])
+            per[k][row.get("Dispatch_Id") or row.get("Correlation_Id")] += float(row["Counter_Value"])
+    return {k: (len(v), sum(v.values()) / len(v)) for k, v in per.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats")
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--workload", default="c5")
+    ap.add_argument("--kernels", default="pipeline_v4_kernel,hint_kernel")
+    a = ap.parse_args()
+    prof = os.path.join(ROOT, "profiles")
+    stats = _find(a.stats, "*kernel_stats.csv")
+    shutil.copy(stats, os.path.join(prof, "%s_%s_kernel_stats.csv" % (a.tag, a.workload)))
+    avg_ns = {}
+    with open(stats) as f:
+        for row in csv.DictReader(f):
+            avg_ns[kname(row["Name"])] = float(row["AverageNs"])
+    fetch = counter_avg(a.fetch, "FETCH_SIZE")
+    write = counter_avg(a.write, "WRITE_SIZE")
+    out = {}
+    for k in a.kernels.split(","):
+        if k not in fetch or k not in write:
+            continue
+        fr, wr = fetch[k][1] * 1024, write[k][1] * 1024
+        traffic = 2 * fr + wr
+        ns = avg_ns.get(k)
+        out[k] = {"launches_fetch_pass": fetch[k][0], "fetch_bytes_raw": fr,
+                  "fetch_bytes_x2": 2 * fr, "write_bytes": wr, "traffic_bytes": traffic,
+                  "avg_ns_kernel_trace": ns,
+                  "traffic_GBps": traffic / ns if ns else None}
+    path = os.path.join(prof, "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            allw = json.load(f)
+    except (OSError, ValueError):
+        allw = {}
+    allw[a.workload] = {"tag": a.tag, "kernels": out,
+                        "note": "per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024, read side x2 "
+                                "per MI355X_MICROARCH.md §HBM (gfx950 half-count)"}
+    with open(path, "w") as f:
+        json.dump(allw, f, indent=1)
+    for src, name in ((a.fetch, "fetch"), (a.write, "write")):
+        p = _find(src, "*counter_collection.csv")
+        rows = [r for r in csv.DictReader(open(p))
+                if kname(r["Kernel_Name"]) in a.kernels.split(",")]
+        if rows:
+            with open(os.path.join(prof, "%s_%s_pmc_%s.csv" % (a.tag, a.workload, name)), "w",
+                      newline="") as f:
+                w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+                w.writeheader()
+                w.writerows(rows)
+    print(json.dumps(allw[a.workload], indent=1))
+
+
+if __name__ == "__main__":
+    main()

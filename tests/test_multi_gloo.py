@@ -1,0 +1,106 @@
+"""N > 1 path on CPU: world-size-2 `gloo` process groups.
+
+The data path has no collective: each rank classifies its own shard of a
+seeded global batch.  Here the oracle stands in for the per-rank kernels
+(CPU tier, no GPU), and the test checks the host logic bench.py uses on
+the GPU box: the shard split, the single-bucket counter layout and the
+all-reduce, against the hit counters of the whole batch on one rank.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_ffi as O
+from vproxy_amd import workloads as W
+from vproxy_amd.dist import HitCounterBucket, shard
+
+
+def test_shard_covers_batch_once():
+    for n in (0, 1, 7, 1000, 125_000_001):
+        for world in (1, 2, 3, 8):
+            parts = [shard(n, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            sizes = [hi - lo for lo, hi in parts]
+            assert max(sizes) - min(sizes) <= (1 if n else 0)
+    with pytest.raises(ValueError):
+        shard(10, 2, 2)
+
+
+def _tables():
+    tcp, udp = W.gen_sg_rules(200, 71, p_range=0.4)
+    net, plen = W.gen_v4_prefixes(2000, 72)
+    nets = W.v4_nets(net, plen)
+    return tcp, udp, net, plen, nets
+
+
+def _counters(tcp, udp, nets, proto, src, port, dst):
+    """Library counter layout (include/vclassify.h VC_COUNTERS_*) from the
+    oracle's outputs: ACL [tcp][udp][tcp default][udp default], ROUTE
+    [v4][v6][v4 null][v6 null] (v4 only here)."""
+    acl, _ = O.sg_batch_v4_np(tcp, udp, False, proto, src, port)
+    route = O.rt_batch_v4_np(nets, dst)
+    nt, nu = len(tcp), len(udp)
+    is_t = proto == 6
+    ca = np.bincount(np.where(acl >= 0, np.where(is_t, acl, nt + acl), nt + nu + (~is_t)),
+                     minlength=nt + nu + 2)
+    cr = np.bincount(np.where(route >= 0, route, len(nets)), minlength=len(nets) + 2)
+    return [torch.from_numpy(ca.astype(np.int64)), torch.from_numpy(cr.astype(np.int64))]
+
+
+def _batch(tcp, udp, net, plen, n):
+    proto, src, port = W.gen_acl_queries(tcp, udp, n, 73)
+    dst = W.v4_lookups(net, plen, n, 74)
+    return proto, src, port, dst
+
+
+def _worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tcp, udp, net, plen, nets = _tables()                 # replicated tables
+        proto, src, dport, dst = _batch(tcp, udp, net, plen, n)
+        lo, hi = shard(n, rank, world)
+        mine = _counters(tcp, udp, nets, proto[lo:hi], src[lo:hi], dport[lo:hi], dst[lo:hi])
+        b = HitCounterBucket([t.numel() for t in mine], "cpu")
+        for i, t in enumerate(mine):
+            b.fill(i, t)
+        views = b.reduce()
+        q.put((rank, [v.numpy().copy() for v in views], hi - lo))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2])
+def test_counter_allreduce_equals_single_rank(world):
+    n = 30011                                                  # odd: uneven shards
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tcp, udp, net, plen, nets = _tables()
+    want = [t.numpy() for t in _counters(tcp, udp, nets, *_batch(tcp, udp, net, plen, n))]
+    assert sum(r[2] for r in res) == n
+    for rank, views, _ in res:
+        for got, exp in zip(views, want):
+            np.testing.assert_array_equal(got, exp)
