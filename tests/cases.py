@@ -119,3 +119,47 @@ def hint_cases_random(rng, ng, nq):
             int(rng.integers(0, 10))]
         queries.append((host, port, uri))
     return groups, _HOSTS, queries
+
+
+def hint_cases_shapes(rng, n):
+    """Groups keyed on short, long (> 48 B inline key) and deep (many-label)
+    hint-hosts, and hostnames that stress the word-at-a-time fast path:
+    every length mod 4, more labels than the batched probe holds, names
+    long enough that a wave's 64 names overflow its LDS stage (the global
+    slow path), ':port' and 'www.' forms, IPv6 literals with and without
+    ports, empty labels and empty hosts."""
+    def label(lo=1, hi=12):
+        k = int(rng.integers(lo, hi + 1))
+        return "".join(chr(97 + int(c)) for c in rng.integers(0, 26, k))
+    keys = set()
+    while len(keys) < 300:
+        depth = int(rng.integers(1, 12))
+        keys.add(".".join(label(1, 30 if rng.random() < 0.2 else 8) for _ in range(depth)))
+    keys = sorted(keys)
+    keys += ["*", "", "com", "a.b.c.d.e.f.g.h.i.j.k", "x" * 47, "y" * 48, "z" * 49, "w" * 200]
+    groups = []
+    for i, k in enumerate(keys):
+        a = {"host": k}
+        if rng.random() < 0.15:
+            a["port"] = int(rng.choice([80, 443, 8080]))
+        groups.append(({} if rng.random() < 0.8 else {"host": keys[(i + 1) % len(keys)]}, a))
+    names = []
+    for _ in range(n):
+        r = rng.random()
+        base = keys[int(rng.integers(0, len(keys)))]
+        if r < 0.3:
+            h = base
+        elif r < 0.6:
+            h = ".".join(label() for _ in range(int(rng.integers(1, 9)))) + "." + base
+        elif r < 0.7:
+            h = label(60, 250)                                   # long, no dots
+        elif r < 0.8:
+            h = ".".join(label(1, 3) for _ in range(int(rng.integers(8, 40))))
+        else:
+            h = rng.choice(["[::1]", "::1", "fe80::1:2", "1.2.3.4", "www.", "www", ".", "..",
+                            "a..b", "", ":", "www.:80", "[::1]:8080", "::ffff:1.2.3.4",
+                            "w" * 200, "x" * 47 + ".y", "." + base])
+        if rng.random() < 0.25:
+            h = ("www." if rng.random() < 0.5 else "") + h + ":" + str(int(rng.integers(0, 70000)))
+        names.append(str(h).encode())
+    return groups, names

@@ -29,15 +29,15 @@ AclFamilyImage fam_img(const vc::AclFamilyBuilt& b) {
 HintImage hint_img(const vc::HintBuilt& b) {
     HintImage h{};
     h.blob = b.blob.data();
-    h.host_slots = reinterpret_cast<const KeySlot*>(b.host_slots.data());
+    h.host_recs = b.host.recs.data();
+    h.host_ext = b.host.ext.data();
+    h.host_tags = b.host.tags.data();
     h.uri_slots = reinterpret_cast<const KeySlot*>(b.uri_slots.data());
-    h.host_tags = b.host_tags.data();
     h.uri_tags = b.uri_tags.data();
     h.lists = b.lists.data();
     h.port_mins = reinterpret_cast<const PortMin*>(b.port_mins.data());
-    h.port_min_off = b.port_min_off.data();
     h.groups = reinterpret_cast<const GroupRec*>(b.groups.data());
-    h.host_mask = uint32_t(b.host_slots.size() - 1);
+    h.host_mask = uint32_t(b.host.tags.size() - 1);
     h.uri_mask = uint32_t(b.uri_slots.size() - 1);
     h.n_groups = b.n_groups;
     h.wildcard_slot = b.wildcard_slot;
@@ -45,6 +45,18 @@ HintImage hint_img(const vc::HintBuilt& b) {
     h.has_uri_keys = b.has_uri_keys;
     return h;
 }
+// A name copied into a buffer with a 16-byte apron of junk either side, the
+// way the kernels stage a wave's names in LDS, read through LdsSrc.
+struct Staged {
+    std::vector<uint32_t> words;
+    LdsSrc src;
+    Staged(const uint8_t* p, int n, int align) {
+        words.assign(size_t(n + 48) / 4 + 2, 0xA5A5A5A5u);
+        uint8_t* b = reinterpret_cast<uint8_t*>(words.data());
+        std::memcpy(b + 16 + align, p, size_t(n));
+        src = LdsSrc{words.data(), 16 + align};
+    }
+};
 }  // namespace
 
 extern "C" {
@@ -110,7 +122,21 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
         DStr h{nullptr, -1}, u{nullptr, -1};
         if (hb && !(hn && hn[i])) h = DStr{hb + ho[i], int(ho[i + 1] - ho[i])};
         if (ub && !(un && un[i])) u = DStr{ub + uo[i], int(uo[i + 1] - uo[i])};
-        out[i] = search_for_group(img, format_host(h), port ? port[i] : 0, format_uri(u));
+        const int p = port ? port[i] : 0;
+        // reference form: formatHost then the general / sequential search
+        const int32_t want = (u.n >= 0 && img.has_uri_keys)
+                                 ? hint_general(img, format_host(h), p, format_uri(u))
+                                 : hint_host_only(img, format_host(h), p);
+        out[i] = want;
+        if (u.n >= 0 && img.has_uri_keys) continue;
+        if (h.n < 0) { if (want != -1) return -100; continue; }
+        // the kernels' fused fast path, from a plain pointer and from a
+        // staged copy at every word alignment: all must agree
+        if (host_only_fast(img, &img, PtrSrc{h.p}, h.n, p) != want) return -101;
+        for (int al = 0; al < 4; ++al) {
+            Staged st(h.p, h.n, al);
+            if (host_only_fast(img, &img, st.src, h.n, p) != want) return -102;
+        }
     }
     return 0;
 }
@@ -124,26 +150,19 @@ int ic_dns(const char* const* keys, const int32_t* key_lens, const int32_t* valu
     if (rc == 0) rc = vc::build_hints(g, ng, &b);
     if (rc) return rc;
     HintImage img = hint_img(b);
-    HostsImage hosts{hb.blob.data(), reinterpret_cast<const KeySlot*>(hb.slots.data()),
-                     hb.tags.data(), uint32_t(hb.slots.size() - 1), hb.n};
+    HostsImage hosts{hb.blob.data(), hb.table.recs.data(), hb.table.tags.data(),
+                     uint32_t(hb.table.tags.size() - 1), hb.n};
     for (int64_t i = 0; i < n; ++i) {
         const uint8_t* q = qb + qo[i];
         const int qn = int(qo[i + 1] - qo[i]);
-        uint32_t h = kFnvBasis;
-        for (int j = 0; j < qn; ++j) h = fnv_step(h, q[j]);
-        KeySlot k;
-        if (hosts.n > 0 && probe(hosts.tags, hosts.slots, hosts.mask, hosts.blob, h, q, qn, &k) >= 0) {
-            kind[i] = VC_DNS_HOSTS;
-            value[i] = k.a;
-            continue;
+        dns_one(hosts, img, &img, PtrSrc{q}, qn, kind + i, value + i);
+        for (int al = 0; al < 4; ++al) {
+            Staged st(q, qn, al);
+            uint8_t k2;
+            int32_t v2;
+            dns_one(hosts, img, &img, st.src, qn, &k2, &v2);
+            if (k2 != kind[i] || v2 != value[i]) return -103;
         }
-        const int dn = (qn > 0 && q[qn - 1] == '.') ? qn - 1 : qn;
-        const int32_t gg = hint_host_only(img, format_host(DStr{q, dn}), 0);
-        if (gg >= 0) { kind[i] = VC_DNS_GROUP; value[i] = gg; continue; }
-        if (d_is_ip_literal(q, dn)) { kind[i] = VC_DNS_IP_LITERAL; value[i] = d_count(q, dn, ':') ? 6 : 4; continue; }
-        bool internal = dn >= 13 && std::memcmp(q + dn - 13, ".vproxy.local", 13) == 0;
-        kind[i] = internal ? VC_DNS_INTERNAL : VC_DNS_RECURSIVE;
-        value[i] = 0;
     }
     return 0;
 }

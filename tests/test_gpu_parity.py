@@ -309,6 +309,28 @@ def test_hint_c4_scale(clf):
     assert (got >= 0).mean() > 0.5
 
 
+def test_hint_shapes(clf):
+    """Fast-path shapes (lengths mod 4, > 6 labels, waves whose names
+    overflow the LDS stage, ':port' / 'www.' / IPv6 forms) vs the oracle,
+    from the host entry point and from an unaligned device blob."""
+    import torch
+    from cases import hint_cases_shapes
+    groups, names = hint_cases_shapes(np.random.default_rng(93), 40000)
+    clf.compile_upstream(groups)
+    ports = np.random.default_rng(94).choice(np.array([0, 0, 80, 8080], np.uint16), len(names))
+    og = O.Groups(groups)
+    blob, off = W.pack(names)
+    want = O.hint_batch_np(og, blob, off, ports, nthreads=THREADS)
+    np.testing.assert_array_equal(clf.hint_search(names, ports), want)
+    # device blob at an odd address: the launcher's unstaged kernel
+    raw = torch.zeros(len(blob) + 1, dtype=torch.uint8, device="cuda")
+    raw[1:] = torch.from_numpy(blob.astype(np.uint8)).cuda()
+    o = torch.from_numpy(off.astype(np.int32)).cuda()
+    got = clf.hint_search((raw[1:], o, None), torch.from_numpy(ports.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
 def test_dns_kats_and_random(clf):
     with open(os.path.join(G, "kats.json")) as f:
         kats = json.load(f)

@@ -193,3 +193,19 @@ def test_dns_image():
     oh = O.Hosts(pairs)
     want = [O.dns_classify(oh, og, q) for q in names]
     assert [(int(k), int(v)) for k, v in zip(kind, val)] == want
+
+
+def test_hint_fast_path_shapes():
+    """The kernels' word-at-a-time fast path (plain and LDS-staged sources at
+    every alignment, checked inside the harness) vs the oracle on the hard
+    hostname shapes of cases.hint_cases_shapes."""
+    from cases import hint_cases_shapes
+    groups, names = hint_cases_shapes(np.random.default_rng(91), 6000)
+    arr, ng, keep = group_array(groups)
+    h = pack_strings(names)
+    ports = np.random.default_rng(92).choice(np.array([0, 0, 80, 8080], np.uint16), len(names))
+    got = IC.hint(arr, ng, h, ports, None)
+    og = O.Groups(groups)
+    blob, off = W.pack(names)
+    want = O.hint_batch_np(og, blob, off, ports, nthreads=8)
+    np.testing.assert_array_equal(got, want)

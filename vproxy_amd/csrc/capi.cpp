@@ -410,16 +410,17 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     auto s = std::make_shared<HintSnap>();
     hipError_t e = hipSuccess;
     static_assert(sizeof(KeySlot) == sizeof(vc::KeySlotH), "slot layout");
+    static_assert(sizeof(HostRec) == 64 && sizeof(HostExt) == 16, "record layout");
     s->img.blob = s->upload(b.blob, &e);
-    s->img.host_slots = reinterpret_cast<const KeySlot*>(s->upload(b.host_slots, &e));
+    s->img.host_recs = s->upload(b.host.recs, &e);
+    s->img.host_ext = s->upload(b.host.ext, &e);
+    s->img.host_tags = s->upload(b.host.tags, &e);
     s->img.uri_slots = reinterpret_cast<const KeySlot*>(s->upload(b.uri_slots, &e));
-    s->img.host_tags = s->upload(b.host_tags, &e);
     s->img.uri_tags = s->upload(b.uri_tags, &e);
     s->img.lists = s->upload(b.lists, &e);
     s->img.port_mins = reinterpret_cast<const PortMin*>(s->upload(b.port_mins, &e));
-    s->img.port_min_off = s->upload(b.port_min_off, &e);
     s->img.groups = reinterpret_cast<const GroupRec*>(s->upload(b.groups, &e));
-    s->img.host_mask = static_cast<uint32_t>(b.host_slots.size() - 1);
+    s->img.host_mask = static_cast<uint32_t>(b.host.tags.size() - 1);
     s->img.uri_mask = static_cast<uint32_t>(b.uri_slots.size() - 1);
     s->img.n_groups = n;
     s->img.wildcard_slot = b.wildcard_slot;
@@ -485,9 +486,9 @@ int vc_compile_hosts(vc_ctx* ctx, const char* const* keys, const int32_t* key_le
     auto s = std::make_shared<HostsSnap>();
     hipError_t e = hipSuccess;
     s->img.blob = s->upload(b.blob, &e);
-    s->img.slots = reinterpret_cast<const KeySlot*>(s->upload(b.slots, &e));
-    s->img.tags = s->upload(b.tags, &e);
-    s->img.mask = static_cast<uint32_t>(b.slots.size() - 1);
+    s->img.recs = s->upload(b.table.recs, &e);
+    s->img.tags = s->upload(b.table.tags, &e);
+    s->img.mask = static_cast<uint32_t>(b.table.tags.size() - 1);
     s->img.n = b.n;
     if (e != hipSuccess) return hip_fail(e, "hosts upload");
     ctx->publish(ctx->hosts, std::shared_ptr<const HostsSnap>(std::move(s)));

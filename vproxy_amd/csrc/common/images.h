@@ -60,22 +60,43 @@ struct RouteImage {
 // ---------------------------------------------------------------------------
 // Upstream hint matching + DNS hosts.
 //
-// Keys are hashed with 32-bit FNV-1a.  Host keys (merged hint-host H) hash
-// the string right-to-left, so one right-to-left scan of a query host yields
-// the hash of every dot-suffix incrementally (a reversed-suffix index).  URI
-// keys (merged hint-uri U) and hosts-map keys hash left-to-right, so one scan
-// of a URI yields the hash of every prefix.  Open addressing,
-// power-of-two capacity, linear probing.  Probes walk a compact tag array
-// (4 B per slot, hash | 1, 0 = empty; L2-resident for 100k keys) and only
-// read the 32-byte slot on a tag hit; every tag hit is confirmed by a full
-// byte compare of the key.
+// Host-name keys (merged hint-host H, and the DNS hosts map) live in
+// open-addressing tables keyed by the end-aligned chunk hash of
+// common/khash.h, so one right-to-left pass over a query host hashes the
+// host and every dot-suffix.  Power-of-two capacity, linear probing from the
+// hash's 4-slot group.  Probes walk a compact tag array (4 B per slot,
+// hash | 1, 0 = empty; L2-resident for 100k keys) and read the slot's
+// 64-byte record -- one cache line holding the key inline and the answer --
+// only on a tag hit; every tag hit is confirmed by a full key compare.
+//
+// URI keys (merged hint-uri U) are matched by prefix, so they hash
+// left-to-right with 32-bit FNV-1a: one scan of a URI yields the hash of
+// every prefix.  They use the older 32-byte KeySlot (general path only).
 // ---------------------------------------------------------------------------
-struct KeySlot {                   // 32 bytes
+#define VC_REC_INLINE 48           // key bytes held inline in a HostRec
+#define VC_REC_HAS_PM 0x80000000u  // HostRec.len_pm: key has hint-port minima
+
+struct HostRec {                   // 64 bytes, 64-byte aligned
+    uint32_t len_pm;               // key length | VC_REC_HAS_PM
+    int32_t a;                     // hint table: min handle index (any port); hosts: value
+    int32_t b;                     // hint table: min handle index with no hint-port
+    uint32_t key_off;              // whole key in the blob (16-byte aligned, zero padded)
+    uint8_t key[VC_REC_INLINE];    // first 48 key bytes, zero padded
+};
+
+struct HostExt {                   // 16 bytes per host slot (slow paths only)
+    uint32_t list_off;             // member list (handle indices ascending) in lists[]
+    uint32_t list_cnt;
+    uint32_t pm_off;               // distinct nonzero hint-ports in port_mins[]
+    uint32_t pm_cnt;
+};
+
+struct KeySlot {                   // 32 bytes (URI table)
     uint64_t hash;                 // 32-bit FNV-1a in the low word
     int32_t key_len;               // -1 = empty slot
     uint32_t key_off;              // into HintImage.blob
-    int32_t a;                     // host table: min handle index (any port); hosts: value
-    int32_t b;                     // host table: min handle index with no hint-port
+    int32_t a;
+    int32_t b;
     uint32_t list_off;             // member list (handle indices ascending) in lists[]
     uint32_t list_cnt;
 };
@@ -96,13 +117,13 @@ struct GroupRec {                  // merged annotations of one ServerGroupHandl
 
 struct HintImage {
     const uint8_t* blob;           // key / annotation bytes
-    const KeySlot* host_slots;     // keyed by H (reverse hash)
-    const KeySlot* uri_slots;      // keyed by U (forward hash)
+    const HostRec* host_recs;      // keyed by H (chunk hash)
+    const HostExt* host_ext;
     const uint32_t* host_tags;     // hash | 1 per host slot, 0 = empty
+    const KeySlot* uri_slots;      // keyed by U (forward FNV-1a)
     const uint32_t* uri_tags;
     const uint32_t* lists;         // member lists
-    const PortMin* port_mins;      // per host key: distinct nonzero hint-ports
-    const uint32_t* port_min_off;  // 2 words per host slot: (off, cnt) into port_mins
+    const PortMin* port_mins;
     const GroupRec* groups;
     uint32_t host_mask;            // capacity - 1
     uint32_t uri_mask;
@@ -114,7 +135,7 @@ struct HintImage {
 
 struct HostsImage {
     const uint8_t* blob;
-    const KeySlot* slots;          // keyed by the exact qname (forward hash); value in .a
+    const HostRec* recs;           // keyed by the exact qname (chunk hash); value in .a
     const uint32_t* tags;
     uint32_t mask;
     int32_t n;

@@ -356,6 +356,34 @@ uint32_t table_insert(std::vector<KeySlotH>* t, std::vector<uint32_t>* tags, uin
 
 }  // namespace
 
+void HostTableBuilt::init(size_t n_keys) {
+    const uint32_t cap = pow2_cap(n_keys);
+    tags.assign(cap, 0);
+    HostRec empty{};
+    recs.assign(cap, empty);
+    ext.assign(cap, HostExt{0, 0, 0, 0});
+    n = 0;
+}
+
+uint32_t HostTableBuilt::insert(const std::string& k, int32_t a, int32_t b,
+                                std::vector<uint8_t>* blob) {
+    const uint32_t h = vck::khash(reinterpret_cast<const uint8_t*>(k.data()),
+                                  static_cast<int>(k.size()));
+    const uint32_t mask = static_cast<uint32_t>(tags.size() - 1);
+    uint32_t s = h & mask & ~3u;
+    while (tags[s] != 0) s = (s + 1) & mask;
+    tags[s] = h | 1u;
+    HostRec& r = recs[s];
+    r = HostRec{};
+    r.len_pm = static_cast<uint32_t>(k.size());
+    r.a = a;
+    r.b = b;
+    r.key_off = append_blob(blob, k.data(), static_cast<int>(k.size()));
+    std::memcpy(r.key, k.data(), std::min<size_t>(k.size(), VC_REC_INLINE));
+    ++n;
+    return s;
+}
+
 int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
     *out = HintBuilt{};
     out->n_groups = n;
@@ -407,25 +435,22 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         }
     }
     KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
-    out->host_slots.assign(pow2_cap(host_order.size()), empty);
+    for (auto& k : host_order)
+        if (k.size() > 0x7FFFFFFFu) return VC_EINVAL;
+    out->host.init(host_order.size());
     out->uri_slots.assign(pow2_cap(uri_order.size()), empty);
-    out->host_tags.assign(out->host_slots.size(), 0);
     out->uri_tags.assign(out->uri_slots.size(), 0);
-    out->port_min_off.assign(out->host_slots.size() * 2, 0);
     for (auto& k : host_order) {
         KeyAcc& acc = hostk[k];
-        KeySlotH s{};
-        s.hash = fnv_rev(reinterpret_cast<const uint8_t*>(k.data()), k.size());
-        s.key_len = static_cast<int32_t>(k.size());
-        s.key_off = append_blob(&out->blob, k.data(), static_cast<int>(k.size()));
-        s.a = acc.a;
-        s.b = acc.b < 0 ? static_cast<int32_t>(VC_NONE) : acc.b;
-        s.list_off = static_cast<uint32_t>(out->lists.size());
-        s.list_cnt = static_cast<uint32_t>(acc.members.size());
+        const uint32_t slot = out->host.insert(
+            k, acc.a, acc.b < 0 ? static_cast<int32_t>(VC_NONE) : acc.b, &out->blob);
+        HostExt& x = out->host.ext[slot];
+        x.list_off = static_cast<uint32_t>(out->lists.size());
+        x.list_cnt = static_cast<uint32_t>(acc.members.size());
         out->lists.insert(out->lists.end(), acc.members.begin(), acc.members.end());
-        uint32_t slot = table_insert(&out->host_slots, &out->host_tags, uint32_t(s.hash), s);
-        out->port_min_off[2 * slot] = static_cast<uint32_t>(out->port_mins.size() / 2);
-        out->port_min_off[2 * slot + 1] = static_cast<uint32_t>(acc.port_min.size());
+        x.pm_off = static_cast<uint32_t>(out->port_mins.size() / 2);
+        x.pm_cnt = static_cast<uint32_t>(acc.port_min.size());
+        if (!acc.port_min.empty()) out->host.recs[slot].len_pm |= VC_REC_HAS_PM;
         for (auto& pm : acc.port_min) {
             out->port_mins.push_back(pm.first);
             out->port_mins.push_back(pm.second);
@@ -456,26 +481,20 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
 int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
                 HostsBuilt* out) {
     *out = HostsBuilt{};
-    KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
-    out->slots.assign(pow2_cap(static_cast<size_t>(n)), empty);
-    out->tags.assign(out->slots.size(), 0);
     std::unordered_map<std::string, int> seen;
+    std::vector<int> order;
     for (int i = 0; i < n; ++i) {
         if (key_lens[i] < 0 || (!keys[i] && key_lens[i] > 0)) return VC_EINVAL;
         std::string k(keys[i] ? keys[i] : "", key_lens[i]);
         if (seen.count(k)) continue;     // first key wins
         seen.emplace(k, i);
-        KeySlotH s{};
-        s.hash = fnv_fwd(reinterpret_cast<const uint8_t*>(k.data()), k.size());
-        s.key_len = key_lens[i];
-        s.key_off = append_blob(&out->blob, k.data(), key_lens[i]);
-        s.a = values[i];
-        s.b = 0;
-        s.list_off = 0;
-        s.list_cnt = 0;
-        table_insert(&out->slots, &out->tags, uint32_t(s.hash), s);
-        ++out->n;
+        order.push_back(i);
     }
+    out->table.init(order.size());
+    for (int i : order)
+        out->table.insert(std::string(keys[i] ? keys[i] : "", key_lens[i]), values[i], 0,
+                          &out->blob);
+    out->n = out->table.n;
     if (out->blob.empty()) out->blob.assign(16, 0);
     return VC_OK;
 }

@@ -7,6 +7,8 @@
 #include <vector>
 
 #include "vclassify.h"
+#include "../common/images.h"
+#include "../common/khash.h"
 
 namespace vc {
 
@@ -38,7 +40,7 @@ struct TrieBuilt {
 // One RouteTable family list (list order = priority) -> stride trie.
 int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out);
 
-struct KeySlotH {                    // host mirror of KeySlot
+struct KeySlotH {                    // host mirror of KeySlot (URI table)
     uint64_t hash;
     int32_t key_len;
     uint32_t key_off;
@@ -46,13 +48,25 @@ struct KeySlotH {                    // host mirror of KeySlot
     uint32_t list_off, list_cnt;
 };
 
+// Host-name key table (hint-host keys, hosts map): tags + 64-byte records
+// (common/images.h HostRec) + per-slot extension, keyed by vck::khash.
+struct HostTableBuilt {
+    std::vector<uint32_t> tags;
+    std::vector<HostRec> recs;
+    std::vector<HostExt> ext;
+    int32_t n = 0;
+    void init(size_t n_keys);
+    // insert a key (not present yet); returns its slot
+    uint32_t insert(const std::string& key, int32_t a, int32_t b, std::vector<uint8_t>* blob);
+};
+
 struct HintBuilt {
     std::vector<uint8_t> blob;
-    std::vector<KeySlotH> host_slots, uri_slots;
-    std::vector<uint32_t> host_tags, uri_tags;
+    HostTableBuilt host;
+    std::vector<KeySlotH> uri_slots;
+    std::vector<uint32_t> uri_tags;
     std::vector<uint32_t> lists;
     std::vector<int32_t> port_mins;      // (port, idx) pairs
-    std::vector<uint32_t> port_min_off;  // (off, cnt) per host slot
     std::vector<int32_t> groups;         // 6 words per GroupRec
     int32_t n_groups = 0;
     int32_t wildcard_slot = -1, uri_star_slot = -1, has_uri_keys = 0;
@@ -62,8 +76,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out);
 
 struct HostsBuilt {
     std::vector<uint8_t> blob;
-    std::vector<KeySlotH> slots;
-    std::vector<uint32_t> tags;
+    HostTableBuilt table;
     int32_t n = 0;
 };
 

@@ -18,28 +18,33 @@ namespace vcd {
 constexpr int kHintBlock = 256;
 constexpr int kWaves = kHintBlock / 64;
 constexpr uint32_t kStageBytes = 4096;   // per wave: 64 names of up to 64 B on average
+constexpr uint32_t kApron = 16;          // readable bytes before and after the names
+constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 
 // A wave's 64 names are contiguous in the blob: copy them into LDS with
-// coalesced dword loads once, so the per-lane character scans (reversed
-// suffix hashing, key compares) read LDS instead of issuing scattered byte
-// loads to HBM.  Returns the LDS base for this wave's names (names then sit
-// at stage + (off[i] - a0)), or nullptr when the span does not fit.
-__device__ __forceinline__ const uint8_t* stage_wave(const uint8_t* blob, uint32_t o0, uint32_t o1,
-                                                     uint8_t* stage, uint32_t* a0_out) {
+// coalesced dword loads once, so the per-lane word scans (suffix hashing,
+// key compares) read LDS.  Names then sit at byte kApron + (off[i] - a0) of
+// the wave's stage.  Returns false when the span does not fit.
+__device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uint32_t o1,
+                                           uint32_t* stage, uint32_t* a0_out) {
     const uint32_t a0 = o0 & ~3u;                  // blob is dword aligned (launcher checks)
     *a0_out = a0;
-    if (o1 - a0 > kStageBytes) return nullptr;
+    if (o1 - a0 > kStageBytes) return false;
     const int lane = int(threadIdx.x & 63);
     const uint32_t full = (o1 & ~3u) - a0;         // whole dwords inside [a0, o1)
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(blob + a0);
-    uint32_t* lw = reinterpret_cast<uint32_t*>(stage);
+    uint32_t* lw = stage + kApron / 4;
     for (uint32_t k = uint32_t(lane); k < full / 4; k += 64) lw[k] = gw[k];
     const uint32_t tail = o1 - (o1 & ~3u);
-    if (uint32_t(lane) < tail) stage[full + lane] = blob[(o1 & ~3u) + lane];
+    if (lane == 0 && tail) {                       // last partial dword, byte loads
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < tail; ++b) v |= uint32_t(blob[(o1 & ~3u) + b]) << (8 * b);
+        lw[full / 4] = v;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    return stage;
+    return true;
 }
 
 __device__ __forceinline__ void wave_done() {
@@ -55,27 +60,46 @@ __global__ __launch_bounds__(kHintBlock) void hint_kernel(
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
     const uint8_t* __restrict__ uri_blob, const uint32_t* __restrict__ uri_off,
     const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kStageBytes];
+    __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
+    const bool general = uri_blob && img.has_uri_keys;
+    // Out-of-line slow paths take the image by address; give them their own
+    // copy so the fast path keeps reading the kernel argument (whose table
+    // pointers the compiler then knows to be global).
+    HintImage slow_img = img;
     for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
-        const uint8_t* names = nullptr;
         uint32_t a0 = 0;
-        if (kStage) names = stage_wave(host_blob, host_off[base], host_off[last], stage[w], &a0);
+        const bool staged =
+            kStage && host_blob && stage_wave(host_blob, host_off[base], host_off[last], stage[w], &a0);
         if (i < n) {
-            DStr h{nullptr, -1}, u{nullptr, -1};
-            if (host_blob && !(host_null && host_null[i])) {
-                const uint32_t a = host_off[i], e = host_off[i + 1];
-                h = DStr{names ? names + (a - a0) : host_blob + a, int(e - a)};
-            }
-            if (uri_blob && !(uri_null && uri_null[i])) {
+            const int p = port ? int(port[i]) : 0;
+            const bool has_host = host_blob && !(host_null && host_null[i]);
+            const bool has_uri = uri_blob && !(uri_null && uri_null[i]);
+            int32_t r = -1;
+            if (!general || !has_uri) {
+                // uri null (or no hint-uri anywhere): host-only levels
+                if (has_host) {
+                    const uint32_t a = host_off[i], e = host_off[i + 1];
+                    if (staged)
+                        r = host_only_fast(img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
+                                           int(e - a), p);
+                    else
+                        r = host_only_slow(slow_img, host_blob + a, int(e - a), p);
+                }
+            } else {
+                DStr h{nullptr, -1}, u{nullptr, -1};
+                if (has_host) {
+                    const uint32_t a = host_off[i], e = host_off[i + 1];
+                    h = DStr{host_blob + a, int(e - a)};
+                }
                 const uint32_t a = uri_off[i], e = uri_off[i + 1];
                 u = DStr{uri_blob + a, int(e - a)};
+                r = hint_general(slow_img, format_host(h), p, format_uri(u));
             }
-            const int p = port ? int(port[i]) : 0;
-            out[i] = search_for_group(img, format_host(h), p, format_uri(u));
+            out[i] = r;
         }
         if (kStage) wave_done();
     }
@@ -86,49 +110,23 @@ __global__ __launch_bounds__(kHintBlock) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
     int32_t* __restrict__ value) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kWaves][kStageBytes];
+    __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
+    HintImage slow_img = img;
     for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
-        const uint8_t* names = nullptr;
         uint32_t a0 = 0;
-        if (kStage) names = stage_wave(qblob, qoff[base], qoff[last], stage[w], &a0);
+        const bool staged = kStage && stage_wave(qblob, qoff[base], qoff[last], stage[w], &a0);
         if (i < n) {
             const uint32_t a = qoff[i], e = qoff[i + 1];
-            const uint8_t* q = names ? names + (a - a0) : qblob + a;
-            const int qn = int(e - a);
-            // (1) hosts.get(qname) on the raw qname (trailing dot kept), :127
-            uint32_t h = kFnvBasis;
-            for (int j = 0; j < qn; ++j) h = fnv_step(h, q[j]);
-            KeySlot k;
-            int32_t g = -1;
             uint8_t kd;
-            int32_t val = 0;
-            if (hosts.n > 0 &&
-                probe(hosts.tags, hosts.slots, hosts.mask, hosts.blob, h, q, qn, &k) >= 0) {
-                kd = VC_DNS_HOSTS;
-                val = k.a;
-            } else {
-                // (2) strip one trailing dot, :133-135
-                const int dn = (qn > 0 && q[qn - 1] == '.') ? qn - 1 : qn;
-                // (3) rrsets.searchForGroup(Hint.ofHost(domain)), :136
-                g = hint_host_only(img, format_host(DStr{q, dn}), 0);
-                if (g >= 0) {
-                    kd = VC_DNS_GROUP;
-                    val = g;
-                } else if (d_is_ip_literal(q, dn)) {             // (4) IP literal, :140-149
-                    kd = VC_DNS_IP_LITERAL;
-                    val = d_count(q, dn, ':') ? 6 : 4;
-                } else {                                          // (5) *.vproxy.local, :150-157
-                    const char* sfx = ".vproxy.local";
-                    bool internal = dn >= 13;
-                    for (int j = 0; internal && j < 13; ++j)
-                        internal = q[dn - 13 + j] == uint8_t(sfx[j]);
-                    kd = internal ? VC_DNS_INTERNAL : VC_DNS_RECURSIVE;   // (6) :164
-                }
-            }
+            int32_t val;
+            if (staged)
+                dns_one(hosts, img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a), &kd, &val);
+            else
+                dns_one(hosts, img, &slow_img, PtrSrc{qblob + a}, int(e - a), &kd, &val);
             kind[i] = kd;
             value[i] = val;
         }

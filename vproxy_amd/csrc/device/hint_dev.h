@@ -13,6 +13,7 @@
 // the whole host; each probe is confirmed by a byte compare.
 #pragma once
 
+#include "../common/khash.h"
 #include "dev_common.h"
 
 #define VC_HDN __host__ __device__
@@ -105,7 +106,7 @@ VC_HDN int d_last_bits(const uint8_t* s, int n) {
 }
 
 // IP.isIpv6 == parseIpv6String(s) != null (IP.java:158-197)
-VC_HDN bool d_is_ipv6(const uint8_t* s, int n) {
+__host__ __device__ __noinline__ bool d_is_ipv6(const uint8_t* s, int n) {
     if (n >= 2 && s[0] == '[' && s[n - 1] == ']') {
         s += 1;
         n -= 2;
@@ -160,7 +161,342 @@ VC_HDN DStr format_uri(DStr s) {
 }
 
 // ---------------------------------------------------------------------------
-// key tables
+// Byte sources.  The fast path reads a name a 32-bit word at a time; PtrSrc
+// serves plain pointers (global memory, the host harness) byte by byte and
+// never touches bytes outside the requested range; LdsSrc serves a name
+// staged in LDS, whose neighbourhood (>= 4 bytes either side) is readable.
+// ---------------------------------------------------------------------------
+
+// bytes j of a word at `pos` kept iff lo <= pos + j < hi
+VC_HD uint32_t keep_mask(int pos, int lo, int hi) {
+    int a = lo - pos, b = hi - pos;
+    a = a < 0 ? 0 : (a > 4 ? 4 : a);
+    b = b < 0 ? 0 : (b > 4 ? 4 : b);
+    const uint32_t m_lo = a >= 4 ? 0u : (~0u << (8 * a));
+    const uint32_t m_hi = b >= 4 ? ~0u : ((1u << (8 * b)) - 1u);
+    return m_lo & m_hi;
+}
+
+struct PtrSrc {
+    const uint8_t* p;
+    VC_HD const uint8_t* ptr() const { return p; }
+    VC_HD uint32_t word(int pos, int lo, int hi) const {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = pos + j;
+            if (i >= lo && i < hi) w |= uint32_t(p[i]) << (8 * j);
+        }
+        return w;
+    }
+};
+
+// LE word from two aligned words: bytes [sh, sh + 4) of (hi:lo)
+VC_HD uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {
+    return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * sh));
+}
+
+struct LdsSrc {
+    const uint32_t* w;            // the wave's LDS stage (dword array)
+    int off;                      // byte offset of the name's byte 0 in the stage
+    VC_HD const uint8_t* ptr() const { return reinterpret_cast<const uint8_t*>(w) + off; }
+    VC_HD uint32_t word(int pos, int lo, int hi) const {
+        const int a = off + pos;                // >= 0: the stage has a 16-byte apron
+        const uint32_t v = funnel(w[a >> 2], w[(a >> 2) + 1], uint32_t(a & 3));
+        return v & keep_mask(pos, lo, hi);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Host-name key table: tags + 64-byte records (common/images.h HostRec),
+// keyed by vck::khash.
+// ---------------------------------------------------------------------------
+struct HostTable {
+    const uint32_t* tags;
+    const HostRec* recs;
+    const uint8_t* blob;
+    uint32_t mask;
+};
+
+struct Rec {                      // a HostRec in registers
+    uint4 m, k0, k1, k2;          // meta (len_pm, a, b, key_off), key words 0..11
+};
+
+VC_HD Rec load_rec(const HostRec* r, uint32_t s) {
+    const uint4* p = reinterpret_cast<const uint4*>(r + s);
+    return Rec{p[0], p[1], p[2], p[3]};
+}
+
+VC_HD uint32_t rec_word(const Rec& r, int j) {       // j < 12, unrolled callers
+    const uint32_t k[12] = {r.k0.x, r.k0.y, r.k0.z, r.k0.w, r.k1.x, r.k1.y,
+                            r.k1.z, r.k1.w, r.k2.x, r.k2.y, r.k2.z, r.k2.w};
+    return k[j];
+}
+
+// record key == query bytes [st, st + n)?
+template <class Src>
+VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n) {
+    if ((r.m.x & ~VC_REC_HAS_PM) != uint32_t(n)) return false;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < VC_REC_INLINE / 4; ++j)
+        if (4 * j < n) diff |= q.word(st + 4 * j, st, st + n) ^ rec_word(r, j);
+    if (diff) return false;
+    if (n > VC_REC_INLINE) {      // long key: the rest from the blob copy
+        const uint32_t* kw = reinterpret_cast<const uint32_t*>(blob + r.m.w);
+        for (int j = VC_REC_INLINE / 4; 4 * j < n; ++j)
+            if (q.word(st + 4 * j, st, st + n) != kw[j]) return false;
+    }
+    return true;
+}
+
+// Global-memory load through an explicitly global pointer: table pointers
+// travel inside image structs, where the compiler cannot infer the address
+// space and would emit flat loads.
+template <class T>
+VC_HD T gload(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(1))) T*)(p);
+#else
+    return *p;
+#endif
+}
+
+VC_HD uint4 tag_group(const uint32_t* tags, uint32_t mask, uint32_t h) {
+    return gload(reinterpret_cast<const uint4*>(tags + (h & mask & ~3u)));
+}
+
+VC_HD Rec load_rec_g(const HostRec* r, uint32_t s) {
+    const uint4* p = reinterpret_cast<const uint4*>(r + s);
+    return Rec{gload(p), gload(p + 1), gload(p + 2), gload(p + 3)};
+}
+
+// Tag matches of a 4-slot group that belong to the probe chain (before the
+// group's first empty slot), bits 0-3; bit 4 set when the group has no
+// empty slot (the chain continues into the next group).
+VC_HD uint32_t group_hits(uint4 g, uint32_t want) {
+    const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
+    uint32_t m = 0, open = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (!open && tg[k] == want) m |= 1u << k;
+        if (tg[k] == 0) open = 1;
+    }
+    return open ? m : (m | 16u);
+}
+
+// slot of key [st, st + n) with hash h; -1 if absent.  *out = its record.
+template <class Src>
+VC_HD int host_find(const HostTable& t, uint32_t h, const Src& q, int st, int n, Rec* out) {
+    const uint32_t want = h | 1u;
+    uint32_t s = h & t.mask & ~3u;
+    for (;;) {
+        uint32_t m = group_hits(gload(reinterpret_cast<const uint4*>(t.tags + s)), want);
+        while (m & 15u) {
+            const uint32_t k = __builtin_ctz(m);
+            m &= m - 1;
+            const Rec r = load_rec_g(t.recs, s + k);
+            if (rec_eq(r, t.blob, q, st, n)) {
+                *out = r;
+                return int(s + k);
+            }
+        }
+        if (!(m & 16u)) return -1;
+        s = (s + 4) & t.mask;
+    }
+}
+
+VC_HD HostTable host_table(const HintImage& img) {
+    return HostTable{img.host_tags, img.host_recs, img.blob, img.host_mask};
+}
+
+// port filter over a key's distinct hint-port minima (rare: out of line)
+__host__ __device__ __noinline__ uint32_t pick_ports(const HostExt* ext, const PortMin* pms,
+                                                      int slot, uint32_t v, int port) {
+    const HostExt x = ext[slot];
+    for (uint32_t i = 0; i < x.pm_cnt; ++i) {
+        const PortMin pm = pms[x.pm_off + i];
+        if (pm.port == port) v = uint32_t(pm.idx) < v ? uint32_t(pm.idx) : v;
+    }
+    return v;
+}
+
+// min handle index of a hint-host key not excluded by the port filter
+// (Hint.java:124-128): port == 0 -> any; else hint-port 0 or equal.
+VC_HD uint32_t pick(const HintImage& img, int slot, const Rec& r, int port) {
+    if (port == 0) return r.m.y;
+    if (!(r.m.x & VC_REC_HAS_PM)) return r.m.z;
+    return pick_ports(img.host_ext, img.port_mins, slot, r.m.z, port);
+}
+
+// Hash of [st, e) of a source (khash over a source, a word at a time).
+template <class Src>
+VC_HD uint32_t src_khash(const Src& q, int st, int e) {
+    uint32_t S = vck::kSeed;
+    for (int pos = e - 4; pos > st - 4; pos -= 4) S = vck::mix(S, q.word(pos, st, e));
+    return vck::fin(S, uint32_t(e - st));
+}
+
+// Exact lookup of [st, st + n).
+template <class Src>
+VC_HD int host_lookup(const HostTable& t, const Src& q, int st, int n, Rec* out) {
+    return host_find(t, src_khash(q, st, st + n), q, st, n, out);
+}
+
+VC_HD uint32_t wildcard_pick(const HintImage& img, int port) {
+    if (img.wildcard_slot < 0) return VC_NONE;
+    return pick(img, img.wildcard_slot, load_rec_g(img.host_recs, uint32_t(img.wildcard_slot)),
+                port);
+}
+
+// ---------------------------------------------------------------------------
+// Upstream.searchForGroup for hints whose uri is null (or when no group has
+// a hint-uri): level = hostLevel << 10, so exact (3) beats any suffix (2)
+// beats "*" (1), and within a level the lowest handle index wins (strict
+// '>' scan, Upstream.java:187-198).
+// ---------------------------------------------------------------------------
+
+// Reference-shaped form over a formatted host [s, e) of a plain string: any
+// number of labels, each dot-suffix probed as it is found.  Out of line: the
+// kernels reach it only for names the fast path does not take.
+__host__ __device__ __noinline__ int32_t host_only_seq(const HintImage& img, const uint8_t* p,
+                                                       int s, int e, int port) {
+    const HostTable t = host_table(img);
+    const PtrSrc q{p};
+    Rec r;
+    int slot = host_lookup(t, q, s, e - s, &r);
+    if (slot >= 0) {
+        const uint32_t v = pick(img, slot, r, port);
+        if (v != VC_NONE) return int32_t(v);
+    }
+    uint32_t best = VC_NONE;
+    for (int j = e - 1; j >= s; --j) {
+        if (p[j] != '.') continue;
+        slot = host_lookup(t, q, j + 1, e - j - 1, &r);
+        if (slot >= 0) {
+            const uint32_t v = pick(img, slot, r, port);
+            best = v < best ? v : best;
+        }
+    }
+    if (best != VC_NONE) return int32_t(best);
+    const uint32_t v = wildcard_pick(img, port);
+    return v != VC_NONE ? int32_t(v) : -1;
+}
+
+// Formatted host given as a plain string (the general path, the harness).
+VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
+    if (host.n < 0) return -1;
+    return host_only_seq(img, host.p, 0, host.n, port);
+}
+
+// Hint.formatHost + host-only search on a raw host of a plain string.
+__host__ __device__ __noinline__ int32_t host_only_slow(const HintImage& img, const uint8_t* p,
+                                                        int n, int port) {
+    return hint_host_only(img, format_host(DStr{p, n}), port);
+}
+
+constexpr int kMaxSuffix = 6;
+constexpr int kProbes = kMaxSuffix + 1;      // [0] = the whole host
+
+// Fast path: one right-to-left word scan of the raw host [0, n) computes
+// Hint.formatHost's cut at the first ':' (restarting the scan there) and the
+// hash of the host and of every dot-suffix; all first tag groups are then
+// loaded together, and only tag hits touch a record.  Names the scan does
+// not cover (two or more ':' -- a possible IPv6 literal -- or more than
+// kMaxSuffix labels) go to the reference-shaped slow path.
+template <class Src>
+VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
+                             int port) {
+    uint32_t h[kProbes];
+    int st[kProbes];
+    int e = n, np = 0, nc = 0;
+    uint32_t S = vck::kSeed;
+    for (int pos = n - 4; pos > -4;) {
+        const uint32_t valid = keep_mask(pos, 0, e);
+        const uint32_t w = q.word(pos, 0, e);
+        const uint32_t cf = vck::byte_eq_flags(w, 0x3A3A3A3Au) & valid;
+        if (cf) {                       // restart at the leftmost ':' so far
+            nc += __builtin_popcount(cf);
+            e = pos + (__builtin_ctz(cf) >> 3);
+            pos = e - 4;
+            S = vck::kSeed;
+            np = 0;
+            continue;
+        }
+        uint32_t df = vck::byte_eq_flags(w, 0x2E2E2E2Eu) & valid;
+        while (df) {                    // rightmost dot first: shortest suffix first
+            const int b = (31 - __builtin_clz(df)) >> 3;
+            df &= ~(0x80u << (8 * b));
+            const int sp = pos + b + 1;
+            const uint32_t len = uint32_t(e - sp);
+            const uint32_t hv = b == 3 ? vck::fin(S, len)
+                                       : vck::fin(vck::mix(S, w & (~0u << (8 * (b + 1)))), len);
+            ++np;
+#pragma unroll
+            for (int k = 1; k < kProbes; ++k)
+                if (k == np) {
+                    h[k] = hv;
+                    st[k] = sp;
+                }
+        }
+        S = vck::mix(S, w);
+        pos -= 4;
+    }
+    if (nc >= 2 || np > kMaxSuffix) return host_only_slow(*slow_img, q.ptr(), n, port);
+    h[0] = vck::fin(S, uint32_t(e));
+    st[0] = 0;
+    if (nc) {
+        // cut at the colon; strip "www." (then the whole host is the suffix
+        // after the dot at 3, recorded last); empty -> null
+        if (e >= 4 && q.word(0, 0, 4) == 0x2E777777u) {
+#pragma unroll
+            for (int k = 1; k < kProbes; ++k)
+                if (k == np) {
+                    h[0] = h[k];
+                    st[0] = 4;
+                }
+            np -= 1;
+        }
+        if (e - st[0] <= 0) return -1;
+    }
+    const HostTable t = host_table(img);
+    uint32_t hits = 0;
+    {
+        uint4 g[kProbes];
+#pragma unroll
+        for (int k = 0; k < kProbes; ++k)    // all first tag groups in flight together
+            g[k] = k <= np ? tag_group(t.tags, t.mask, h[k]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < kProbes; ++k)
+            if (group_hits(g[k], h[k] | 1u)) hits |= 1u << k;
+    }
+    uint32_t best = VC_NONE;
+    while (hits) {
+        const int k = __builtin_ctz(hits);
+        hits &= hits - 1;
+        uint32_t hk = h[0];
+        int sk = st[0];
+#pragma unroll
+        for (int j = 1; j < kProbes; ++j) {
+            hk = k == j ? h[j] : hk;
+            sk = k == j ? st[j] : sk;
+        }
+        Rec r;
+        const int slot = host_find(t, hk, q, sk, e - sk, &r);
+        if (slot < 0) continue;
+        const uint32_t v = pick(img, slot, r, port);
+        if (k == 0) {
+            if (v != VC_NONE) return int32_t(v);          // exact level wins
+        } else {
+            best = v < best ? v : best;
+        }
+    }
+    if (best == VC_NONE) best = wildcard_pick(img, port);
+    return best != VC_NONE ? int32_t(best) : -1;
+}
+
+// ---------------------------------------------------------------------------
+// URI keys (forward FNV-1a, 32-byte KeySlot): general path only
 // ---------------------------------------------------------------------------
 VC_HD KeySlot load_slot(const KeySlot* t, uint32_t s) {
     const uint4* p = reinterpret_cast<const uint4*>(t + s);
@@ -176,244 +512,25 @@ VC_HD KeySlot load_slot(const KeySlot* t, uint32_t s) {
     return k;
 }
 
-// key (16-byte aligned, zero padded in the blob) == query bytes p[0, n)?
-// One uint4 key load per 16 bytes and branch-free byte gathers of the query
-// (LDS when staged), instead of a byte-by-byte loop of dependent loads.
-VC_HD bool key_eq(const uint8_t* key, const uint8_t* q, int n) {
-    for (int base = 0; base < n; base += 16) {
-        const uint4 kw = *reinterpret_cast<const uint4*>(key + base);
-        const uint32_t k[4] = {kw.x, kw.y, kw.z, kw.w};
-        uint32_t diff = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            uint32_t qw = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int i = base + 4 * w + b;
-                qw |= uint32_t(i < n ? q[i] : 0) << (8 * b);
-            }
-            diff |= qw ^ k[w];
-        }
-        if (diff) return false;
-    }
-    return true;
-}
-
-// slot index of key (p, n) with hash h, or -1.  Linear probing from the
-// hash's 4-slot group: one 16-byte tag-group load per step; the 32-byte slot
-// and the key are read only on a tag hit.
-VC_HDN int probe(const uint32_t* tags, const KeySlot* t, uint32_t mask, const uint8_t* blob,
-                 uint32_t h, const uint8_t* p, int n, KeySlot* out) {
+VC_HDN int uri_probe(const HintImage& img, uint32_t h, const uint8_t* p, int n, KeySlot* out) {
     const uint32_t want = h | 1u;
-    uint32_t s = h & mask & ~3u;
+    uint32_t s = h & img.uri_mask & ~3u;
     for (;;) {
-        const uint4 g = *reinterpret_cast<const uint4*>(tags + s);
+        const uint4 g = *reinterpret_cast<const uint4*>(img.uri_tags + s);
         const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (tg[k] == 0) return -1;
             if (tg[k] == want) {
-                KeySlot ks = load_slot(t, s + k);
-                if (ks.key_len == n && key_eq(blob + ks.key_off, p, n)) {
+                KeySlot ks = load_slot(img.uri_slots, s + k);
+                if (ks.key_len == n && bytes_eq(img.blob + ks.key_off, p, n)) {
                     *out = ks;
                     return int(s + k);
                 }
             }
         }
-        s = (s + 4) & mask;
+        s = (s + 4) & img.uri_mask;
     }
-}
-
-// min handle index of a host key not excluded by the port filter
-// (Hint.java:124-128): port == 0 -> any; else hint-port 0 or equal.
-VC_HD uint32_t pick(const HintImage& img, int slot, const KeySlot& k, int port) {
-    if (port == 0) return uint32_t(k.a);
-    uint32_t v = uint32_t(k.b);
-    const uint32_t off = img.port_min_off[2 * slot], cnt = img.port_min_off[2 * slot + 1];
-    for (uint32_t i = 0; i < cnt; ++i) {
-        const PortMin pm = img.port_mins[off + i];
-        if (pm.port == port) v = uint32_t(pm.idx) < v ? uint32_t(pm.idx) : v;
-    }
-    return v;
-}
-
-// Continue a probe at group start `s` whose 16-byte tag group `g` is already
-// loaded (linear probing moves on only when that group is full of other keys).
-VC_HDN int probe_from(const uint32_t* tags, const KeySlot* t, uint32_t mask, const uint8_t* blob,
-                      uint32_t h, const uint8_t* p, int n, uint32_t s, uint4 g, KeySlot* out) {
-    const uint32_t want = h | 1u;
-    for (;;) {
-        const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (tg[k] == 0) return -1;
-            if (tg[k] == want) {
-                KeySlot ks = load_slot(t, s + k);
-                if (ks.key_len == n && key_eq(blob + ks.key_off, p, n)) {
-                    *out = ks;
-                    return int(s + k);
-                }
-            }
-        }
-        s = (s + 4) & mask;
-        g = *reinterpret_cast<const uint4*>(tags + s);
-    }
-}
-
-VC_HD uint4 tag_group(const uint32_t* tags, uint32_t mask, uint32_t h) {
-    return *reinterpret_cast<const uint4*>(tags + (h & mask & ~3u));
-}
-
-// Sequential form (any number of labels): scan right-to-left, probe at dots.
-VC_HDN int32_t hint_host_only_seq(const HintImage& img, DStr host, int port) {
-    uint32_t h = kFnvBasis;
-    uint32_t best_suffix = VC_NONE;
-    KeySlot k;
-    for (int j = host.n - 1; j >= 0; --j) {
-        const uint8_t c = host.p[j];
-        if (c == '.') {   // host.endsWith("." + H) with H = host[j+1..]
-            int s = probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
-                          host.n - j - 1, &k);
-            if (s >= 0) {
-                uint32_t c2 = pick(img, s, k, port);
-                best_suffix = c2 < best_suffix ? c2 : best_suffix;
-            }
-        }
-        h = fnv_step(h, c);
-    }
-    int s = probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k);
-    if (s >= 0) {
-        uint32_t e = pick(img, s, k, port);
-        if (e != VC_NONE) return int32_t(e);
-    }
-    if (best_suffix != VC_NONE) return int32_t(best_suffix);
-    if (img.wildcard_slot >= 0) {
-        KeySlot w = load_slot(img.host_slots, uint32_t(img.wildcard_slot));
-        uint32_t v = pick(img, img.wildcard_slot, w, port);
-        if (v != VC_NONE) return int32_t(v);
-    }
-    return -1;
-}
-
-// Per-probe summary of a loaded 16-byte tag group: bits 0-3 = slots whose
-// tag matches, bit 4 = the group holds no empty slot (probing may continue).
-VC_HD uint32_t group_code(uint4 g, uint32_t h) {
-    const uint32_t want = h | 1u;
-    const uint32_t tg[4] = {g.x, g.y, g.z, g.w};
-    uint32_t code = 0, open = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        // slots past the first empty one are never part of this key's chain
-        const bool before_empty = open == 0;
-        if (tg[k] == 0) open = 1;
-        if (before_empty && tg[k] == want) code |= 1u << k;
-    }
-    if (!open) code |= 16u;
-    return code;
-}
-
-// Resolve one probe given its first-group summary (slot loads + key compare
-// only for tag hits); -1 when absent.  Kept out of line: it runs about once
-// per name, and inlining it per suffix multiplied the register footprint.
-// Returns pick(...) of the matching host key, or VC_NONE when the key is
-// absent (or every member is excluded by the port filter).
-// (Takes the image's arrays one by one: passing the HintImage by reference
-// to an out-of-line function put a copy of it on the scratch stack.)
-__host__ __device__ __noinline__ uint32_t resolve_pick(
-    const uint32_t* tags, const KeySlot* slots, uint32_t mask, const uint8_t* blob,
-    const uint32_t* pm_off, const PortMin* pms, uint32_t h, const uint8_t* p, int n,
-    uint32_t code, int port) {
-    const uint32_t s0 = h & mask & ~3u;
-    int s = -1;
-    KeySlot ks;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (s < 0 && (code & (1u << k))) {
-            const KeySlot c = load_slot(slots, s0 + k);
-            if (c.key_len == n && key_eq(blob + c.key_off, p, n)) {
-                s = int(s0 + k);
-                ks = c;
-            }
-        }
-    }
-    if (s < 0) {
-        if (!(code & 16u)) return VC_NONE;
-        // the first group was full of other keys: continue linear probing
-        const uint32_t s1 = (s0 + 4) & mask;
-        s = probe_from(tags, slots, mask, blob, h, p, n, s1,
-                       *reinterpret_cast<const uint4*>(tags + s1), &ks);
-        if (s < 0) return VC_NONE;
-    }
-    if (port == 0) return uint32_t(ks.a);            // pick() (Hint.java:124-128)
-    uint32_t v = uint32_t(ks.b);
-    const uint32_t off = pm_off[2 * s], cnt = pm_off[2 * s + 1];
-    for (uint32_t i = 0; i < cnt; ++i) {
-        const PortMin pm = pms[off + i];
-        if (pm.port == port) v = uint32_t(pm.idx) < v ? uint32_t(pm.idx) : v;
-    }
-    return v;
-}
-
-// searchForGroup for hints whose uri is null (or no group has a hint-uri):
-// level = hostLevel << 10, so exact (3) beats any suffix (2) beats "*" (1),
-// and within a level the lowest handle index wins (strict '>' scan).
-// Batched form: one register-only scan hashes the whole host and every
-// dot-suffix, then all first tag groups are loaded together (independent
-// loads in flight) before any slot or key is touched.
-constexpr int kMaxSuffix = 6;
-
-VC_HDN int32_t hint_host_only(const HintImage& img, DStr host, int port) {
-    if (host.n < 0) return -1;
-    uint32_t hs[kMaxSuffix];
-    int st[kMaxSuffix];
-    int np = 0;
-    uint32_t h = kFnvBasis;
-    for (int j = host.n - 1; j >= 0; --j) {
-        const uint8_t c = host.p[j];
-        if (c == '.') {
-#pragma unroll
-            for (int k = 0; k < kMaxSuffix; ++k)
-                if (k == np) {
-                    hs[k] = h;
-                    st[k] = j + 1;
-                }
-            ++np;
-        }
-        h = fnv_step(h, c);
-    }
-    if (np > kMaxSuffix) return hint_host_only_seq(img, host, port);
-    uint4 g[kMaxSuffix + 1];
-    g[kMaxSuffix] = tag_group(img.host_tags, img.host_mask, h);
-#pragma unroll
-    for (int k = 0; k < kMaxSuffix; ++k)
-        if (k < np) g[k] = tag_group(img.host_tags, img.host_mask, hs[k]);
-    uint32_t code[kMaxSuffix + 1];
-    code[kMaxSuffix] = group_code(g[kMaxSuffix], h);
-#pragma unroll
-    for (int k = 0; k < kMaxSuffix; ++k) code[k] = k < np ? group_code(g[k], hs[k]) : 0u;
-    if (code[kMaxSuffix]) {
-        const uint32_t e = resolve_pick(img.host_tags, img.host_slots, img.host_mask, img.blob,
-                                        img.port_min_off, img.port_mins, h, host.p, host.n,
-                                        code[kMaxSuffix], port);
-        if (e != VC_NONE) return int32_t(e);
-    }
-    uint32_t best = VC_NONE;
-#pragma unroll
-    for (int k = 0; k < kMaxSuffix; ++k) {
-        if (code[k]) {
-            const uint32_t c = resolve_pick(img.host_tags, img.host_slots, img.host_mask,
-                                            img.blob, img.port_min_off, img.port_mins, hs[k],
-                                            host.p + st[k], host.n - st[k], code[k], port);
-            best = c < best ? c : best;
-        }
-    }
-    if (best != VC_NONE) return int32_t(best);
-    if (img.wildcard_slot >= 0) {
-        KeySlot w = load_slot(img.host_slots, uint32_t(img.wildcard_slot));
-        const uint32_t v = pick(img, img.wildcard_slot, w, port);
-        if (v != VC_NONE) return int32_t(v);
-    }
-    return -1;
 }
 
 // Hint.matchLevel for one merged group (Hint.java:100-160)
@@ -452,45 +569,51 @@ struct Best {
     }
 };
 
-VC_HDN void consider_list(const HintImage& img, const KeySlot& k, DStr host, int port, DStr uri,
-                              Best* b) {
-    for (uint32_t i = 0; i < k.list_cnt; ++i) {
-        uint32_t g = img.lists[k.list_off + i];
+VC_HDN void consider_members(const HintImage& img, uint32_t off, uint32_t cnt, DStr host,
+                             int port, DStr uri, Best* b) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+        uint32_t g = img.lists[off + i];
         b->consider(match_level(img, g, host, port, uri), int32_t(g));
     }
+}
+
+VC_HDN void consider_host_slot(const HintImage& img, int slot, DStr host, int port, DStr uri,
+                               Best* b) {
+    const HostExt x = img.host_ext[slot];
+    consider_members(img, x.list_off, x.list_cnt, host, port, uri, b);
 }
 
 // General searchForGroup: every group with a nonzero level has its hint-host
 // equal to / a dot-suffix of / "*" for the host, or its hint-uri a prefix
 // of / "*" for the uri; those candidate lists are scored exactly.
-VC_HDN int32_t hint_general(const HintImage& img, DStr host, int port, DStr uri) {
+__host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr host, int port,
+                                                      DStr uri) {
     Best b;
-    KeySlot k;
     if (host.n >= 0) {
-        uint32_t h = kFnvBasis;
+        const HostTable t = host_table(img);
+        const PtrSrc q{host.p};
+        Rec r;
         for (int j = host.n - 1; j >= 0; --j) {
-            const uint8_t c = host.p[j];
-            if (c == '.' && probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p + j + 1,
-                                  host.n - j - 1, &k) >= 0)
-                consider_list(img, k, host, port, uri, &b);
-            h = fnv_step(h, c);
+            if (host.p[j] != '.') continue;
+            const int slot = host_lookup(t, q, j + 1, host.n - j - 1, &r);
+            if (slot >= 0) consider_host_slot(img, slot, host, port, uri, &b);
         }
-        if (probe(img.host_tags, img.host_slots, img.host_mask, img.blob, h, host.p, host.n, &k) >= 0)
-            consider_list(img, k, host, port, uri, &b);
-        if (img.wildcard_slot >= 0)
-            consider_list(img, load_slot(img.host_slots, uint32_t(img.wildcard_slot)), host, port,
-                          uri, &b);
+        const int slot = host_lookup(t, q, 0, host.n, &r);
+        if (slot >= 0) consider_host_slot(img, slot, host, port, uri, &b);
+        if (img.wildcard_slot >= 0) consider_host_slot(img, img.wildcard_slot, host, port, uri, &b);
     }
     if (uri.n >= 0) {
+        KeySlot k;
         uint32_t h = kFnvBasis;
         for (int j = 0; j <= uri.n; ++j) {
-            if (probe(img.uri_tags, img.uri_slots, img.uri_mask, img.blob, h, uri.p, j, &k) >= 0)
-                consider_list(img, k, host, port, uri, &b);
+            if (uri_probe(img, h, uri.p, j, &k) >= 0)
+                consider_members(img, k.list_off, k.list_cnt, host, port, uri, &b);
             if (j < uri.n) h = fnv_step(h, uri.p[j]);
         }
-        if (img.uri_star_slot >= 0)
-            consider_list(img, load_slot(img.uri_slots, uint32_t(img.uri_star_slot)), host, port,
-                          uri, &b);
+        if (img.uri_star_slot >= 0) {
+            const KeySlot u = load_slot(img.uri_slots, uint32_t(img.uri_star_slot));
+            consider_members(img, u.list_off, u.list_cnt, host, port, uri, &b);
+        }
     }
     return b.idx;
 }
@@ -499,6 +622,42 @@ VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,
                                                     DStr uri) {
     if (uri.n < 0 || !img.has_uri_keys) return hint_host_only(img, host, port);
     return hint_general(img, host, port, uri);
+}
+
+// DNSServer.handleRequest classification (DNSServer.java:116-166) on the
+// query name bytes (trailing dot included, Formatter.parseDomainName).
+template <class Src>
+VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
+                   const Src& q,
+                                        int qn, uint8_t* kind, int32_t* value) {
+    // (1) hosts.get(qname) on the raw qname (trailing dot kept), :127
+    if (hosts.n > 0) {
+        Rec r;
+        const HostTable t{hosts.tags, hosts.recs, hosts.blob, hosts.mask};
+        if (host_lookup(t, q, 0, qn, &r) >= 0) {
+            *kind = VC_DNS_HOSTS;
+            *value = int32_t(r.m.y);
+            return;
+        }
+    }
+    // (2) strip one trailing dot, :133-135
+    const uint8_t* qp = q.ptr();
+    const int dn = (qn > 0 && (q.word(qn - 1, qn - 1, qn) & 0xFFu) == '.') ? qn - 1 : qn;
+    // (3) rrsets.searchForGroup(Hint.ofHost(domain)), :136
+    const int32_t g = host_only_fast(img, slow_img, q, dn, 0);
+    if (g >= 0) {
+        *kind = VC_DNS_GROUP;
+        *value = g;
+    } else if (d_is_ip_literal(qp, dn)) {            // (4) IP literal, :140-149
+        *kind = VC_DNS_IP_LITERAL;
+        *value = d_count(qp, dn, ':') ? 6 : 4;
+    } else {                                          // (5) *.vproxy.local, :150-157
+        const char* sfx = ".vproxy.local";
+        bool internal = dn >= 13;
+        for (int j = 0; internal && j < 13; ++j) internal = qp[dn - 13 + j] == uint8_t(sfx[j]);
+        *kind = internal ? VC_DNS_INTERNAL : VC_DNS_RECURSIVE;   // (6) :164
+        *value = 0;
+    }
 }
 
 }  // namespace vcd
