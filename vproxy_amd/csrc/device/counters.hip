@@ -3,106 +3,100 @@
 // Counting with one device atomic per item is memory-side and serialises on
 // hot bins: a wildcard group or default route taking 20 % of a batch ran at
 // 0.4 G adds/s on MI355X (tools/atomics_probe.hip), 60x slower than the
-// classify kernel itself.  Instead each workgroup histograms a slice of the
-// output array in LDS (hot bins cost LDS atomics only), one 32K-bin chunk of
-// the counter space per grid row, then flushes its non-zero bins with
-// consecutive-lane (coalesced) device atomics into the uint64 counters.
+// classify kernel itself.  So counts are built in LDS and flushed once per
+// workgroup with consecutive-lane (coalesced) device atomics:
+//
+// * small counter spaces (<= 64K bins: ACL rules): every workgroup
+//   histograms a contiguous slice of the outputs into a 32K-bin LDS
+//   histogram per grid row, 4 items per lane per 16-byte load;
+// * large spaces (routes: ~1.2M bins; groups: 100K) are first partitioned
+//   into 8K-bin buckets -- count, scan, then a scatter that sorts each
+//   8K-item tile by bucket in LDS so the bucket runs leave as contiguous
+//   stores -- and each bucket is then histogrammed in LDS by segments of at
+//   most kSeg items (a hot bucket is split over many workgroups).
+//
+// Null results (no rule / default) are counted in registers and added once
+// per workgroup; a thread collapses runs of equal values before touching
+// LDS, which keeps hot bins off a single LDS address.
 #include "dev_common.h"
 #include "launch.h"
 
 namespace vcd {
 
-constexpr int kHistBins = 32768;   // 128 KiB of LDS per workgroup
 constexpr int kHistBlock = 1024;
-
-// bin of item i in the chunked value space [0, nval); -1 = the null bin
-__device__ __forceinline__ int64_t hist_value(int mode, const int32_t* idx, const uint8_t* aux,
-                                              int64_t i, int32_t nt, bool* tcp_null) {
-    const int32_t v = idx[i];
-    *tcp_null = false;
-    if (mode == VC_HIST_ACL) {
-        const bool tcp = aux[i] == VC_PROTO_TCP;
-        if (v < 0) {
-            *tcp_null = tcp;
-            return -1;
-        }
-        return tcp ? int64_t(v) : int64_t(nt) + v;
-    }
-    if (mode == VC_HIST_DNS && aux[i] != VC_DNS_GROUP) return -1;
-    return v;
-}
-
-__global__ __launch_bounds__(kHistBlock) void hist_kernel(
-    int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
-    int64_t nval, int64_t base, int64_t null_bin, int32_t nt, unsigned long long* __restrict__ cnt) {
-    __shared__ uint32_t h[kHistBins];
-    __shared__ uint32_t nulls[2];
-    const int64_t lo_bin = int64_t(blockIdx.y) * kHistBins;
-    for (int k = threadIdx.x; k < kHistBins; k += blockDim.x) h[k] = 0;
-    if (threadIdx.x < 2) nulls[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = int64_t(blockIdx.x) * per;
-    const int64_t hi = lo + per < n ? lo + per : n;
-    const bool count_nulls = blockIdx.y == 0;
-    uint32_t my_null[2] = {0, 0};
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        bool tcp_null;
-        const int64_t v = hist_value(mode, idx, aux, i, nt, &tcp_null);
-        if (v < 0) {
-            my_null[tcp_null ? 0 : 1] += count_nulls;
-        } else {
-            const uint64_t d = uint64_t(v - lo_bin);
-            if (d < uint64_t(kHistBins)) atomicAdd(&h[d], 1u);
-        }
-    }
-    if (count_nulls) {
-        if (my_null[0]) atomicAdd(&nulls[0], my_null[0]);
-        if (my_null[1]) atomicAdd(&nulls[1], my_null[1]);
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < kHistBins && lo_bin + k < nval; k += blockDim.x)
-        if (h[k]) atomicAdd(cnt + base + lo_bin + k, (unsigned long long)h[k]);
-    if (count_nulls && threadIdx.x == 0) {
-        // ACL: [tcp default, udp default] at null_bin, null_bin + 1
-        if (mode == VC_HIST_ACL) {
-            if (nulls[0]) atomicAdd(cnt + null_bin, (unsigned long long)nulls[0]);
-            if (nulls[1]) atomicAdd(cnt + null_bin + 1, (unsigned long long)nulls[1]);
-        } else if (nulls[1]) {
-            atomicAdd(cnt + null_bin, (unsigned long long)nulls[1]);
-        }
-    }
-}
-
-// ---- bucketed path for large counter spaces (route tables) ----------------
-// Items are first partitioned by 32K-bin chunk ("bucket") with a per-block
-// count / scan / scatter, so each chunk's histogram then reads only its own
-// items: ~4 passes over the outputs instead of one pass per chunk.
+constexpr int kHistBins = 32768;      // small path: 128 KiB of LDS per workgroup
+constexpr int kBW = 8192;             // large path: bins per bucket (32 KiB of LDS)
 constexpr int kMaxBuckets = 4096;
+constexpr int kTile = 8192;           // scatter tile: items sorted by bucket in LDS
+constexpr uint32_t kSeg = 256 * 1024; // max items per histogram segment
 
-__global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
-    int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
-    int32_t nt, int nbk, uint32_t* __restrict__ counts, unsigned long long* __restrict__ cnt,
-    int64_t null_bin) {
-    __shared__ uint32_t c[kMaxBuckets];
+// Item i -> bin in [0, nval), or -1 for a null result (*udp_or_plain_null
+// tells the ACL's two default bins apart).
+struct Item {
+    int64_t v;
+    bool tcp_null;
+};
+
+__device__ __forceinline__ Item item_of(int mode, int32_t v, uint8_t a, int32_t nt) {
+    if (mode == VC_HIST_ACL) {
+        const bool tcp = a == VC_PROTO_TCP;
+        if (v < 0) return Item{-1, tcp};
+        return Item{tcp ? int64_t(v) : int64_t(nt) + v, false};
+    }
+    if (mode == VC_HIST_DNS && a != VC_DNS_GROUP) return Item{-2, false};   // not counted
+    return Item{v < 0 ? -1 : int64_t(v), false};
+}
+
+// 4 consecutive items starting at i (i % 4 == 0, i + 3 < n) with one 16-byte
+// load of the outputs (and one 4-byte load of aux).
+__device__ __forceinline__ void load4(int mode, const int32_t* idx, const uint8_t* aux, int64_t i,
+                                      int32_t nt, Item it[4]) {
+    const int4 v = *reinterpret_cast<const int4*>(idx + i);
+    const uint32_t a = aux ? *reinterpret_cast<const uint32_t*>(aux + i) : 0u;
+    it[0] = item_of(mode, v.x, a & 255u, nt);
+    it[1] = item_of(mode, v.y, (a >> 8) & 255u, nt);
+    it[2] = item_of(mode, v.z, (a >> 16) & 255u, nt);
+    it[3] = item_of(mode, v.w, a >> 24, nt);
+}
+
+__device__ __forceinline__ Item load1(int mode, const int32_t* idx, const uint8_t* aux, int64_t i,
+                                      int32_t nt) {
+    return item_of(mode, idx[i], aux ? aux[i] : 0, nt);
+}
+
+// Adds n (>0) to LDS bin b.
+__device__ __forceinline__ void lds_add(uint32_t* h, int64_t b, uint32_t c) {
+    if (c) atomicAdd(&h[b], c);
+}
+
+// Per-thread run-length collapse in front of LDS atomics.
+struct Run {
+    int64_t v = -1;
+    uint32_t c = 0;
+    __device__ __forceinline__ void add(int64_t x, uint32_t* h, int64_t lo, int64_t width) {
+        if (x == v) {
+            ++c;
+            return;
+        }
+        if (c && uint64_t(v - lo) < uint64_t(width)) atomicAdd(&h[v - lo], c);
+        v = x;
+        c = 1;
+    }
+    __device__ __forceinline__ void flush(uint32_t* h, int64_t lo, int64_t width) {
+        if (c && uint64_t(v - lo) < uint64_t(width)) atomicAdd(&h[v - lo], c);
+        c = 0;
+    }
+};
+
+__device__ __forceinline__ void flush_nulls(int mode, uint32_t n_tcp, uint32_t n_other,
+                                            int64_t null_bin, unsigned long long* cnt) {
+    // ACL: [tcp default, udp default] at null_bin, null_bin + 1
     __shared__ uint32_t nulls[2];
-    for (int k = threadIdx.x; k < nbk; k += blockDim.x) c[k] = 0;
     if (threadIdx.x < 2) nulls[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = int64_t(blockIdx.x) * per;
-    const int64_t hi = lo + per < n ? lo + per : n;
-    uint32_t my_null[2] = {0, 0};
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        bool tcp_null;
-        const int64_t v = hist_value(mode, idx, aux, i, nt, &tcp_null);
-        if (v < 0) my_null[tcp_null ? 0 : 1]++;
-        else atomicAdd(&c[v / kHistBins], 1u);
-    }
-    if (my_null[0]) atomicAdd(&nulls[0], my_null[0]);
-    if (my_null[1]) atomicAdd(&nulls[1], my_null[1]);
+    if (n_tcp) atomicAdd(&nulls[0], n_tcp);
+    if (n_other) atomicAdd(&nulls[1], n_other);
     __syncthreads();
-    for (int k = threadIdx.x; k < nbk; k += blockDim.x) counts[int64_t(k) * gridDim.x + blockIdx.x] = c[k];
     if (threadIdx.x == 0) {
         if (mode == VC_HIST_ACL) {
             if (nulls[0]) atomicAdd(cnt + null_bin, (unsigned long long)nulls[0]);
@@ -113,69 +107,272 @@ __global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
     }
 }
 
-// exclusive scan of counts (bucket-major, m entries) -> offsets; one block
-__global__ __launch_bounds__(kHistBlock) void bucket_scan_kernel(const uint32_t* __restrict__ counts,
-                                                                 uint32_t* __restrict__ offsets,
-                                                                 int64_t m) {
-    __shared__ uint32_t part[kHistBlock];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < m; base += kHistBlock) {
-        const int64_t i = base + threadIdx.x;
-        const uint32_t v = i < m ? counts[i] : 0;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (int off = 1; off < kHistBlock; off <<= 1) {      // Hillis-Steele inclusive scan
-            const uint32_t t = int(threadIdx.x) >= off ? part[threadIdx.x - off] : 0;
-            __syncthreads();
-            part[threadIdx.x] += t;
-            __syncthreads();
-        }
-        if (i < m) offsets[i] = carry + part[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == kHistBlock - 1) carry += part[kHistBlock - 1];
-        __syncthreads();
+__device__ __forceinline__ void count_null(const Item& it, uint32_t* nt, uint32_t* no) {
+    if (it.v == -1) {
+        if (it.tcp_null) ++*nt;
+        else ++*no;
     }
-    if (threadIdx.x == 0) offsets[m] = carry;     // grand total: end of the last bucket
 }
 
+// Contiguous slice [lo, hi) of n items owned by this workgroup, split on
+// 4-item boundaries.
+__device__ __forceinline__ void slice_of(int64_t n, int64_t* lo, int64_t* hi) {
+    const int64_t groups = (n + 3) >> 2;
+    const int64_t per = (groups + gridDim.x - 1) / gridDim.x;
+    *lo = int64_t(blockIdx.x) * per * 4;
+    const int64_t h = *lo + per * 4;
+    *hi = h < n ? h : n;
+    if (*lo > n) *lo = n;
+}
+
+// ---- small counter spaces --------------------------------------------------
+template <bool kVec>
+__global__ __launch_bounds__(kHistBlock) void hist_kernel(
+    int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
+    int64_t nval, int64_t base, int64_t null_bin, int32_t nt, unsigned long long* __restrict__ cnt) {
+    __shared__ uint32_t h[kHistBins];
+    const int64_t lo_bin = int64_t(blockIdx.y) * kHistBins;
+    for (int k = threadIdx.x; k < kHistBins; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    int64_t lo, hi;
+    slice_of(n, &lo, &hi);
+    uint32_t ntc = 0, noth = 0;
+    Run run;
+    if (kVec) {
+        for (int64_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+            Item it[4];
+            if (i + 3 < n) {
+                load4(mode, idx, aux, i, nt, it);
+            } else {
+                for (int k = 0; k < 4; ++k) it[k] = i + k < n ? load1(mode, idx, aux, i + k, nt)
+                                                               : Item{-2, false};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                count_null(it[k], &ntc, &noth);
+                if (it[k].v >= 0) run.add(it[k].v, h, lo_bin, kHistBins);
+            }
+        }
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            const Item it = load1(mode, idx, aux, i, nt);
+            count_null(it, &ntc, &noth);
+            if (it.v >= 0) run.add(it.v, h, lo_bin, kHistBins);
+        }
+    }
+    run.flush(h, lo_bin, kHistBins);
+    if (blockIdx.y != 0) ntc = noth = 0;      // nulls counted by grid row 0 only
+    flush_nulls(mode, ntc, noth, null_bin, cnt);
+    for (int k = threadIdx.x; k < kHistBins && lo_bin + k < nval; k += blockDim.x)
+        if (h[k]) atomicAdd(cnt + base + lo_bin + k, (unsigned long long)h[k]);
+}
+
+// ---- large counter spaces --------------------------------------------------
+// (1) per-workgroup bucket counts: counts[b * nblk + blk]
+template <bool kVec>
+__global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
+    int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
+    int32_t nt, int nbk, uint32_t* __restrict__ counts, unsigned long long* __restrict__ cnt,
+    int64_t null_bin) {
+    __shared__ uint32_t c[kMaxBuckets];
+    for (int k = threadIdx.x; k < nbk; k += blockDim.x) c[k] = 0;
+    __syncthreads();
+    int64_t lo, hi;
+    slice_of(n, &lo, &hi);
+    uint32_t ntc = 0, noth = 0;
+    Run run;
+    const int64_t step = (kVec ? 4 : 1) * int64_t(blockDim.x);
+    for (int64_t i = lo + (kVec ? 4 : 1) * threadIdx.x; i < hi; i += step) {
+        Item it[4];
+        int m = 1;
+        if (kVec && i + 3 < n) {
+            load4(mode, idx, aux, i, nt, it);
+            m = 4;
+        } else if (kVec) {
+            for (int k = 0; k < 4; ++k) it[k] = i + k < n ? load1(mode, idx, aux, i + k, nt)
+                                                           : Item{-2, false};
+            m = 4;
+        } else {
+            it[0] = load1(mode, idx, aux, i, nt);
+        }
+        for (int k = 0; k < m; ++k) {
+            count_null(it[k], &ntc, &noth);
+            if (it[k].v >= 0) run.add(it[k].v / kBW, c, 0, nbk);
+        }
+    }
+    run.flush(c, 0, nbk);
+    flush_nulls(mode, ntc, noth, null_bin, cnt);
+    for (int k = threadIdx.x; k < nbk; k += blockDim.x)
+        counts[int64_t(k) * gridDim.x + blockIdx.x] = c[k];
+}
+
+// (2) one workgroup: exclusive scan of counts (bucket-major, m entries) ->
+// offsets[0..m]; then the segment table seg_off[0..nbk] (segments of at
+// most kSeg items per bucket, prefix-summed).
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* part, uint32_t* total) {
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < kHistBlock; off <<= 1) {      // Hillis-Steele inclusive scan
+        const uint32_t t = int(threadIdx.x) >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+    }
+    const uint32_t incl = part[threadIdx.x];
+    *total = part[kHistBlock - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(kHistBlock) void bucket_scan_kernel(
+    const uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets, int64_t m, int nbk,
+    int nblk, uint32_t* __restrict__ seg_off) {
+    __shared__ uint32_t part[kHistBlock];
+    // each thread scans a contiguous run of the m entries
+    const int64_t per = (m + kHistBlock - 1) / kHistBlock;
+    const int64_t a = int64_t(threadIdx.x) * per;
+    const int64_t b = a + per < m ? a + per : m;
+    uint32_t sum = 0;
+    for (int64_t i = a; i < b; ++i) sum += counts[i];
+    uint32_t total;
+    uint32_t run = block_scan_excl(sum, part, &total);
+    for (int64_t i = a; i < b; ++i) {
+        const uint32_t v = counts[i];
+        offsets[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) offsets[m] = total;
+    __syncthreads();
+    __threadfence_block();
+    // segment table over buckets (nbk <= kMaxBuckets = 4 * kHistBlock)
+    uint32_t segs[4];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int bk = threadIdx.x * 4 + k;
+        uint32_t s = 0;
+        if (bk < nbk) {
+            const uint32_t len = offsets[int64_t(bk + 1) * nblk] - offsets[int64_t(bk) * nblk];
+            s = (len + kSeg - 1) / kSeg;
+        }
+        segs[k] = s;
+        mine += s;
+    }
+    uint32_t st = block_scan_excl(mine, part, &total);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int bk = threadIdx.x * 4 + k;
+        if (bk < nbk) seg_off[bk] = st;
+        st += segs[k];
+    }
+    if (threadIdx.x == 0) seg_off[nbk] = total;
+}
+
+// (3) scatter each workgroup's slice into bucket-contiguous order, a tile of
+// kTile items at a time sorted by bucket in LDS, so bucket runs are written
+// with consecutive lanes.
+template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
     int32_t nt, int nbk, const uint32_t* __restrict__ offsets, int32_t* __restrict__ tmp) {
-    __shared__ uint32_t cur[kMaxBuckets];
-    for (int k = threadIdx.x; k < nbk; k += blockDim.x)
+    __shared__ uint32_t cur[kMaxBuckets];     // next global write position per bucket
+    __shared__ uint32_t tcnt[kMaxBuckets];    // this tile's count per bucket
+    __shared__ uint32_t tst[kMaxBuckets];     // this tile's exclusive start per bucket
+    __shared__ int32_t sorted[kTile];
+    __shared__ uint32_t part[kHistBlock];
+    for (int k = threadIdx.x; k < nbk; k += blockDim.x) {
         cur[k] = offsets[int64_t(k) * gridDim.x + blockIdx.x];
+        tcnt[k] = 0;
+    }
     __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = int64_t(blockIdx.x) * per;
-    const int64_t hi = lo + per < n ? lo + per : n;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        bool tcp_null;
-        const int64_t v = hist_value(mode, idx, aux, i, nt, &tcp_null);
-        if (v >= 0) tmp[atomicAdd(&cur[v / kHistBins], 1u)] = int32_t(v);
+    int64_t lo, hi;
+    slice_of(n, &lo, &hi);
+    constexpr int kPer = kTile / kHistBlock;  // items per thread per tile
+    for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
+        int32_t v[kPer];
+        uint32_t r[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; q += 4) {
+            const int64_t i = t0 + int64_t(q) * kHistBlock + 4 * threadIdx.x;
+            Item it[4];
+            if (kVec && i + 3 < hi) {
+                load4(mode, idx, aux, i, nt, it);
+            } else {
+                for (int k = 0; k < 4; ++k) it[k] = i + k < hi ? load1(mode, idx, aux, i + k, nt)
+                                                                : Item{-2, false};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[q + k] = it[k].v >= 0 ? int32_t(it[k].v) : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < kPer; ++q)
+            r[q] = v[q] >= 0 ? atomicAdd(&tcnt[v[q] / kBW], 1u) : 0u;
+        __syncthreads();
+        // exclusive scan of tcnt over the buckets: 4 per thread, then block scan
+        uint32_t c4[4], s4 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int bk = threadIdx.x * 4 + k;
+            c4[k] = bk < nbk ? tcnt[bk] : 0u;
+            s4 += c4[k];
+        }
+        uint32_t total;
+        uint32_t st = block_scan_excl(s4, part, &total);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int bk = threadIdx.x * 4 + k;
+            if (bk < nbk) tst[bk] = st;
+            st += c4[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kPer; ++q)
+            if (v[q] >= 0) sorted[tst[v[q] / kBW] + r[q]] = v[q];
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < total; j += blockDim.x) {
+            const int32_t x = sorted[j];
+            const int bk = x / kBW;
+            tmp[cur[bk] + (j - tst[bk])] = x;
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < nbk; k += blockDim.x) {
+            cur[k] += tcnt[k];
+            tcnt[k] = 0;
+        }
+        __syncthreads();
     }
 }
 
-// grid (slices, buckets): histogram bucket b's items in LDS, flush
+// (4) one workgroup per segment of a bucket: LDS histogram, coalesced flush
 __global__ __launch_bounds__(kHistBlock) void bucket_hist_kernel(
-    const int32_t* __restrict__ tmp, const uint32_t* __restrict__ offsets, int nblk, int nbk,
-    int64_t nval, int64_t base, unsigned long long* __restrict__ cnt) {
-    __shared__ uint32_t h[kHistBins];
-    const int b = blockIdx.y;
-    const uint32_t s0 = offsets[int64_t(b) * nblk];
-    const uint32_t s1 = offsets[int64_t(b + 1) * nblk];   // offsets[nbk * nblk] = total
-    for (int k = threadIdx.x; k < kHistBins; k += blockDim.x) h[k] = 0;
+    const int32_t* __restrict__ tmp, const uint32_t* __restrict__ offsets,
+    const uint32_t* __restrict__ seg_off, int nblk, int nbk, int64_t nval, int64_t base,
+    unsigned long long* __restrict__ cnt) {
+    __shared__ uint32_t h[kBW];
+    __shared__ int s_bucket;
+    const uint32_t seg = blockIdx.x;
+    if (seg >= seg_off[nbk]) return;                       // uniform per workgroup
+    if (threadIdx.x == 0) {                                // last bucket with seg_off <= seg
+        int a = 0, len = nbk + 1;
+        while (len > 1) {
+            const int half = len >> 1;
+            a = seg_off[a + half] <= seg ? a + half : a;
+            len -= half;
+        }
+        s_bucket = a;
+    }
+    for (int k = threadIdx.x; k < kBW; k += blockDim.x) h[k] = 0;
     __syncthreads();
-    const uint32_t len = s1 - s0;
-    const uint32_t per = (len + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = s0 + blockIdx.x * per;
-    const uint32_t hi = lo + per < s1 ? lo + per : s1;
-    const int64_t lo_bin = int64_t(b) * kHistBins;
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-        atomicAdd(&h[tmp[i] - lo_bin], 1u);
+    const int b = s_bucket;
+    const uint32_t b0 = offsets[int64_t(b) * nblk], b1 = offsets[int64_t(b + 1) * nblk];
+    const uint32_t s0 = b0 + (seg - seg_off[b]) * kSeg;
+    const uint32_t s1 = s0 + kSeg < b1 ? s0 + kSeg : b1;
+    const int64_t lo_bin = int64_t(b) * kBW;
+    Run run;
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) run.add(tmp[i], h, lo_bin, kBW);
+    run.flush(h, lo_bin, kBW);
     __syncthreads();
-    for (int k = threadIdx.x; k < kHistBins && lo_bin + k < nval; k += blockDim.x)
+    for (int k = threadIdx.x; k < kBW && lo_bin + k < nval; k += blockDim.x)
         if (h[k]) atomicAdd(cnt + base + lo_bin + k, (unsigned long long)h[k]);
 }
 
@@ -187,46 +384,62 @@ hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const u
                        int64_t n, int64_t nval, int64_t base, int64_t null_bin, int32_t nt,
                        unsigned long long* counters) {
     if (n <= 0 || !counters) return hipSuccess;
+    const bool vec = (reinterpret_cast<uintptr_t>(idx) & 15) == 0 &&
+                     (!aux || (reinterpret_cast<uintptr_t>(aux) & 3) == 0);
     const int64_t chunks = nval > 0 ? (nval + vcd::kHistBins - 1) / vcd::kHistBins : 1;
-    if (chunks <= 2 || chunks > vcd::kMaxBuckets || n >= (int64_t(1) << 32)) {
-        // small counter space: one pass per chunk over the outputs
+    const int64_t nbk64 = nval > 0 ? (nval + vcd::kBW - 1) / vcd::kBW : 1;
+    if (chunks <= 2 || nbk64 > vcd::kMaxBuckets || n >= (int64_t(1) << 32)) {
+        // small counter space: one pass per 32K-bin chunk over the outputs
         int64_t slices = (int64_t(c.num_cus) * 2 + chunks - 1) / chunks;
         const int64_t max_slices = (n + 65535) / 65536;     // >= 64K items per workgroup
         if (slices > max_slices) slices = max_slices;
         if (slices < 1) slices = 1;
-        hipLaunchKernelGGL(vcd::hist_kernel, dim3(unsigned(slices), unsigned(chunks)),
-                           dim3(vcd::kHistBlock), 0, c.stream, mode, idx, aux, n, nval, base,
-                           null_bin, nt, counters);
+        if (vec)
+            hipLaunchKernelGGL(vcd::hist_kernel<true>, dim3(unsigned(slices), unsigned(chunks)),
+                               dim3(vcd::kHistBlock), 0, c.stream, mode, idx, aux, n, nval, base,
+                               null_bin, nt, counters);
+        else
+            hipLaunchKernelGGL(vcd::hist_kernel<false>, dim3(unsigned(slices), unsigned(chunks)),
+                               dim3(vcd::kHistBlock), 0, c.stream, mode, idx, aux, n, nval, base,
+                               null_bin, nt, counters);
         return hipGetLastError();
     }
-    // large counter space: partition by chunk first (count, scan, scatter)
-    const int nbk = int(chunks);
+    // large counter space: bucket partition (count, scan, sorted scatter),
+    // then per-segment LDS histograms
+    const int nbk = int(nbk64);
     int nblk = c.num_cus * 2;
-    const int64_t max_blk = (n + 16383) / 16384;
+    const int64_t max_blk = (n + 65535) / 65536;
     if (nblk > max_blk) nblk = int(max_blk < 1 ? 1 : max_blk);
     const int64_t m = int64_t(nbk) * nblk;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    const int64_t max_segs = (n + vcd::kSeg - 1) / vcd::kSeg + nbk;
+    uint32_t *counts = nullptr, *offsets = nullptr, *seg_off = nullptr;
     int32_t* tmp = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&counts), size_t(m) * 4, c.stream);
     if (e == hipSuccess)
         e = hipMallocAsync(reinterpret_cast<void**>(&offsets), size_t(m + 1) * 4, c.stream);
+    if (e == hipSuccess)
+        e = hipMallocAsync(reinterpret_cast<void**>(&seg_off), size_t(nbk + 1) * 4, c.stream);
     if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&tmp), size_t(n) * 4, c.stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(vcd::bucket_count_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0,
-                           c.stream, mode, idx, aux, n, nt, nbk, counts, counters, null_bin);
+#define VC_BK(K, ...)                                                                              \
+    do {                                                                                           \
+        if (vec) hipLaunchKernelGGL(K<true>, __VA_ARGS__);                                         \
+        else hipLaunchKernelGGL(K<false>, __VA_ARGS__);                                            \
+    } while (0)
+        VC_BK(vcd::bucket_count_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0, c.stream, mode, idx,
+              aux, n, nt, nbk, counts, counters, null_bin);
         hipLaunchKernelGGL(vcd::bucket_scan_kernel, dim3(1), dim3(vcd::kHistBlock), 0, c.stream,
-                           counts, offsets, m);
-        hipLaunchKernelGGL(vcd::bucket_scatter_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0,
-                           c.stream, mode, idx, aux, n, nt, nbk, offsets, tmp);
-        int64_t per_bucket = (n / nbk + 65535) / 65536;
-        int slices = int(per_bucket < 1 ? 1 : (per_bucket > 64 ? 64 : per_bucket));
-        if (slices * nbk < c.num_cus) slices = (c.num_cus + nbk - 1) / nbk;
-        hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(slices, nbk), dim3(vcd::kHistBlock), 0,
-                           c.stream, tmp, offsets, nblk, nbk, nval, base, counters);
+                           counts, offsets, m, nbk, nblk, seg_off);
+        VC_BK(vcd::bucket_scatter_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0, c.stream, mode,
+              idx, aux, n, nt, nbk, offsets, tmp);
+#undef VC_BK
+        hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(unsigned(max_segs)), dim3(vcd::kHistBlock),
+                           0, c.stream, tmp, offsets, seg_off, nblk, nbk, nval, base, counters);
         e = hipGetLastError();
     }
     if (counts) (void)hipFreeAsync(counts, c.stream);
     if (offsets) (void)hipFreeAsync(offsets, c.stream);
+    if (seg_off) (void)hipFreeAsync(seg_off, c.stream);
     if (tmp) (void)hipFreeAsync(tmp, c.stream);
     return e;
 }
