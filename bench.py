@@ -139,6 +139,33 @@ def cpu_baseline_c5(tcp, udp, v4_list, groups, names_blob, names_off, seed, thre
                       "them, %d threads, %.1f s" % (n, len(v4_list), len(groups), threads, t)}
 
 
+def hip_stream(dev):
+    """A fresh non-blocking HIP stream wrapped for torch.  HIP spreads the
+    streams a process creates round-robin over its hardware queues; three
+    created back to back land on three queues, so the kernels on them can
+    run concurrently (torch's pooled streams shared a queue here)."""
+    hip = C.CDLL("libamdhip64.so")
+    h = C.c_void_p()
+    rc = hip.hipStreamCreateWithFlags(C.byref(h), C.c_uint(1))      # hipStreamNonBlocking
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def gather_ceiling(table_mb=64):
+    """Measured random 4-byte gather rate (G gathers/s) from a table of
+    `table_mb`, two independent gathers per item (tools/gather_probe.hip,
+    profiles/r01_gather_probe.csv): the ceiling of the pipeline kernel,
+    whose route-root and pool tables are 64 MB each."""
+    import csv
+    try:
+        with open(os.path.join(PROFILES, "r01_gather_probe.csv")) as f:
+            rows = [r for r in csv.DictReader(f) if int(r["table_MB"]) == table_mb and
+                    int(r["gathers_per_item"]) == 2]
+        return max(float(r["G_gathers_per_s"]) for r in rows) if rows else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def load_traffic(workload, kernel):
     """Per-launch HBM-side bytes of `kernel` from the committed PMC passes
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
@@ -163,6 +190,8 @@ def main():
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true", help="ablation: skip hit counters")
+    ap.add_argument("--serial", action="store_true",
+                    help="ablation: one stream, no overlap between consecutive batches")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -209,57 +238,104 @@ def main():
     B = args.packets
     proto, src, dst, dport, hid = gen_packets(B, tcp, udp, net, plen, args.pool,
                                               1234 + rank, dev)
-    outs = tuple(torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)) + (None,)
+    # Two batches in flight: outputs and pool results are double-buffered so
+    # batch j's hit counters (and batch j+1's hostname pool) run on their own
+    # streams while batch j+1's pipeline runs.  Every step still does all of
+    # its work inside the timed region.
+    nbuf = 1 if args.serial else 2
+    pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(nbuf - 1)]
+    outsb = [tuple(torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)) + (None,)
+             for _ in range(nbuf)]
     torch.cuda.synchronize()
     log("packets generated (%d per GPU), setup %.1fs" % (B, time.time() - t_setup))
 
-    # Hit counters: the library's histogram pass over this batch's outputs,
-    # scheduled explicitly after the pipeline so each kernel is timed alone.
+    # Hit counters: the library's histogram passes over each batch's outputs,
+    # scheduled explicitly (counters_add) on the counting stream.
     clf.counters_enable(False)
     count = not args.no_counters
     csrc = [clf.counters_device(k) for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
     bucket = HitCounterBucket([n for _, n in csrc], dev) if world > 1 else None
-    stream = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if args.serial:
+        s_pipe = s_hint = s_cnt = torch.cuda.current_stream()
+    else:
+        s_pipe, s_hint, s_cnt = (hip_stream(dev) for _ in range(3))
+    ev_hint, ev_pipe, ev_cnt = {}, {}, {}
+    timing = []                     # (hint, pipe, count) event pairs of timed steps
+    TE = lambda: torch.cuda.Event(enable_timing=True)
 
-    ev = []
+    def hint(j, rec):
+        with torch.cuda.stream(s_hint):
+            if j - nbuf in ev_pipe:               # pool buffer no longer read
+                s_hint.wait_event(ev_pipe[j - nbuf])
+            e0, e1 = TE(), TE()
+            e0.record()
+            V.check(V.lib().vc_hint_search_dev(clf.h, C.c_void_p(pool_blob.data_ptr()),
+                                               C.c_void_p(pool_off.data_ptr()), None, None, None,
+                                               None, None, args.pool,
+                                               C.c_void_p(pools[j % nbuf].data_ptr()),
+                                               C.c_void_p(s_hint.cuda_stream)))
+            e1.record()
+            ev_hint[j] = e1
+            rec["hint"] = (e0, e1)
 
-    def step(timed):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
-        if timed:
-            e[0].record()
-        V.check(V.lib().vc_hint_search_dev(clf.h, C.c_void_p(pool_blob.data_ptr()),
-                                           C.c_void_p(pool_off.data_ptr()), None, None, None,
-                                           None, None, args.pool,
-                                           C.c_void_p(pool_out.data_ptr()), stream()))
-        if timed:
-            e[1].record()
-            e[2].record()
-        clf.pipeline_v4(proto, src, dst, dport, hid, pool_out, outs=outs)
-        if timed:
-            e[3].record()
-            e[4].record()
-        if count:
-            clf.counters_add(V.COUNTERS_ACL, outs[0], aux=proto)
-            clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
-            clf.counters_add(V.COUNTERS_GROUP, outs[2])
-        if timed:
-            e[5].record()
-            ev.append(e)
-        if bucket is not None:     # hit counters: one RCCL all-reduce per batch
-            for i, cs in enumerate(csrc):
-                bucket.fill(i, cs)
-            bucket.reduce()
+    def pipe(j, rec):
+        with torch.cuda.stream(s_pipe):
+            s_pipe.wait_event(ev_hint[j])
+            if j - nbuf in ev_cnt:                # output buffers counted
+                s_pipe.wait_event(ev_cnt[j - nbuf])
+            e0, e1 = TE(), TE()
+            e0.record()
+            clf.pipeline_v4(proto, src, dst, dport, hid, pools[j % nbuf], outs=outsb[j % nbuf])
+            e1.record()
+            ev_pipe[j] = e1
+            rec["pipe"] = (e0, e1)
 
-    for _ in range(args.warmup):
-        step(False)
+    def counters(j, rec):
+        outs = outsb[j % nbuf]
+        with torch.cuda.stream(s_cnt):
+            s_cnt.wait_event(ev_pipe[j])
+            e0, e1 = TE(), TE()
+            e0.record()
+            if count:
+                clf.counters_add(V.COUNTERS_ACL, outs[0], aux=proto)
+                clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
+                clf.counters_add(V.COUNTERS_GROUP, outs[2])
+            e1.record()
+            if bucket is not None:                # one RCCL all-reduce per batch
+                for i, cs in enumerate(csrc):
+                    bucket.fill(i, cs)
+                bucket.reduce()
+            done = torch.cuda.Event()
+            done.record()
+            ev_cnt[j] = done
+            rec["count"] = (e0, e1)
+
+    def run(first, k, timed):
+        """Steps first .. first+k-1; step j = hint(j), pipe(j), counters(j).
+        The hostname pool of the next step is issued before this step's
+        counters, so it overlaps this step's pipeline."""
+        if k <= 0:
+            return
+        recs = [dict() for _ in range(k)]
+        hint(first, recs[0])
+        for i in range(k):
+            j = first + i
+            pipe(j, recs[i])
+            if i + 1 < k:
+                hint(j + 1, recs[i + 1])
+            counters(j, recs[i])
+        if timed:
+            timing.extend(recs)
+
+    run(0, args.warmup, False)
     torch.cuda.synchronize()
+    ev_hint.clear(); ev_pipe.clear(); ev_cnt.clear()
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run(args.warmup, args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -270,9 +346,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    hint_ms = float(np.mean([x[0].elapsed_time(x[1]) for x in ev]))
-    pipe_ms = float(np.mean([x[2].elapsed_time(x[3]) for x in ev]))
-    count_ms = float(np.mean([x[4].elapsed_time(x[5]) for x in ev]))
+    span = lambda key: float(np.mean([r[key][0].elapsed_time(r[key][1]) for r in timing]))
+    hint_ms, pipe_ms, count_ms = span("hint"), span("pipe"), span("count")
     total = float(B) * world * args.steps
     value = total / elapsed / 1e6
     # roofline of the dominant kernel, algorithmic bytes only
@@ -284,9 +359,18 @@ def main():
         per_unit = (pool_bytes / args.pool) + 4 + 4
         unit_desc = "%.1f B/hostname (avg bytes + 4 offset + 4 out)" % per_unit
     achieved = per_unit * units / (ms / 1e3) / 1e9
+    ceil = gather_ceiling()
+    g_rate = 2.0 * B / (pipe_ms / 1e3) / 1e9
+    gather_bound = {"kernel": "pipeline_v4_kernel",
+                    "per_packet": "2 random 4-byte gathers (route root 64 MB, pool 64 MB)",
+                    "achieved_G_gathers_per_s": round(g_rate, 2),
+                    "ceiling_G_gathers_per_s": ceil,
+                    "frac": round(g_rate / ceil, 4) if ceil else None,
+                    "ceiling_source": "tools/gather_probe.hip -> profiles/r01_gather_probe.csv"}
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic("c5", dom),
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
+            "gather_bound": gather_bound,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
                                 "pipeline_v4_kernel": round(pipe_ms, 4),
                                 "hit_counter_passes": round(count_ms, 4)}}
@@ -304,7 +388,10 @@ def main():
                            "acl_rules": int(len(tcp) + len(udp)), "routes_v4": int(n4),
                            "routes_v6": int(len(hi)), "groups": len(groups),
                            "hostname_pool": args.pool, "packets_per_gpu_per_step": B,
-                           "parallelism": "dp%d" % world},
+                           "parallelism": "dp%d" % world,
+                           "schedule": ("serial, one stream" if args.serial else
+                                        "2 batches in flight: pool / pipeline / counters on "
+                                        "3 HIP streams")},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()

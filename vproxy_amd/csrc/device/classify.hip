@@ -11,6 +11,11 @@
 namespace vcd {
 
 constexpr int kBlock = 512;
+// The pipeline is bound by the rate of random table gathers, which 16 waves
+// per CU already saturate (tools/gather_probe.hip): one 1024-thread
+// workgroup per CU, so the LDS it does not use stays free for kernels
+// running beside it on other streams (hit counters, the next hostname pool).
+constexpr int kPipeBlock = 1024;
 
 // ---------------------------------------------------------------------------
 // ACL (SecurityGroup.allow) on IPv4 sources
@@ -229,7 +234,7 @@ __device__ __forceinline__ void pipeline_one(
 // kVec: 4 packets per lane per step -- 16-byte SoA loads/stores and four
 // independent route-root and pool gathers in flight before the ACL search.
 template <bool kLds, bool kVec>
-__global__ __launch_bounds__(kBlock) void pipeline_v4_kernel(
+__global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     AclImage img, const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ proto,
     const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
     const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
@@ -411,17 +416,18 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
     if (n <= 0) return hipSuccess;
     const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
     const bool lds = words <= kLdsWords;
-    const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
     const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(dst4, 16) &&
                      aligned(dport, 8) && aligned(host_id, 16) && aligned(out_acl, 16) &&
                      aligned(out_route, 16) && aligned(out_group, 16) &&
                      (!out_allow || aligned(out_allow, 4));
-    const int grid = grid_for(c, vec ? (n + 3) / 4 : n, per_cu);
+    int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
+    const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
     const size_t shmem = lds ? size_t(words) * 4 : 0;
 #define VC_PIPE(L, V)                                                                              \
     do {                                                                                           \
         if (L) allow_lds(vcd::pipeline_v4_kernel<L, V>);                                           \
-        hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V>), dim3(grid), dim3(vcd::kBlock), shmem,  \
+        hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V>), dim3(grid), dim3(vcd::kPipeBlock),       \
+                           shmem, \
                            c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,        \
                            host_id, pool_group, n_pool, n, out_acl, out_route, out_group,         \
                            out_allow);                                                             \

@@ -130,9 +130,10 @@ template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void hist_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
     int64_t nval, int64_t base, int64_t null_bin, int32_t nt, unsigned long long* __restrict__ cnt) {
-    __shared__ uint32_t h[kHistBins];
+    extern __shared__ uint32_t h[];            // `width` words: one chunk of the counter space
+    const int width = nval < kHistBins ? int(nval < 1 ? 1 : nval) : kHistBins;
     const int64_t lo_bin = int64_t(blockIdx.y) * kHistBins;
-    for (int k = threadIdx.x; k < kHistBins; k += blockDim.x) h[k] = 0;
+    for (int k = threadIdx.x; k < width; k += blockDim.x) h[k] = 0;
     __syncthreads();
     int64_t lo, hi;
     slice_of(n, &lo, &hi);
@@ -150,20 +151,20 @@ __global__ __launch_bounds__(kHistBlock) void hist_kernel(
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 count_null(it[k], &ntc, &noth);
-                if (it[k].v >= 0) run.add(it[k].v, h, lo_bin, kHistBins);
+                if (it[k].v >= 0) run.add(it[k].v, h, lo_bin, width);
             }
         }
     } else {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
             const Item it = load1(mode, idx, aux, i, nt);
             count_null(it, &ntc, &noth);
-            if (it.v >= 0) run.add(it.v, h, lo_bin, kHistBins);
+            if (it.v >= 0) run.add(it.v, h, lo_bin, width);
         }
     }
-    run.flush(h, lo_bin, kHistBins);
+    run.flush(h, lo_bin, width);
     if (blockIdx.y != 0) ntc = noth = 0;      // nulls counted by grid row 0 only
     flush_nulls(mode, ntc, noth, null_bin, cnt);
-    for (int k = threadIdx.x; k < kHistBins && lo_bin + k < nval; k += blockDim.x)
+    for (int k = threadIdx.x; k < width && lo_bin + k < nval; k += blockDim.x)
         if (h[k]) atomicAdd(cnt + base + lo_bin + k, (unsigned long long)h[k]);
 }
 
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
     int32_t nt, int nbk, uint32_t* __restrict__ counts, unsigned long long* __restrict__ cnt,
     int64_t null_bin) {
-    __shared__ uint32_t c[kMaxBuckets];
+    extern __shared__ uint32_t c[];            // nbk words
     for (int k = threadIdx.x; k < nbk; k += blockDim.x) c[k] = 0;
     __syncthreads();
     int64_t lo, hi;
@@ -275,9 +276,12 @@ template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
     int32_t nt, int nbk, const uint32_t* __restrict__ offsets, int32_t* __restrict__ tmp) {
-    __shared__ uint32_t cur[kMaxBuckets];     // next global write position per bucket
-    __shared__ uint32_t tcnt[kMaxBuckets];    // this tile's count per bucket
-    __shared__ uint32_t tst[kMaxBuckets];     // this tile's exclusive start per bucket
+    // LDS sized by the bucket count, so the kernel can share a CU with the
+    // classify kernels of the next batch
+    extern __shared__ uint32_t dyn[];
+    uint32_t* cur = dyn;                      // next global write position per bucket
+    uint32_t* tcnt = dyn + nbk;               // this tile's count per bucket
+    uint32_t* tst = dyn + 2 * nbk;            // this tile's exclusive start per bucket
     __shared__ int32_t sorted[kTile];
     __shared__ uint32_t part[kHistBlock];
     for (int k = threadIdx.x; k < nbk; k += blockDim.x) {
@@ -380,6 +384,20 @@ __global__ __launch_bounds__(kHistBlock) void bucket_hist_kernel(
 
 namespace vc {
 
+namespace {
+// Dynamic LDS beyond 64 KiB must be opted into per kernel (once).
+void allow_big_lds() {
+    static const bool once = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(vcd::hist_kernel<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, vcd::kHistBins * 4);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(vcd::hist_kernel<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, vcd::kHistBins * 4);
+        return true;
+    }();
+    (void)once;
+}
+}  // namespace
+
 hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const uint8_t* aux,
                        int64_t n, int64_t nval, int64_t base, int64_t null_bin, int32_t nt,
                        unsigned long long* counters) {
@@ -394,14 +412,16 @@ hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const u
         const int64_t max_slices = (n + 65535) / 65536;     // >= 64K items per workgroup
         if (slices > max_slices) slices = max_slices;
         if (slices < 1) slices = 1;
+        const size_t shmem = size_t(nval < vcd::kHistBins ? (nval < 1 ? 1 : nval) : vcd::kHistBins) * 4;
+        if (shmem > 64 * 1024) allow_big_lds();
         if (vec)
             hipLaunchKernelGGL(vcd::hist_kernel<true>, dim3(unsigned(slices), unsigned(chunks)),
-                               dim3(vcd::kHistBlock), 0, c.stream, mode, idx, aux, n, nval, base,
-                               null_bin, nt, counters);
+                               dim3(vcd::kHistBlock), shmem, c.stream, mode, idx, aux, n, nval,
+                               base, null_bin, nt, counters);
         else
             hipLaunchKernelGGL(vcd::hist_kernel<false>, dim3(unsigned(slices), unsigned(chunks)),
-                               dim3(vcd::kHistBlock), 0, c.stream, mode, idx, aux, n, nval, base,
-                               null_bin, nt, counters);
+                               dim3(vcd::kHistBlock), shmem, c.stream, mode, idx, aux, n, nval,
+                               base, null_bin, nt, counters);
         return hipGetLastError();
     }
     // large counter space: bucket partition (count, scan, sorted scatter),
@@ -426,12 +446,12 @@ hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const u
         if (vec) hipLaunchKernelGGL(K<true>, __VA_ARGS__);                                         \
         else hipLaunchKernelGGL(K<false>, __VA_ARGS__);                                            \
     } while (0)
-        VC_BK(vcd::bucket_count_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0, c.stream, mode, idx,
-              aux, n, nt, nbk, counts, counters, null_bin);
+        VC_BK(vcd::bucket_count_kernel, dim3(nblk), dim3(vcd::kHistBlock), size_t(nbk) * 4, c.stream,
+              mode, idx, aux, n, nt, nbk, counts, counters, null_bin);
         hipLaunchKernelGGL(vcd::bucket_scan_kernel, dim3(1), dim3(vcd::kHistBlock), 0, c.stream,
                            counts, offsets, m, nbk, nblk, seg_off);
-        VC_BK(vcd::bucket_scatter_kernel, dim3(nblk), dim3(vcd::kHistBlock), 0, c.stream, mode,
-              idx, aux, n, nt, nbk, offsets, tmp);
+        VC_BK(vcd::bucket_scatter_kernel, dim3(nblk), dim3(vcd::kHistBlock), size_t(nbk) * 12,
+              c.stream, mode, idx, aux, n, nt, nbk, offsets, tmp);
 #undef VC_BK
         hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(unsigned(max_segs)), dim3(vcd::kHistBlock),
                            0, c.stream, tmp, offsets, seg_off, nblk, nbk, nval, base, counters);
