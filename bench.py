@@ -139,6 +139,29 @@ def cpu_baseline_c5(tcp, udp, v4_list, groups, names_blob, names_off, seed, thre
                       "them, %d threads, %.1f s" % (n, len(v4_list), len(groups), threads, t)}
 
 
+class RawEvent:
+    """hipEvent_t through ctypes (torch events cannot be handed to the C ABI)."""
+    _hip = None
+
+    def __init__(self):
+        if RawEvent._hip is None:
+            h = C.CDLL("libamdhip64.so")
+            h.hipEventCreate.argtypes = [C.c_void_p]
+            h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+            h.hipEventElapsedTime.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+            RawEvent._hip = h
+        self.h = C.c_void_p()
+        assert RawEvent._hip.hipEventCreate(C.byref(self.h)) == 0
+
+    def record(self, stream):
+        assert RawEvent._hip.hipEventRecord(self.h, C.c_void_p(stream.cuda_stream)) == 0
+
+    def elapsed_time(self, other):
+        ms = C.c_float()
+        assert RawEvent._hip.hipEventElapsedTime(C.byref(ms), self.h, other.h) == 0
+        return ms.value
+
+
 def hip_stream(dev):
     """A fresh non-blocking HIP stream wrapped for torch.  HIP spreads the
     streams a process creates round-robin over its hardware queues; three
@@ -190,6 +213,10 @@ def main():
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true", help="ablation: skip hit counters")
+    ap.add_argument("--counters", choices=["fused", "passes"], default="fused",
+                    help="fused: the pipeline kernel counts ACL hits and route/group buckets "
+                         "itself and the library finishes the large spaces; passes: separate "
+                         "counting passes over the outputs (counters_add)")
     ap.add_argument("--serial", action="store_true",
                     help="ablation: one stream, no overlap between consecutive batches")
     args = ap.parse_args()
@@ -251,8 +278,9 @@ def main():
 
     # Hit counters: the library's histogram passes over each batch's outputs,
     # scheduled explicitly (counters_add) on the counting stream.
-    clf.counters_enable(False)
     count = not args.no_counters
+    fused = count and args.counters == "fused"
+    clf.counters_enable(False)
     csrc = [clf.counters_device(k) for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
     bucket = HitCounterBucket([n for _, n in csrc], dev) if world > 1 else None
     if args.serial:
@@ -283,12 +311,21 @@ def main():
             s_pipe.wait_event(ev_hint[j])
             if j - nbuf in ev_cnt:                # output buffers counted
                 s_pipe.wait_event(ev_cnt[j - nbuf])
-            e0, e1 = TE(), TE()
-            e0.record()
-            clf.pipeline_v4(proto, src, dst, dport, hid, pools[j % nbuf], outs=outsb[j % nbuf])
+            k0, k1 = RawEvent(), RawEvent()       # the classify kernel alone
+            e1 = TE()
+            k0.record(s_pipe)
+            if fused:                              # count packets only, not the pool pass
+                clf.counters_enable(True)
+            clf.pipeline_v4(proto, src, dst, dport, hid, pools[j % nbuf], outs=outsb[j % nbuf],
+                            kernel_done_event=k1.h.value)
+            if fused:
+                clf.counters_enable(False)
+            k2 = RawEvent()                       # + in-library counter passes (fused)
+            k2.record(s_pipe)
             e1.record()
             ev_pipe[j] = e1
-            rec["pipe"] = (e0, e1)
+            rec["pipe"] = (k0, k1)
+            rec["pipe_call"] = (k1, k2)
 
     def counters(j, rec):
         outs = outsb[j % nbuf]
@@ -296,7 +333,7 @@ def main():
             s_cnt.wait_event(ev_pipe[j])
             e0, e1 = TE(), TE()
             e0.record()
-            if count:
+            if count and not fused:
                 clf.counters_add(V.COUNTERS_ACL, outs[0], aux=proto)
                 clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
                 clf.counters_add(V.COUNTERS_GROUP, outs[2])
@@ -347,7 +384,8 @@ def main():
         elapsed = float(t.item())
 
     span = lambda key: float(np.mean([r[key][0].elapsed_time(r[key][1]) for r in timing]))
-    hint_ms, pipe_ms, count_ms = span("hint"), span("pipe"), span("count")
+    hint_ms, pipe_ms = span("hint"), span("pipe")
+    count_ms = span("pipe_call") if fused else span("count")
     total = float(B) * world * args.steps
     value = total / elapsed / 1e6
     # roofline of the dominant kernel, algorithmic bytes only
@@ -373,7 +411,10 @@ def main():
             "gather_bound": gather_bound,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
                                 "pipeline_v4_kernel": round(pipe_ms, 4),
-                                "hit_counter_passes": round(count_ms, 4)}}
+                                "hit_counter_passes": round(count_ms, 4),
+                                "counting": ("in the pipeline kernel (ACL + route/group "
+                                             "buckets) + library passes for the large spaces"
+                                             if fused else "separate passes")}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)

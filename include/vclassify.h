@@ -188,6 +188,15 @@ int vc_pipeline_v4_dev(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
                        const uint32_t *dst4, const uint16_t *dport, const uint32_t *host_id,
                        const int32_t *pool_group, int64_t n_pool, int64_t n, int32_t *out_acl,
                        int32_t *out_route, int32_t *out_group, uint8_t *out_allow, void *stream);
+/* Same, plus an optional hipEvent_t recorded on `stream` right after the
+ * classify kernel, before the hit-counter passes that follow it when
+ * counters are enabled (the kernel counts the ACL and the route/group
+ * buckets itself; the passes finish the large counter spaces). */
+int vc_pipeline_v4_dev_ex(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
+                          const uint32_t *dst4, const uint16_t *dport, const uint32_t *host_id,
+                          const int32_t *pool_group, int64_t n_pool, int64_t n, int32_t *out_acl,
+                          int32_t *out_route, int32_t *out_group, uint8_t *out_allow, void *stream,
+                          void *kernel_done_event);
 
 /* ------------------------------------------------------------------------ */
 /* Per-rule hit counters (no reference counterpart)          */

@@ -938,3 +938,65 @@ int vo_hosts_parse(const char *text, int len,
     }
     return nkeys;
 }
+
+/* ------------------------------------------------------------------------ */
+/* ServerGroup source hashing                                               */
+/* ------------------------------------------------------------------------ */
+
+/* SOURCE.hash, ServerGroup.java:387-397: Java int arithmetic (wrapping),
+ * `aByte` sign-extended. */
+int32_t vo_source_hash(const uint8_t *bytes, int len) {
+    uint32_t hash = 0;
+    for (int i = 0; i < len; ++i) {
+        const int32_t b = (int8_t)bytes[i];
+        hash = (uint32_t)b + (hash << 6) + (hash << 16) - hash;
+    }
+    int32_t h = (int32_t)hash;
+    if (h == INT32_MIN) return 0;             /* Math.abs(MIN_VALUE) < 0 -> 0 */
+    return h < 0 ? -h : h;
+}
+
+/* the comparator of sourceReset, ServerGroup.java:629-642 */
+static int vo_server_cmp(const vo_server *a, const vo_server *b) {
+    if (a->ip_len > b->ip_len) return 1;
+    if (b->ip_len > a->ip_len) return -1;
+    for (int i = 0; i < a->ip_len; ++i) {
+        const int diff = (int8_t)a->ip[i] - (int8_t)b->ip[i];
+        if (diff != 0) return diff;
+    }
+    return a->port - b->port;
+}
+
+int vo_source_list(const vo_server *servers, int n, int view, int32_t *order) {
+    int k = 0;
+    for (int i = 0; i < n; ++i) {
+        if (view == 4 && servers[i].ip_len != 4) continue;   /* :622 instanceof IPv4 */
+        if (view == 6 && servers[i].ip_len != 16) continue;  /* :623 instanceof IPv6 */
+        if (servers[i].weight <= 0) continue;                /* :628 weight > 0 */
+        /* stable insertion sort (List.sort is stable) */
+        int j = k++;
+        while (j > 0 && vo_server_cmp(&servers[order[j - 1]], &servers[i]) > 0) {
+            order[j] = order[j - 1];
+            --j;
+        }
+        order[j] = i;
+    }
+    return k;
+}
+
+int vo_source_select(const vo_server *servers, int n, int view, const uint8_t *src, int src_len) {
+    int32_t *order = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    const int size = vo_source_list(servers, n, view, order);
+    int32_t hash = vo_source_hash(src, src_len);
+    int result = -1;
+    for (int recurse = 0; recurse < size; ++recurse) {      /* :480 recurse >= size -> null */
+        const int idx = hash % size;                         /* :483 */
+        if (servers[order[idx]].healthy) {
+            result = order[idx];
+            break;
+        }
+        hash = idx + 1;                                      /* :489 next server in the list */
+    }
+    free(order);
+    return result;
+}

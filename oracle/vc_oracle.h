@@ -147,6 +147,28 @@ int vo_hosts_parse(const char *text, int len,
                    int32_t *value, int cap,
                    uint8_t *line_ip, int32_t *line_iplen, int line_cap);
 
+/* ---- ServerGroup source-hash selection:
+ *      base/src/main/java/vproxybase/component/svrgroup/ServerGroup.java ---- */
+typedef struct {
+    uint8_t ip[16];
+    int32_t ip_len;    /* 4 (IPv4 server) or 16 */
+    int32_t port;
+    int32_t weight;
+    int32_t healthy;
+} vo_server;
+
+/* SOURCE.hash (sdbm over the signed address bytes, Math.abs, MIN_VALUE -> 0)
+ * ServerGroup.java:387-397 */
+int32_t vo_source_hash(const uint8_t *bytes, int len);
+/* sourceReset (ServerGroup.java:626-664): the weight > 0 servers of `view`
+ * (0 = all, 4 = IPv4 servers, 6 = IPv6 servers, :620-624) sorted by address
+ * length, then signed address bytes, then port (stable).  Writes indices
+ * into `servers` to order[] and returns how many. */
+int vo_source_list(const vo_server *servers, int n, int view, int32_t *order);
+/* sourceHashGet (ServerGroup.java:464-490): index into `servers` of the
+ * chosen server, or -1 (null: empty list or no healthy server). */
+int vo_source_select(const vo_server *servers, int n, int view, const uint8_t *src, int src_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,3 +85,48 @@ def test_counter_dns_kinds(clf):
     torch.cuda.synchronize()
     exp = np.bincount(val[kind == 2], minlength=ng + 1)
     np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp.astype(np.uint64))
+
+
+@pytest.mark.parametrize("n,off", [(2_000_003, 0), (700_001, 1)])
+def test_pipeline_counts_in_kernel(clf, n, off):
+    """Counters enabled on the pipeline: the kernel histograms the ACL in
+    LDS and counts route/group buckets itself (large spaces: 300k routes,
+    100k groups), the library finishes them; exact vs numpy histograms of
+    the outputs, aligned (16-byte loads) and unaligned (scalar) inputs,
+    n % 4 != 0; outputs vs the oracle on a sample."""
+    import torch
+    import oracle_ffi as O
+    nt, nu, n4, ng = _compile(clf)
+    tcp, udp = W.gen_sg_rules(4000, 124)
+    net, plen = W.gen_v4_prefixes(300000, 125)
+    groups, ghosts = W.gen_groups(100000, 126)
+    names = W.gen_hostnames(ghosts, 200000, 127)
+    pool = clf.hint_search(names)
+    m = n + off
+    proto, src, port = W.gen_acl_queries(tcp, udp, m, 128)
+    dst = W.v4_lookups(net, plen, m, 129)
+    hid = np.random.default_rng(130).integers(0, len(names), m).astype(np.uint32)
+    hid[::53] = 0xFFFFFFFF
+    T = lambda x: torch.from_numpy(x).cuda()
+    dev = [T(x)[off:] for x in (proto, src, dst, port, hid)]
+    clf.counters_enable(True)
+    clf.counters_reset()
+    acl, route, grp, _ = clf.pipeline_v4(*dev, T(pool))
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    acl, route, grp = (x.cpu().numpy() for x in (acl, route, grp))
+    proto, src, dst, port, hid = (x[off:] for x in (proto, src, dst, port, hid))
+    is_t = proto == 6
+    exp = np.bincount(np.where(acl >= 0, np.where(is_t, acl, nt + acl), nt + nu + (~is_t)),
+                      minlength=nt + nu + 2)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ACL), exp.astype(np.uint64))
+    exp = np.bincount(np.where(route >= 0, route, n4), minlength=n4 + 2)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE), exp.astype(np.uint64))
+    exp = np.bincount(np.where(grp >= 0, grp, ng), minlength=ng + 1)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp.astype(np.uint64))
+    np.testing.assert_array_equal(grp, np.where(hid == 0xFFFFFFFF, -1,
+                                                pool[np.minimum(hid, len(pool) - 1)]))
+    s = np.random.default_rng(131).integers(0, n, 3000)
+    want, _ = O.sg_batch_v4_np(tcp, udp, False, proto[s], src[s], port[s])
+    np.testing.assert_array_equal(acl[s], want)
+    np.testing.assert_array_equal(route[s], O.rt_batch_v4_np(W.v4_nets(net, plen), dst[s]))

@@ -115,6 +115,8 @@ def lib():
         L.vc_dns_classify_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp]
         L.vc_dns_classify.argtypes = [vp, vp, vp, i64, vp, vp]
         L.vc_pipeline_v4_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
+        L.vc_pipeline_v4_dev_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
+                                            vp, vp]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

@@ -113,8 +113,12 @@ class SecurityGroup:
         self._default = bool(default_allow)
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            lib().vc_secgroup_free(self.h)
+        try:
+            if getattr(self, "h", None) and self.h.value:
+                lib().vc_secgroup_free(self.h)
+                self.h = C.c_void_p()
+        except Exception:       # interpreter shutdown: module globals already gone
+            pass
 
     @property
     def default_allow(self):
@@ -151,8 +155,12 @@ class RouteTable:
                                       int(vni), C.byref(self.h)))
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            lib().vc_routetable_free(self.h)
+        try:
+            if getattr(self, "h", None) and self.h.value:
+                lib().vc_routetable_free(self.h)
+                self.h = C.c_void_p()
+        except Exception:       # interpreter shutdown: module globals already gone
+            pass
 
     def add_rule(self, alias, network, to_vni=0, via=None):
         net = network if isinstance(network, Network) else Network(network)
@@ -461,8 +469,10 @@ class Classifier:
         return kind, val
 
     def pipeline_v4(self, proto, src4, dst4, dport, host_id, pool_group, outs=None,
-                    want_allow=False):
-        """Combined ACL -> route -> host pipeline on device tensors."""
+                    want_allow=False, kernel_done_event=None):
+        """Combined ACL -> route -> host pipeline on device tensors.
+        kernel_done_event: optional raw hipEvent_t (int) recorded right after
+        the classify kernel, before any hit-counter passes."""
         import torch
         n = len(src4)
         if outs is None:
@@ -472,10 +482,11 @@ class Classifier:
                     torch.empty(n, dtype=torch.int32, device=dev),
                     torch.empty(n, dtype=torch.uint8, device=dev) if want_allow else None)
         a, r, g, al = outs
-        check(lib().vc_pipeline_v4_dev(self.h, _ptr(proto), _ptr(src4), _ptr(dst4), _ptr(dport),
-                                       _ptr(host_id), _ptr(pool_group), len(pool_group), n,
-                                       _ptr(a), _ptr(r),
-                                       _ptr(g), _ptr(al), _stream()))
+        check(lib().vc_pipeline_v4_dev_ex(self.h, _ptr(proto), _ptr(src4), _ptr(dst4),
+                                          _ptr(dport), _ptr(host_id), _ptr(pool_group),
+                                          len(pool_group), n, _ptr(a), _ptr(r), _ptr(g), _ptr(al),
+                                          _stream(), C.c_void_p(kernel_done_event)
+                                          if kernel_done_event else None))
         return outs
 
     # ---------------- counters ----------------

@@ -89,6 +89,7 @@ struct HostsSnap : Snapshot {
 struct vc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipMemPool_t pool = nullptr;   // scratch of the counter passes
     int num_cus = 256;
     std::atomic<bool> counters_on{false};
     std::mutex compile_mu;   // serialises compiles; classify never takes it
@@ -111,6 +112,7 @@ struct vc_ctx {
         vc::LaunchCfg c;
         c.num_cus = num_cus;
         c.stream = static_cast<hipStream_t>(s);
+        c.pool = pool;
         return c;
     }
 };
@@ -179,6 +181,22 @@ int vc_create(int device, vc_ctx** out) {
         delete c;
         return hip_fail(e, "stream create");
     }
+    // Scratch pool of the counter passes: calls may come on several streams
+    // at once, so a block freed on one stream is never handed to another
+    // without a stream-order dependency; memory stays cached between calls.
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return hip_fail(e, "mem pool create");
+    }
+    int off = 0;
+    uint64_t keep = ~uint64_t(0);
+    (void)hipMemPoolSetAttribute(c->pool, hipMemPoolReuseAllowOpportunistic, &off);
+    (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep);
     *out = c;
     return VC_OK;
 }
@@ -192,6 +210,12 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->hint.reset();
     ctx->hosts.reset();
     (void)hipStreamDestroy(ctx->stream);
+    if (ctx->pool) {
+        // batches may still run on callers' streams: their scratch is freed
+        // in stream order, so wait for the device before the pool goes
+        (void)hipDeviceSynchronize();
+        (void)hipMemPoolDestroy(ctx->pool);
+    }
     delete ctx;
 }
 
@@ -552,6 +576,15 @@ int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
                        const int32_t* pool_group, int64_t n_pool, int64_t n, int32_t* out_acl,
                        int32_t* out_route,
                        int32_t* out_group, uint8_t* out_allow, void* stream) {
+    return vc_pipeline_v4_dev_ex(ctx, proto, src4, dst4, dport, host_id, pool_group, n_pool, n,
+                                 out_acl, out_route, out_group, out_allow, stream, nullptr);
+}
+
+int vc_pipeline_v4_dev_ex(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
+                          const uint32_t* dst4, const uint16_t* dport, const uint32_t* host_id,
+                          const int32_t* pool_group, int64_t n_pool, int64_t n, int32_t* out_acl,
+                          int32_t* out_route, int32_t* out_group, uint8_t* out_allow, void* stream,
+                          void* kernel_done_event) {
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n < 0 || n_pool < 0 || (n > 0 && (!proto || !src4 || !dst4 || !dport || !host_id ||
@@ -568,7 +601,8 @@ int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
         ctx->cfg(stream), a->img, r->img.fam[0], proto, src4, dst4, dport, host_id, pool_group,
         n_pool, n,
         out_acl, out_route, out_group, out_allow, on ? a->counters : nullptr,
-        on ? r->counters : nullptr, int64_t(r->n4) + r->n6, on && h ? h->counters : nullptr, ng);
+        on ? r->counters : nullptr, int64_t(r->n4) + r->n6, on && h ? h->counters : nullptr, ng,
+        static_cast<hipEvent_t>(kernel_done_event));
     return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");
 }
 

@@ -214,86 +214,193 @@ __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, u
     return e;
 }
 
+// In-kernel hit counting of the pipeline (launch_pipeline_v4): the ACL
+// histogram in LDS next to the staged boundaries, and per-workgroup bucket
+// counts of the route and group outputs -- the first pass of the large
+// counter-space histogram (counters.hip), which then only scans, scatters
+// and histograms.  The kernel is bound by its table gathers, so the LDS
+// atomics ride along for free and two passes over the outputs disappear.
+struct PipeCount {
+    unsigned long long* acl;       // ACL counters, or null: not counted here
+    int32_t acl_bins;              // n_tcp + n_udp (LDS words)
+    int32_t n_tcp;
+    uint32_t* rcounts;             // route bucket counts [bucket * grid + block], or null
+    int32_t r_nbk;
+    unsigned long long* route;     // route counters (null bin at route_none_at)
+    int64_t route_none_at;
+    uint32_t* gcounts;             // group bucket counts, or null
+    int32_t g_nbk;
+    unsigned long long* group;     // group counters (null bin at n_groups)
+    int32_t n_groups;
+    int32_t bw_shift;              // log2(bucket width)
+};
+
+struct PipeTally {                 // per-thread null counts
+    uint32_t acl_tcp = 0, acl_udp = 0, route = 0, group = 0;
+};
+
+__device__ __forceinline__ void pipe_count(const PipeCount& pc, uint32_t* ah, uint32_t* rc,
+                                           uint32_t* gc, bool tcp, uint32_t v, int32_t r,
+                                           int32_t g, PipeTally* t) {
+    if (pc.acl) {
+        if (v != VC_NONE) atomicAdd(&ah[tcp ? v : uint32_t(pc.n_tcp) + v], 1u);
+        else if (tcp) ++t->acl_tcp;
+        else ++t->acl_udp;
+    }
+    if (pc.rcounts) {
+        if (r >= 0) atomicAdd(&rc[r >> pc.bw_shift], 1u);
+        else ++t->route;
+    }
+    if (pc.gcounts) {
+        if (g >= 0) atomicAdd(&gc[g >> pc.bw_shift], 1u);
+        else ++t->group;
+    }
+}
+
 // One packet through ACL -> route -> pool group (scalar form, also the tail).
+template <bool kCount>
 __device__ __forceinline__ void pipeline_one(
     const AclImage& img, const AclV4Ctx& a, const uint32_t* nodes, int rb, const uint8_t* proto,
     const uint32_t* src, const uint32_t* dst, const uint16_t* dport, const uint32_t* host_id,
     const int32_t* pool_group, int64_t n_pool, int64_t i, int32_t* out_acl, int32_t* out_route,
-    int32_t* out_group, uint8_t* out_allow) {
+    int32_t* out_group, uint8_t* out_allow, const PipeCount& pc, uint32_t* ah, uint32_t* rc,
+    uint32_t* gc, PipeTally* t) {
     const uint32_t d = dst[i];
     const uint32_t e = nodes[d >> (32 - rb)];
     const uint32_t h = host_id[i];
     const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
-    const bool t = proto[i] == VC_PROTO_TCP;
-    const uint32_t v = acl_v4_one(a, t, src[i], dport[i]);
-    acl_emit(img, t, v, out_allow ? out_allow + i : nullptr, out_acl + i);
-    route_emit(route_chase(nodes, rb, e, d), out_route + i);
+    const bool tcp = proto[i] == VC_PROTO_TCP;
+    const uint32_t v = acl_v4_one(a, tcp, src[i], dport[i]);
+    acl_emit(img, tcp, v, out_allow ? out_allow + i : nullptr, out_acl + i);
+    const int32_t r = out_index(route_chase(nodes, rb, e, d));
+    out_route[i] = r;
     out_group[i] = grp;
+    if (kCount) pipe_count(pc, ah, rc, gc, tcp, v, r, grp, t);
+}
+
+// Contiguous slice [lo, hi) of n items owned by this workgroup, on 4-item
+// boundaries (the same split as counters.hip, which reads the bucket counts
+// per workgroup).
+__device__ __forceinline__ void pipe_slice(int64_t n, int64_t* lo, int64_t* hi) {
+    const int64_t groups = (n + 3) >> 2;
+    const int64_t per = (groups + gridDim.x - 1) / gridDim.x;
+    *lo = int64_t(blockIdx.x) * per * 4;
+    const int64_t h = *lo + per * 4;
+    *hi = h < n ? h : n;
+    if (*lo > n) *lo = n;
 }
 
 // kVec: 4 packets per lane per step -- 16-byte SoA loads/stores and four
 // independent route-root and pool gathers in flight before the ACL search.
-template <bool kLds, bool kVec>
+template <bool kLds, bool kVec, bool kCount>
 __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     AclImage img, const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ proto,
     const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
     const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
     const int32_t* __restrict__ pool_group, int64_t n_pool, int64_t n,
     int32_t* __restrict__ out_acl, int32_t* __restrict__ out_route,
-    int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow) {
+    int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow, PipeCount pc) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int words = kLds ? img.fam[0][0].nb + img.fam[1][0].nb : 0;
+    uint32_t* ah = lds + words;                                  // ACL histogram
+    uint32_t* rc = ah + (pc.acl ? pc.acl_bins : 0);             // route bucket counts
+    uint32_t* gc = rc + (pc.rcounts ? pc.r_nbk : 0);            // group bucket counts
+    __shared__ uint32_t tally[4];
+    if (kCount) {
+        const int cw = (pc.acl ? pc.acl_bins : 0) + (pc.rcounts ? pc.r_nbk : 0) +
+                       (pc.gcounts ? pc.g_nbk : 0);
+        for (int k = threadIdx.x; k < cw; k += blockDim.x) ah[k] = 0;
+        if (threadIdx.x < 4) tally[threadIdx.x] = 0;
+    }
     if (kLds) stage_bounds(img, lds);
+    else if (kCount) __syncthreads();
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
-    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    int64_t lo, hi;
+    pipe_slice(n, &lo, &hi);
+    PipeTally t;
     if (!kVec) {
-        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-            pipeline_one(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group, n_pool, i,
-                         out_acl, out_route, out_group, out_allow);
-        return;
-    }
-    const int64_t n4 = n >> 2;
-    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
-        const uint4 d4 = reinterpret_cast<const uint4*>(dst)[g];
-        const uint4 h4 = reinterpret_cast<const uint4*>(host_id)[g];
-        const uint4 s4 = reinterpret_cast<const uint4*>(src)[g];
-        const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
-        const uint2 pt = reinterpret_cast<const uint2*>(dport)[g];
-        const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
-        const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
-        const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
-        const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
-        uint32_t e[4];
-        int32_t grp[4];
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+            pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
+                                 n_pool, i, out_acl, out_route, out_group, out_allow, pc, ah, rc,
+                                 gc, &t);
+    } else {
+        for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
+            const int64_t g = i >> 2;
+            const uint4 d4 = reinterpret_cast<const uint4*>(dst)[g];
+            const uint4 h4 = reinterpret_cast<const uint4*>(host_id)[g];
+            const uint4 s4 = reinterpret_cast<const uint4*>(src)[g];
+            const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
+            const uint2 pt = reinterpret_cast<const uint2*>(dport)[g];
+            const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
+            const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
+            const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
+            const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
+            uint32_t e[4];
+            int32_t grp[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) e[k] = nodes[d[k] >> (32 - rb)];
+            for (int k = 0; k < 4; ++k) e[k] = nodes[d[k] >> (32 - rb)];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) grp[k] = int64_t(h[k]) < n_pool ? pool_group[h[k]] : -1;
-        uint32_t v[4];
-        bool tcp[4];
+            for (int k = 0; k < 4; ++k) grp[k] = int64_t(h[k]) < n_pool ? pool_group[h[k]] : -1;
+            uint32_t v[4];
+            bool tcp[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-            v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+            for (int k = 0; k < 4; ++k) {
+                tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+                v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+            }
+            int4 oa, orr;
+            uint32_t al = 0;
+            int32_t* pa = reinterpret_cast<int32_t*>(&oa);
+            int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint8_t b = 0;
+                acl_emit(img, tcp[k], v[k], out_allow ? &b : nullptr, pa + k);
+                al |= uint32_t(b) << (8 * k);
+                pr_[k] = out_index(route_chase(nodes, rb, e[k], d[k]));
+            }
+            reinterpret_cast<int4*>(out_acl)[g] = oa;
+            reinterpret_cast<int4*>(out_route)[g] = orr;
+            reinterpret_cast<int4*>(out_group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+            if (out_allow) reinterpret_cast<uint32_t*>(out_allow)[g] = al;
+            if (kCount) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pipe_count(pc, ah, rc, gc, tcp[k], v[k], pr_[k], grp[k], &t);
+            }
         }
-        int4 oa, orr;
-        uint32_t al = 0;
-        int32_t* pa = reinterpret_cast<int32_t*>(&oa);
-        int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint8_t b = 0;
-            acl_emit(img, tcp[k], v[k], out_allow ? &b : nullptr, pa + k);
-            al |= uint32_t(b) << (8 * k);
-            pr_[k] = out_index(route_chase(nodes, rb, e[k], d[k]));
-        }
-        reinterpret_cast<int4*>(out_acl)[g] = oa;
-        reinterpret_cast<int4*>(out_route)[g] = orr;
-        reinterpret_cast<int4*>(out_group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
-        if (out_allow) reinterpret_cast<uint32_t*>(out_allow)[g] = al;
+        // last partial group of 4 (only the final slice, when n % 4 != 0)
+        const int64_t tail = hi & ~int64_t(3);
+        if (hi == n && tail >= lo && threadIdx.x < int(hi - tail))
+            pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
+                                 n_pool, tail + threadIdx.x, out_acl, out_route, out_group,
+                                 out_allow, pc, ah, rc, gc, &t);
     }
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3))
-        pipeline_one(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group, n_pool,
-                     (n4 << 2) + threadIdx.x, out_acl, out_route, out_group, out_allow);
+    if (!kCount) return;
+    if (t.acl_tcp) atomicAdd(&tally[0], t.acl_tcp);
+    if (t.acl_udp) atomicAdd(&tally[1], t.acl_udp);
+    if (t.route) atomicAdd(&tally[2], t.route);
+    if (t.group) atomicAdd(&tally[3], t.group);
+    __syncthreads();
+    if (pc.acl) {
+        for (int k = threadIdx.x; k < pc.acl_bins; k += blockDim.x)
+            if (ah[k]) atomicAdd(pc.acl + k, (unsigned long long)ah[k]);
+        if (threadIdx.x == 0) {                   // [tcp default][udp default]
+            if (tally[0]) atomicAdd(pc.acl + pc.acl_bins, (unsigned long long)tally[0]);
+            if (tally[1]) atomicAdd(pc.acl + pc.acl_bins + 1, (unsigned long long)tally[1]);
+        }
+    }
+    if (pc.rcounts) {
+        for (int k = threadIdx.x; k < pc.r_nbk; k += blockDim.x)
+            pc.rcounts[int64_t(k) * gridDim.x + blockIdx.x] = rc[k];
+        if (threadIdx.x == 0 && tally[2])
+            atomicAdd(pc.route + pc.route_none_at, (unsigned long long)tally[2]);
+    }
+    if (pc.gcounts) {
+        for (int k = threadIdx.x; k < pc.g_nbk; k += blockDim.x)
+            pc.gcounts[int64_t(k) * gridDim.x + blockIdx.x] = gc[k];
+        if (threadIdx.x == 0 && tally[3])
+            atomicAdd(pc.group + pc.n_groups, (unsigned long long)tally[3]);
+    }
 }
 
 }  // namespace vcd
@@ -315,13 +422,12 @@ int grid_for(const LaunchCfg& c, int64_t work_items, int blocks_per_cu) {
 
 bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
-// Dynamic LDS beyond 64 KiB must be opted into per kernel (once).
+// Dynamic LDS beyond 64 KiB must be opted into per kernel.  Keyed by the
+// kernel's address: template instances share a function-pointer type.
 template <class K>
-void allow_lds(K kernel) {
-    static const hipError_t once = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-        kLdsWords * 4);
-    (void)once;
+hipError_t allow_lds(K kernel, size_t bytes = kLdsWords * 4) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
 }
 
 }  // namespace
@@ -412,8 +518,8 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
                               int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
                               unsigned long long* acl_cnt, unsigned long long* route_cnt,
                               int64_t route_none_at, unsigned long long* group_cnt,
-                              int32_t n_groups) {
-    if (n <= 0) return hipSuccess;
+                              int32_t n_groups, hipEvent_t kernel_done) {
+    if (n <= 0) return kernel_done ? hipEventRecord(kernel_done, c.stream) : hipSuccess;
     const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
     const bool lds = words <= kLdsWords;
     const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(dst4, 16) &&
@@ -422,29 +528,87 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
                      (!out_allow || aligned(out_allow, 4));
     int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
     const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
-    const size_t shmem = lds ? size_t(words) * 4 : 0;
-#define VC_PIPE(L, V)                                                                              \
+    // In-kernel counting where it fits the workgroup's LDS; the rest is
+    // counted by separate passes over the outputs afterwards.
+    constexpr size_t kLdsMax = 160 * 1024 - 256;
+    size_t shmem = lds ? size_t(words) * 4 : 0;
+    vcd::PipeCount pc{};
+    pc.bw_shift = big_hist_bucket_shift();
+    BigHist rh, gh;
+    hipError_t e = hipSuccess;
+    const int32_t acl_bins = acl.n_tcp + acl.n_udp;
+    if (acl_cnt && shmem + size_t(acl_bins) * 4 <= kLdsMax) {
+        pc.acl = acl_cnt;
+        pc.acl_bins = acl_bins;
+        pc.n_tcp = acl.n_tcp;
+        shmem += size_t(acl_bins) * 4;
+    }
+    if (route_cnt && big_hist_applies(n, r4.n_rules)) {
+        e = big_hist_begin(c, n, r4.n_rules, grid, &rh);
+        if (e == hipSuccess && shmem + size_t(rh.nbk) * 4 <= kLdsMax) {
+            pc.rcounts = rh.counts;
+            pc.r_nbk = rh.nbk;
+            pc.route = route_cnt;
+            pc.route_none_at = route_none_at;
+            shmem += size_t(rh.nbk) * 4;
+        }
+    }
+    if (e == hipSuccess && group_cnt && big_hist_applies(n, n_groups)) {
+        e = big_hist_begin(c, n, n_groups, grid, &gh);
+        if (e == hipSuccess && shmem + size_t(gh.nbk) * 4 <= kLdsMax) {
+            pc.gcounts = gh.counts;
+            pc.g_nbk = gh.nbk;
+            pc.group = group_cnt;
+            pc.n_groups = n_groups;
+            shmem += size_t(gh.nbk) * 4;
+        }
+    }
+    const bool cnt = pc.acl || pc.rcounts || pc.gcounts;
+    if (e == hipSuccess) {
+#define VC_PIPE(L, V, K)                                                                           \
     do {                                                                                           \
-        if (L) allow_lds(vcd::pipeline_v4_kernel<L, V>);                                           \
-        hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V>), dim3(grid), dim3(vcd::kPipeBlock),       \
-                           shmem, \
-                           c.stream, acl, r4.nodes, r4.root_bits, proto, src4, dst4, dport,        \
-                           host_id, pool_group, n_pool, n, out_acl, out_route, out_group,         \
-                           out_allow);                                                             \
+        if (shmem > 64 * 1024) e = allow_lds(vcd::pipeline_v4_kernel<L, V, K>, kLdsMax);           \
+        if (e != hipSuccess) break;                                                                \
+        hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V, K>), dim3(grid),                         \
+                           dim3(vcd::kPipeBlock), shmem, c.stream, acl, r4.nodes, r4.root_bits,   \
+                           proto, src4, dst4, dport, host_id, pool_group, n_pool, n, out_acl,      \
+                           out_route, out_group, out_allow, pc);                                   \
     } while (0)
-    if (lds && vec) VC_PIPE(true, true);
-    else if (lds) VC_PIPE(true, false);
-    else if (vec) VC_PIPE(false, true);
-    else VC_PIPE(false, false);
+        if (cnt) {
+            if (lds && vec) VC_PIPE(true, true, true);
+            else if (lds) VC_PIPE(true, false, true);
+            else if (vec) VC_PIPE(false, true, true);
+            else VC_PIPE(false, false, true);
+        } else {
+            if (lds && vec) VC_PIPE(true, true, false);
+            else if (lds) VC_PIPE(true, false, false);
+            else if (vec) VC_PIPE(false, true, false);
+            else VC_PIPE(false, false, false);
+        }
 #undef VC_PIPE
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && acl_cnt)
-        e = launch_hist(c, VC_HIST_ACL, out_acl, proto, n, int64_t(acl.n_tcp) + acl.n_udp, 0,
-                        int64_t(acl.n_tcp) + acl.n_udp, acl.n_tcp, acl_cnt);
-    if (e == hipSuccess && route_cnt)
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess && kernel_done) e = hipEventRecord(kernel_done, c.stream);
+    }
+    // second halves of the in-kernel counts, and whatever was not counted inside
+    if (rh.counts) {
+        const hipError_t e2 = big_hist_finish(c, &rh, VC_HIST_PLAIN, out_route, nullptr, n, 0,
+                                              r4.n_rules, 0, route_cnt,
+                                              e == hipSuccess && pc.rcounts != nullptr);
+        if (e == hipSuccess) e = e2;
+    }
+    if (gh.counts) {
+        const hipError_t e2 = big_hist_finish(c, &gh, VC_HIST_PLAIN, out_group, nullptr, n, 0,
+                                              n_groups, 0, group_cnt,
+                                              e == hipSuccess && pc.gcounts != nullptr);
+        if (e == hipSuccess) e = e2;
+    }
+    if (e == hipSuccess && acl_cnt && !pc.acl)
+        e = launch_hist(c, VC_HIST_ACL, out_acl, proto, n, acl_bins, 0, acl_bins, acl.n_tcp,
+                        acl_cnt);
+    if (e == hipSuccess && route_cnt && !pc.rcounts)
         e = launch_hist(c, VC_HIST_PLAIN, out_route, nullptr, n, r4.n_rules, 0, route_none_at, 0,
                         route_cnt);
-    if (e == hipSuccess && group_cnt)
+    if (e == hipSuccess && group_cnt && !pc.gcounts)
         e = launch_hist(c, VC_HIST_PLAIN, out_group, nullptr, n, n_groups, 0, n_groups, 0,
                         group_cnt);
     return e;

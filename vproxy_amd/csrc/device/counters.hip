@@ -426,41 +426,81 @@ hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const u
     }
     // large counter space: bucket partition (count, scan, sorted scatter),
     // then per-segment LDS histograms
-    const int nbk = int(nbk64);
     int nblk = c.num_cus * 2;
     const int64_t max_blk = (n + 65535) / 65536;
     if (nblk > max_blk) nblk = int(max_blk < 1 ? 1 : max_blk);
-    const int64_t m = int64_t(nbk) * nblk;
-    const int64_t max_segs = (n + vcd::kSeg - 1) / vcd::kSeg + nbk;
-    uint32_t *counts = nullptr, *offsets = nullptr, *seg_off = nullptr;
-    int32_t* tmp = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&counts), size_t(m) * 4, c.stream);
-    if (e == hipSuccess)
-        e = hipMallocAsync(reinterpret_cast<void**>(&offsets), size_t(m + 1) * 4, c.stream);
-    if (e == hipSuccess)
-        e = hipMallocAsync(reinterpret_cast<void**>(&seg_off), size_t(nbk + 1) * 4, c.stream);
-    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&tmp), size_t(n) * 4, c.stream);
+    BigHist h;
+    hipError_t e = big_hist_begin(c, n, nval, nblk, &h);
     if (e == hipSuccess) {
-#define VC_BK(K, ...)                                                                              \
-    do {                                                                                           \
-        if (vec) hipLaunchKernelGGL(K<true>, __VA_ARGS__);                                         \
-        else hipLaunchKernelGGL(K<false>, __VA_ARGS__);                                            \
-    } while (0)
-        VC_BK(vcd::bucket_count_kernel, dim3(nblk), dim3(vcd::kHistBlock), size_t(nbk) * 4, c.stream,
-              mode, idx, aux, n, nt, nbk, counts, counters, null_bin);
-        hipLaunchKernelGGL(vcd::bucket_scan_kernel, dim3(1), dim3(vcd::kHistBlock), 0, c.stream,
-                           counts, offsets, m, nbk, nblk, seg_off);
-        VC_BK(vcd::bucket_scatter_kernel, dim3(nblk), dim3(vcd::kHistBlock), size_t(nbk) * 12,
-              c.stream, mode, idx, aux, n, nt, nbk, offsets, tmp);
-#undef VC_BK
-        hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(unsigned(max_segs)), dim3(vcd::kHistBlock),
-                           0, c.stream, tmp, offsets, seg_off, nblk, nbk, nval, base, counters);
+        if (vec)
+            hipLaunchKernelGGL(vcd::bucket_count_kernel<true>, dim3(nblk), dim3(vcd::kHistBlock),
+                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, h.counts,
+                               counters, null_bin);
+        else
+            hipLaunchKernelGGL(vcd::bucket_count_kernel<false>, dim3(nblk), dim3(vcd::kHistBlock),
+                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, h.counts,
+                               counters, null_bin);
         e = hipGetLastError();
     }
-    if (counts) (void)hipFreeAsync(counts, c.stream);
-    if (offsets) (void)hipFreeAsync(offsets, c.stream);
-    if (seg_off) (void)hipFreeAsync(seg_off, c.stream);
-    if (tmp) (void)hipFreeAsync(tmp, c.stream);
+    const hipError_t e2 = big_hist_finish(c, &h, mode, idx, aux, n, nt, nval, base, counters,
+                                          e == hipSuccess);
+    return e != hipSuccess ? e : e2;
+}
+
+bool big_hist_applies(int64_t n, int64_t nval) {
+    const int64_t chunks = nval > 0 ? (nval + vcd::kHistBins - 1) / vcd::kHistBins : 1;
+    const int64_t nbk = nval > 0 ? (nval + vcd::kBW - 1) / vcd::kBW : 1;
+    return !(chunks <= 2 || nbk > vcd::kMaxBuckets || n >= (int64_t(1) << 32));
+}
+
+int big_hist_bucket_shift() { return 13; }   // log2(kBW)
+
+hipError_t big_hist_begin(const LaunchCfg& c, int64_t n, int64_t nval, int nblk, BigHist* h) {
+    static_assert(vcd::kBW == 8192, "big_hist_bucket_shift");
+    *h = BigHist{};
+    h->nbk = int((nval + vcd::kBW - 1) / vcd::kBW);
+    h->nblk = nblk;
+    const int64_t m = int64_t(h->nbk) * nblk;
+    hipError_t e = scratch_alloc(c, reinterpret_cast<void**>(&h->counts), size_t(m) * 4);
+    if (e == hipSuccess)
+        e = scratch_alloc(c, reinterpret_cast<void**>(&h->offsets), size_t(m + 1) * 4);
+    if (e == hipSuccess)
+        e = scratch_alloc(c, reinterpret_cast<void**>(&h->seg_off), size_t(h->nbk + 1) * 4);
+    if (e == hipSuccess)
+        e = scratch_alloc(c, reinterpret_cast<void**>(&h->tmp), size_t(n > 0 ? n : 1) * 4);
+    return e;
+}
+
+hipError_t big_hist_finish(const LaunchCfg& c, BigHist* h, int mode, const int32_t* idx,
+                           const uint8_t* aux, int64_t n, int32_t nt, int64_t nval, int64_t base,
+                           unsigned long long* counters, bool run) {
+    hipError_t e = hipSuccess;
+    if (run) {
+        const bool vec = (reinterpret_cast<uintptr_t>(idx) & 15) == 0 &&
+                         (!aux || (reinterpret_cast<uintptr_t>(aux) & 3) == 0);
+        const int nbk = h->nbk, nblk = h->nblk;
+        const int64_t m = int64_t(nbk) * nblk;
+        const int64_t max_segs = (n + vcd::kSeg - 1) / vcd::kSeg + nbk;
+        hipLaunchKernelGGL(vcd::bucket_scan_kernel, dim3(1), dim3(vcd::kHistBlock), 0, c.stream,
+                           h->counts, h->offsets, m, nbk, nblk, h->seg_off);
+        if (vec)
+            hipLaunchKernelGGL(vcd::bucket_scatter_kernel<true>, dim3(nblk), dim3(vcd::kHistBlock),
+                               size_t(nbk) * 12, c.stream, mode, idx, aux, n, nt, nbk, h->offsets,
+                               h->tmp);
+        else
+            hipLaunchKernelGGL(vcd::bucket_scatter_kernel<false>, dim3(nblk),
+                               dim3(vcd::kHistBlock), size_t(nbk) * 12, c.stream, mode, idx, aux,
+                               n, nt, nbk, h->offsets, h->tmp);
+        hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(unsigned(max_segs)), dim3(vcd::kHistBlock),
+                           0, c.stream, h->tmp, h->offsets, h->seg_off, nblk, nbk, nval, base,
+                           counters);
+        e = hipGetLastError();
+    }
+    if (h->counts) (void)hipFreeAsync(h->counts, c.stream);
+    if (h->offsets) (void)hipFreeAsync(h->offsets, c.stream);
+    if (h->seg_off) (void)hipFreeAsync(h->seg_off, c.stream);
+    if (h->tmp) (void)hipFreeAsync(h->tmp, c.stream);
+    *h = BigHist{};
     return e;
 }
 

@@ -16,7 +16,14 @@ namespace vc {
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
     hipStream_t stream = nullptr;
+    hipMemPool_t pool = nullptr;   // scratch pool (stream-ordered), null = device default
 };
+
+// Stream-ordered scratch allocation from the context's pool.
+inline hipError_t scratch_alloc(const LaunchCfg& c, void** p, size_t bytes) {
+    return c.pool ? hipMallocFromPoolAsync(p, bytes, c.pool, c.stream)
+                  : hipMallocAsync(p, bytes, c.stream);
+}
 
 hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
                          const uint32_t* src4, const uint16_t* port, int64_t n, int32_t* out,
@@ -46,7 +53,26 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
                               int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
                               unsigned long long* acl_cnt, unsigned long long* route_cnt,
                               int64_t route_none_at, unsigned long long* group_cnt,
-                              int32_t n_groups);
+                              int32_t n_groups, hipEvent_t kernel_done = nullptr);
+
+// Large counter spaces (counters.hip): bucket partition + per-bucket LDS
+// histograms, split so a producer kernel (the pipeline) can supply the
+// per-workgroup bucket counts itself: begin (allocate), producer writes
+// counts[bucket * nblk + block] over pipe_slice() slices of nblk
+// workgroups, finish (scan, scatter, histogram, free).
+struct BigHist {
+    int nbk = 0, nblk = 0;
+    uint32_t* counts = nullptr;
+    uint32_t* offsets = nullptr;
+    uint32_t* seg_off = nullptr;
+    int32_t* tmp = nullptr;
+};
+bool big_hist_applies(int64_t n, int64_t nval);
+int big_hist_bucket_shift();
+hipError_t big_hist_begin(const LaunchCfg& c, int64_t n, int64_t nval, int nblk, BigHist* h);
+hipError_t big_hist_finish(const LaunchCfg& c, BigHist* h, int mode, const int32_t* idx,
+                           const uint8_t* aux, int64_t n, int32_t nt, int64_t nval, int64_t base,
+                           unsigned long long* counters, bool run);
 
 // Histogram a classify output array into uint64 hit counters.  Values in
 // [0, nval) land at counters[base + v]; nulls at counters[null_bin].
