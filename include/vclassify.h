@@ -199,6 +199,43 @@ int vc_pipeline_v4_dev_ex(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src
                           void *kernel_done_event);
 
 /* ------------------------------------------------------------------------ */
+/* Server choice after the group match, method == source:                    */
+/* base/src/main/java/vproxybase/component/svrgroup/ServerGroup.java         */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    uint8_t ip[16];     /* server address bytes (IPv4: first 4) */
+    int32_t ip_len;     /* 4 (IPv4 server) or 16 */
+    int32_t port;
+    int32_t weight;     /* ServerHandle.weight; <= 0 never chosen (:628) */
+    int32_t healthy;    /* ServerHandle.healthy */
+} vc_server;
+
+/* The servers of every group of the compiled Upstream, each group's list in
+ * ServerGroup.getServerHandles() order: group g owns servers[group_off[g] ..
+ * group_off[g + 1]).  Builds the three source-hash lists of each group
+ * (sourceReset, ServerGroup.java:620-664: weight > 0, sorted by address
+ * length, signed address bytes, port; all / IPv4-only / IPv6-only). */
+int vc_compile_servers(vc_ctx *ctx, const vc_server *servers, const int32_t *group_off,
+                       int n_groups);
+/* Health-check result changed: healthy[i] for every server (same indexing
+ * as vc_compile_servers).  Takes effect for batches issued afterwards. */
+int vc_servers_set_health(vc_ctx *ctx, const uint8_t *healthy, int64_t n_servers);
+#define VC_SOURCE_ALL   0   /* ServerGroup.next(source)      :422-434 */
+#define VC_SOURCE_IPV4  4   /* ServerGroup.nextIPv4(source)  :436-448 */
+#define VC_SOURCE_IPV6  6   /* ServerGroup.nextIPv6(source)  :450-462 */
+/* sourceHashGet per item (ServerGroup.java:464-490): group[i] (e.g. the
+ * searchForGroup result; -1 or out of range -> -1) and the client address;
+ * out_server[i] = index into that group's server list, or -1 for null. */
+int vc_source_select_v4_dev(vc_ctx *ctx, const int32_t *group, const uint32_t *src4, int64_t n,
+                            int view, int32_t *out_server, void *stream);
+int vc_source_select_v6_dev(vc_ctx *ctx, const int32_t *group, const uint8_t *src6, int64_t n,
+                            int view, int32_t *out_server, void *stream);
+int vc_source_select_v4(vc_ctx *ctx, const int32_t *group, const uint32_t *src4, int64_t n,
+                        int view, int32_t *out_server);
+int vc_source_select_v6(vc_ctx *ctx, const int32_t *group, const uint8_t *src6, int64_t n,
+                        int view, int32_t *out_server);
+
+/* ------------------------------------------------------------------------ */
 /* Per-rule hit counters (no reference counterpart)          */
 /* ------------------------------------------------------------------------ */
 #define VC_COUNTERS_ACL    0  /* [tcp rules][udp rules][tcp default][udp default] */

@@ -44,6 +44,11 @@ class VoRouteTable(C.Structure):
                 ("v6", C.POINTER(VoNet)), ("n6", C.c_int), ("cap6", C.c_int)]
 
 
+class VoServer(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 16), ("ip_len", C.c_int32), ("port", C.c_int32),
+                ("weight", C.c_int32), ("healthy", C.c_int32)]
+
+
 class VoHosts(C.Structure):
     _fields_ = [("keys", C.POINTER(C.c_char_p)), ("key_lens", C.POINTER(C.c_int32)),
                 ("values", C.POINTER(C.c_int32)), ("n", C.c_int)]
@@ -95,6 +100,10 @@ def lib():
                                       P(C.c_int32)]
         L.vo_hosts_parse.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p,
                                      C.c_int, u8p, i32p, C.c_int]
+        L.vo_source_hash.argtypes = [u8p, C.c_int]
+        L.vo_source_hash.restype = C.c_int32
+        L.vo_source_list.argtypes = [P(VoServer), C.c_int, C.c_int, i32p]
+        L.vo_source_select.argtypes = [P(VoServer), C.c_int, C.c_int, u8p, C.c_int]
         _lib = L
     return _lib
 
@@ -436,3 +445,32 @@ def hint_batch_np(groups, blob, off, port, nthreads=1):
                         _ptr(np.ascontiguousarray(port, np.uint16)) if port is not None else None,
                         n, _ptr(out), nthreads)
     return out
+
+
+# ---- ServerGroup source hashing (ServerGroup.java:377-490) ----
+def servers_arr(servers):
+    """[(ip bytes, port, weight, healthy)] -> VoServer array"""
+    arr = (VoServer * max(1, len(servers)))()
+    for i, (ip, port, w, h) in enumerate(servers):
+        arr[i].ip[:len(ip)] = list(ip)
+        arr[i].ip_len = len(ip)
+        arr[i].port = port
+        arr[i].weight = w
+        arr[i].healthy = 1 if h else 0
+    return arr
+
+
+def source_hash(b):
+    return lib().vo_source_hash(_u8(bytes(b)), len(b))
+
+
+def source_list(servers, view):
+    arr = servers_arr(servers)
+    order = (C.c_int32 * max(1, len(servers)))()
+    k = lib().vo_source_list(arr, len(servers), view, order)
+    return list(order[:k])
+
+
+def source_select(servers, view, src):
+    arr = servers_arr(servers)
+    return lib().vo_source_select(arr, len(servers), view, _u8(bytes(src)), len(src))

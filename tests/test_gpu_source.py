@@ -1,0 +1,93 @@
+"""GPU tier: ServerGroup source hashing (device/select.hip) through the C ABI
+against the oracle (vo_source_select, ServerGroup.java:464-490), bit-exact:
+random groups of mixed IPv4/IPv6 servers with duplicate addresses, zero
+weights and unhealthy servers; IPv4 and IPv6 clients; all three views;
+health updates; out-of-range and -1 groups."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import vproxy_amd as V
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def clf():
+    c = V.Classifier(0)
+    yield c
+    c.close()
+
+
+def _groups(rng, ng):
+    groups = []
+    for _ in range(ng):
+        g = []
+        for _ in range(int(rng.integers(0, 14))):
+            if g and rng.random() < 0.15:
+                ip = g[int(rng.integers(0, len(g)))][0]
+            else:
+                ip = bytes(rng.integers(0, 256, 4 if rng.random() < 0.7 else 16).astype(np.uint8))
+            g.append((ip, int(rng.choice([80, 443, 8080])), int(rng.choice([0, 1, 1, 3])),
+                      bool(rng.random() < 0.8)))
+        groups.append(g)
+    return groups
+
+
+def _want(groups, grp, src, view):
+    out = np.empty(len(grp), np.int32)
+    for i, g in enumerate(grp):
+        if g < 0 or g >= len(groups):
+            out[i] = -1
+        else:
+            out[i] = O.source_select(groups[g], view, bytes(src[i]))
+    return out
+
+
+def test_source_select_vs_oracle(clf):
+    import torch
+    rng = np.random.default_rng(21)
+    groups = _groups(rng, 700)
+    clf.compile_servers(groups)
+    n = 20000
+    grp = rng.integers(-1, len(groups) + 2, n).astype(np.int32)
+    src4 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    src4_bytes = src4.astype(">u4").view(np.uint8).reshape(-1, 4)
+    src6 = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    for view in (V.SOURCE_ALL, V.SOURCE_IPV4, V.SOURCE_IPV6):
+        got = clf.source_select(grp, src4, view)
+        np.testing.assert_array_equal(got, _want(groups, grp, src4_bytes, view))
+        got6 = clf.source_select(grp, src6, view)
+        np.testing.assert_array_equal(got6, _want(groups, grp, src6, view))
+        dev = clf.source_select(torch.from_numpy(grp).cuda(),
+                                torch.from_numpy(src4.view(np.int32)).cuda(), view)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy(), got)
+    # health checks flip: the device table follows vc_servers_set_health
+    flat = [sv for g in groups for sv in g]
+    healthy = rng.random(len(flat)) < 0.5
+    clf.set_server_health(healthy.astype(np.uint8))
+    k = 0
+    sick = []
+    for g in groups:
+        sick.append([(a, p, w, bool(healthy[k + j])) for j, (a, p, w, h) in enumerate(g)])
+        k += len(g)
+    got = clf.source_select(grp, src4, V.SOURCE_ALL)
+    np.testing.assert_array_equal(got, _want(sick, grp, src4_bytes, V.SOURCE_ALL))
+
+
+def test_source_sticky_like_tcplb(clf):
+    """TestTcpLB.proxySource: every connection of one client reaches the
+    same backend (TestTcpLB.java:383-405)."""
+    clf.compile_servers([[("127.0.0.1", 19080, 10, True), ("127.0.0.1", 19081, 10, True)]])
+    src = np.full(100, (127 << 24) | 1, np.uint32)
+    got = clf.source_select(np.zeros(100, np.int32), src)
+    assert len(set(got.tolist())) == 1 and got[0] in (0, 1)
+
+
+def test_source_errors(clf):
+    clf.compile_servers([[("10.0.0.1", 80, 1, True)]])
+    with pytest.raises(V.IllegalArgumentException):
+        clf.set_server_health(np.ones(2, np.uint8))
+    with pytest.raises(V.IllegalArgumentException):
+        clf.source_select(np.zeros(1, np.int32), np.zeros(1, np.uint32), view=5)

@@ -7,8 +7,10 @@ HIP kernels for gfx950 behind the C ABI in include/vclassify.h.
 from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,  # noqa: F401
                    NotFoundException, StateError, VcError, XException, check, lib,
                    COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP, PROTO_TCP, PROTO_UDP,
-                   DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE)
+                   DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE,
+                   SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
-                         acl_rule_array, group_array, net_array, pack_strings, parse_ip)
+                         acl_rule_array, group_array, net_array, pack_strings, parse_ip,
+                         server_array)
 
 __all__ = ["Classifier", "Network", "SecurityGroup", "RouteTable", "Annotations", "parse_ip"]

@@ -15,6 +15,7 @@ VC_OK, VC_EINVAL, VC_EEXIST, VC_ENOTFOUND, VC_EXEXC, VC_EDEVICE, VC_ENOMEM, VC_E
 PROTO_TCP, PROTO_UDP = 6, 17
 DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE = 1, 2, 3, 4, 5
 COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP = 0, 1, 2
+SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6 = 0, 4, 6
 
 
 class VcNet(C.Structure):
@@ -34,6 +35,11 @@ class VcAnnos(C.Structure):
 
 class VcGroupAnnos(C.Structure):
     _fields_ = [("handle", VcAnnos), ("group", VcAnnos)]
+
+
+class VcServer(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 16), ("ip_len", C.c_int32), ("port", C.c_int32),
+                ("weight", C.c_int32), ("healthy", C.c_int32)]
 
 
 # ---- exceptions mirroring the reference's (vproxybase.util.exception.*) ----
@@ -117,6 +123,12 @@ def lib():
         L.vc_pipeline_v4_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
         L.vc_pipeline_v4_dev_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                             vp, vp]
+        L.vc_compile_servers.argtypes = [vp, P(VcServer), vp, i32]
+        L.vc_servers_set_health.argtypes = [vp, vp, i64]
+        for f in ("vc_source_select_v4_dev", "vc_source_select_v6_dev"):
+            getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp, vp]
+        for f in ("vc_source_select_v4", "vc_source_select_v6"):
+            getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

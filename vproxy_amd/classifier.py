@@ -18,7 +18,8 @@ import ipaddress
 import numpy as np
 
 from . import _lib
-from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, check, lib)
+from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, VcServer, check,
+                   lib)
 
 HINT_HOST = "vproxy/hint-host"   # AnnotationKeys.ServerGroup_HintHost
 HINT_PORT = "vproxy/hint-port"   # AnnotationKeys.ServerGroup_HintPort
@@ -288,6 +289,26 @@ def pack_strings(items):
     return blob.copy(), off.astype(np.uint32), null
 
 
+def server_array(groups):
+    """ServerGroup server lists -> (vc_server array, group_off int32 array).
+    groups: one list per group of (ip, port, weight, healthy) with ip a
+    string or raw 4/16 bytes, in ServerGroup.getServerHandles() order."""
+    flat = [sv for g in groups for sv in g]
+    arr = (VcServer * max(1, len(flat)))()
+    for i, (ip, port, weight, healthy) in enumerate(flat):
+        b = parse_ip(ip) if isinstance(ip, str) else bytes(ip)
+        if b is None or len(b) not in (4, 16):
+            raise _lib.IllegalArgumentException("bad server address %r" % (ip,))
+        arr[i].ip[:len(b)] = list(b)
+        arr[i].ip_len = len(b)
+        arr[i].port = int(port)
+        arr[i].weight = int(weight)
+        arr[i].healthy = 1 if healthy else 0
+    off = np.zeros(len(groups) + 1, np.int32)
+    off[1:] = np.cumsum([len(g) for g in groups])
+    return arr, off
+
+
 def _is_dev(x):
     return x is not None and hasattr(x, "is_cuda") and x.is_cuda
 
@@ -488,6 +509,37 @@ class Classifier:
                                           _stream(), C.c_void_p(kernel_done_event)
                                           if kernel_done_event else None))
         return outs
+
+    # ---------------- ServerGroup source hashing ----------------
+    def compile_servers(self, groups):
+        """Server lists per group (see server_array)."""
+        arr, off = server_array(groups)
+        self._server_off = off
+        check(lib().vc_compile_servers(self.h, arr, _ptr(off), len(groups)))
+
+    def set_server_health(self, healthy):
+        h = np.ascontiguousarray(healthy, np.uint8)
+        check(lib().vc_servers_set_health(self.h, _ptr(h), len(h)))
+
+    def source_select(self, group, src, view=0):
+        """ServerGroup.next/nextIPv4/nextIPv6(source) (method source) per item:
+        group indices + client addresses (uint32 v4 keys, or n x 16 bytes for
+        IPv6) -> server index within the group, -1 = null."""
+        n = len(group)
+        v6 = (src.dtype == np.uint8 or (hasattr(src, "dtype") and "uint8" in str(src.dtype))) \
+            and src.ndim == 2
+        if _is_dev(group):
+            import torch
+            out = torch.empty(n, dtype=torch.int32, device=group.device)
+            f = lib().vc_source_select_v6_dev if v6 else lib().vc_source_select_v4_dev
+            check(f(self.h, _ptr(group), _ptr(src), n, int(view), _ptr(out), _stream()))
+            return out
+        group = np.ascontiguousarray(group, np.int32)
+        src = np.ascontiguousarray(src, np.uint8 if v6 else np.uint32)
+        out = np.empty(n, np.int32)
+        f = lib().vc_source_select_v6 if v6 else lib().vc_source_select_v4
+        check(f(self.h, _ptr(group), _ptr(src), n, int(view), _ptr(out)))
+        return out
 
     # ---------------- counters ----------------
     def counters_enable(self, on=True):

@@ -83,6 +83,10 @@ struct HintSnap : Snapshot {
 struct HostsSnap : Snapshot {
     HostsImage img{};
 };
+struct ServerSnap : Snapshot {
+    ServerImage img{};
+    uint8_t* healthy = nullptr;    // device copy, updated in place (vc_servers_set_health)
+};
 
 }  // namespace
 
@@ -97,6 +101,7 @@ struct vc_ctx {
     std::shared_ptr<const RouteSnap> route;
     std::shared_ptr<const HintSnap> hint;
     std::shared_ptr<const HostsSnap> hosts;
+    std::shared_ptr<const ServerSnap> servers;
 
     template <class S>
     std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
@@ -209,6 +214,7 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->route.reset();
     ctx->hint.reset();
     ctx->hosts.reset();
+    ctx->servers.reset();
     (void)hipStreamDestroy(ctx->stream);
     if (ctx->pool) {
         // batches may still run on callers' streams: their scratch is freed
@@ -566,6 +572,96 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
     st.back(out_value, dv, size_t(n) * 4, s);
     hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
     return e == hipSuccess ? VC_OK : hip_fail(e, "dns classify");
+}
+
+// ---------------------------------------------------------------------------
+// ServerGroup source hashing
+// ---------------------------------------------------------------------------
+int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* group_off,
+                       int n_groups) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    vc::ServersBuilt b;
+    if ((rc = vc::build_servers(servers, group_off, n_groups, &b)) != VC_OK)
+        return fail(rc, "invalid server lists");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<ServerSnap>();
+    hipError_t e = hipSuccess;
+    s->img.view_off = s->upload(b.view_off, &e);
+    s->img.order = s->upload(b.order, &e);
+    s->healthy = const_cast<uint8_t*>(s->upload(b.healthy, &e));
+    s->img.healthy = s->healthy;
+    s->img.group_base = s->upload(b.group_base, &e);
+    s->img.n_groups = b.n_groups;
+    s->img.n_servers = b.n_servers;
+    if (e != hipSuccess) return hip_fail(e, "server upload");
+    ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(s)));
+    return VC_OK;
+}
+
+int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    auto s = ctx->get(ctx->servers);
+    if (!s) return fail(VC_ESTATE, "no servers compiled");
+    if (n_servers != s->img.n_servers || (n_servers > 0 && !healthy))
+        return fail(VC_EINVAL, "health array does not match the compiled servers");
+    std::vector<uint8_t> h(healthy, healthy + n_servers);
+    for (auto& x : h) x = x ? 1 : 0;
+    hipError_t e = n_servers ? hipMemcpy(s->healthy, h.data(), size_t(n_servers),
+                                         hipMemcpyHostToDevice)
+                             : hipSuccess;
+    return e == hipSuccess ? VC_OK : hip_fail(e, "health upload");
+}
+
+static int source_dev(vc_ctx* ctx, int fam, const int32_t* group, const void* src, int64_t n,
+                      int view, int32_t* out, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!group || !src || !out))) return fail(VC_EINVAL, "bad batch arguments");
+    if (view != VC_SOURCE_ALL && view != VC_SOURCE_IPV4 && view != VC_SOURCE_IPV6)
+        return fail(VC_EINVAL, "view must be VC_SOURCE_ALL, _IPV4 or _IPV6");
+    if (fam == 6 && (reinterpret_cast<uintptr_t>(src) & 15))
+        return fail(VC_EINVAL, "IPv6 addresses must be 16-byte aligned");
+    auto s = ctx->get(ctx->servers);
+    if (!s) return fail(VC_ESTATE, "no servers compiled");
+    hipError_t e = vc::launch_source(ctx->cfg(stream), s->img, group, src, fam, n, view, out);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "source launch");
+}
+
+static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* src, int64_t n,
+                       int view, int32_t* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    Staging st;
+    hipStream_t hs = ctx->stream;
+    auto* dg = static_cast<int32_t*>(st.in(group, size_t(n) * 4, hs));
+    void* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), hs);
+    auto* dout = static_cast<int32_t*>(st.out(out, size_t(n) * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = source_dev(ctx, fam, dg, ds, n, view, dout, hs);
+    if (rc) return rc;
+    st.back(out, dout, size_t(n) * 4, hs);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(hs);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "source select");
+}
+
+int vc_source_select_v4_dev(vc_ctx* ctx, const int32_t* group, const uint32_t* src4, int64_t n,
+                            int view, int32_t* out_server, void* stream) {
+    return source_dev(ctx, 4, group, src4, n, view, out_server, stream);
+}
+int vc_source_select_v6_dev(vc_ctx* ctx, const int32_t* group, const uint8_t* src6, int64_t n,
+                            int view, int32_t* out_server, void* stream) {
+    return source_dev(ctx, 6, group, src6, n, view, out_server, stream);
+}
+int vc_source_select_v4(vc_ctx* ctx, const int32_t* group, const uint32_t* src4, int64_t n,
+                        int view, int32_t* out_server) {
+    return source_host(ctx, 4, group, src4, n, view, out_server);
+}
+int vc_source_select_v6(vc_ctx* ctx, const int32_t* group, const uint8_t* src6, int64_t n,
+                        int view, int32_t* out_server) {
+    return source_host(ctx, 6, group, src6, n, view, out_server);
 }
 
 // ---------------------------------------------------------------------------

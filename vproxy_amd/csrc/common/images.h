@@ -140,3 +140,20 @@ struct HostsImage {
     uint32_t mask;
     int32_t n;
 };
+
+// ---------------------------------------------------------------------------
+// ServerGroup source hashing (method == source): per group, three lists of
+// server indices (all / IPv4 / IPv6 servers with weight > 0, in
+// sourceReset's sort order).  view_off holds (offset, count) into order[]
+// for [group][view 0..2]; order[] holds global server indices; healthy[]
+// is per global server (updated in place by vc_servers_set_health);
+// group_base[g] is the global index of group g's first server.
+// ---------------------------------------------------------------------------
+struct ServerImage {
+    const uint32_t* view_off;      // 6 words per group
+    const int32_t* order;
+    const uint8_t* healthy;
+    const int32_t* group_base;
+    int32_t n_groups;
+    int32_t n_servers;
+};

@@ -499,4 +499,65 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
     return VC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// ServerGroup source hashing
+// ---------------------------------------------------------------------------
+namespace {
+
+// sourceReset's comparator (ServerGroup.java:629-642): address length,
+// then signed address bytes, then port.
+int server_cmp(const vc_server& a, const vc_server& b) {
+    if (a.ip_len > b.ip_len) return 1;
+    if (b.ip_len > a.ip_len) return -1;
+    for (int i = 0; i < a.ip_len; ++i) {
+        const int diff = int(int8_t(a.ip[i])) - int(int8_t(b.ip[i]));
+        if (diff != 0) return diff;
+    }
+    return a.port - b.port;
+}
+
+}  // namespace
+
+int build_servers(const vc_server* servers, const int32_t* group_off, int n_groups,
+                  ServersBuilt* out) {
+    *out = ServersBuilt{};
+    if (n_groups < 0 || (n_groups > 0 && !group_off)) return VC_EINVAL;
+    const int32_t total = n_groups > 0 ? group_off[n_groups] : 0;
+    if (n_groups > 0 && group_off[0] != 0) return VC_EINVAL;
+    for (int g = 0; g < n_groups; ++g)
+        if (group_off[g + 1] < group_off[g]) return VC_EINVAL;
+    if (total > 0 && !servers) return VC_EINVAL;
+    for (int32_t i = 0; i < total; ++i)
+        if (servers[i].ip_len != 4 && servers[i].ip_len != 16) return VC_EINVAL;
+    out->n_groups = n_groups;
+    out->n_servers = total;
+    out->view_off.assign(size_t(n_groups) * 6, 0);
+    out->group_base.assign(size_t(n_groups) + 1, 0);
+    out->healthy.resize(size_t(total) + 1, 0);
+    for (int32_t i = 0; i < total; ++i) out->healthy[i] = servers[i].healthy ? 1 : 0;
+    for (int g = 0; g < n_groups; ++g) {
+        out->group_base[g] = group_off[g];
+        for (int v = 0; v < 3; ++v) {
+            std::vector<int32_t> ids;
+            for (int32_t i = group_off[g]; i < group_off[g + 1]; ++i) {
+                const vc_server& sv = servers[i];
+                if (v == 1 && sv.ip_len != 4) continue;    // :622 instanceof IPv4
+                if (v == 2 && sv.ip_len != 16) continue;   // :623 instanceof IPv6
+                if (sv.weight <= 0) continue;              // :628 weight > 0
+                ids.push_back(i);
+            }
+            std::stable_sort(ids.begin(), ids.end(), [&](int32_t a, int32_t b) {
+                return server_cmp(servers[a], servers[b]) < 0;   // List.sort is stable
+            });
+            out->view_off[size_t(g) * 6 + 2 * v] = static_cast<uint32_t>(out->order.size());
+            out->view_off[size_t(g) * 6 + 2 * v + 1] = static_cast<uint32_t>(ids.size());
+            out->order.insert(out->order.end(), ids.begin(), ids.end());
+        }
+    }
+    out->group_base[n_groups] = total;
+    if (out->order.empty()) out->order.push_back(0);
+    if (out->view_off.empty()) out->view_off.assign(6, 0);
+    return VC_OK;
+}
+
 }  // namespace vc

@@ -83,6 +83,19 @@ struct HostsBuilt {
 int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
                 HostsBuilt* out);
 
+// ServerGroup source-hash lists (ServerGroup.java:620-664), see ServerImage.
+struct ServersBuilt {
+    std::vector<uint32_t> view_off;      // 6 words per group
+    std::vector<int32_t> order;
+    std::vector<uint8_t> healthy;
+    std::vector<int32_t> group_base;
+    int32_t n_groups = 0;
+    int32_t n_servers = 0;
+};
+
+int build_servers(const vc_server* servers, const int32_t* group_off, int n_groups,
+                  ServersBuilt* out);
+
 // 32-bit FNV-1a over bytes, forwards and right-to-left (must match device code).
 inline uint32_t fnv_fwd(const uint8_t* p, size_t n) {
     uint32_t h = 2166136261u;

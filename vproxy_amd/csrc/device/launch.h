@@ -55,6 +55,11 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
                               int64_t route_none_at, unsigned long long* group_cnt,
                               int32_t n_groups, hipEvent_t kernel_done = nullptr);
 
+// ServerGroup source hashing (select.hip); family 4: src = uint32 v4 keys,
+// 6: 16-byte addresses (16-byte aligned); view = VC_SOURCE_*.
+hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32_t* group,
+                         const void* src, int family, int64_t n, int view, int32_t* out);
+
 // Large counter spaces (counters.hip): bucket partition + per-bucket LDS
 // histograms, split so a producer kernel (the pipeline) can supply the
 // per-workgroup bucket counts itself: begin (allocate), producer writes

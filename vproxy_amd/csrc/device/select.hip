@@ -1,0 +1,93 @@
+// select.hip -- ServerGroup.next(source) for method == source, batched.
+//
+//   SOURCE.hash       base/.../component/svrgroup/ServerGroup.java:387-397
+//   sourceHashGet     ServerGroup.java:464-490
+//   sourceReset       ServerGroup.java:620-664 (host side: compile.cpp)
+//
+// One lane per item: the sdbm hash of the client address bytes (Java int
+// arithmetic on sign-extended bytes), then the first healthy server from
+// hash % size on, probing forward as the Java recursion does.
+#include "dev_common.h"
+#include "launch.h"
+
+namespace vcd {
+
+constexpr int kSelBlock = 256;
+
+// sdbm over the address bytes, Math.abs, MIN_VALUE -> 0
+__device__ __forceinline__ int32_t sdbm_step(uint32_t h, uint32_t byte) {
+    const uint32_t b = uint32_t(int32_t(int8_t(uint8_t(byte))));
+    return int32_t(b + (h << 6) + (h << 16) - h);
+}
+
+__device__ __forceinline__ int32_t java_abs_hash(int32_t h) {
+    if (h == INT32_MIN) return 0;
+    return h < 0 ? -h : h;
+}
+
+__device__ __forceinline__ int32_t source_pick(const ServerImage& img, int32_t g, int view,
+                                               int32_t hash) {
+    if (g < 0 || g >= img.n_groups) return -1;
+    const uint2 vo = reinterpret_cast<const uint2*>(img.view_off)[g * 3 + view];
+    const int32_t size = int32_t(vo.y);
+    for (int32_t recurse = 0; recurse < size; ++recurse) {   // :480
+        const int32_t idx = hash % size;                     // :483
+        const int32_t s = img.order[vo.x + idx];
+        if (img.healthy[s]) return s - img.group_base[g];
+        hash = idx + 1;                                      // :489
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(kSelBlock) void source_v4_kernel(
+    ServerImage img, const int32_t* __restrict__ group, const uint32_t* __restrict__ src4,
+    int64_t n, int view, int32_t* __restrict__ out) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t a = src4[i];                          // IP.ipv4Bytes2Int order
+        uint32_t h = 0;
+        h = uint32_t(sdbm_step(h, a >> 24));
+        h = uint32_t(sdbm_step(h, (a >> 16) & 255u));
+        h = uint32_t(sdbm_step(h, (a >> 8) & 255u));
+        h = uint32_t(sdbm_step(h, a & 255u));
+        out[i] = source_pick(img, group[i], view, java_abs_hash(int32_t(h)));
+    }
+}
+
+__global__ __launch_bounds__(kSelBlock) void source_v6_kernel(
+    ServerImage img, const int32_t* __restrict__ group, const uint8_t* __restrict__ src6,
+    int64_t n, int view, int32_t* __restrict__ out) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint4 w = reinterpret_cast<const uint4*>(src6)[i];
+        const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+        uint32_t h = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) h = uint32_t(sdbm_step(h, (words[k] >> (8 * b)) & 255u));
+        out[i] = source_pick(img, group[i], view, java_abs_hash(int32_t(h)));
+    }
+}
+
+}  // namespace vcd
+
+namespace vc {
+
+hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32_t* group,
+                         const void* src, int family, int64_t n, int view, int32_t* out) {
+    if (n <= 0) return hipSuccess;
+    const int vi = view == VC_SOURCE_IPV4 ? 1 : (view == VC_SOURCE_IPV6 ? 2 : 0);
+    int64_t want = (n + vcd::kSelBlock - 1) / vcd::kSelBlock;
+    const int64_t cap = int64_t(c.num_cus) * 8;
+    const int grid = int(want < cap ? want : cap);
+    if (family == 4)
+        hipLaunchKernelGGL(vcd::source_v4_kernel, dim3(grid), dim3(vcd::kSelBlock), 0, c.stream, img,
+                           group, static_cast<const uint32_t*>(src), n, vi, out);
+    else
+        hipLaunchKernelGGL(vcd::source_v6_kernel, dim3(grid), dim3(vcd::kSelBlock), 0, c.stream, img,
+                           group, static_cast<const uint8_t*>(src), n, vi, out);
+    return hipGetLastError();
+}
+
+}  // namespace vc
