@@ -236,6 +236,64 @@ int vc_source_select_v6(vc_ctx *ctx, const int32_t *group, const uint8_t *src6, 
                         int view, int32_t *out_server);
 
 /* ------------------------------------------------------------------------ */
+/* Header extraction from raw frames: the vswitch's  */
+/* parse chain base/src/main/java/vpacket/: VXLanPacket.from (:16-33) ->     */
+/* EthernetPacket.from (:14-50) -> ArpPacket / Ipv4Packet (:28-101) /         */
+/* Ipv6Packet (:24-106) .from -> TcpPacket (:164-227) / IcmpPacket .from.    */
+/* ------------------------------------------------------------------------ */
+#define VC_LAYER_VXLAN  0   /* frames are VXLAN UDP payloads (Switch.java:679-690) */
+#define VC_LAYER_ETHER  1
+#define VC_LAYER_IPV4   4
+#define VC_LAYER_IPV6   6
+
+#define VC_PKT_OK          0   /* `from` returned null */
+#define VC_PKT_ERR_VXLAN   1   /* VXLAN header too short */
+#define VC_PKT_ERR_ETHER   2   /* Ethernet too short, or an ARP error */
+#define VC_PKT_ERR_IP      3   /* IP/TCP/ICMP error (layer VC_LAYER_IPV4/6 only; under
+                                  Ethernet the IP payload is kept as bytes: VC_L3_BAD_IP) */
+#define VC_PKT_EXCEPTION   4   /* the Java parser throws (a TCP option of length 0 or 1) */
+#define VC_PKT_LOOP        5   /* the Java parser never returns (IPv6 extension header whose
+                                  next header is an extension header, Ipv6Packet.java:63-78) */
+
+#define VC_L3_OTHER   0   /* PacketBytes */
+#define VC_L3_ARP     1
+#define VC_L3_IPV4    4
+#define VC_L3_BAD_IP  5   /* IP ether type whose parse failed (EthernetPacket.java:36-45) */
+#define VC_L3_IPV6    6
+
+#define VC_L4_BYTES   0   /* PacketBytes (UDP included, as in the reference) */
+#define VC_L4_ICMP    1
+#define VC_L4_TCP     6
+#define VC_L4_ICMPV6  58
+
+#define VC_TCPOPT_END  0
+#define VC_TCPOPT_NOP  1
+#define VC_TCPOPT_MSS  2
+#define VC_TCPOPT_WS   3
+
+/* Per-frame outputs (SoA); any pointer may be NULL.  Fields a frame does
+ * not have are 0.  src4/dst4 feed the ACL / route / pipeline entry points
+ * directly (IP.ipv4Bytes2Int order). */
+typedef struct {
+    uint8_t *status;       /* VC_PKT_* */
+    uint8_t *l3;           /* VC_L3_* */
+    uint8_t *l4;           /* VC_L4_* */
+    uint8_t *proto;        /* IPv4 protocol / IPv6 final next header */
+    uint32_t *vni;         /* VXLAN vni */
+    uint16_t *ether_type;
+    uint32_t *src4, *dst4; /* IPv4 addresses */
+    uint8_t *src6, *dst6;  /* IPv6 addresses, 16 bytes per frame */
+    uint16_t *sport, *dport;   /* TCP ports */
+} vc_pkt_out;
+
+/* frames: blob + uint32 offsets (n + 1 entries).  Device pointers in `out`. */
+int vc_parse_packets_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
+                         int layer, const vc_pkt_out *out, void *stream);
+/* Host pointers (blob, off and every array in `out`). */
+int vc_parse_packets(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n, int layer,
+                     const vc_pkt_out *out);
+
+/* ------------------------------------------------------------------------ */
 /* Per-rule hit counters (no reference counterpart)          */
 /* ------------------------------------------------------------------------ */
 #define VC_COUNTERS_ACL    0  /* [tcp rules][udp rules][tcp default][udp default] */

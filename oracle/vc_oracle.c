@@ -1000,3 +1000,189 @@ int vo_source_select(const vo_server *servers, int n, int view, const uint8_t *s
     free(order);
     return result;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Packet header extraction (base/src/main/java/vpacket)                    */
+/* ------------------------------------------------------------------------ */
+/* Result codes of one `from` call: NULL (ok) / an error string / a thrown
+ * exception / no return at all. */
+enum { VO_OK = 0, VO_ERR = 1, VO_THROW = 2, VO_HANG = 3 };
+
+static int vo_u8(const uint8_t *p, int i) { return p[i]; }
+static int vo_u16(const uint8_t *p, int i) { return (p[i] << 8) | p[i + 1]; }
+
+/* TcpPacket.from, TcpPacket.java:164-227, with TcpOption.from/check
+ * (:399-434): an option of length 0 or 1 makes TcpOption.from read past its
+ * own sub-array, which throws. */
+static int vo_tcp(const uint8_t *p, int len, vo_pkt *o) {
+    if (len < 20) return VO_ERR;
+    o->sport = vo_u16(p, 0);
+    o->dport = vo_u16(p, 2);
+    const int data_offset = ((vo_u16(p, 12) >> 12) & 0xf) * 4;
+    if (data_offset > len) return VO_ERR;
+    if (data_offset > 20) {
+        int off = 20;
+        while (off < data_offset) {
+            const int kind = (int8_t)p[off];
+            if (kind == 0 || kind == 1) {              /* CASE_1_OPTION_KINDS: END, NOP */
+                off += 1;
+                if (kind == 0) break;
+            } else {
+                if (off + 1 >= data_offset) return VO_ERR;
+                const int olen = vo_u8(p, off + 1);
+                if (off + olen > data_offset) return VO_ERR;
+                if (olen < 2) return VO_THROW;         /* get(0) / uint8(1) out of the sub-array */
+                if (kind == 3 && olen != 3) return VO_ERR;   /* window scale */
+                if (kind == 2 && olen != 4) return VO_ERR;   /* mss */
+                off += olen;
+            }
+        }
+    }
+    return VO_OK;
+}
+
+/* IcmpPacket.from, IcmpPacket.java:22-33 */
+static int vo_icmp(int len) { return len < 8 ? VO_ERR : VO_OK; }
+
+/* the transport of an IP packet: ICMP / TCP / PacketBytes */
+static int vo_l4(const uint8_t *p, int len, int proto, int v6, vo_pkt *o) {
+    if (proto == 1 || (v6 && proto == 58)) {
+        o->l4 = proto == 58 ? 58 : 1;
+        return vo_icmp(len);
+    }
+    if (proto == 6) {
+        o->l4 = 6;
+        return vo_tcp(p, len, o);
+    }
+    o->l4 = 0;
+    return VO_OK;                                       /* PacketBytes.from never fails */
+}
+
+/* Ipv4Packet.from, Ipv4Packet.java:28-101 */
+static int vo_ipv4(const uint8_t *p, int len, vo_pkt *o) {
+    if (len < 20) return VO_ERR;
+    const int version = (vo_u8(p, 0) >> 4) & 0xff;
+    if (version != 4) return VO_ERR;
+    const int ihl = vo_u8(p, 0) & 0x0f;
+    if (len < ihl * 4) return VO_ERR;
+    if (ihl < 5) return VO_ERR;
+    const int total = vo_u16(p, 2);
+    if (total < ihl * 4) return VO_ERR;
+    if (total != len) return VO_ERR;
+    o->proto = vo_u8(p, 9);
+    memcpy(o->src, p + 12, 4);
+    memcpy(o->dst, p + 16, 4);
+    return vo_l4(p + ihl * 4, total - ihl * 4, o->proto, 0, o);
+}
+
+static int vo_v6_ext(int nh) {                          /* Consts.IPv6_needs_next_header */
+    return nh == 0 || nh == 60 || nh == 43 || nh == 44 || nh == 51 || nh == 50 || nh == 135 ||
+           nh == 139 || nh == 140 || nh == 253 || nh == 254;
+}
+
+/* Ipv6Packet.from, Ipv6Packet.java:24-106.  The extension-header loop
+ * re-parses the first header (xhBuf = xhBuf.sub(0, len), :77): when that
+ * header's next header is itself an extension header the loop never ends. */
+static int vo_ipv6(const uint8_t *p, int len, vo_pkt *o) {
+    if (len < 40) return VO_ERR;
+    const int version = (((int8_t)p[0]) >> 4) & 0x0f;
+    if (version != 6) return VO_ERR;
+    const int payload = vo_u16(p, 4);
+    const int next = vo_u8(p, 6);
+    if (payload == 0) return VO_ERR;
+    if (40 + payload != len) return VO_ERR;
+    memcpy(o->src, p + 8, 16);
+    memcpy(o->dst, p + 24, 16);
+    int skip = 0, proto = next;
+    if (vo_v6_ext(next)) {
+        const uint8_t *x = p + 40;
+        const int xlen = len - 40;
+        if (xlen < 8) return VO_ERR;                    /* ExtHeader.from */
+        const int hdr_ext_len = vo_u8(x, 1);
+        if (xlen < 8 + hdr_ext_len) return VO_ERR;
+        const int xnext = vo_u8(x, 0);
+        if (vo_v6_ext(xnext)) return VO_HANG;
+        skip = 8 + hdr_ext_len;
+        proto = xnext;
+    }
+    o->proto = proto;
+    const int rest = len - 40 - skip;
+    if (proto == 59 && rest != 0) return VO_ERR;        /* NO_NEXT_HEADER with bytes */
+    return vo_l4(p + 40 + skip, rest, proto, 1, o);
+}
+
+/* ArpPacket.from, ArpPacket.java:22-64 */
+static int vo_arp(const uint8_t *p, int len) {
+    if (len < 8) return VO_ERR;
+    const int hs = vo_u8(p, 4), ps = vo_u8(p, 5);
+    if (len != 8 + 2 * hs + 2 * ps) return VO_ERR;      /* every shorter length errs first */
+    return VO_OK;
+}
+
+/* EthernetPacket.from, EthernetPacket.java:14-50: an IP parse error is
+ * logged and the payload kept as PacketBytes (mayIgnoreError) */
+static int vo_ether(const uint8_t *p, int len, vo_pkt *o) {
+    if (len < 14) return VO_ERR;
+    o->ether_type = vo_u16(p, 12);
+    const uint8_t *d = p + 14;
+    const int dl = len - 14;
+    if (o->ether_type == 0x0806) {
+        o->l3 = 1;
+        return vo_arp(d, dl);
+    }
+    if (o->ether_type == 0x0800 || o->ether_type == 0x86dd) {
+        vo_pkt ip;
+        memset(&ip, 0, sizeof(ip));
+        const int v6 = o->ether_type == 0x86dd;
+        const int r = v6 ? vo_ipv6(d, dl, &ip) : vo_ipv4(d, dl, &ip);
+        if (r == VO_THROW || r == VO_HANG) return r;
+        if (r == VO_ERR) {
+            o->l3 = 5;
+            return VO_OK;
+        }
+        o->l3 = v6 ? 6 : 4;
+        o->l4 = ip.l4;
+        o->proto = ip.proto;
+        memcpy(o->src, ip.src, 16);
+        memcpy(o->dst, ip.dst, 16);
+        o->sport = ip.sport;
+        o->dport = ip.dport;
+        return VO_OK;
+    }
+    o->l3 = 0;
+    return VO_OK;
+}
+
+void vo_parse_packet(const uint8_t *p, int len, int layer, vo_pkt *out) {
+    memset(out, 0, sizeof(*out));
+    int r;
+    if (layer == 0) {                                   /* VXLanPacket.from, :16-33 */
+        if (len < 8) {
+            out->status = 1;
+            return;
+        }
+        out->vni = (uint32_t)((p[4] << 16) | (p[5] << 8) | p[6]);
+        r = vo_ether(p + 8, len - 8, out);
+        out->status = r == VO_OK ? 0 : r == VO_ERR ? 2 : r == VO_THROW ? 4 : 5;
+    } else if (layer == 1) {
+        r = vo_ether(p, len, out);
+        out->status = r == VO_OK ? 0 : r == VO_ERR ? 2 : r == VO_THROW ? 4 : 5;
+    } else {
+        vo_pkt ip;
+        memset(&ip, 0, sizeof(ip));
+        r = layer == 6 ? vo_ipv6(p, len, &ip) : vo_ipv4(p, len, &ip);
+        *out = ip;
+        out->l3 = layer == 6 ? 6 : 4;
+        out->status = r == VO_OK ? 0 : r == VO_ERR ? 3 : r == VO_THROW ? 4 : 5;
+    }
+    if (out->status != 0) {                             /* no packet object: fields unset */
+        const uint32_t vni = out->vni;
+        const int et = out->ether_type;
+        memset(out->src, 0, 16);
+        memset(out->dst, 0, 16);
+        out->l3 = out->l4 = out->proto = out->sport = out->dport = 0;
+        out->vni = vni;
+        out->ether_type = et;
+        if (out->status == 1) out->vni = 0;
+    }
+}

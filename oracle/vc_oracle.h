@@ -169,6 +169,25 @@ int vo_source_list(const vo_server *servers, int n, int view, int32_t *order);
  * chosen server, or -1 (null: empty list or no healthy server). */
 int vo_source_select(const vo_server *servers, int n, int view, const uint8_t *src, int src_len);
 
+/* ---- Packet header extraction: base/src/main/java/vpacket/ ----
+ * VXLanPacket.from (:16-33) -> EthernetPacket.from (:14-50) -> ArpPacket /
+ * Ipv4Packet (:28-101) / Ipv6Packet (:24-106) .from -> TcpPacket (:164-227) /
+ * IcmpPacket (:22-33) .from.  `layer` names the class the caller starts with
+ * (0 VXLAN, 1 Ethernet, 4 IPv4, 6 IPv6). */
+typedef struct {
+    int status;        /* 0 ok, 1 vxlan error, 2 ethernet/ARP error, 3 IP-layer error (layer 4/6),
+                          4 the Java parser throws, 5 the Java parser never returns */
+    int l3;            /* 0 PacketBytes, 1 ARP, 4 IPv4, 6 IPv6, 5 IP ether type kept as bytes */
+    int l4;            /* 0 bytes, 1 ICMP, 58 ICMPv6, 6 TCP */
+    int proto;
+    uint32_t vni;
+    int ether_type;
+    uint8_t src[16], dst[16];   /* IPv4: first 4 bytes */
+    int sport, dport;
+} vo_pkt;
+
+void vo_parse_packet(const uint8_t *p, int len, int layer, vo_pkt *out);
+
 #ifdef __cplusplus
 }
 #endif

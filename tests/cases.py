@@ -163,3 +163,105 @@ def hint_cases_shapes(rng, n):
             h = ("www." if rng.random() < 0.5 else "") + h + ":" + str(int(rng.integers(0, 70000)))
         names.append(str(h).encode())
     return groups, names
+
+
+def gen_frames(rng, n):
+    """VXLAN payloads (layer 0) covering the vpacket parse chain: IPv4 and
+    IPv6 over Ethernet with TCP (with valid, malformed and throwing options),
+    UDP, ICMP/ICMPv6, IPv4 options, IPv6 extension headers (including the
+    looping chain), ARP of every size relation, other ether types, wrong
+    versions / lengths, and truncation at every offset."""
+    import numpy as np
+
+    def rb(k):
+        return bytes(rng.integers(0, 256, k).astype(np.uint8))
+
+    def tcp(opts=b""):
+        pad = (-len(opts)) % 4
+        opts += bytes(pad)
+        doff = 20 + len(opts)
+        flags = bytes([(doff // 4) << 4, int(rng.integers(0, 64))])
+        return rb(4) + rb(8) + flags + rb(6) + opts + rb(int(rng.integers(0, 40)))
+
+    def options():
+        r = rng.random()
+        if r < 0.3:
+            return b""
+        if r < 0.5:     # typical SYN options
+            return bytes([2, 4, 5, 180, 1, 3, 3, 6, 1, 1, 8, 10]) + rb(8) + bytes([4, 2, 0, 0])
+        if r < 0.6:
+            return bytes([0]) + rb(3)                       # END first
+        if r < 0.7:
+            return bytes([8, int(rng.integers(0, 2))]) + rb(2)   # length 0/1: throws
+        if r < 0.8:
+            return bytes([2, 3, 0, 0])                      # MSS of the wrong length
+        if r < 0.85:
+            return bytes([3, 4, 0, 0])                      # window scale of the wrong length
+        if r < 0.9:
+            return bytes([9, 40]) + rb(2)                   # longer than data offset
+        return rb(int(rng.integers(1, 20)))
+
+    def ipv4(payload, proto):
+        ihl = 5 if rng.random() < 0.8 else int(rng.integers(5, 8))
+        hdr_opts = rb(4 * (ihl - 5))
+        total = 4 * ihl + len(payload)
+        if rng.random() < 0.05:
+            total += int(rng.integers(-3, 4))
+        ver = 4 if rng.random() < 0.95 else int(rng.integers(0, 16))
+        h = bytes([(ver << 4) | ihl, 0, (total >> 8) & 255, total & 255]) + rb(4) + \
+            bytes([64, proto]) + rb(2) + rb(8) + hdr_opts
+        return h + payload
+
+    def ipv6(payload, proto):
+        body = payload
+        nh = proto
+        r = rng.random()
+        if r < 0.2:                                       # one extension header
+            hl = int(rng.integers(0, 12))
+            nxt = proto if rng.random() < 0.85 else int(rng.choice([0, 43, 60]))
+            body = bytes([nxt, hl]) + rb(6 + hl) + payload
+            nh = int(rng.choice([0, 43, 44, 60]))
+        elif r < 0.25:
+            nh = 59
+            body = b"" if rng.random() < 0.5 else rb(4)
+        plen = len(body)
+        if rng.random() < 0.05:
+            plen = 0 if rng.random() < 0.5 else plen + 1
+        ver = 6 if rng.random() < 0.95 else int(rng.integers(0, 16))
+        return bytes([(ver << 4), 0, 0, 0, (plen >> 8) & 255, plen & 255, nh, 64]) + rb(32) + body
+
+    def l4(v6):
+        r = rng.random()
+        if r < 0.6:
+            return 6, tcp(options())
+        if r < 0.8:
+            return 17, rb(int(rng.integers(8, 40)))
+        if r < 0.95:
+            return (58 if v6 and rng.random() < 0.7 else 1), rb(int(rng.integers(4, 40)))
+        return int(rng.integers(0, 256)), rb(int(rng.integers(0, 30)))
+
+    frames = []
+    for _ in range(n):
+        r = rng.random()
+        eth = rb(12)
+        if r < 0.45:
+            p, pl = l4(False)
+            l3 = b"\x08\x00" + ipv4(pl, p)
+        elif r < 0.75:
+            p, pl = l4(True)
+            l3 = b"\x86\xdd" + ipv6(pl, p)
+        elif r < 0.85:
+            hs, ps = int(rng.integers(0, 9)), int(rng.integers(0, 17))
+            body = bytes([0, 1, 8, 0, hs, ps]) + rb(2) + rb(2 * hs + 2 * ps)
+            if rng.random() < 0.3:
+                body = body[:int(rng.integers(0, len(body) + 1))] + rb(int(rng.integers(0, 3)))
+            l3 = b"\x08\x06" + body
+        elif r < 0.9:
+            l3 = rb(2) + rb(int(rng.integers(0, 60)))
+        else:
+            l3 = rb(int(rng.integers(0, 80)))
+        frame = bytes([0x08, 0, 0, 0]) + rb(3) + b"\0" + eth + l3
+        if rng.random() < 0.1:
+            frame = frame[:int(rng.integers(0, len(frame) + 1))]
+        frames.append(frame)
+    return frames

@@ -25,6 +25,7 @@ def lib():
         L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
         L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
+        L.ic_packets.argtypes = [vp, vp, C.c_int64, C.c_int, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
         L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
         _lib = L
@@ -94,3 +95,24 @@ def dns(pairs, group_arr, ng, qblob, qoff):
                       P(kind), P(val))
     assert rc == 0, rc
     return kind, val
+
+
+def packets(frames, layer):
+    """the device parse_packet run on the host: list of dicts like
+    oracle_ffi.parse_packet"""
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.uint32)
+    off[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(frames) or b"\0", np.uint8).copy()
+    n = len(frames)
+    f = np.zeros((n, 8), np.int32)
+    a = np.zeros((n, 32), np.uint8)
+    assert lib().ic_packets(P(blob), P(off), n, layer, P(f), P(a)) == 0
+    out = []
+    for i in range(n):
+        w = 16 if f[i, 1] == 6 else 4
+        out.append({"status": int(f[i, 0]), "l3": int(f[i, 1]), "l4": int(f[i, 2]),
+                    "proto": int(f[i, 3]), "vni": int(np.uint32(f[i, 4])),
+                    "ether_type": int(f[i, 5]), "sport": int(f[i, 6]), "dport": int(f[i, 7]),
+                    "src": bytes(a[i, :w]).hex(), "dst": bytes(a[i, 16:16 + w]).hex()})
+    return out

@@ -10,6 +10,7 @@
 #include "../../vproxy_amd/csrc/compile/compile.hpp"
 #include "../../vproxy_amd/csrc/device/acl_dev.h"
 #include "../../vproxy_amd/csrc/device/hint_dev.h"
+#include "../../vproxy_amd/csrc/device/packet_dev.h"
 #include "../../vproxy_amd/csrc/device/route_dev.h"
 
 using namespace vcd;
@@ -163,6 +164,21 @@ int ic_dns(const char* const* keys, const int32_t* key_lens, const int32_t* valu
             dns_one(hosts, img, &img, st.src, qn, &k2, &v2);
             if (k2 != kind[i] || v2 != value[i]) return -103;
         }
+    }
+    return 0;
+}
+
+// the kernels' parse_packet on the host: 8 ints + 32 address bytes per frame
+int ic_packets(const uint8_t* blob, const uint32_t* off, int64_t n, int layer, int32_t* fields,
+               uint8_t* addrs) {
+    for (int64_t i = 0; i < n; ++i) {
+        PktOut o;
+        parse_packet(blob + off[i], int(off[i + 1] - off[i]), layer, &o);
+        int32_t* f = fields + 8 * i;
+        f[0] = o.status; f[1] = o.l3; f[2] = o.l4; f[3] = o.proto;
+        f[4] = int32_t(o.vni); f[5] = o.ether_type; f[6] = o.sport; f[7] = o.dport;
+        std::memcpy(addrs + 32 * i, o.src, 16);
+        std::memcpy(addrs + 32 * i + 16, o.dst, 16);
     }
     return 0;
 }

@@ -49,6 +49,12 @@ class VoServer(C.Structure):
                 ("weight", C.c_int32), ("healthy", C.c_int32)]
 
 
+class VoPkt(C.Structure):
+    _fields_ = [("status", C.c_int), ("l3", C.c_int), ("l4", C.c_int), ("proto", C.c_int),
+                ("vni", C.c_uint32), ("ether_type", C.c_int), ("src", C.c_uint8 * 16),
+                ("dst", C.c_uint8 * 16), ("sport", C.c_int), ("dport", C.c_int)]
+
+
 class VoHosts(C.Structure):
     _fields_ = [("keys", C.POINTER(C.c_char_p)), ("key_lens", C.POINTER(C.c_int32)),
                 ("values", C.POINTER(C.c_int32)), ("n", C.c_int)]
@@ -100,6 +106,7 @@ def lib():
                                       P(C.c_int32)]
         L.vo_hosts_parse.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p,
                                      C.c_int, u8p, i32p, C.c_int]
+        L.vo_parse_packet.argtypes = [u8p, C.c_int, C.c_int, P(VoPkt)]
         L.vo_source_hash.argtypes = [u8p, C.c_int]
         L.vo_source_hash.restype = C.c_int32
         L.vo_source_list.argtypes = [P(VoServer), C.c_int, C.c_int, i32p]
@@ -474,3 +481,14 @@ def source_list(servers, view):
 def source_select(servers, view, src):
     arr = servers_arr(servers)
     return lib().vo_source_select(arr, len(servers), view, _u8(bytes(src)), len(src))
+
+
+# ---- packet header extraction (base/src/main/java/vpacket) ----
+def parse_packet(b, layer):
+    """-> dict of the oracle's fields (src/dst as hex of 4 or 16 bytes)"""
+    o = VoPkt()
+    lib().vo_parse_packet(_u8(bytes(b)), len(b), layer, C.byref(o))
+    n = 16 if o.l3 == 6 else 4
+    return {"status": o.status, "l3": o.l3, "l4": o.l4, "proto": o.proto, "vni": o.vni,
+            "ether_type": o.ether_type, "src": bytes(o.src[:n]).hex(),
+            "dst": bytes(o.dst[:n]).hex(), "sport": o.sport, "dport": o.dport}

@@ -16,6 +16,7 @@ PROTO_TCP, PROTO_UDP = 6, 17
 DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE = 1, 2, 3, 4, 5
 COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP = 0, 1, 2
 SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6 = 0, 4, 6
+LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6 = 0, 1, 4, 6
 
 
 class VcNet(C.Structure):
@@ -35,6 +36,13 @@ class VcAnnos(C.Structure):
 
 class VcGroupAnnos(C.Structure):
     _fields_ = [("handle", VcAnnos), ("group", VcAnnos)]
+
+
+class VcPktOut(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("l3", C.c_void_p), ("l4", C.c_void_p),
+                ("proto", C.c_void_p), ("vni", C.c_void_p), ("ether_type", C.c_void_p),
+                ("src4", C.c_void_p), ("dst4", C.c_void_p), ("src6", C.c_void_p),
+                ("dst6", C.c_void_p), ("sport", C.c_void_p), ("dport", C.c_void_p)]
 
 
 class VcServer(C.Structure):
@@ -129,6 +137,8 @@ def lib():
             getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp, vp]
         for f in ("vc_source_select_v4", "vc_source_select_v6"):
             getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp]
+        L.vc_parse_packets_dev.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut), vp]
+        L.vc_parse_packets.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut)]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

@@ -18,8 +18,8 @@ import ipaddress
 import numpy as np
 
 from . import _lib
-from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, VcServer, check,
-                   lib)
+from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, VcPktOut,
+                   VcServer, check, lib)
 
 HINT_HOST = "vproxy/hint-host"   # AnnotationKeys.ServerGroup_HintHost
 HINT_PORT = "vproxy/hint-port"   # AnnotationKeys.ServerGroup_HintPort
@@ -509,6 +509,39 @@ class Classifier:
                                           _stream(), C.c_void_p(kernel_done_event)
                                           if kernel_done_event else None))
         return outs
+
+    # ---------------- header extraction ----------------
+    _PKT_FIELDS = (("status", 1, "u8"), ("l3", 1, "u8"), ("l4", 1, "u8"), ("proto", 1, "u8"),
+                   ("vni", 1, "u32"), ("ether_type", 1, "u16"), ("src4", 1, "u32"),
+                   ("dst4", 1, "u32"), ("src6", 16, "u8"), ("dst6", 16, "u8"),
+                   ("sport", 1, "u16"), ("dport", 1, "u16"))
+
+    def parse_packets(self, frames, layer=0):
+        """VXLanPacket/EthernetPacket/Ipv4Packet/Ipv6Packet.from over a batch
+        of raw frames: a list of bytes (host path) or (blob, off) torch
+        tensors (device path).  Returns a dict of arrays (vclassify.h
+        vc_pkt_out); src6/dst6 are n x 16."""
+        if isinstance(frames, tuple) and _is_dev(frames[0]):
+            import torch
+            blob, off = frames
+            n = len(off) - 1
+            tdt = {"u8": torch.uint8, "u16": torch.int16, "u32": torch.int32}
+            res = {k: torch.empty((n, w) if w > 1 else (n,), dtype=tdt[t], device=blob.device)
+                   for k, w, t in self._PKT_FIELDS}
+            o = VcPktOut(**{k: v.data_ptr() for k, v in res.items()})
+            check(lib().vc_parse_packets_dev(self.h, _ptr(blob), _ptr(off), n, int(layer),
+                                             C.byref(o), _stream()))
+            return res
+        lens = np.array([len(f) for f in frames], np.int64)
+        off = np.zeros(len(frames) + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        blob = np.frombuffer(b"".join(bytes(f) for f in frames) or b"\0", np.uint8).copy()
+        n = len(frames)
+        ndt = {"u8": np.uint8, "u16": np.uint16, "u32": np.uint32}
+        res = {k: np.zeros((n, w) if w > 1 else (n,), ndt[t]) for k, w, t in self._PKT_FIELDS}
+        o = VcPktOut(**{k: v.ctypes.data for k, v in res.items()})
+        check(lib().vc_parse_packets(self.h, _ptr(blob), _ptr(off), n, int(layer), C.byref(o)))
+        return res
 
     # ---------------- ServerGroup source hashing ----------------
     def compile_servers(self, groups):

@@ -665,6 +665,67 @@ int vc_source_select_v6(vc_ctx* ctx, const int32_t* group, const uint8_t* src6, 
 }
 
 // ---------------------------------------------------------------------------
+// Header extraction
+// ---------------------------------------------------------------------------
+int vc_parse_packets_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
+                         int layer, const vc_pkt_out* out, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!blob || !off || !out))) return fail(VC_EINVAL, "bad batch arguments");
+    if (layer != VC_LAYER_VXLAN && layer != VC_LAYER_ETHER && layer != VC_LAYER_IPV4 &&
+        layer != VC_LAYER_IPV6)
+        return fail(VC_EINVAL, "layer must be VC_LAYER_VXLAN, _ETHER, _IPV4 or _IPV6");
+    if (n > 0 && ((reinterpret_cast<uintptr_t>(out->src6) & 15) ||
+                  (reinterpret_cast<uintptr_t>(out->dst6) & 15)))
+        return fail(VC_EINVAL, "src6/dst6 must be 16-byte aligned");
+    hipError_t e = vc::launch_packets(ctx->cfg(stream), blob, off, n, layer, *out);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "packet launch");
+}
+
+int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                     const vc_pkt_out* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!blob || !off || !out) return fail(VC_EINVAL, "bad batch arguments");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
+    auto* doff = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
+    vc_pkt_out d{};
+    const size_t un = size_t(n);
+    d.status = static_cast<uint8_t*>(st.out(out->status, un));
+    d.l3 = static_cast<uint8_t*>(st.out(out->l3, un));
+    d.l4 = static_cast<uint8_t*>(st.out(out->l4, un));
+    d.proto = static_cast<uint8_t*>(st.out(out->proto, un));
+    d.vni = static_cast<uint32_t*>(st.out(out->vni, un * 4));
+    d.ether_type = static_cast<uint16_t*>(st.out(out->ether_type, un * 2));
+    d.src4 = static_cast<uint32_t*>(st.out(out->src4, un * 4));
+    d.dst4 = static_cast<uint32_t*>(st.out(out->dst4, un * 4));
+    d.src6 = static_cast<uint8_t*>(st.out(out->src6, un * 16));
+    d.dst6 = static_cast<uint8_t*>(st.out(out->dst6, un * 16));
+    d.sport = static_cast<uint16_t*>(st.out(out->sport, un * 2));
+    d.dport = static_cast<uint16_t*>(st.out(out->dport, un * 2));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_parse_packets_dev(ctx, db, doff, n, layer, &d, s);
+    if (rc) return rc;
+    st.back(out->status, d.status, un, s);
+    st.back(out->l3, d.l3, un, s);
+    st.back(out->l4, d.l4, un, s);
+    st.back(out->proto, d.proto, un, s);
+    st.back(out->vni, d.vni, un * 4, s);
+    st.back(out->ether_type, d.ether_type, un * 2, s);
+    st.back(out->src4, d.src4, un * 4, s);
+    st.back(out->dst4, d.dst4, un * 4, s);
+    st.back(out->src6, d.src6, un * 16, s);
+    st.back(out->dst6, d.dst6, un * 16, s);
+    st.back(out->sport, d.sport, un * 2, s);
+    st.back(out->dport, d.dport, un * 2, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "parse packets");
+}
+
+// ---------------------------------------------------------------------------
 // Pipeline
 // ---------------------------------------------------------------------------
 int vc_pipeline_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,

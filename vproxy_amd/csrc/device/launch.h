@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../common/images.h"
+#include "vclassify.h"
 
 namespace vc {
 
@@ -59,6 +60,11 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
 // 6: 16-byte addresses (16-byte aligned); view = VC_SOURCE_*.
 hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32_t* group,
                          const void* src, int family, int64_t n, int view, int32_t* out);
+
+// Header extraction (packet.hip); out arrays are device pointers, src6/dst6
+// 16-byte aligned.
+hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_t* off, int64_t n,
+                          int layer, const vc_pkt_out& out);
 
 // Large counter spaces (counters.hip): bucket partition + per-bucket LDS
 // histograms, split so a producer kernel (the pipeline) can supply the
