@@ -317,6 +317,40 @@ int vc_counters_add_dev(vc_ctx *ctx, int kind, const int32_t *out, const uint8_t
                         int64_t n, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* Prometheus text exposition                       */
+/* ------------------------------------------------------------------------ */
+/* Text functions write NUL-terminated text into (buf, cap) and set *len to
+ * its length; VC_ENOMEM (and *len = the length needed) when cap <= *len.    */
+#define VC_METRIC_COUNTER 0   /* prometheus/Counter.java */
+#define VC_METRIC_GAUGE   1   /* prometheus/Gauge.java */
+typedef struct vc_metric {
+    const char *metric;
+    int32_t type;                    /* VC_METRIC_* */
+    int32_t n_labels;                /* a repeated key: the later value wins */
+    const char *const *label_keys;
+    const char *const *label_values; /* raw; quoted as Metric's constructor does */
+    int64_t value;
+} vc_metric;
+/* Metrics.toString (prometheus/Metrics.java:27-64): metrics given in
+ * creation order, help messages as registerHelpMessage (later wins). */
+int vc_prometheus_format(const vc_metric *metrics, int32_t n, const char *const *help_metric,
+                         const char *const *help_text, int32_t n_help, char *buf, int64_t cap,
+                         int64_t *len);
+/* The hit counters of the VC_COUNTERS_* layouts above (host arrays; NULL
+ * skips a kind) as security_group_rule_hit_count{protocol,rule},
+ * route_table_rule_hit_count{family,rule} and
+ * upstream_server_group_hit_count{group}, each added through the rules of
+ * GlobalInspection.addMetric (GlobalInspection.java:118-125) with
+ * `extra_labels` parsed as getExtraLabels (GlobalInspection.java:95-116):
+ * "k1=v1,k2=v2"; VC_EINVAL for a piece without '='. */
+int vc_prometheus_hits(const uint64_t *acl, int n_tcp, int n_udp, const uint64_t *route, int n4,
+                       int n6, const uint64_t *group, int n_groups, const char *extra_labels,
+                       char *buf, int64_t cap, int64_t *len);
+/* Same over the context's current device counters (synchronises). */
+int vc_counters_prometheus(vc_ctx *ctx, const char *extra_labels, char *buf, int64_t cap,
+                           int64_t *len);
+
+/* ------------------------------------------------------------------------ */
 /* Control-plane mirrors (host only, no GPU): the reference's list-ordering  */
 /* and validation rules, so a caller can keep the exact Java list order.    */
 /* ------------------------------------------------------------------------ */

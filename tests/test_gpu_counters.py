@@ -130,3 +130,24 @@ def test_pipeline_counts_in_kernel(clf, n, off):
     want, _ = O.sg_batch_v4_np(tcp, udp, False, proto[s], src[s], port[s])
     np.testing.assert_array_equal(acl[s], want)
     np.testing.assert_array_equal(route[s], O.rt_batch_v4_np(W.v4_nets(net, plen), dst[s]))
+
+
+def test_counters_prometheus(clf):
+    """vc_counters_prometheus renders the device counters exactly as
+    vc_prometheus_hits renders the same counters read back to the host."""
+    import torch
+    from vproxy_amd import prometheus as P
+    nt, nu, n4, ng = _compile(clf)
+    rng = np.random.default_rng(11)
+    clf.counters_reset()
+    val = rng.integers(-1, ng, 100_000).astype(np.int32)
+    clf.counters_add(V.COUNTERS_GROUP, torch.from_numpy(val).cuda())
+    torch.cuda.synchronize()
+    text = clf.counters_prometheus("zone=eu")
+    want = P.hits_text(acl=clf.counters_read(V.COUNTERS_ACL), n_tcp=nt, n_udp=nu,
+                       route=clf.counters_read(V.COUNTERS_ROUTE), n4=n4, n6=0,
+                       group=clf.counters_read(V.COUNTERS_GROUP), n_groups=ng,
+                       extra_labels="zone=eu")
+    assert text == want
+    assert ('upstream_server_group_hit_count{group="none",zone="eu"} %d\n'
+            % int((val < 0).sum())) in text

@@ -50,6 +50,15 @@ class VcServer(C.Structure):
                 ("weight", C.c_int32), ("healthy", C.c_int32)]
 
 
+class VcMetric(C.Structure):
+    _fields_ = [("metric", C.c_char_p), ("type", C.c_int32), ("n_labels", C.c_int32),
+                ("label_keys", C.POINTER(C.c_char_p)), ("label_values", C.POINTER(C.c_char_p)),
+                ("value", C.c_int64)]
+
+
+METRIC_COUNTER, METRIC_GAUGE = 0, 1
+
+
 # ---- exceptions mirroring the reference's (vproxybase.util.exception.*) ----
 class VcError(Exception):
     code = None
@@ -144,6 +153,11 @@ def lib():
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]
         L.vc_counters_reset.argtypes = [vp]
         L.vc_counters_add_dev.argtypes = [vp, i32, vp, vp, i32, i64, vp]
+        cpp = P(C.c_char_p)
+        L.vc_prometheus_format.argtypes = [P(VcMetric), i32, cpp, cpp, i32, vp, i64, P(i64)]
+        L.vc_prometheus_hits.argtypes = [vp, i32, i32, vp, i32, i32, vp, i32, C.c_char_p, vp, i64,
+                                         P(i64)]
+        L.vc_counters_prometheus.argtypes = [vp, C.c_char_p, vp, i64, P(i64)]
         L.vc_secgroup_new.argtypes = [C.c_char_p, i32, P(vp)]
         L.vc_secgroup_free.argtypes = [vp]
         L.vc_secgroup_set_default.argtypes = [vp, i32]

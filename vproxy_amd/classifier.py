@@ -593,6 +593,12 @@ class Classifier:
     def counters_reset(self):
         check(lib().vc_counters_reset(self.h))
 
+    def counters_prometheus(self, extra_labels=None):
+        """The current hit counters as Prometheus text (vc_counters_prometheus)."""
+        from .prometheus import _b as pb, _call_text
+        return _call_text(lib().vc_counters_prometheus, self.h,
+                          None if extra_labels is None else pb(extra_labels))
+
     def counters_add(self, kind, out, aux=None, family=4):
         """Explicit counting pass over a device output array (torch tensor)."""
         check(lib().vc_counters_add_dev(self.h, kind, _ptr(out), _ptr(aux), family, len(out),

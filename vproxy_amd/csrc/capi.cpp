@@ -14,6 +14,7 @@
 #include "device/launch.h"
 #include "host/mirror.hpp"
 #include "host/net.hpp"
+#include "host/prometheus.hpp"
 #include "vclassify.h"
 
 namespace {
@@ -854,6 +855,81 @@ int vc_counters_add_dev(vc_ctx* ctx, int kind, const int32_t* out, const uint8_t
         return fail(VC_EINVAL, "unknown counter kind");
     }
     return e == hipSuccess ? VC_OK : hip_fail(e, "counter pass");
+}
+
+// ---------------------------------------------------------------------------
+// Prometheus text (host/prometheus.cpp)
+// ---------------------------------------------------------------------------
+static int text_out(const std::string& text, char* buf, int64_t cap, int64_t* len) {
+    int rc = vc::copy_text(text, buf, cap, len);
+    return rc == VC_OK ? rc : fail(rc, "buffer too small for the exposition text");
+}
+
+int vc_prometheus_format(const vc_metric* metrics, int32_t n, const char* const* help_metric,
+                         const char* const* help_text, int32_t n_help, char* buf, int64_t cap,
+                         int64_t* len) {
+    if (n < 0 || n_help < 0 || (n && !metrics) || (n_help && (!help_metric || !help_text)))
+        return fail(VC_EINVAL, "bad metric arrays");
+    std::vector<vc::PromMetric> ms;
+    ms.reserve(size_t(n));
+    for (int32_t i = 0; i < n; ++i) {
+        const vc_metric& m = metrics[i];
+        if (!m.metric || m.n_labels < 0 || (m.n_labels && (!m.label_keys || !m.label_values)))
+            return fail(VC_EINVAL, "bad metric " + std::to_string(i));
+        if (m.type != VC_METRIC_COUNTER && m.type != VC_METRIC_GAUGE)
+            return fail(VC_EINVAL, "unknown metric type");
+        vc::PromMetric p{m.metric, m.type == VC_METRIC_COUNTER ? "counter" : "gauge", {}, m.value};
+        for (int32_t k = 0; k < m.n_labels; ++k) {
+            if (!m.label_keys[k] || !m.label_values[k]) return fail(VC_EINVAL, "null label");
+            p.labels[m.label_keys[k]] = m.label_values[k];
+        }
+        ms.push_back(std::move(p));
+    }
+    std::map<std::string, std::string> help;
+    for (int32_t i = 0; i < n_help; ++i) {
+        if (!help_metric[i] || !help_text[i]) return fail(VC_EINVAL, "null help message");
+        help[help_metric[i]] = help_text[i];
+    }
+    return text_out(vc::prometheus_text(ms, help), buf, cap, len);
+}
+
+int vc_prometheus_hits(const uint64_t* acl, int n_tcp, int n_udp, const uint64_t* route, int n4,
+                       int n6, const uint64_t* group, int n_groups, const char* extra_labels,
+                       char* buf, int64_t cap, int64_t* len) {
+    if (n_tcp < 0 || n_udp < 0 || n4 < 0 || n6 < 0 || n_groups < 0)
+        return fail(VC_EINVAL, "negative counter size");
+    std::map<std::string, std::string> extra;
+    if (vc::parse_extra_labels(extra_labels, &extra) != VC_OK)
+        return fail(VC_EINVAL, "invalid format, expecting k=v");
+    std::vector<vc::PromMetric> ms;
+    std::map<std::string, std::string> help;
+    vc::hit_metrics(acl, n_tcp, n_udp, route, n4, n6, group, n_groups, extra, &ms, &help);
+    return text_out(vc::prometheus_text(ms, help), buf, cap, len);
+}
+
+int vc_counters_prometheus(vc_ctx* ctx, const char* extra_labels, char* buf, int64_t cap,
+                           int64_t* len) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    auto a = ctx->get(ctx->acl);
+    auto r = ctx->get(ctx->route);
+    auto h = ctx->get(ctx->hint);
+    std::vector<uint64_t> ha, hr, hg;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    auto fetch = [&](const Snapshot* s, std::vector<uint64_t>* v) {
+        if (!s || e != hipSuccess) return;
+        v->resize(size_t(std::max<int64_t>(s->n_counters, 1)));
+        e = hipMemcpy(v->data(), s->counters, size_t(s->n_counters) * 8, hipMemcpyDeviceToHost);
+    };
+    fetch(a.get(), &ha);
+    fetch(r.get(), &hr);
+    fetch(h.get(), &hg);
+    if (e != hipSuccess) return hip_fail(e, "counter read");
+    return vc_prometheus_hits(a ? ha.data() : nullptr, a ? a->img.n_tcp : 0, a ? a->img.n_udp : 0,
+                              r ? hr.data() : nullptr, r ? r->n4 : 0, r ? r->n6 : 0,
+                              h ? hg.data() : nullptr, h ? h->img.n_groups : 0, extra_labels, buf,
+                              cap, len);
 }
 
 // ---------------------------------------------------------------------------
