@@ -177,6 +177,26 @@ int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int
                     uint8_t *out_kind, int32_t *out_value);
 
 /* ------------------------------------------------------------------------ */
+/* TLS certificate choice by SNI (SSLContextHolder.java:47-186)             */
+/* ------------------------------------------------------------------------ */
+/* Replaces SSLContextHolder.add(ctx, certs) for a whole holder list: holder
+ * h (add() order, 0..n_holders-1) lists the names of its certificates --
+ * each certificate's subject CN (if any) and its SAN dNSNames (type 2) --
+ * as names[i] with holder[i] == h; order within a holder is irrelevant.  A
+ * name "*.S" is a wildcard (compare(), :171-186).  Names are raw bytes,
+ * compared case-sensitively as Java's String.equals/endsWith do. */
+int vc_compile_certs(vc_ctx *ctx, const char *const *names, const int32_t *name_lens,
+                     const int32_t *holder, int n_names, int n_holders);
+/* SSLContextHolder.choose(sni) per SNI (:51-63): the holder index; 0 (the
+ * default first holder) for one holder, a null SNI (sni_null[i] != 0) or no
+ * match; -1 (null) when there are no holders.  SNIs as blob + uint32
+ * offsets (n + 1 entries); sni_null may be NULL.  Device pointers. */
+int vc_cert_choose_dev(vc_ctx *ctx, const uint8_t *sni_blob, const uint32_t *sni_off,
+                       const uint8_t *sni_null, int64_t n, int32_t *out_holder, void *stream);
+int vc_cert_choose(vc_ctx *ctx, const uint8_t *sni_blob, const uint32_t *sni_off,
+                   const uint8_t *sni_null, int64_t n, int32_t *out_holder);
+
+/* ------------------------------------------------------------------------ */
 /* Combined per-packet pipeline: ACL -> route -> host      */
 /* ------------------------------------------------------------------------ */
 /* For each IPv4 packet: out_acl = SecurityGroup.allow index on (proto, src,

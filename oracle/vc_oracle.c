@@ -1186,3 +1186,38 @@ void vo_parse_packet(const uint8_t *p, int len, int layer, vo_pkt *out) {
         if (out->status == 1) out->vni = 0;
     }
 }
+
+/* ------------------------------------------------------------------------
+ * SSLContextHolder.choose / chooseNoDefault / checkSNI / compare
+ * (SSLContextHolder.java:51-186), restated as the literal scan: holders in
+ * add() order, each holder's names in order, first holder with a match.
+ * The quickAccess cache (:68-72, :111, :163) only memoises that scan's
+ * result for an SNI; holders are only ever appended, so a memoised answer
+ * equals a fresh scan and the cache is omitted.
+ * ------------------------------------------------------------------------ */
+static int cert_compare(const char *dns, int dl, const uint8_t *sni, int sl) {
+    if (dl >= 2 && dns[0] == '*' && dns[1] == '.') {     /* wildcard record, :172-181 */
+        const char *suffix = dns + 1;                     /* dnsName.substring(1) */
+        int xl = dl - 1;
+        if (sl > xl && memcmp(sni + sl - xl, suffix, (size_t)xl) == 0) {
+            for (int i = 0; i < sl - xl; ++i)             /* !prefix.contains(".") */
+                if (sni[i] == '.') return 0;
+            return 1;
+        }
+        return 0;
+    }
+    return sl == dl && (dl == 0 || memcmp(sni, dns, (size_t)dl) == 0);  /* equals, :184 */
+}
+
+int vo_cert_choose(const char *const *names, const int32_t *name_lens, const int32_t *holder,
+                   int n_names, int n_holders, const uint8_t *sni, int sni_len, int sni_null) {
+    if (n_holders == 1) return 0;                         /* :53-55 */
+    if (n_holders == 0) return -1;                        /* :56-58 */
+    if (!sni_null) {                                      /* chooseNoDefault, :67-79 */
+        for (int h = 0; h < n_holders; ++h)
+            for (int i = 0; i < n_names; ++i)
+                if (holder[i] == h && cert_compare(names[i], name_lens[i], sni, sni_len))
+                    return h;
+    }
+    return 0;                                             /* the default (first) one, :62 */
+}

@@ -188,6 +188,14 @@ typedef struct {
 
 void vo_parse_packet(const uint8_t *p, int len, int layer, vo_pkt *out);
 
+/* ---- SSLContextHolder.choose (base/src/main/java/vproxybase/util/ringbuffer/ssl/
+ *      SSLContextHolder.java:51-186) ----
+ * Holders 0..n_holders-1 in add() order; names[i] (length name_lens[i]) is a
+ * CN or SAN dNSName of a certificate of holder[i], in the holder's own
+ * certificate order.  Returns the chosen holder, or -1 (null, no holders). */
+int vo_cert_choose(const char *const *names, const int32_t *name_lens, const int32_t *holder,
+                   int n_names, int n_holders, const uint8_t *sni, int sni_len, int sni_null);
+
 #ifdef __cplusplus
 }
 #endif

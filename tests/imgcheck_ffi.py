@@ -25,6 +25,7 @@ def lib():
         L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
         L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
+        L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
         L.ic_packets.argtypes = [vp, vp, C.c_int64, C.c_int, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
         L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
@@ -115,4 +116,24 @@ def packets(frames, layer):
                     "proto": int(f[i, 3]), "vni": int(np.uint32(f[i, 4])),
                     "ether_type": int(f[i, 5]), "sport": int(f[i, 6]), "dport": int(f[i, 7]),
                     "src": bytes(a[i, :w]).hex(), "dst": bytes(a[i, 16:16 + w]).hex()})
+    return out
+
+
+def certs(holders, snis):
+    """the device cert_one over a host-built certificate table; snis: list of
+    bytes/str/None"""
+    names = [s.encode() if isinstance(s, str) else s for hs in holders for s in hs]
+    hold = np.array([h for h, hs in enumerate(holders) for _ in hs] or [0], np.int32)
+    karr = (C.c_char_p * max(1, len(names)))(*names)
+    kl = np.array([len(k) for k in names] or [0], np.int32)
+    qs = [b"" if q is None else (q.encode() if isinstance(q, str) else q) for q in snis]
+    qnull = np.array([q is None for q in snis] or [0], np.uint8)
+    lens = np.array([len(q) for q in qs], np.int64)
+    qoff = np.zeros(len(qs) + 1, np.uint32)
+    qoff[1:] = np.cumsum(lens)
+    qb = np.frombuffer(b"".join(qs) or b"\0", np.uint8).copy()
+    out = np.empty(len(qs), np.int32)
+    rc = lib().ic_certs(karr, P(kl), P(hold), len(names), len(holders), P(qb), P(qoff), P(qnull),
+                        len(qs), P(out))
+    assert rc == 0, rc
     return out

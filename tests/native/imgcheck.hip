@@ -183,6 +183,31 @@ int ic_packets(const uint8_t* blob, const uint32_t* off, int64_t n, int layer, i
     return 0;
 }
 
+// SSLContextHolder.choose through the compiled certificate table, from a
+// plain pointer and from a staged copy at every word alignment.
+int ic_certs(const char* const* names, const int32_t* lens, const int32_t* holder, int nn,
+             int nh, const uint8_t* qb, const uint32_t* qo, const uint8_t* qnull, int64_t n,
+             int32_t* out) {
+    vc::HostsBuilt b;
+    int rc = vc::build_certs(names, lens, holder, nn, nh, &b);
+    if (rc) return rc;
+    CertImage c{};
+    c.names = HostsImage{b.blob.data(), b.table.recs.data(), b.table.tags.data(),
+                         uint32_t(b.table.tags.size() - 1), b.n};
+    c.n_holders = nh;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* q = qb + qo[i];
+        const int qn = int(qo[i + 1] - qo[i]);
+        const bool nul = qnull && qnull[i];
+        out[i] = cert_one(c, PtrSrc{q}, qn, nul);
+        for (int al = 0; al < 4; ++al) {
+            Staged st(q, qn, al);
+            if (cert_one(c, st.src, qn, nul) != out[i]) return -104;
+        }
+    }
+    return 0;
+}
+
 int ic_is_ipv6(const uint8_t* s, int n) { return d_is_ipv6(s, n) ? 1 : 0; }
 int ic_is_ip_literal(const uint8_t* s, int n) { return d_is_ip_literal(s, n) ? 1 : 0; }
 

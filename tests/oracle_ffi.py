@@ -111,6 +111,8 @@ def lib():
         L.vo_source_hash.restype = C.c_int32
         L.vo_source_list.argtypes = [P(VoServer), C.c_int, C.c_int, i32p]
         L.vo_source_select.argtypes = [P(VoServer), C.c_int, C.c_int, u8p, C.c_int]
+        L.vo_cert_choose.argtypes = [P(C.c_char_p), i32p, i32p, C.c_int, C.c_int, u8p, C.c_int,
+                                     C.c_int]
         _lib = L
     return _lib
 
@@ -492,3 +494,25 @@ def parse_packet(b, layer):
     return {"status": o.status, "l3": o.l3, "l4": o.l4, "proto": o.proto, "vni": o.vni,
             "ether_type": o.ether_type, "src": bytes(o.src[:n]).hex(),
             "dst": bytes(o.dst[:n]).hex(), "sport": o.sport, "dport": o.dport}
+
+
+# ---- SSLContextHolder.choose (SSLContextHolder.java:51-186) ----
+class Certs:
+    """holders: list (add() order) of name lists (CN + SAN dNSNames)."""
+
+    def __init__(self, holders):
+        self.n_holders = len(holders)
+        self.names = [_b(s) for hs in holders for s in hs]
+        hold = [h for h, hs in enumerate(holders) for _ in hs]
+        n = len(self.names)
+        self.karr = (C.c_char_p * max(1, n))(*self.names)
+        self.larr = (C.c_int32 * max(1, n))(*[len(k) for k in self.names])
+        self.harr = (C.c_int32 * max(1, n))(*hold)
+
+    def choose(self, sni):
+        if sni is None:
+            return lib().vo_cert_choose(self.karr, self.larr, self.harr, len(self.names),
+                                        self.n_holders, _u8(b""), 0, 1)
+        s = _b(sni)
+        return lib().vo_cert_choose(self.karr, self.larr, self.harr, len(self.names),
+                                    self.n_holders, _u8(s), len(s), 0)

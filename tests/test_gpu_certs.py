@@ -1,0 +1,71 @@
+"""GPU tier: SSLContextHolder.choose (device/hint.hip cert_kernel) through the
+C ABI against the oracle (vo_cert_choose, SSLContextHolder.java:51-186),
+bit-exact: the hand-derived vectors, random holder sets hitting every
+compare() branch, a large table (20k holders) with 200k SNIs from the
+staged (aligned) and unstaged (unaligned blob) kernels, and the 0/1-holder
+cases."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import vproxy_amd as V
+from test_certs_cpu import HOLDERS, VECTORS, _random_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def clf():
+    c = V.Classifier(0)
+    yield c
+    c.close()
+
+
+def test_vectors(clf):
+    clf.compile_certs(HOLDERS)
+    got = clf.cert_choose([s for s, _ in VECTORS])
+    np.testing.assert_array_equal(got, [w for _, w in VECTORS])
+
+
+@pytest.mark.parametrize("seed,n_holders", [(11, 0), (12, 1), (13, 5), (14, 300)])
+def test_random_vs_oracle(clf, seed, n_holders):
+    holders, snis = _random_case(np.random.default_rng(seed), n_holders, 20000)
+    clf.compile_certs(holders)
+    got = clf.cert_choose(snis)
+    c = O.Certs(holders)
+    want = np.array([c.choose(s) for s in snis], np.int32)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_large_table_device_paths(clf):
+    import torch
+    from vproxy_amd import workloads as W
+    rng = np.random.default_rng(15)
+    _, hosts = W.gen_groups(40000, 16, wildcard=False)
+    holders = []
+    for i in range(0, len(hosts), 2):           # 20k holders: CN + "*." SAN + a shared name
+        holders.append([hosts[i], "*." + hosts[i + 1], "shared%d.example" % (i % 97)])
+    clf.compile_certs(holders)
+    names = W.gen_hostnames(hosts, 200000, 17)
+    snis = [n.split(b":")[0] for n in names]
+    snis[::41] = [None] * len(snis[::41])
+    got = clf.cert_choose(snis)
+    c = O.Certs(holders)
+    samp = rng.integers(0, len(snis), 4000)
+    np.testing.assert_array_equal(got[samp], [c.choose(snis[i]) for i in samp])
+    assert (got > 0).mean() > 0.3                   # the table is really hit
+    blob, off, nul = V.pack_strings(snis)
+    for shift in (0, 1):                            # staged kernel / unaligned blob
+        b = np.concatenate([np.zeros(shift, np.uint8), blob])
+        db = torch.from_numpy(b).cuda()[shift:]
+        dev = clf.cert_choose((db, torch.from_numpy(off.astype(np.int32)).cuda(),
+                               torch.from_numpy(nul).cuda()))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy(), got)
+
+
+def test_errors(clf):
+    with pytest.raises(V.IllegalArgumentException):
+        V.check(V.lib().vc_compile_certs(clf.h, None, None, None, 1, 1))
+    clf.compile_certs([["a.com"], ["b.com"]])
+    assert clf.cert_choose([]).shape == (0,)

@@ -12,6 +12,6 @@ from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,
                    LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
                          acl_rule_array, group_array, net_array, pack_strings, parse_ip,
-                         server_array)
+                         server_array, cn_of_dn)
 
 __all__ = ["Classifier", "Network", "SecurityGroup", "RouteTable", "Annotations", "parse_ip"]

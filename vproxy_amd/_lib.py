@@ -146,6 +146,9 @@ def lib():
             getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp, vp]
         for f in ("vc_source_select_v4", "vc_source_select_v6"):
             getattr(L, f).argtypes = [vp, vp, vp, i64, i32, vp]
+        L.vc_compile_certs.argtypes = [vp, P(C.c_char_p), vp, vp, i32, i32]
+        L.vc_cert_choose_dev.argtypes = [vp, vp, vp, vp, i64, vp, vp]
+        L.vc_cert_choose.argtypes = [vp, vp, vp, vp, i64, vp]
         L.vc_parse_packets_dev.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut), vp]
         L.vc_parse_packets.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut)]
         L.vc_counters_enable.argtypes = [vp, i32]

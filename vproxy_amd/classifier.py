@@ -309,6 +309,15 @@ def server_array(groups):
     return arr, off
 
 
+def cn_of_dn(dn):
+    """The CN of an RFC 2253 subject name as checkSNI takes it: the first
+    comma-separated piece starting with "CN=" (SSLContextHolder.java:89-104)."""
+    for s in dn.split(","):
+        if s.startswith("CN="):
+            return s[3:]
+    return None
+
+
 def _is_dev(x):
     return x is not None and hasattr(x, "is_cuda") and x.is_cuda
 
@@ -572,6 +581,36 @@ class Classifier:
         out = np.empty(n, np.int32)
         f = lib().vc_source_select_v6 if v6 else lib().vc_source_select_v4
         check(f(self.h, _ptr(group), _ptr(src), n, int(view), _ptr(out)))
+        return out
+
+    # ---------------- TLS certificate choice by SNI ----------------
+    def compile_certs(self, holders):
+        """SSLContextHolder.add for every holder in order (SSLContextHolder.java:47-49):
+        holders = list of name lists, each the CNs and SAN dNSNames of the
+        holder's certificates (see cn_of_dn)."""
+        names = [_b(s) for hs in holders for s in hs]
+        hold = np.array([h for h, hs in enumerate(holders) for _ in hs] or [0], np.int32)
+        karr = (C.c_char_p * max(1, len(names)))(*names)
+        lens = np.array([len(s) for s in names] or [0], np.int32)
+        check(lib().vc_compile_certs(self.h, karr, _ptr(lens), _ptr(hold), len(names),
+                                     len(holders)))
+
+    def cert_choose(self, snis):
+        """Batched SSLContextHolder.choose(sni) -> holder index (-1: no holders).
+        snis: list of str/bytes/None, or a packed (blob, off, null) tuple of
+        torch CUDA tensors (device path)."""
+        if isinstance(snis, tuple) and _is_dev(snis[0]):
+            import torch
+            b, o, nul = snis
+            n = len(o) - 1
+            out = torch.empty(n, dtype=torch.int32, device=b.device)
+            check(lib().vc_cert_choose_dev(self.h, _ptr(b), _ptr(o), _ptr(nul), n, _ptr(out),
+                                           _stream()))
+            return out
+        n = len(snis)
+        b, o, nul = pack_strings(snis)
+        out = np.empty(n, np.int32)
+        check(lib().vc_cert_choose(self.h, _ptr(b), _ptr(o), _ptr(nul), n, _ptr(out)))
         return out
 
     # ---------------- counters ----------------

@@ -84,6 +84,9 @@ struct HintSnap : Snapshot {
 struct HostsSnap : Snapshot {
     HostsImage img{};
 };
+struct CertSnap : Snapshot {
+    CertImage img{};
+};
 struct ServerSnap : Snapshot {
     ServerImage img{};
     uint8_t* healthy = nullptr;    // device copy, updated in place (vc_servers_set_health)
@@ -103,6 +106,7 @@ struct vc_ctx {
     std::shared_ptr<const HintSnap> hint;
     std::shared_ptr<const HostsSnap> hosts;
     std::shared_ptr<const ServerSnap> servers;
+    std::shared_ptr<const CertSnap> certs;
 
     template <class S>
     std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
@@ -216,6 +220,7 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->hint.reset();
     ctx->hosts.reset();
     ctx->servers.reset();
+    ctx->certs.reset();
     (void)hipStreamDestroy(ctx->stream);
     if (ctx->pool) {
         // batches may still run on callers' streams: their scratch is freed
@@ -573,6 +578,65 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
     st.back(out_value, dv, size_t(n) * 4, s);
     hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
     return e == hipSuccess ? VC_OK : hip_fail(e, "dns classify");
+}
+
+// ---------------------------------------------------------------------------
+// SSLContextHolder certificate choice by SNI
+// ---------------------------------------------------------------------------
+int vc_compile_certs(vc_ctx* ctx, const char* const* names, const int32_t* name_lens,
+                     const int32_t* holder, int n_names, int n_holders) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n_names < 0 || n_holders < 0 || (n_names && (!names || !name_lens || !holder)))
+        return fail(VC_EINVAL, "bad certificate name arrays");
+    vc::HostsBuilt b;
+    if ((rc = vc::build_certs(names, name_lens, holder, n_names, n_holders, &b)) != VC_OK)
+        return fail(rc, "invalid certificate name or holder index");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<CertSnap>();
+    hipError_t e = hipSuccess;
+    s->img.names.blob = s->upload(b.blob, &e);
+    s->img.names.recs = s->upload(b.table.recs, &e);
+    s->img.names.tags = s->upload(b.table.tags, &e);
+    s->img.names.mask = static_cast<uint32_t>(b.table.tags.size() - 1);
+    s->img.names.n = b.n;
+    s->img.n_holders = n_holders;
+    if (e != hipSuccess) return hip_fail(e, "certificate table upload");
+    ctx->publish(ctx->certs, std::shared_ptr<const CertSnap>(std::move(s)));
+    return VC_OK;
+}
+
+int vc_cert_choose_dev(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off,
+                       const uint8_t* sni_null, int64_t n, int32_t* out_holder, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!sni_blob || !sni_off || !out_holder)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto s = ctx->get(ctx->certs);
+    if (!s) return fail(VC_ESTATE, "no certificate holders compiled");
+    hipError_t e = vc::launch_certs(ctx->cfg(stream), s->img, sni_blob, sni_off, sni_null, n,
+                                    out_holder);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "cert launch");
+}
+
+int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off,
+                   const uint8_t* sni_null, int64_t n, int32_t* out_holder) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!sni_blob || !sni_off || !out_holder) return fail(VC_EINVAL, "bad batch arguments");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    auto* db = static_cast<uint8_t*>(st.in(sni_blob, sni_off[n], s));
+    auto* dof = static_cast<uint32_t*>(st.in(sni_off, size_t(n + 1) * 4, s));
+    auto* dn = static_cast<uint8_t*>(st.in(sni_null, size_t(n), s));
+    auto* dout = static_cast<int32_t*>(st.out(out_holder, size_t(n) * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_cert_choose_dev(ctx, db, dof, dn, n, dout, s);
+    if (rc) return rc;
+    st.back(out_holder, dout, size_t(n) * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "cert choose");
 }
 
 // ---------------------------------------------------------------------------

@@ -142,6 +142,20 @@ struct HostsImage {
 };
 
 // ---------------------------------------------------------------------------
+// SSLContextHolder.choose (SNI -> certificate holder): one host-key table
+// over every certificate name.  A plain name N is the key N with .a = the
+// first holder listing it; a wildcard "*.S" is the key ".S" with .b = the
+// first holder listing it.  A query matches plain names by the whole SNI
+// and wildcards by the SNI's suffix from its first dot (the prefix before a
+// wildcard suffix holds no dot), so two exact probes replace the linear
+// scan over holders and names.
+// ---------------------------------------------------------------------------
+struct CertImage {
+    HostsImage names;              // .a = plain-name holder, .b = wildcard holder (VC_NONE)
+    int32_t n_holders;
+};
+
+// ---------------------------------------------------------------------------
 // ServerGroup source hashing (method == source): per group, three lists of
 // server indices (all / IPv4 / IPv6 servers with weight > 0, in
 // sourceReset's sort order).  view_off holds (offset, count) into order[]

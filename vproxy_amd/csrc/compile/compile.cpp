@@ -499,6 +499,39 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
     return VC_OK;
 }
 
+// SSLContextHolder.compare (SSLContextHolder.java:171-186): "*.S" matches an
+// SNI ending in ".S" whose remaining prefix is non-empty and dot-free; any
+// other name matches by equality.  choose() returns the first holder with
+// any matching name, so each key keeps the minimum holder per kind.
+int build_certs(const char* const* names, const int32_t* name_lens, const int32_t* holder, int n,
+                int n_holders, HostsBuilt* out) {
+    *out = HostsBuilt{};
+    std::unordered_map<std::string, std::pair<int32_t, int32_t>> keys;   // key -> (plain, wild)
+    std::vector<std::string> order;
+    for (int i = 0; i < n; ++i) {
+        if (name_lens[i] < 0 || (!names[i] && name_lens[i] > 0)) return VC_EINVAL;
+        if (holder[i] < 0 || holder[i] >= n_holders) return VC_EINVAL;
+        std::string k(names[i] ? names[i] : "", name_lens[i]);
+        const bool wild = k.size() >= 2 && k[0] == '*' && k[1] == '.';
+        if (wild) k.erase(0, 1);
+        auto it = keys.find(k);
+        if (it == keys.end()) {
+            it = keys.emplace(k, std::make_pair(int32_t(VC_NONE), int32_t(VC_NONE))).first;
+            order.push_back(k);
+        }
+        int32_t& v = wild ? it->second.second : it->second.first;
+        v = std::min(v, holder[i]);
+    }
+    out->table.init(order.size());
+    for (const auto& k : order) {
+        const auto& v = keys[k];
+        out->table.insert(k, v.first, v.second, &out->blob);
+    }
+    out->n = out->table.n;
+    if (out->blob.empty()) out->blob.assign(16, 0);
+    return VC_OK;
+}
+
 // ---------------------------------------------------------------------------
 // ServerGroup source hashing
 // ---------------------------------------------------------------------------

@@ -83,6 +83,11 @@ struct HostsBuilt {
 int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t* values, int n,
                 HostsBuilt* out);
 
+// SSLContextHolder certificate names -> CertImage table (see images.h).
+// holder[i] in [0, n_holders) is the holder (add() order) listing names[i].
+int build_certs(const char* const* names, const int32_t* name_lens, const int32_t* holder, int n,
+                int n_holders, HostsBuilt* out);
+
 // ServerGroup source-hash lists (ServerGroup.java:620-664), see ServerImage.
 struct ServersBuilt {
     std::vector<uint32_t> view_off;      // 6 words per group

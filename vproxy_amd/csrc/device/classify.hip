@@ -370,7 +370,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
         }
         // last partial group of 4 (only the final slice, when n % 4 != 0)
         const int64_t tail = hi & ~int64_t(3);
-        if (hi == n && tail >= lo && threadIdx.x < int(hi - tail))
+        if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
             pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
                                  n_pool, tail + threadIdx.x, out_acl, out_route, out_group,
                                  out_allow, pc, ah, rc, gc, &t);
@@ -445,7 +445,7 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
     if (vec) {
         const int grid = grid_for(c, (n + 3) / 4, per_cu);
         if (lds) {
-            allow_lds(vcd::acl_v4_kernel<true>);
+            if (hipError_t e = allow_lds(vcd::acl_v4_kernel<true>)) return e;
             hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
                                c.stream, img, proto, src4, port, n, out, allow);
         } else {
@@ -455,7 +455,7 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
     } else {
         const int grid = grid_for(c, n, per_cu);
         if (lds) {
-            allow_lds(vcd::acl_v4_kernel_scalar<true>);
+            if (hipError_t e = allow_lds(vcd::acl_v4_kernel_scalar<true>)) return e;
             hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
                                shmem, c.stream, img, proto, src4, port, n, out, allow);
         } else

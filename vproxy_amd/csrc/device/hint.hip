@@ -134,9 +134,47 @@ __global__ __launch_bounds__(kHintBlock) void dns_kernel(
     }
 }
 
+template <bool kStage>
+__global__ __launch_bounds__(kHintBlock) void cert_kernel(
+    CertImage certs, const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off,
+    const uint8_t* __restrict__ null, int64_t n, int32_t* __restrict__ out) {
+    __shared__ uint32_t stage[kWaves][kStageWords];
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
+    for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
+        const int64_t i = base + lane;
+        const int64_t last = base + 64 < n ? base + 64 : n;
+        uint32_t a0 = 0;
+        const bool staged = kStage && stage_wave(blob, off[base], off[last], stage[w], &a0);
+        if (i < n) {
+            const uint32_t a = off[i], e = off[i + 1];
+            const bool is_null = null && null[i];
+            out[i] = staged ? cert_one(certs, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a),
+                                       is_null)
+                            : cert_one(certs, PtrSrc{blob + a}, int(e - a), is_null);
+        }
+        if (kStage) wave_done();
+    }
+}
+
 }  // namespace vcd
 
 namespace vc {
+
+hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
+                        const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out) {
+    if (n <= 0) return hipSuccess;
+    int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
+    int64_t cap = int64_t(c.num_cus) * 8;
+    int grid = int(want < cap ? want : cap);
+    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
+        hipLaunchKernelGGL(vcd::cert_kernel<true>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+                           certs, blob, off, null, n, out);
+    else
+        hipLaunchKernelGGL(vcd::cert_kernel<false>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+                           certs, blob, off, null, n, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* host_blob,
                        const uint32_t* host_off, const uint8_t* host_null, const uint16_t* port,

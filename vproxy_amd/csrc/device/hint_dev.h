@@ -660,4 +660,26 @@ VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImag
     }
 }
 
+// SSLContextHolder.choose(sni) (SSLContextHolder.java:51-79) over the
+// CertImage table (common/images.h): no holder -> -1 (null), one holder or
+// a null SNI or no match -> 0 (the default, first holder).
+template <class Src>
+VC_HD int32_t cert_one(const CertImage& c, const Src& q, int n, bool sni_null) {
+    if (c.n_holders <= 0) return -1;
+    if (c.n_holders == 1 || sni_null || c.names.n == 0) return 0;
+    const HostTable t{c.names.tags, c.names.recs, c.names.blob, c.names.mask};
+    uint32_t best = VC_NONE;
+    Rec r;
+    if (host_lookup(t, q, 0, n, &r) >= 0) best = r.m.y;              // plain: sni.equals(name)
+    int dot = -1;                                                     // first '.' of the SNI
+    for (int pos = 0; pos < n && dot < 0; pos += 4) {
+        const uint32_t f = vck::byte_eq_flags(q.word(pos, 0, n), 0x2E2E2E2Eu) &
+                           (keep_mask(pos, 0, n) & 0x80808080u);
+        if (f) dot = pos + (__builtin_ctz(f) >> 3);
+    }
+    if (dot > 0 && host_lookup(t, q, dot, n - dot, &r) >= 0)         // wildcard "*" + sni[dot:]
+        best = r.m.z < best ? r.m.z : best;
+    return best == VC_NONE ? 0 : int32_t(best);
+}
+
 }  // namespace vcd

@@ -46,6 +46,9 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
 hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintImage& hints,
                       const uint8_t* qblob, const uint32_t* qoff, int64_t n, uint8_t* kind,
                       int32_t* value, unsigned long long* group_counters);
+// SSLContextHolder.choose over a batch of SNI names (hint.hip)
+hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
+                        const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out);
 hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
                               const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
                               const uint16_t* dport, const uint32_t* host_id,
