@@ -314,6 +314,57 @@ int vc_parse_packets(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int6
                      const vc_pkt_out *out);
 
 /* ------------------------------------------------------------------------ */
+/* Traffic-mirror filters (vmirror/FilterConfig.java:27-94, Mirror.java)   */
+/* ------------------------------------------------------------------------ */
+/* One FilterConfig as Mirror.parseAndLoadFilter builds it (Mirror.java:545-601).
+ * Strings (origin, transport and application protocol names) are passed as
+ * ids from an interning the caller keeps: equal strings <-> equal ids. */
+typedef struct vc_mirror_filter {
+    int32_t origin;                 /* OriginConfig.origin id */
+    int32_t mirror;                 /* the origin's MirrorConfig (tap) as an index, 0..63 */
+    int32_t has_mac_x, has_mac_y;   /* "mac", "mac2" */
+    uint8_t mac_x[6], mac_y[6];
+    int32_t has_net_x, has_net_y;   /* "network", "network2" */
+    vc_net net_x, net_y;
+    int32_t transport;              /* "transportLayerProtocol" id, -1 = null */
+    int32_t has_port_x, has_port_y; /* "port", "port2": [min, max] */
+    int32_t port_x[2], port_y[2];
+    int32_t app;                    /* "applicationLayerProtocol" id, -1 = null */
+} vc_mirror_filter;
+/* Replaces the filter list Mirror.loadConfig publishes (Mirror.java:506-543).
+ * VC_EINVAL: mirror outside 0..63, a port range with min > max, or a
+ * network whose address / mask is not 4 or 16 bytes. */
+int vc_compile_mirror(vc_ctx *ctx, const vc_mirror_filter *filters, int n);
+
+/* MirrorData fields per item (MirrorData.java:13-26), SoA.  Any array may
+ * be NULL: MACs then read as 00:00:00:00:00:00 / ff:ff:ff:ff:ff:ff (the
+ * MirrorData defaults), a NULL length array makes every IP null, NULL id
+ * arrays make every protocol null, NULL ports read 0. */
+typedef struct vc_mirror_items {
+    const uint8_t *mac_src, *mac_dst;         /* 6 bytes per item */
+    const uint8_t *ip_src_len, *ip_dst_len;   /* 0 = null, 4 or 16 */
+    const uint8_t *ip_src, *ip_dst;           /* 16 bytes per item (IPv4 in the first 4) */
+    const int32_t *transport;                 /* id, -1 = null */
+    const int32_t *port_src, *port_dst;
+    const int32_t *app;                       /* id, -1 = null */
+} vc_mirror_items;
+/* Mirror.mirror(MirrorData) filter step (Mirror.java:89-118): per item the
+ * set of mirrors (bit m = MirrorConfig m) whose filters of `origin` match,
+ * at the level the item's null fields select (ether / ip / transport /
+ * application).  Device pointers (every array in `items` and out). */
+int vc_mirror_match_dev(vc_ctx *ctx, int32_t origin, const vc_mirror_items *items, int64_t n,
+                        uint64_t *out_mirrors, void *stream);
+int vc_mirror_match(vc_ctx *ctx, int32_t origin, const vc_mirror_items *items, int64_t n,
+                    uint64_t *out_mirrors);
+/* Mirror.switchPacket (Mirror.java:73-87) on raw frames (layer VC_LAYER_VXLAN
+ * or VC_LAYER_ETHER): parse as vc_parse_packets, then matchIp on IPv4/IPv6
+ * packets and matchEthernet on the rest; 0 for frames the parse rejects. */
+int vc_mirror_switch_dev(vc_ctx *ctx, int32_t origin, const uint8_t *blob, const uint32_t *off,
+                         int64_t n, int layer, uint64_t *out_mirrors, void *stream);
+int vc_mirror_switch(vc_ctx *ctx, int32_t origin, const uint8_t *blob, const uint32_t *off,
+                     int64_t n, int layer, uint64_t *out_mirrors);
+
+/* ------------------------------------------------------------------------ */
 /* Per-rule hit counters (no reference counterpart)          */
 /* ------------------------------------------------------------------------ */
 #define VC_COUNTERS_ACL    0  /* [tcp rules][udp rules][tcp default][udp default] */

@@ -1214,10 +1214,100 @@ int vo_cert_choose(const char *const *names, const int32_t *name_lens, const int
     if (n_holders == 1) return 0;                         /* :53-55 */
     if (n_holders == 0) return -1;                        /* :56-58 */
     if (!sni_null) {                                      /* chooseNoDefault, :67-79 */
-        for (int h = 0; h < n_holders; ++h)
-            for (int i = 0; i < n_names; ++i)
-                if (holder[i] == h && cert_compare(names[i], name_lens[i], sni, sni_len))
-                    return h;
+        /* the first holder (add() order) with any matching name = the
+         * smallest holder index over the matching names */
+        int best = n_holders;
+        for (int i = 0; i < n_names; ++i)
+            if (holder[i] < best && cert_compare(names[i], name_lens[i], sni, sni_len))
+                best = holder[i];
+        if (best < n_holders) return best;
     }
     return 0;                                             /* the default (first) one, :62 */
+}
+
+/* ------------------------------------------------------------------------
+ * Traffic-mirror filters: FilterConfig.matchEthernet / matchIp /
+ * matchTransport / matchApplication (FilterConfig.java:27-94), the level
+ * choice of Mirror.mirror (Mirror.java:104-117) and Mirror.switchPacket
+ * (:73-87), each filter tested in list order and the mirrors collected as
+ * a set (checkHelper, :133-139).
+ * ------------------------------------------------------------------------ */
+static int mo_mac_eq(const uint8_t *a, const uint8_t *b) { return memcmp(a, b, 6) == 0; }
+
+static int mo_ether(const vo_mirror_filter *f, const uint8_t *src, const uint8_t *dst) {
+    if (f->has_mac_x && f->has_mac_y)
+        return (mo_mac_eq(f->mac_x, src) && mo_mac_eq(f->mac_y, dst)) ||
+               (mo_mac_eq(f->mac_y, src) && mo_mac_eq(f->mac_x, dst));
+    if (f->has_mac_x) return mo_mac_eq(f->mac_x, src) || mo_mac_eq(f->mac_x, dst);
+    return 1;
+}
+
+static int mo_contains(const vo_net *n, const uint8_t *ip, int len) {   /* Network.contains(IP) */
+    return vo_mask_match(ip, len, n->ip, n->ip_len, n->mask, n->mask_len);
+}
+
+static int mo_ip(const vo_mirror_filter *f, const uint8_t *ms, const uint8_t *md,
+                 const uint8_t *is, int isl, const uint8_t *id, int idl) {
+    if (!mo_ether(f, ms, md)) return 0;
+    if (f->has_net_x && f->has_net_y)
+        return (mo_contains(&f->net_x, is, isl) && mo_contains(&f->net_y, id, idl)) ||
+               (mo_contains(&f->net_y, is, isl) && mo_contains(&f->net_x, id, idl));
+    if (f->has_net_x) return mo_contains(&f->net_x, is, isl) || mo_contains(&f->net_x, id, idl);
+    return 1;
+}
+
+static int mo_in(const int32_t r[2], int p) { return r[0] <= p && p <= r[1]; }
+
+static int mo_transport(const vo_mirror_filter *f, const uint8_t *ms, const uint8_t *md,
+                        const uint8_t *is, int isl, const uint8_t *id, int idl, int transport,
+                        int ps, int pd) {
+    if (!mo_ip(f, ms, md, is, isl, id, idl)) return 0;
+    if (f->transport != -1 && f->transport != transport) return 0;
+    if (f->has_port_x && f->has_port_y)
+        return (mo_in(f->port_x, ps) && mo_in(f->port_y, pd)) ||
+               (mo_in(f->port_y, ps) && mo_in(f->port_x, pd));
+    if (f->has_port_x) return mo_in(f->port_x, ps) || mo_in(f->port_x, pd);
+    return 1;
+}
+
+uint64_t vo_mirror_match(const vo_mirror_filter *f, int n, int origin,
+                         const uint8_t *mac_src, const uint8_t *mac_dst,
+                         const uint8_t *ip_src, int src_len, const uint8_t *ip_dst, int dst_len,
+                         int transport, int port_src, int port_dst, int app) {
+    uint64_t m = 0;
+    for (int i = 0; i < n; ++i) {
+        const vo_mirror_filter *x = &f[i];
+        if (x->origin != origin) continue;
+        int hit;
+        if (src_len == 0 || dst_len == 0)
+            hit = mo_ether(x, mac_src, mac_dst);
+        else if (transport == -1)
+            hit = mo_ip(x, mac_src, mac_dst, ip_src, src_len, ip_dst, dst_len);
+        else if (app == -1)
+            hit = mo_transport(x, mac_src, mac_dst, ip_src, src_len, ip_dst, dst_len, transport,
+                               port_src, port_dst);
+        else
+            hit = mo_transport(x, mac_src, mac_dst, ip_src, src_len, ip_dst, dst_len, transport,
+                               port_src, port_dst) && (x->app == -1 || x->app == app);
+        if (hit) m |= (uint64_t)1 << x->mirror;
+    }
+    return m;
+}
+
+uint64_t vo_mirror_switch(const vo_mirror_filter *f, int n, int origin, const uint8_t *frame,
+                          int len, int layer) {
+    vo_pkt p;
+    vo_parse_packet(frame, len, layer, &p);
+    if (p.status != 0) return 0;
+    const uint8_t *eth = layer == 0 ? frame + 8 : frame;    /* dst 0-5, src 6-11 */
+    uint64_t m = 0;
+    int is_ip = p.l3 == 4 || p.l3 == 6;
+    int al = p.l3 == 6 ? 16 : 4;
+    for (int i = 0; i < n; ++i) {
+        const vo_mirror_filter *x = &f[i];
+        if (x->origin != origin) continue;
+        int hit = is_ip ? mo_ip(x, eth + 6, eth, p.src, al, p.dst, al) : mo_ether(x, eth + 6, eth);
+        if (hit) m |= (uint64_t)1 << x->mirror;
+    }
+    return m;
 }

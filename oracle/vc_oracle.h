@@ -188,6 +188,35 @@ typedef struct {
 
 void vo_parse_packet(const uint8_t *p, int len, int layer, vo_pkt *out);
 
+/* ---- Traffic-mirror filters: base/src/main/java/vmirror/ ----
+ * FilterConfig (FilterConfig.java:7-21) with ids for the strings (origin,
+ * transportLayerProtocol, applicationLayerProtocol; -1 = null) and the
+ * MirrorConfig as an index 0..63. */
+typedef struct {
+    int32_t origin, mirror;
+    int32_t has_mac_x, has_mac_y;
+    uint8_t mac_x[6], mac_y[6];
+    int32_t has_net_x, has_net_y;
+    vo_net net_x, net_y;
+    int32_t transport;
+    int32_t has_port_x, has_port_y;
+    int32_t port_x[2], port_y[2];
+    int32_t app;
+} vo_mirror_filter;
+
+/* Mirror.mirror(MirrorData) filter step (Mirror.java:89-118, checkHelper
+ * :133-139): bit m set when a filter of `origin` whose mirror is m matches
+ * at the level picked by the null fields (ip_*_len 0 = null IP, transport /
+ * app -1 = null). */
+uint64_t vo_mirror_match(const vo_mirror_filter *f, int n, int origin,
+                         const uint8_t *mac_src, const uint8_t *mac_dst,
+                         const uint8_t *ip_src, int src_len, const uint8_t *ip_dst, int dst_len,
+                         int transport, int port_src, int port_dst, int app);
+/* Mirror.switchPacket (Mirror.java:73-87) on a raw VXLAN (layer 0) or
+ * Ethernet (layer 1) frame; 0 when the parse rejects the frame. */
+uint64_t vo_mirror_switch(const vo_mirror_filter *f, int n, int origin, const uint8_t *frame,
+                          int len, int layer);
+
 /* ---- SSLContextHolder.choose (base/src/main/java/vproxybase/util/ringbuffer/ssl/
  *      SSLContextHolder.java:51-186) ----
  * Holders 0..n_holders-1 in add() order; names[i] (length name_lens[i]) is a

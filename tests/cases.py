@@ -265,3 +265,99 @@ def gen_frames(rng, n):
             frame = frame[:int(rng.integers(0, len(frame) + 1))]
         frames.append(frame)
     return frames
+
+
+# ---- traffic-mirror filters (vmirror/FilterConfig.java) ----
+MACS = ["0a:00:27:00:00:%02x" % i for i in range(6)] + ["ff:ff:ff:ff:ff:ff", "00:00:00:00:00:00"]
+MIRROR_NETS = ["10.0.0.0/8", "10.1.0.0/16", "192.168.0.0/24", "0.0.0.0/0", "10.1.2.3/32",
+               "fd00::/8", "fd00:1::/32", "::/0", "::ffff:10.0.0.0/104", "::/96", "::/16",
+               "::10.0.0.0/104"]
+MIRROR_IPS = ["10.0.0.1", "10.1.2.3", "192.168.0.9", "8.8.8.8", "fd00::1", "fd00:1::5",
+              "::ffff:10.1.2.3", "::10.1.2.3", "2001::1", "0.0.0.0"]
+
+
+def gen_mirror_case(rng, nf, n, origins=("switch", "tcp-lb", "socks5")):
+    """Random FilterConfig dicts over small pools (so filters hit), and n
+    MirrorData-like items with every null combination.  Returns
+    (filters, items) where items is a list of dicts with mac_src/mac_dst
+    (str), ip_src/ip_dst (str or None), transport/app (str or None), ports."""
+    def pick(xs):
+        return xs[int(rng.integers(0, len(xs)))]
+
+    filters = []
+    for _ in range(nf):
+        f = {"origin": pick(origins), "mirror": int(rng.integers(0, 64 if rng.random() < 0.2 else 6))}
+        if rng.random() < 0.5:
+            f["mac"] = pick(MACS)
+            if rng.random() < 0.5:
+                f["mac2"] = pick(MACS)
+        if rng.random() < 0.6:
+            f["network"] = pick(MIRROR_NETS)
+            if rng.random() < 0.5:
+                f["network2"] = pick(MIRROR_NETS)
+        if rng.random() < 0.5:
+            f["transportLayerProtocol"] = pick(["tcp", "udp", "sctp"])
+        if rng.random() < 0.5:
+            a = int(rng.integers(0, 100))
+            f["port"] = [a, a + int(rng.integers(0, 50))]
+            if rng.random() < 0.5:
+                b = int(rng.integers(0, 100))
+                f["port2"] = [b, b + int(rng.integers(0, 50))]
+        if rng.random() < 0.3:
+            f["applicationLayerProtocol"] = pick(["http", "dns", "h2"])
+        filters.append(f)
+    items = []
+    for _ in range(n):
+        r = rng.random()
+        it = {"mac_src": pick(MACS), "mac_dst": pick(MACS), "ip_src": None, "ip_dst": None,
+              "transport": None, "app": None, "port_src": int(rng.integers(0, 160)),
+              "port_dst": int(rng.integers(0, 160))}
+        if r > 0.15:
+            it["ip_src"] = pick(MIRROR_IPS)
+            it["ip_dst"] = pick(MIRROR_IPS) if rng.random() > 0.05 else None
+        if r > 0.4:
+            it["transport"] = pick(["tcp", "udp", "quic"])
+        if r > 0.7:
+            it["app"] = pick(["http", "dns", "grpc"])
+        items.append(it)
+    return filters, items
+
+
+def mirror_columns(items, id_of, ip_parse):
+    """items -> numpy vc_mirror_items columns (strings interned by id_of)."""
+    import numpy as np
+    n = len(items)
+    mac = lambda s: bytes(int(p, 16) for p in s.split(":"))
+    cols = {"mac_src": np.frombuffer(b"".join(mac(i["mac_src"]) for i in items), np.uint8).copy(),
+            "mac_dst": np.frombuffer(b"".join(mac(i["mac_dst"]) for i in items), np.uint8).copy()}
+    for side in ("src", "dst"):
+        ln = np.zeros(n, np.uint8)
+        ip = np.zeros((n, 16), np.uint8)
+        for k, i in enumerate(items):
+            if i["ip_" + side] is not None:
+                b = ip_parse(i["ip_" + side])
+                ln[k] = len(b)
+                ip[k, :len(b)] = list(b)
+        cols["ip_%s_len" % side] = ln
+        cols["ip_" + side] = ip
+    cols["transport"] = np.array([id_of(i["transport"]) for i in items], np.int32)
+    cols["app"] = np.array([id_of(i["app"]) for i in items], np.int32)
+    cols["port_src"] = np.array([i["port_src"] for i in items], np.int32)
+    cols["port_dst"] = np.array([i["port_dst"] for i in items], np.int32)
+    return cols
+
+
+def mirror_frames(rng, n):
+    """gen_frames VXLAN payloads with their inner MACs drawn from MACS and
+    some IPv4 addresses drawn from 10.x so network filters hit."""
+    frames = []
+    mac = lambda s: bytes(int(p, 16) for p in s.split(":"))
+    for f in gen_frames(rng, n):
+        f = bytearray(f)
+        if len(f) >= 20:
+            f[8:14] = mac(MACS[int(rng.integers(0, len(MACS)))])
+            f[14:20] = mac(MACS[int(rng.integers(0, len(MACS)))])
+        if len(f) >= 42 and f[20:22] == b"\x08\x00" and rng.random() < 0.6:
+            f[34:38] = bytes([10, int(rng.integers(0, 3)), 2, 3])
+        frames.append(bytes(f))
+    return frames

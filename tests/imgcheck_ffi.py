@@ -26,6 +26,8 @@ def lib():
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
         L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
+        L.ic_mirror.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
+        L.ic_mirror_switch.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp]
         L.ic_packets.argtypes = [vp, vp, C.c_int64, C.c_int, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
         L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]
@@ -135,5 +137,26 @@ def certs(holders, snis):
     out = np.empty(len(qs), np.int32)
     rc = lib().ic_certs(karr, P(kl), P(hold), len(names), len(holders), P(qb), P(qoff), P(qnull),
                         len(qs), P(out))
+    assert rc == 0, rc
+    return out
+
+
+def mirror(filter_arr, nf, origin, items, n):
+    """device mirror_item + mirror_eval on the host; items: VcMirrorItems"""
+    out = np.empty(n, np.uint64)
+    rc = lib().ic_mirror(C.cast(filter_arr, C.c_void_p), nf, origin, C.cast(C.pointer(items),
+                         C.c_void_p), n, P(out))
+    assert rc == 0, rc
+    return out
+
+
+def mirror_switch(filter_arr, nf, origin, frames, layer):
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.uint32)
+    off[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(frames) or b"\0", np.uint8).copy()
+    out = np.empty(len(frames), np.uint64)
+    rc = lib().ic_mirror_switch(C.cast(filter_arr, C.c_void_p), nf, origin, P(blob), P(off),
+                                len(frames), layer, P(out))
     assert rc == 0, rc
     return out

@@ -10,6 +10,7 @@
 #include "../../vproxy_amd/csrc/compile/compile.hpp"
 #include "../../vproxy_amd/csrc/device/acl_dev.h"
 #include "../../vproxy_amd/csrc/device/hint_dev.h"
+#include "../../vproxy_amd/csrc/device/mirror_dev.h"
 #include "../../vproxy_amd/csrc/device/packet_dev.h"
 #include "../../vproxy_amd/csrc/device/route_dev.h"
 
@@ -205,6 +206,31 @@ int ic_certs(const char* const* names, const int32_t* lens, const int32_t* holde
             if (cert_one(c, st.src, qn, nul) != out[i]) return -104;
         }
     }
+    return 0;
+}
+
+// Mirror filters: the kernels' item loading + mirror_eval, and switchPacket.
+int ic_mirror(const vc_mirror_filter* f, int nf, int32_t origin, const vc_mirror_items* items,
+              int64_t n, uint64_t* out) {
+    std::vector<MirrorRec> recs;
+    int rc = vc::build_mirror(f, nf, &recs);
+    if (rc) return rc;
+    const MirrorImage img{recs.data(), nf};
+    for (int64_t i = 0; i < n; ++i) {
+        const MirrorItem it = mirror_item(*items, i);
+        out[i] = mirror_eval(img, origin, it, mirror_level(it));
+    }
+    return 0;
+}
+
+int ic_mirror_switch(const vc_mirror_filter* f, int nf, int32_t origin, const uint8_t* blob,
+                     const uint32_t* off, int64_t n, int layer, uint64_t* out) {
+    std::vector<MirrorRec> recs;
+    int rc = vc::build_mirror(f, nf, &recs);
+    if (rc) return rc;
+    const MirrorImage img{recs.data(), nf};
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = mirror_switch_one(img, origin, blob + off[i], int(off[i + 1] - off[i]), layer);
     return 0;
 }
 

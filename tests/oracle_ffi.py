@@ -55,6 +55,15 @@ class VoPkt(C.Structure):
                 ("dst", C.c_uint8 * 16), ("sport", C.c_int), ("dport", C.c_int)]
 
 
+class VoMirrorFilter(C.Structure):
+    _fields_ = [("origin", C.c_int32), ("mirror", C.c_int32), ("has_mac_x", C.c_int32),
+                ("has_mac_y", C.c_int32), ("mac_x", C.c_uint8 * 6), ("mac_y", C.c_uint8 * 6),
+                ("has_net_x", C.c_int32), ("has_net_y", C.c_int32), ("net_x", VoNet),
+                ("net_y", VoNet), ("transport", C.c_int32), ("has_port_x", C.c_int32),
+                ("has_port_y", C.c_int32), ("port_x", C.c_int32 * 2), ("port_y", C.c_int32 * 2),
+                ("app", C.c_int32)]
+
+
 class VoHosts(C.Structure):
     _fields_ = [("keys", C.POINTER(C.c_char_p)), ("key_lens", C.POINTER(C.c_int32)),
                 ("values", C.POINTER(C.c_int32)), ("n", C.c_int)]
@@ -111,6 +120,11 @@ def lib():
         L.vo_source_hash.restype = C.c_int32
         L.vo_source_list.argtypes = [P(VoServer), C.c_int, C.c_int, i32p]
         L.vo_source_select.argtypes = [P(VoServer), C.c_int, C.c_int, u8p, C.c_int]
+        L.vo_mirror_match.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int, u8p, u8p, u8p, C.c_int,
+                                      u8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.vo_mirror_match.restype = C.c_uint64
+        L.vo_mirror_switch.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int, u8p, C.c_int, C.c_int]
+        L.vo_mirror_switch.restype = C.c_uint64
         L.vo_cert_choose.argtypes = [P(C.c_char_p), i32p, i32p, C.c_int, C.c_int, u8p, C.c_int,
                                      C.c_int]
         _lib = L
@@ -516,3 +530,50 @@ class Certs:
         s = _b(sni)
         return lib().vo_cert_choose(self.karr, self.larr, self.harr, len(self.names),
                                     self.n_holders, _u8(s), len(s), 0)
+
+
+# ---- traffic-mirror filters (vmirror/FilterConfig.java, Mirror.java) ----
+def mirror_filters(filters, ids):
+    """dict configs -> VoMirrorFilter array, parsed as Mirror.parseAndLoadFilter
+    (Mirror.java:545-601) with the oracle's own Network parser; strings
+    interned through `ids` (dict, extended in place)."""
+    def iid(s):
+        if s is None:
+            return -1
+        return ids.setdefault(s, len(ids))
+
+    def mac(s):
+        return [int(p, 16) & 0xFF for p in s.split(":")]
+
+    arr = (VoMirrorFilter * max(1, len(filters)))()
+    for i, f in enumerate(filters):
+        r = arr[i]
+        r.origin, r.mirror = iid(f["origin"]), int(f["mirror"])
+        if "mac" in f:
+            r.has_mac_x, r.mac_x[:] = 1, mac(f["mac"])
+            if "mac2" in f:
+                r.has_mac_y, r.mac_y[:] = 1, mac(f["mac2"])
+        if "network" in f:
+            r.has_net_x, r.net_x = 1, net(f["network"])
+            if "network2" in f:
+                r.has_net_y, r.net_y = 1, net(f["network2"])
+        r.transport = iid(f.get("transportLayerProtocol"))
+        if "port" in f:
+            r.has_port_x, r.port_x[:] = 1, list(f["port"])
+            if "port2" in f:
+                r.has_port_y, r.port_y[:] = 1, list(f["port2"])
+        r.app = iid(f.get("applicationLayerProtocol"))
+    return arr
+
+
+def mirror_match(arr, n, origin, mac_src, mac_dst, ip_src, ip_dst, transport, port_src,
+                 port_dst, app):
+    s = bytes(ip_src or b"")
+    d = bytes(ip_dst or b"")
+    return int(lib().vo_mirror_match(arr, n, origin, _u8(bytes(mac_src)), _u8(bytes(mac_dst)),
+                                     _u8(s), len(s), _u8(d), len(d), transport, port_src,
+                                     port_dst, app))
+
+
+def mirror_switch(arr, n, origin, frame, layer):
+    return int(lib().vo_mirror_switch(arr, n, origin, _u8(bytes(frame)), len(frame), layer))

@@ -50,6 +50,21 @@ class VcServer(C.Structure):
                 ("weight", C.c_int32), ("healthy", C.c_int32)]
 
 
+class VcMirrorFilter(C.Structure):
+    _fields_ = [("origin", C.c_int32), ("mirror", C.c_int32), ("has_mac_x", C.c_int32),
+                ("has_mac_y", C.c_int32), ("mac_x", C.c_uint8 * 6), ("mac_y", C.c_uint8 * 6),
+                ("has_net_x", C.c_int32), ("has_net_y", C.c_int32), ("net_x", VcNet),
+                ("net_y", VcNet), ("transport", C.c_int32), ("has_port_x", C.c_int32),
+                ("has_port_y", C.c_int32), ("port_x", C.c_int32 * 2), ("port_y", C.c_int32 * 2),
+                ("app", C.c_int32)]
+
+
+class VcMirrorItems(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("mac_src", "mac_dst", "ip_src_len", "ip_dst_len",
+                                          "ip_src", "ip_dst", "transport", "port_src",
+                                          "port_dst", "app")]
+
+
 class VcMetric(C.Structure):
     _fields_ = [("metric", C.c_char_p), ("type", C.c_int32), ("n_labels", C.c_int32),
                 ("label_keys", C.POINTER(C.c_char_p)), ("label_values", C.POINTER(C.c_char_p)),
@@ -149,6 +164,11 @@ def lib():
         L.vc_compile_certs.argtypes = [vp, P(C.c_char_p), vp, vp, i32, i32]
         L.vc_cert_choose_dev.argtypes = [vp, vp, vp, vp, i64, vp, vp]
         L.vc_cert_choose.argtypes = [vp, vp, vp, vp, i64, vp]
+        L.vc_compile_mirror.argtypes = [vp, P(VcMirrorFilter), i32]
+        L.vc_mirror_match_dev.argtypes = [vp, i32, P(VcMirrorItems), i64, vp, vp]
+        L.vc_mirror_match.argtypes = [vp, i32, P(VcMirrorItems), i64, vp]
+        L.vc_mirror_switch_dev.argtypes = [vp, i32, vp, vp, i64, i32, vp, vp]
+        L.vc_mirror_switch.argtypes = [vp, i32, vp, vp, i64, i32, vp]
         L.vc_parse_packets_dev.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut), vp]
         L.vc_parse_packets.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut)]
         L.vc_counters_enable.argtypes = [vp, i32]

@@ -613,6 +613,52 @@ class Classifier:
         check(lib().vc_cert_choose(self.h, _ptr(b), _ptr(o), _ptr(nul), n, _ptr(out)))
         return out
 
+    # ---------------- traffic-mirror filters ----------------
+    def compile_mirror(self, filters):
+        """Mirror's filter list (dict configs, list order); returns the
+        MirrorFilters interning used for origins / protocol names."""
+        from .mirror import MirrorFilters
+        mf = MirrorFilters()
+        arr, n = mf.build(filters)
+        check(lib().vc_compile_mirror(self.h, arr, n))
+        self._mirror = mf
+        return mf
+
+    def mirror_match(self, origin, cols, n):
+        """Mirror.mirror's filter step per item -> uint64 mirror bit sets.
+        cols: vc_mirror_items arrays (numpy: host path; torch CUDA: device
+        path), protocol columns already interned (MirrorFilters.id_of)."""
+        from .mirror import items_struct
+        oid = self._mirror.id_of(origin, create=False)
+        it = items_struct(cols)
+        if any(_is_dev(v) for v in cols.values()):
+            import torch
+            dev = next(v for v in cols.values() if _is_dev(v)).device
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            check(lib().vc_mirror_match_dev(self.h, oid, C.byref(it), n, _ptr(out), _stream()))
+            return out
+        out = np.empty(n, np.uint64)
+        check(lib().vc_mirror_match(self.h, oid, C.byref(it), n, _ptr(out)))
+        return out
+
+    def mirror_switch(self, origin, frames, layer=0):
+        """Mirror.switchPacket per raw frame -> uint64 mirror bit sets.
+        frames: list of bytes, or a (blob, off) tuple of torch CUDA tensors."""
+        oid = self._mirror.id_of(origin, create=False)
+        if isinstance(frames, tuple) and _is_dev(frames[0]):
+            import torch
+            b, o = frames
+            n = len(o) - 1
+            out = torch.empty(n, dtype=torch.int64, device=b.device)
+            check(lib().vc_mirror_switch_dev(self.h, oid, _ptr(b), _ptr(o), n, int(layer),
+                                             _ptr(out), _stream()))
+            return out
+        n = len(frames)
+        b, o, _ = pack_strings(frames)
+        out = np.empty(n, np.uint64)
+        check(lib().vc_mirror_switch(self.h, oid, _ptr(b), _ptr(o), n, int(layer), _ptr(out)))
+        return out
+
     # ---------------- counters ----------------
     def counters_enable(self, on=True):
         check(lib().vc_counters_enable(self.h, 1 if on else 0))

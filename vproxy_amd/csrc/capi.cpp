@@ -87,6 +87,9 @@ struct HostsSnap : Snapshot {
 struct CertSnap : Snapshot {
     CertImage img{};
 };
+struct MirrorSnap : Snapshot {
+    MirrorImage img{};
+};
 struct ServerSnap : Snapshot {
     ServerImage img{};
     uint8_t* healthy = nullptr;    // device copy, updated in place (vc_servers_set_health)
@@ -107,6 +110,7 @@ struct vc_ctx {
     std::shared_ptr<const HostsSnap> hosts;
     std::shared_ptr<const ServerSnap> servers;
     std::shared_ptr<const CertSnap> certs;
+    std::shared_ptr<const MirrorSnap> mirror;
 
     template <class S>
     std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
@@ -221,6 +225,7 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->hosts.reset();
     ctx->servers.reset();
     ctx->certs.reset();
+    ctx->mirror.reset();
     (void)hipStreamDestroy(ctx->stream);
     if (ctx->pool) {
         // batches may still run on callers' streams: their scratch is freed
@@ -637,6 +642,105 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
     st.back(out_holder, dout, size_t(n) * 4, s);
     hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
     return e == hipSuccess ? VC_OK : hip_fail(e, "cert choose");
+}
+
+// ---------------------------------------------------------------------------
+// Mirror filters
+// ---------------------------------------------------------------------------
+int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n && !filters)) return fail(VC_EINVAL, "bad filter array");
+    std::vector<MirrorRec> recs;
+    if ((rc = vc::build_mirror(filters, n, &recs)) != VC_OK)
+        return fail(rc, "invalid mirror filter (mirror index, port range or network)");
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    auto s = std::make_shared<MirrorSnap>();
+    hipError_t e = hipSuccess;
+    s->img.f = s->upload(recs, &e);
+    s->img.n = n;
+    if (e != hipSuccess) return hip_fail(e, "mirror filter upload");
+    ctx->publish(ctx->mirror, std::shared_ptr<const MirrorSnap>(std::move(s)));
+    return VC_OK;
+}
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int vc_mirror_match_dev(vc_ctx* ctx, int32_t origin, const vc_mirror_items* items, int64_t n,
+                        uint64_t* out_mirrors, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!items || !out_mirrors))) return fail(VC_EINVAL, "bad batch arguments");
+    if (n == 0) return VC_OK;
+    if ((items->ip_src && !al16(items->ip_src)) || (items->ip_dst && !al16(items->ip_dst)))
+        return fail(VC_EINVAL, "ip_src / ip_dst must be 16-byte aligned");
+    auto s = ctx->get(ctx->mirror);
+    if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
+    hipError_t e = vc::launch_mirror_match(ctx->cfg(stream), s->img, origin, *items, n, out_mirrors);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror launch");
+}
+
+int vc_mirror_match(vc_ctx* ctx, int32_t origin, const vc_mirror_items* items, int64_t n,
+                    uint64_t* out_mirrors) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!items || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    const size_t un = size_t(n);
+    vc_mirror_items d{};
+    d.mac_src = static_cast<const uint8_t*>(st.in(items->mac_src, un * 6, s));
+    d.mac_dst = static_cast<const uint8_t*>(st.in(items->mac_dst, un * 6, s));
+    d.ip_src_len = static_cast<const uint8_t*>(st.in(items->ip_src_len, un, s));
+    d.ip_dst_len = static_cast<const uint8_t*>(st.in(items->ip_dst_len, un, s));
+    d.ip_src = static_cast<const uint8_t*>(st.in(items->ip_src, un * 16, s));
+    d.ip_dst = static_cast<const uint8_t*>(st.in(items->ip_dst, un * 16, s));
+    d.transport = static_cast<const int32_t*>(st.in(items->transport, un * 4, s));
+    d.port_src = static_cast<const int32_t*>(st.in(items->port_src, un * 4, s));
+    d.port_dst = static_cast<const int32_t*>(st.in(items->port_dst, un * 4, s));
+    d.app = static_cast<const int32_t*>(st.in(items->app, un * 4, s));
+    auto* dout = static_cast<uint64_t*>(st.out(out_mirrors, un * 8));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_mirror_match_dev(ctx, origin, &d, n, dout, s);
+    if (rc) return rc;
+    st.back(out_mirrors, dout, un * 8, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror match");
+}
+
+int vc_mirror_switch_dev(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uint32_t* off,
+                         int64_t n, int layer, uint64_t* out_mirrors, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!blob || !off || !out_mirrors)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    if (layer != VC_LAYER_VXLAN && layer != VC_LAYER_ETHER)
+        return fail(VC_EINVAL, "switchPacket takes VXLAN or Ethernet frames");
+    auto s = ctx->get(ctx->mirror);
+    if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
+    hipError_t e = vc::launch_mirror_switch(ctx->cfg(stream), s->img, origin, blob, off, n, layer,
+                                            out_mirrors);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror switch launch");
+}
+
+int vc_mirror_switch(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uint32_t* off,
+                     int64_t n, int layer, uint64_t* out_mirrors) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!blob || !off || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
+    Staging st;
+    hipStream_t s = ctx->stream;
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
+    auto* dof = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
+    auto* dout = static_cast<uint64_t*>(st.out(out_mirrors, size_t(n) * 8));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_mirror_switch_dev(ctx, origin, db, dof, n, layer, dout, s);
+    if (rc) return rc;
+    st.back(out_mirrors, dout, size_t(n) * 8, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror switch");
 }
 
 // ---------------------------------------------------------------------------

@@ -156,6 +156,34 @@ struct CertImage {
 };
 
 // ---------------------------------------------------------------------------
+// Mirror filters (vmirror/FilterConfig.java): one 128-byte record per
+// FilterConfig in list order, read wave-uniformly (scalar loads).
+// Addresses / masks as little-endian words of their left-aligned bytes
+// (common/netmatch.h); MACs as the low 48 bits of a u64, byte 0 lowest.
+// ---------------------------------------------------------------------------
+#define VC_MF_MAC_X  1u
+#define VC_MF_MAC_Y  2u
+#define VC_MF_NET_X  4u
+#define VC_MF_NET_Y  8u
+#define VC_MF_PORT_X 16u
+#define VC_MF_PORT_Y 32u
+
+struct MirrorRec {
+    uint32_t net_x_ip[4], net_x_mask[4], net_y_ip[4], net_y_mask[4];
+    uint64_t mac_x, mac_y;
+    int32_t origin, mirror, flags, transport, app;
+    int32_t port_x0, port_x1, port_y0, port_y1;
+    uint8_t nx_ip_len, nx_mask_len, ny_ip_len, ny_mask_len;
+    uint32_t pad[2];
+};
+static_assert(sizeof(MirrorRec) == 128, "MirrorRec layout");
+
+struct MirrorImage {
+    const MirrorRec* f;
+    int32_t n;
+};
+
+// ---------------------------------------------------------------------------
 // ServerGroup source hashing (method == source): per group, three lists of
 // server indices (all / IPv4 / IPv6 servers with weight > 0, in
 // sourceReset's sort order).  view_off holds (offset, count) into order[]

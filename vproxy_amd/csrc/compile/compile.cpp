@@ -532,6 +532,57 @@ int build_certs(const char* const* names, const int32_t* name_lens, const int32_
     return VC_OK;
 }
 
+// Mirror filters.  Java rejects min > max while parsing the config
+// (Mirror.java:581-582, 590-591); mirror indices are bits of the result.
+int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out) {
+    out->assign(size_t(n), MirrorRec{});
+    auto words = [](const uint8_t* b, int len, uint32_t w[4]) {
+        for (int k = 0; k < 4; ++k) w[k] = 0;
+        for (int k = 0; k < len; ++k) w[k >> 2] |= uint32_t(b[k]) << (8 * (k & 3));
+    };
+    auto mac = [](const uint8_t* b) {
+        uint64_t v = 0;
+        for (int k = 0; k < 6; ++k) v |= uint64_t(b[k]) << (8 * k);
+        return v;
+    };
+    auto len_ok = [](int l) { return l == 4 || l == 16; };
+    for (int i = 0; i < n; ++i) {
+        const vc_mirror_filter& s = f[i];
+        MirrorRec& r = (*out)[size_t(i)];
+        if (s.mirror < 0 || s.mirror > 63) return VC_EINVAL;
+        if (s.has_net_x && (!len_ok(s.net_x.ip_len) || !len_ok(s.net_x.mask_len))) return VC_EINVAL;
+        if (s.has_net_y && (!len_ok(s.net_y.ip_len) || !len_ok(s.net_y.mask_len))) return VC_EINVAL;
+        if (s.has_port_x && s.port_x[0] > s.port_x[1]) return VC_EINVAL;
+        if (s.has_port_y && s.port_y[0] > s.port_y[1]) return VC_EINVAL;
+        r.origin = s.origin;
+        r.mirror = s.mirror;
+        r.flags = (s.has_mac_x ? VC_MF_MAC_X : 0) | (s.has_mac_y ? VC_MF_MAC_Y : 0) |
+                  (s.has_net_x ? VC_MF_NET_X : 0) | (s.has_net_y ? VC_MF_NET_Y : 0) |
+                  (s.has_port_x ? VC_MF_PORT_X : 0) | (s.has_port_y ? VC_MF_PORT_Y : 0);
+        r.mac_x = mac(s.mac_x);
+        r.mac_y = mac(s.mac_y);
+        if (s.has_net_x) {
+            words(s.net_x.ip, s.net_x.ip_len, r.net_x_ip);
+            words(s.net_x.mask, s.net_x.mask_len, r.net_x_mask);
+            r.nx_ip_len = uint8_t(s.net_x.ip_len);
+            r.nx_mask_len = uint8_t(s.net_x.mask_len);
+        }
+        if (s.has_net_y) {
+            words(s.net_y.ip, s.net_y.ip_len, r.net_y_ip);
+            words(s.net_y.mask, s.net_y.mask_len, r.net_y_mask);
+            r.ny_ip_len = uint8_t(s.net_y.ip_len);
+            r.ny_mask_len = uint8_t(s.net_y.mask_len);
+        }
+        r.transport = s.transport;
+        r.app = s.app;
+        r.port_x0 = s.port_x[0];
+        r.port_x1 = s.port_x[1];
+        r.port_y0 = s.port_y[0];
+        r.port_y1 = s.port_y[1];
+    }
+    return VC_OK;
+}
+
 // ---------------------------------------------------------------------------
 // ServerGroup source hashing
 // ---------------------------------------------------------------------------

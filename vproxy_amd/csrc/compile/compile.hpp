@@ -88,6 +88,9 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
 int build_certs(const char* const* names, const int32_t* name_lens, const int32_t* holder, int n,
                 int n_holders, HostsBuilt* out);
 
+// Mirror FilterConfig list -> MirrorRec records (images.h).
+int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out);
+
 // ServerGroup source-hash lists (ServerGroup.java:620-664), see ServerImage.
 struct ServersBuilt {
     std::vector<uint32_t> view_off;      // 6 words per group

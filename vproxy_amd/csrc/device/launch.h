@@ -49,6 +49,12 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
 // SSLContextHolder.choose over a batch of SNI names (hint.hip)
 hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
                         const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out);
+// Mirror filters (mirror.hip)
+hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
+                               const vc_mirror_items& in, int64_t n, uint64_t* out);
+hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
+                                const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                                uint64_t* out);
 hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
                               const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
                               const uint16_t* dport, const uint32_t* host_id,

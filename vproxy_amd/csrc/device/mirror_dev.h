@@ -1,0 +1,152 @@
+// mirror_dev.h -- the traffic-mirror filter checks:
+//
+//   FilterConfig.matchEthernet / matchIp / matchTransport / matchApplication
+//                               base/src/main/java/vmirror/FilterConfig.java:27-94
+//   Mirror.mirror level choice  base/src/main/java/vmirror/Mirror.java:104-117
+//   Mirror.switchPacket         Mirror.java:73-87
+//   Mirror.checkHelper          Mirror.java:133-139 (set of MirrorConfig)
+//
+// __host__ __device__ so the test harness runs this exact code on the host.
+#pragma once
+
+#include "../common/netmatch.h"
+#include "dev_common.h"
+#include "packet_dev.h"
+
+namespace vcd {
+
+enum : int { kLvlEther = 0, kLvlIp = 1, kLvlTransport = 2, kLvlApp = 3 };
+
+struct MirrorItem {
+    uint64_t mac_src, mac_dst;
+    vcn::Addr ip_src, ip_dst;       // len 0 = null
+    int32_t transport, app;         // -1 = null
+    int32_t port_src, port_dst;
+};
+
+VC_HD bool mf_contains(const uint32_t ip[4], const uint32_t mask[4], int ip_len, int mask_len,
+                       const vcn::Addr& a) {
+    const vcn::Addr rule{{ip[0], ip[1], ip[2], ip[3]}, ip_len};
+    const vcn::Addr m{{mask[0], mask[1], mask[2], mask[3]}, mask_len};
+    return vcn::mask_match(a, rule, m);
+}
+
+VC_HD bool mf_ether(const MirrorRec& f, uint64_t src, uint64_t dst) {           // :27-38
+    const bool x = f.flags & VC_MF_MAC_X, y = f.flags & VC_MF_MAC_Y;
+    if (x && y) return (f.mac_x == src && f.mac_y == dst) || (f.mac_y == src && f.mac_x == dst);
+    if (x) return f.mac_x == src || f.mac_x == dst;
+    return true;
+}
+
+VC_HD bool mf_ip(const MirrorRec& f, const MirrorItem& it) {                     // :40-55
+    if (!mf_ether(f, it.mac_src, it.mac_dst)) return false;
+    const bool x = f.flags & VC_MF_NET_X, y = f.flags & VC_MF_NET_Y;
+    if (!x && !y) return true;
+    const bool xs = x && mf_contains(f.net_x_ip, f.net_x_mask, f.nx_ip_len, f.nx_mask_len, it.ip_src);
+    const bool xd = x && mf_contains(f.net_x_ip, f.net_x_mask, f.nx_ip_len, f.nx_mask_len, it.ip_dst);
+    if (x && y) {
+        const bool ys = mf_contains(f.net_y_ip, f.net_y_mask, f.ny_ip_len, f.ny_mask_len, it.ip_src);
+        const bool yd = mf_contains(f.net_y_ip, f.net_y_mask, f.ny_ip_len, f.ny_mask_len, it.ip_dst);
+        return (xs && yd) || (ys && xd);
+    }
+    if (x) return xs || xd;
+    return true;                    // netY without netX: the Java else branch
+}
+
+VC_HD bool in_range(int32_t lo, int32_t hi, int32_t p) { return lo <= p && p <= hi; }
+
+VC_HD bool mf_transport(const MirrorRec& f, const MirrorItem& it) {              // :57-80
+    if (!mf_ip(f, it)) return false;
+    if (f.transport != -1 && f.transport != it.transport) return false;
+    const bool x = f.flags & VC_MF_PORT_X, y = f.flags & VC_MF_PORT_Y;
+    if (x && y)
+        return (in_range(f.port_x0, f.port_x1, it.port_src) &&
+                in_range(f.port_y0, f.port_y1, it.port_dst)) ||
+               (in_range(f.port_y0, f.port_y1, it.port_src) &&
+                in_range(f.port_x0, f.port_x1, it.port_dst));
+    if (x) return in_range(f.port_x0, f.port_x1, it.port_src) ||
+                  in_range(f.port_x0, f.port_x1, it.port_dst);
+    return true;
+}
+
+VC_HD bool mf_app(const MirrorRec& f, const MirrorItem& it) {                    // :82-94
+    if (!mf_transport(f, it)) return false;
+    return f.app == -1 || f.app == it.app;
+}
+
+// Mirror.mirror: the level its null checks pick (Mirror.java:105-117)
+VC_HD int mirror_level(const MirrorItem& it) {
+    if (it.ip_src.len == 0 || it.ip_dst.len == 0) return kLvlEther;
+    if (it.transport == -1) return kLvlIp;
+    if (it.app == -1) return kLvlTransport;
+    return kLvlApp;
+}
+
+// checkHelper: union of the mirrors of the matching filters of `origin`.
+// The filter loop is uniform across the wave (scalar loads of the records).
+VC_HD uint64_t mirror_eval(const MirrorImage& img, int32_t origin, const MirrorItem& it, int lvl) {
+    uint64_t m = 0;
+    for (int k = 0; k < img.n; ++k) {
+        const MirrorRec& f = img.f[k];
+        if (f.origin != origin) continue;
+        bool hit;
+        if (lvl == kLvlEther) hit = mf_ether(f, it.mac_src, it.mac_dst);
+        else if (lvl == kLvlIp) hit = mf_ip(f, it);
+        else if (lvl == kLvlTransport) hit = mf_transport(f, it);
+        else hit = mf_app(f, it);
+        if (hit) m |= uint64_t(1) << f.mirror;
+    }
+    return m;
+}
+
+VC_HD uint64_t mac48(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int k = 0; k < 6; ++k) v |= uint64_t(p[k]) << (8 * k);
+    return v;
+}
+
+VC_HD vcn::Addr item_addr(const uint8_t* base, int64_t i, int len) {
+    if (!base || (len != 4 && len != 16)) return vcn::Addr{{0, 0, 0, 0}, 0};
+    const uint4 w = reinterpret_cast<const uint4*>(base)[i];       // 16-byte aligned rows
+    return len == 16 ? vcn::Addr{{w.x, w.y, w.z, w.w}, 16} : vcn::Addr{{w.x, 0, 0, 0}, 4};
+}
+
+// Item i of a vc_mirror_items batch; absent columns take MirrorData's
+// defaults (MirrorData.java:16-17: 00:00:00:00:00:00 -> ff:ff:ff:ff:ff:ff)
+// or null.  A length other than 4 / 16 reads as a null IP.
+VC_HD MirrorItem mirror_item(const vc_mirror_items& in, int64_t i) {
+    MirrorItem it;
+    it.mac_src = in.mac_src ? mac48(in.mac_src + 6 * i) : 0;
+    it.mac_dst = in.mac_dst ? mac48(in.mac_dst + 6 * i) : 0xFFFFFFFFFFFFull;
+    it.ip_src = item_addr(in.ip_src, i, in.ip_src_len ? in.ip_src_len[i] : 0);
+    it.ip_dst = item_addr(in.ip_dst, i, in.ip_dst_len ? in.ip_dst_len[i] : 0);
+    it.transport = in.transport ? in.transport[i] : -1;
+    it.app = in.app ? in.app[i] : -1;
+    it.port_src = in.port_src ? in.port_src[i] : 0;
+    it.port_dst = in.port_dst ? in.port_dst[i] : 0;
+    return it;
+}
+
+// Mirror.switchPacket: frame -> EthernetPacket (dst MAC bytes 0-5, src
+// 6-11, EthernetPacket.java:19-20) -> matchIp for IPv4/IPv6 packets,
+// matchEthernet otherwise; 0 for a frame the parse rejects.
+VC_HD uint64_t mirror_switch_one(const MirrorImage& img, int32_t origin, const uint8_t* p,
+                                 int len, int layer) {
+    PktOut o;
+    parse_packet(p, len, layer, &o);
+    if (o.status != VC_PKT_OK) return 0;
+    const uint8_t* eth = layer == VC_LAYER_VXLAN ? p + 8 : p;
+    MirrorItem it{};
+    it.mac_dst = mac48(eth);
+    it.mac_src = mac48(eth + 6);
+    int lvl = kLvlEther;
+    if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
+        const int al = o.l3 == VC_L3_IPV4 ? 4 : 16;
+        it.ip_src = vcn::addr_of(o.src, al);
+        it.ip_dst = vcn::addr_of(o.dst, al);
+        lvl = kLvlIp;
+    }
+    return mirror_eval(img, origin, it, lvl);
+}
+
+}  // namespace vcd

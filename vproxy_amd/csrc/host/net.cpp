@@ -1,6 +1,8 @@
 // net.cpp -- see net.hpp.  Java semantics over ASCII bytes.
 #include "net.hpp"
 
+#include "../common/netmatch.h"
+
 #include <cstring>
 #include <vector>
 
@@ -155,44 +157,13 @@ bool valid_network(const uint8_t* a, int alen, const uint8_t* m, int mlen) {
     return true;
 }
 
-namespace {
-// Java `(inputB & maskB) != ruleB` over sign-extended bytes.
-inline bool bne(uint8_t in, uint8_t mask, uint8_t rule) {
-    return ((int)(int8_t)in & (int)(int8_t)mask) != (int)(int8_t)rule;
-}
-// Utils.lowBitsV6V4 (Utils.java:122-133)
-inline bool low_bits_v6v4(const uint8_t* ip, int last, int second) {
-    for (int i = 0; i < second; ++i)
-        if (ip[i] != 0) return false;
-    if (ip[last] == 0) return ip[second] == 0;
-    if (ip[last] == 0xFF) return ip[second] == 0xFF;
-    return false;
-}
-}  // namespace
-
 bool mask_match(const uint8_t* in, int inlen, const uint8_t* rule, int rlen,
                 const uint8_t* mask, int mlen) {
-    if (inlen == rlen && rlen > mlen) {                 // (1) v6 in, v6 rule, 4-byte mask
-        for (int i = 0; i < mlen; ++i)
-            if (bne(in[i], mask[i], rule[i])) return false;
-        return true;
-    }
-    if (inlen < rlen && rlen > mlen) return false;      // (2) v4 in, v6 rule, 4-byte mask
-    if (inlen < rlen && rlen == mlen) {                 // (3) v4 in, v6 rule, 16-byte mask
-        int d = rlen - inlen;
-        for (int i = 0; i < inlen; ++i)
-            if (bne(in[i], mask[i + d], rule[i + d])) return false;
-        return low_bits_v6v4(rule, d - 1, d - 2);
-    }
-    int n = inlen < rlen ? inlen : rlen;                // (4) and (5): compare tails
-    if (mlen < n) n = mlen;
-    for (int i = 1; i <= n; ++i)
-        if (bne(in[inlen - i], mask[mlen - i], rule[rlen - i])) return false;
-    if (inlen > rlen) {
-        int d = inlen - rlen;
-        return low_bits_v6v4(in, d - 1, d - 2);
-    }
-    return true;
+    // lengths other than 4 / 16 never occur in a Network or an IP
+    if ((inlen != 4 && inlen != 16) || (rlen != 4 && rlen != 16) || (mlen != 4 && mlen != 16))
+        return false;
+    return vcn::mask_match(vcn::addr_of(in, inlen), vcn::addr_of(rule, rlen),
+                           vcn::addr_of(mask, mlen));
 }
 
 bool net_equals(const vc_net& a, const vc_net& b) {
