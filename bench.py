@@ -208,7 +208,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c5", choices=["c5", "c2", "c3", "c4"])
+    ap.add_argument("--workload", default="c5",
+                    choices=["c5", "c2", "c3", "c4", "dns", "sni", "parse", "source", "mirror"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -479,6 +480,85 @@ def sub_bench(args, clf, dev, rank, world):
         o6 = torch.empty(n - n4, dtype=torch.int32, device=dev)
         fn = lambda: (clf.route_v4(q4, out=o4), clf.route_v6(q6, out=o6))
         per_unit, unit = (8 * 0.85 + 20 * 0.15), "B/lookup (v4 4+4, v6 16+4, 85/15 mix)"
+    elif args.workload == "dns":
+        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+        clf.compile_upstream(groups)
+        hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
+                           for i in range(50_000))
+        clf.compile_hosts_text(hosts)
+        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+        nblob, noff = W.pack(names)
+        n = 16 << 20
+        pidx = np.random.default_rng(W.SEED + 8).integers(0, len(names), n)
+        blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
+        kind = torch.empty(n, dtype=torch.uint8, device=dev)
+        val = torch.empty(n, dtype=torch.int32, device=dev)
+        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        fn = lambda: V.check(V.lib().vc_dns_classify_dev(
+            clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n,
+            C.c_void_p(kind.data_ptr()), C.c_void_p(val.data_ptr()), s()))
+        per_unit, unit = nbytes / n + 9, "B/qname (bytes + 4 offset + 1 kind + 4 value)"
+    elif args.workload == "sni":
+        _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
+        holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]
+        clf.compile_certs(holders)
+        names = [x.split(b":")[0] for x in W.gen_hostnames(hosts, 1 << 20, W.SEED + 10)]
+        nblob, noff = W.pack(names)
+        n = 16 << 20
+        pidx = np.random.default_rng(W.SEED + 11).integers(0, len(names), n)
+        blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        fn = lambda: V.check(V.lib().vc_cert_choose_dev(
+            clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, n,
+            C.c_void_p(out.data_ptr()), s()))
+        per_unit, unit = nbytes / n + 8, "B/SNI (bytes + 4 offset + 4 out)"
+    elif args.workload in ("parse", "mirror"):
+        frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
+        fblob, foff = W.pack(frames)
+        n = 32 << 20
+        pidx = np.random.default_rng(W.SEED + 13).integers(0, len(frames), n)
+        blob, off, nbytes = gather_strings_dev(fblob, foff, pidx, dev)
+        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if args.workload == "parse":
+            res = {k: torch.empty((n, w) if w > 1 else (n,), dtype={"u8": torch.uint8,
+                   "u16": torch.int16, "u32": torch.int32}[t], device=dev)
+                   for k, w, t in V.Classifier._PKT_FIELDS}
+            o = V._lib.VcPktOut(**{k: v.data_ptr() for k, v in res.items()})
+            fn = lambda: V.check(V.lib().vc_parse_packets_dev(
+                clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, 0,
+                C.byref(o), s()))
+            per_unit = nbytes / n + 4 + 54
+            unit = "B/frame (frame bytes + 4 offset in; 54 B of SoA fields out)"
+        else:
+            from vproxy_amd.mirror import MirrorFilters  # noqa: F401
+            filters = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
+                        "network2": "10.0.0.0/8"} for i in range(16)] + \
+                      [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}]
+            mf = clf.compile_mirror(filters)
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            oid = mf.id_of("switch", create=False)
+            fn = lambda: V.check(V.lib().vc_mirror_switch_dev(
+                clf.h, oid, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, 0,
+                C.c_void_p(out.data_ptr()), s()))
+            per_unit = nbytes / n + 4 + 8
+            unit = "B/frame (frame bytes + 4 offset in; 8 B mirror set out), 17 filters"
+    elif args.workload == "source":
+        rng = np.random.default_rng(W.SEED + 14)
+        groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
+                   for _ in range(int(rng.integers(1, 32)))] for _ in range(10_000)]
+        clf.compile_servers(groups)
+        n = 128 << 20
+        g = torch.Generator(device=dev)
+        g.manual_seed(15)
+        grp = torch.randint(0, len(groups), (n,), generator=g, device=dev, dtype=torch.int32)
+        src = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, device=dev, dtype=torch.int32)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        fn = lambda: V.check(V.lib().vc_source_select_v4_dev(
+            clf.h, C.c_void_p(grp.data_ptr()), C.c_void_p(src.data_ptr()), n, 0,
+            C.c_void_p(out.data_ptr()), s()))
+        per_unit, unit = 12, "B/item (group 4 + v4 source 4 in, 4 out)"
     else:  # c4
         groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
         clf.compile_upstream(groups)

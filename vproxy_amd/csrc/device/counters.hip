@@ -12,7 +12,7 @@
 // * large spaces (routes: ~1.2M bins; groups: 100K) are first partitioned
 //   into 8K-bin buckets -- count, scan, then a scatter that sorts each
 //   8K-item tile by bucket in LDS so the bucket runs leave as contiguous
-//   stores -- and each bucket is then histogrammed in LDS by segments of at
+//   stores of 16-bit in-bucket bins -- and each bucket is then histogrammed in LDS by segments of at
 //   most kSeg items (a hot bucket is split over many workgroups).
 //
 // Null results (no rule / default) are counted in registers and added once
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scan_kernel(
 template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
-    int32_t nt, int nbk, const uint32_t* __restrict__ offsets, int32_t* __restrict__ tmp) {
+    int32_t nt, int nbk, const uint32_t* __restrict__ offsets, uint16_t* __restrict__ tmp) {
     // LDS sized by the bucket count, so the kernel can share a CU with the
     // classify kernels of the next batch
     extern __shared__ uint32_t dyn[];
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
         for (uint32_t j = threadIdx.x; j < total; j += blockDim.x) {
             const int32_t x = sorted[j];
             const int bk = x / kBW;
-            tmp[cur[bk] + (j - tst[bk])] = x;
+            tmp[cur[bk] + (j - tst[bk])] = uint16_t(x & (kBW - 1));   // bin within its bucket
         }
         __syncthreads();
         for (int k = threadIdx.x; k < nbk; k += blockDim.x) {
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
 
 // (4) one workgroup per segment of a bucket: LDS histogram, coalesced flush
 __global__ __launch_bounds__(kHistBlock) void bucket_hist_kernel(
-    const int32_t* __restrict__ tmp, const uint32_t* __restrict__ offsets,
+    const uint16_t* __restrict__ tmp, const uint32_t* __restrict__ offsets,
     const uint32_t* __restrict__ seg_off, int nblk, int nbk, int64_t nval, int64_t base,
     unsigned long long* __restrict__ cnt) {
     __shared__ uint32_t h[kBW];
@@ -373,7 +373,8 @@ __global__ __launch_bounds__(kHistBlock) void bucket_hist_kernel(
     const uint32_t s1 = s0 + kSeg < b1 ? s0 + kSeg : b1;
     const int64_t lo_bin = int64_t(b) * kBW;
     Run run;
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) run.add(tmp[i], h, lo_bin, kBW);
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += blockDim.x)
+        run.add(lo_bin + tmp[i], h, lo_bin, kBW);
     run.flush(h, lo_bin, kBW);
     __syncthreads();
     for (int k = threadIdx.x; k < kBW && lo_bin + k < nval; k += blockDim.x)
@@ -467,7 +468,7 @@ hipError_t big_hist_begin(const LaunchCfg& c, int64_t n, int64_t nval, int nblk,
     if (e == hipSuccess)
         e = scratch_alloc(c, reinterpret_cast<void**>(&h->seg_off), size_t(h->nbk + 1) * 4);
     if (e == hipSuccess)
-        e = scratch_alloc(c, reinterpret_cast<void**>(&h->tmp), size_t(n > 0 ? n : 1) * 4);
+        e = scratch_alloc(c, reinterpret_cast<void**>(&h->tmp), size_t(n > 0 ? n : 1) * 2);
     return e;
 }
 

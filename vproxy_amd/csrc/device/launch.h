@@ -85,7 +85,7 @@ struct BigHist {
     uint32_t* counts = nullptr;
     uint32_t* offsets = nullptr;
     uint32_t* seg_off = nullptr;
-    int32_t* tmp = nullptr;
+    uint16_t* tmp = nullptr;       // bucket-partitioned bins (within-bucket index)
 };
 bool big_hist_applies(int64_t n, int64_t nval);
 int big_hist_bucket_shift();

@@ -141,9 +141,11 @@ VC_HD uint64_t mirror_switch_one(const MirrorImage& img, int32_t origin, const u
     it.mac_src = mac48(eth + 6);
     int lvl = kLvlEther;
     if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
-        const int al = o.l3 == VC_L3_IPV4 ? 4 : 16;
-        it.ip_src = vcn::addr_of(o.src, al);
-        it.ip_dst = vcn::addr_of(o.dst, al);
+        const bool v6 = o.l3 == VC_L3_IPV6;
+        const uint4 s = *reinterpret_cast<const uint4*>(o.src);   // PktOut: 16-byte aligned
+        const uint4 d = *reinterpret_cast<const uint4*>(o.dst);
+        it.ip_src = v6 ? vcn::Addr{{s.x, s.y, s.z, s.w}, 16} : vcn::Addr{{s.x, 0, 0, 0}, 4};
+        it.ip_dst = v6 ? vcn::Addr{{d.x, d.y, d.z, d.w}, 16} : vcn::Addr{{d.x, 0, 0, 0}, 4};
         lvl = kLvlIp;
     }
     return mirror_eval(img, origin, it, lvl);

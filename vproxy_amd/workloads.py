@@ -309,3 +309,38 @@ def pack(names):
     np.cumsum(lens, out=off[1:])
     blob = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8).copy()
     return blob, off.astype(np.uint32)
+
+
+def gen_vxlan_frames(n, seed):
+    """n distinct VXLAN frames as the vswitch receives them (benchmark
+    templates): 70 % IPv4/TCP (half with SYN-style options), 15 % IPv4/UDP,
+    10 % IPv6/TCP, 5 % ARP; 0-64 payload bytes.  list[bytes]."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        rb = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()
+        payload = rb(int(rng.integers(0, 65)))
+        vx = bytes([8, 0, 0, 0]) + rb(3) + b"\0"
+        eth = rb(12)
+        if r < 0.95:
+            opts = bytes([2, 4, 5, 180, 1, 3, 3, 6, 1, 1, 8, 10]) + rb(8) + bytes([4, 2, 0, 0]) \
+                if (r < 0.70 and rng.random() < 0.5) else b""
+            if r < 0.85 or r >= 0.85 + 0.10:
+                if r < 0.70:
+                    l4 = rb(12) + bytes([((20 + len(opts)) // 4) << 4, 0x18]) + rb(6) + opts + payload
+                    proto = 6
+                else:
+                    l4 = rb(4) + bytes([0, 8 + len(payload) >> 8 & 255]) + rb(2) + payload
+                    proto = 17
+                total = 20 + len(l4)
+                ip = bytes([0x45, 0, total >> 8, total & 255]) + rb(4) + bytes([64, proto]) + \
+                    rb(2) + rb(8)
+                out.append(vx + eth + b"\x08\x00" + ip + l4)
+            else:
+                l4 = rb(12) + bytes([5 << 4, 0x18]) + rb(6) + payload
+                ip = bytes([0x60, 0, 0, 0, len(l4) >> 8, len(l4) & 255, 6, 64]) + rb(32)
+                out.append(vx + eth + b"\x86\xdd" + ip + l4)
+        else:
+            out.append(vx + eth + b"\x08\x06" + bytes([0, 1, 8, 0, 6, 4]) + rb(2) + rb(20))
+    return out
