@@ -13,7 +13,10 @@
  *
  * Pinned by: tests/golden/ fixtures (vectors transcribed from the reference's
  * own JUnit tests TestNetMask, TestRouteTable, TestIpParser, the behavioural
- * tests TestSocks5/TestProtocols/CI, and SURVEY.md Appendix B quirk KATs).
+ * tests TestSocks5/TestProtocols/CI, TestPacket, and SURVEY.md Appendix B
+ * quirk KATs).  ServerGroup source hashing, SSLContextHolder.choose and the
+ * vmirror filters have no reference test: they are pinned by hand-derived
+ * vectors (tests/test_source_cpu.py, test_certs_cpu.py, test_mirror_cpu.py).
  */
 #ifndef VC_ORACLE_H
 #define VC_ORACLE_H
