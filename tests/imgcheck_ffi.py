@@ -28,6 +28,7 @@ def lib():
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
         L.ic_mirror.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
         L.ic_mirror_switch.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp]
+        L.ic_net_match.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
         L.ic_packets.argtypes = [vp, vp, C.c_int64, C.c_int, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
         L.ic_is_ip_literal.argtypes = [C.c_char_p, C.c_int]

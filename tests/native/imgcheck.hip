@@ -234,6 +234,14 @@ int ic_mirror_switch(const vc_mirror_filter* f, int nf, int32_t origin, const ui
     return 0;
 }
 
+// the mirror filters' compiled Network.contains (common/netmatch.h NetMatch)
+int ic_net_match(const uint8_t* in, int inlen, const uint8_t* rule, int rlen, const uint8_t* mask,
+                 int mlen) {
+    const vcn::Addr a = vcn::addr_of(in, inlen);
+    const vcn::NetMatch m = vcn::net_matcher(vcn::addr_of(rule, rlen), vcn::addr_of(mask, mlen));
+    return vcn::net_match(m, a, vcn::low_bits_v6v4(a)) ? 1 : 0;
+}
+
 int ic_is_ipv6(const uint8_t* s, int n) { return d_is_ipv6(s, n) ? 1 : 0; }
 int ic_is_ip_literal(const uint8_t* s, int n) { return d_is_ip_literal(s, n) ? 1 : 0; }
 

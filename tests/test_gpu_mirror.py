@@ -85,3 +85,24 @@ def test_errors(clf):
     clf.compile_mirror([{"origin": "switch", "mirror": 0}])
     with pytest.raises(V.IllegalArgumentException):
         clf.mirror_switch("switch", [b"\0" * 20], layer=4)
+
+
+@pytest.mark.parametrize("shift,pad", [(1, 0), (0, 1400)])
+def test_switch_unstaged(clf, shift, pad):
+    import torch
+    rng = np.random.default_rng(80 + shift)
+    filters, _ = gen_mirror_case(rng, 30, 0, origins=("switch",))
+    frames = [f + bytes(int(rng.integers(0, pad + 1))) if pad else f
+              for f in mirror_frames(rng, 5000)]
+    mf = clf.compile_mirror(filters)
+    oarr = O.mirror_filters(filters, {})
+    oid = mf.id_of("switch", create=False)
+    want = np.array([O.mirror_switch(oarr, len(filters), oid, f, 0) for f in frames], np.uint64)
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    b = np.concatenate([np.zeros(shift, np.uint8), np.frombuffer(b"".join(frames), np.uint8)])
+    blob = torch.from_numpy(b).cuda()[shift:]
+    dev = clf.mirror_switch("switch", (blob, torch.from_numpy(off.astype(np.int32)).cuda()), 0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev.cpu().numpy().view(np.uint64), want)

@@ -82,3 +82,30 @@ def test_parse_then_classify(clf):
                                 res["dport"][ok])
     np.testing.assert_array_equal(idx, want)
     np.testing.assert_array_equal(allow, wv)
+
+
+@pytest.mark.parametrize("shift,pad", [(1, 0), (0, 1400), (3, 1400)])
+def test_unstaged_paths(clf, shift, pad):
+    """The kernel's global-memory parse: an unaligned blob (no LDS stage) and
+    waves of jumbo frames whose span exceeds the per-wave stage."""
+    import torch
+    rng = np.random.default_rng(70 + shift + pad)
+    frames = [f + bytes(int(rng.integers(0, pad + 1))) if pad else f
+              for f in gen_frames(rng, 5000)]
+    want = [O.parse_packet(f, 0) for f in frames]
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    b = np.concatenate([np.zeros(shift, np.uint8), np.frombuffer(b"".join(frames), np.uint8)])
+    blob = torch.from_numpy(b).cuda()[shift:]
+    res = clf.parse_packets((blob, torch.from_numpy(off.astype(np.int32)).cuda()), 0)
+    torch.cuda.synchronize()
+    res = {k: v.cpu().numpy() for k, v in res.items()}
+    for k in ("src6", "dst6"):
+        res[k] = res[k].view(np.uint8)
+    for k in ("src4", "dst4", "vni"):
+        res[k] = res[k].view(np.uint32)
+    for k in ("sport", "dport", "ether_type"):
+        res[k] = res[k].view(np.uint16)
+    for i, w in enumerate(want):
+        assert _rows(res, i) == w, (i, frames[i][:80].hex())

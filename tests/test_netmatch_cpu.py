@@ -2,11 +2,13 @@
 host control plane and the mirror-filter kernels) against the oracle's
 byte-wise restatement (Network.java:183-278) for every length combination,
 with random bytes and the IPv4-compatible / IPv4-mapped prefixes that
-lowBitsV6V4 accepts."""
+lowBitsV6V4 accepts; and the compiled per-input-family form the mirror
+kernels use (NetMatch), run on the host."""
 import ctypes as C
 
 import numpy as np
 
+import imgcheck_ffi as I
 import oracle_ffi as O
 import vproxy_amd as V
 
@@ -49,5 +51,8 @@ def test_mask_match_all_length_cases():
                     buf = (C.c_uint8 * 16).from_buffer_copy(bytes(inp).ljust(16, b"\0"))
                     got = bool(L.vc_net_contains_ip(C.byref(net), buf, inl))
                     assert got == want, (inp.hex(), rule.hex(), mask.hex())
+                    # the mirror kernels' compiled per-family form
+                    got2 = bool(I.lib().ic_net_match(bytes(inp), inl, bytes(rule), rl, mask, ml))
+                    assert got2 == want, ("matcher", inp.hex(), rule.hex(), mask.hex())
                     checked += want
     assert checked > 1000

@@ -156,10 +156,10 @@ struct CertImage {
 };
 
 // ---------------------------------------------------------------------------
-// Mirror filters (vmirror/FilterConfig.java): one 128-byte record per
-// FilterConfig in list order, read wave-uniformly (scalar loads).
-// Addresses / masks as little-endian words of their left-aligned bytes
-// (common/netmatch.h); MACs as the low 48 bits of a u64, byte 0 lowest.
+// Mirror filters (vmirror/FilterConfig.java): one 160-byte record per
+// FilterConfig in list order, staged in LDS and read by all lanes at once.
+// Each network is compiled to its per-input-family masked compare
+// (common/netmatch.h NetMatch); MACs as the low 48 bits of a u64.
 // ---------------------------------------------------------------------------
 #define VC_MF_MAC_X  1u
 #define VC_MF_MAC_Y  2u
@@ -168,15 +168,19 @@ struct CertImage {
 #define VC_MF_PORT_X 16u
 #define VC_MF_PORT_Y 32u
 
-struct MirrorRec {
-    uint32_t net_x_ip[4], net_x_mask[4], net_y_ip[4], net_y_mask[4];
+struct MirrorNet {                 // common/netmatch.h NetMatch, 48 bytes
+    uint32_t m6[4], r6[4];
+    uint32_t low6, m4, r4, pad;
+};
+
+struct MirrorRec {                 // 160 bytes
+    MirrorNet net_x, net_y;        // Network.contains per input family
     uint64_t mac_x, mac_y;
     int32_t origin, mirror, flags, transport, app;
     int32_t port_x0, port_x1, port_y0, port_y1;
-    uint8_t nx_ip_len, nx_mask_len, ny_ip_len, ny_mask_len;
-    uint32_t pad[2];
+    uint32_t pad[3];
 };
-static_assert(sizeof(MirrorRec) == 128, "MirrorRec layout");
+static_assert(sizeof(MirrorRec) == 160, "MirrorRec layout");
 
 struct MirrorImage {
     const MirrorRec* f;

@@ -50,6 +50,56 @@ VC_NM bool mask_match(const Addr& in, const Addr& rule, const Addr& mask) {
     return in.len > rule.len ? low_bits_v6v4(in) : true;
 }
 
+// Network.contains(IP) compiled per input family (common to the mirror
+// filters): maskMatch's case analysis depends only on the three lengths, so
+// for a fixed rule and mask every case reduces to
+//   (in & m) == r  (word-wise)  [&& lowBitsV6V4(in) when `low`]
+// -- "never" is m = 0, r != 0.
+struct NetMatch {
+    uint32_t m6[4], r6[4];        // 16-byte inputs
+    uint32_t low6;                // 16-byte inputs also need lowBitsV6V4(input)
+    uint32_t m4, r4;              // 4-byte inputs
+    uint32_t pad;
+};
+
+VC_NM NetMatch net_matcher(const Addr& rule, const Addr& mask) {
+    NetMatch n{{0, 0, 0, 0}, {0, 0, 0, 0}, 0, 0, 0, 0};
+    // 4-byte input
+    if (rule.len == 4) {                                  // (5): tails, the last mask word
+        n.m4 = last_word(mask);
+        n.r4 = rule.w[0];
+    } else if (mask.len == 16 && low_bits_v6v4(rule)) {   // (3)
+        n.m4 = mask.w[3];
+        n.r4 = rule.w[3];
+    } else {                                              // (2), or (3) failing lowBits
+        n.m4 = 0;
+        n.r4 = 1;
+    }
+    // 16-byte input
+    if (rule.len == 16 && mask.len == 4) {                // (1): first 4 bytes
+        n.m6[0] = mask.w[0];
+        n.r6[0] = rule.w[0];
+    } else if (rule.len == 16) {                          // (5): all 16 bytes
+        for (int k = 0; k < 4; ++k) {
+            n.m6[k] = mask.w[k];
+            n.r6[k] = rule.w[k];
+        }
+    } else {                                              // (4): last 4 bytes + lowBits(input)
+        n.m6[3] = last_word(mask);
+        n.r6[3] = rule.w[0];
+        n.low6 = 1;
+    }
+    return n;
+}
+
+// in.len 4 or 16; in_low = low_bits_v6v4(in) for 16-byte inputs
+VC_NM bool net_match(const NetMatch& n, const Addr& in, bool in_low) {
+    if (in.len == 4) return (in.w[0] & n.m4) == n.r4;
+    const uint32_t d = ((in.w[0] & n.m6[0]) ^ n.r6[0]) | ((in.w[1] & n.m6[1]) ^ n.r6[1]) |
+                       ((in.w[2] & n.m6[2]) ^ n.r6[2]) | ((in.w[3] & n.m6[3]) ^ n.r6[3]);
+    return d == 0 && (!n.low6 || in_low);
+}
+
 VC_NM Addr addr_of(const uint8_t* p, int len) {
     Addr a{{0, 0, 0, 0}, len};
     for (int k = 0; k < len && k < 16; ++k) a.w[k >> 2] |= uint32_t(p[k]) << (8 * (k & 3));

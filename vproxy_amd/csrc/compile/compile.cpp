@@ -10,6 +10,7 @@
 #include <unordered_map>
 
 #include "../common/images.h"
+#include "../common/netmatch.h"
 #include "../host/net.hpp"
 
 namespace vc {
@@ -536,16 +537,18 @@ int build_certs(const char* const* names, const int32_t* name_lens, const int32_
 // (Mirror.java:581-582, 590-591); mirror indices are bits of the result.
 int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out) {
     out->assign(size_t(n), MirrorRec{});
-    auto words = [](const uint8_t* b, int len, uint32_t w[4]) {
-        for (int k = 0; k < 4; ++k) w[k] = 0;
-        for (int k = 0; k < len; ++k) w[k >> 2] |= uint32_t(b[k]) << (8 * (k & 3));
-    };
     auto mac = [](const uint8_t* b) {
         uint64_t v = 0;
         for (int k = 0; k < 6; ++k) v |= uint64_t(b[k]) << (8 * k);
         return v;
     };
     auto len_ok = [](int l) { return l == 4 || l == 16; };
+    auto net = [](const vc_net& v, MirrorNet* o) {
+        const vcn::NetMatch m = vcn::net_matcher(vcn::addr_of(v.ip, v.ip_len),
+                                                 vcn::addr_of(v.mask, v.mask_len));
+        static_assert(sizeof(MirrorNet) == sizeof(vcn::NetMatch), "NetMatch layout");
+        std::memcpy(o, &m, sizeof m);
+    };
     for (int i = 0; i < n; ++i) {
         const vc_mirror_filter& s = f[i];
         MirrorRec& r = (*out)[size_t(i)];
@@ -561,18 +564,8 @@ int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out) 
                   (s.has_port_x ? VC_MF_PORT_X : 0) | (s.has_port_y ? VC_MF_PORT_Y : 0);
         r.mac_x = mac(s.mac_x);
         r.mac_y = mac(s.mac_y);
-        if (s.has_net_x) {
-            words(s.net_x.ip, s.net_x.ip_len, r.net_x_ip);
-            words(s.net_x.mask, s.net_x.mask_len, r.net_x_mask);
-            r.nx_ip_len = uint8_t(s.net_x.ip_len);
-            r.nx_mask_len = uint8_t(s.net_x.mask_len);
-        }
-        if (s.has_net_y) {
-            words(s.net_y.ip, s.net_y.ip_len, r.net_y_ip);
-            words(s.net_y.mask, s.net_y.mask_len, r.net_y_mask);
-            r.ny_ip_len = uint8_t(s.net_y.ip_len);
-            r.ny_mask_len = uint8_t(s.net_y.mask_len);
-        }
+        if (s.has_net_x) net(s.net_x, &r.net_x);
+        if (s.has_net_y) net(s.net_y, &r.net_y);
         r.transport = s.transport;
         r.app = s.app;
         r.port_x0 = s.port_x[0];

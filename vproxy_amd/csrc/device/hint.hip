@@ -12,47 +12,14 @@
 // the whole host; each probe is confirmed by a byte compare.
 #include "hint_dev.h"
 #include "launch.h"
+#include "stage.h"
 
 namespace vcd {
 
 constexpr int kHintBlock = 256;
 constexpr int kWaves = kHintBlock / 64;
 constexpr uint32_t kStageBytes = 4096;   // per wave: 64 names of up to 64 B on average
-constexpr uint32_t kApron = 16;          // readable bytes before and after the names
 constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
-
-// A wave's 64 names are contiguous in the blob: copy them into LDS with
-// coalesced dword loads once, so the per-lane word scans (suffix hashing,
-// key compares) read LDS.  Names then sit at byte kApron + (off[i] - a0) of
-// the wave's stage.  Returns false when the span does not fit.
-__device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uint32_t o1,
-                                           uint32_t* stage, uint32_t* a0_out) {
-    const uint32_t a0 = o0 & ~3u;                  // blob is dword aligned (launcher checks)
-    *a0_out = a0;
-    if (o1 - a0 > kStageBytes) return false;
-    const int lane = int(threadIdx.x & 63);
-    const uint32_t full = (o1 & ~3u) - a0;         // whole dwords inside [a0, o1)
-    const uint32_t* gw = reinterpret_cast<const uint32_t*>(blob + a0);
-    uint32_t* lw = stage + kApron / 4;
-    for (uint32_t k = uint32_t(lane); k < full / 4; k += 64) lw[k] = gw[k];
-    const uint32_t tail = o1 - (o1 & ~3u);
-    if (lane == 0 && tail) {                       // last partial dword, byte loads
-        uint32_t v = 0;
-        for (uint32_t b = 0; b < tail; ++b) v |= uint32_t(blob[(o1 & ~3u) + b]) << (8 * b);
-        lw[full / 4] = v;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    return true;
-}
-
-__device__ __forceinline__ void wave_done() {
-    // every lane has finished reading the staged names before the next copy
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <bool kStage>
 __global__ __launch_bounds__(kHintBlock) void hint_kernel(
@@ -73,7 +40,7 @@ __global__ __launch_bounds__(kHintBlock) void hint_kernel(
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
         const bool staged =
-            kStage && host_blob && stage_wave(host_blob, host_off[base], host_off[last], stage[w], &a0);
+            kStage && host_blob && stage_wave<kStageBytes>(host_blob, host_off[base], host_off[last], stage[w], &a0);
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
             const bool has_host = host_blob && !(host_null && host_null[i]);
@@ -118,7 +85,7 @@ __global__ __launch_bounds__(kHintBlock) void dns_kernel(
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
-        const bool staged = kStage && stage_wave(qblob, qoff[base], qoff[last], stage[w], &a0);
+        const bool staged = kStage && stage_wave<kStageBytes>(qblob, qoff[base], qoff[last], stage[w], &a0);
         if (i < n) {
             const uint32_t a = qoff[i], e = qoff[i + 1];
             uint8_t kd;
@@ -145,7 +112,7 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
-        const bool staged = kStage && stage_wave(blob, off[base], off[last], stage[w], &a0);
+        const bool staged = kStage && stage_wave<kStageBytes>(blob, off[base], off[last], stage[w], &a0);
         if (i < n) {
             const uint32_t a = off[i], e = off[i + 1];
             const bool is_null = null && null[i];

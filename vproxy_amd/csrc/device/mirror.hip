@@ -1,33 +1,19 @@
 // mirror.hip -- traffic-mirror filter kernels (see mirror_dev.h).
 //
 // One lane per item.  The filter list is small and read by every lane of a
-// wave at the same address (uniform loop), so it stays in the scalar cache;
-// the kernels are bound by their item streams.
+// wave at the same address (uniform loop): it is read through the scalar
+// cache into SGPRs (mirror_dev.h load_filter), so the per-filter branches
+// are scalar and the compares take SGPR operands.
 #include "launch.h"
 #include "mirror_dev.h"
+#include "stage.h"
 
 namespace vcd {
 
 constexpr int kMirrorBlock = 256;
-constexpr int kLdsFilters = 128;          // 16 KiB of records staged per workgroup
-
-// The filter records are read by every lane at the same address: staged in
-// LDS once per workgroup they are broadcast reads; a longer list stays in
-// global memory (L2).
-__device__ __forceinline__ MirrorImage stage_filters(const MirrorImage& img, MirrorRec* lds) {
-    if (img.n > kLdsFilters) return img;
-    const uint4* g = reinterpret_cast<const uint4*>(img.f);
-    uint4* l = reinterpret_cast<uint4*>(lds);
-    const int words = img.n * int(sizeof(MirrorRec) / 16);
-    for (int k = threadIdx.x; k < words; k += blockDim.x) l[k] = g[k];
-    __syncthreads();
-    return MirrorImage{lds, img.n};
-}
-
 __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
     MirrorImage img, int32_t origin, vc_mirror_items in, int64_t n, uint64_t* __restrict__ out) {
-    __shared__ MirrorRec lds[kLdsFilters];
-    const MirrorImage fi = stage_filters(img, lds);
+    const MirrorImage& fi = img;
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const MirrorItem it = mirror_item(in, i);
@@ -35,15 +21,36 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
     }
 }
 
+// Frames staged per wave in LDS as in packet.hip (kStage), parsed from there.
+constexpr int kMirrorWaves = kMirrorBlock / 64;
+constexpr uint32_t kMirrorStage = 8192;
+constexpr uint32_t kMirrorStageWords = (kMirrorStage + 2 * kApron) / 4;
+
+template <bool kStage>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     MirrorImage img, int32_t origin, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, int layer, uint64_t* __restrict__ out) {
-    __shared__ MirrorRec lds[kLdsFilters];
-    const MirrorImage fi = stage_filters(img, lds);
-    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t a = off[i], e = off[i + 1];
-        out[i] = mirror_switch_one(fi, origin, blob + a, int(e - a), layer);
+    __shared__ uint32_t stage[kStage ? kMirrorWaves : 1][kStage ? kMirrorStageWords : 1];
+    const MirrorImage& fi = img;
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const int64_t wstride = int64_t(gridDim.x) * kMirrorWaves * 64;
+    for (int64_t base = (int64_t(blockIdx.x) * kMirrorWaves + w) * 64; base < n; base += wstride) {
+        const int64_t i = base + lane;
+        const int64_t last = base + 64 < n ? base + 64 : n;
+        uint32_t a0 = 0;
+        const bool staged =
+            kStage && stage_wave<kMirrorStage>(blob, off[base], off[last], stage[w], &a0);
+        if (i < n) {
+            const uint32_t a = off[i], e = off[i + 1];
+            uint64_t m;
+            if (staged)
+                m = mirror_switch_one(fi, origin, reinterpret_cast<const uint8_t*>(stage[w]) +
+                                                      kApron + (a - a0), int(e - a), layer);
+            else
+                m = mirror_switch_one(fi, origin, blob + a, int(e - a), layer);
+            out[i] = m;
+        }
+        if (kStage) wave_done();
     }
 }
 
@@ -71,8 +78,14 @@ hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int3
                                 const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                                 uint64_t* out) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vcd::mirror_switch_kernel, dim3(mirror_grid(c, n)),
-                       dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer, out);
+    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
+        hipLaunchKernelGGL(vcd::mirror_switch_kernel<true>, dim3(mirror_grid(c, n)),
+                           dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
+                           out);
+    else
+        hipLaunchKernelGGL(vcd::mirror_switch_kernel<false>, dim3(mirror_grid(c, n)),
+                           dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
+                           out);
     return hipGetLastError();
 }
 

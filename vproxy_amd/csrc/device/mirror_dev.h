@@ -20,15 +20,13 @@ enum : int { kLvlEther = 0, kLvlIp = 1, kLvlTransport = 2, kLvlApp = 3 };
 struct MirrorItem {
     uint64_t mac_src, mac_dst;
     vcn::Addr ip_src, ip_dst;       // len 0 = null
+    bool low_src, low_dst;          // lowBitsV6V4 of 16-byte addresses
     int32_t transport, app;         // -1 = null
     int32_t port_src, port_dst;
 };
 
-VC_HD bool mf_contains(const uint32_t ip[4], const uint32_t mask[4], int ip_len, int mask_len,
-                       const vcn::Addr& a) {
-    const vcn::Addr rule{{ip[0], ip[1], ip[2], ip[3]}, ip_len};
-    const vcn::Addr m{{mask[0], mask[1], mask[2], mask[3]}, mask_len};
-    return vcn::mask_match(a, rule, m);
+VC_HD bool mf_contains(const MirrorNet& n, const vcn::Addr& a, bool low) {
+    return vcn::net_match(*reinterpret_cast<const vcn::NetMatch*>(&n), a, low);
 }
 
 VC_HD bool mf_ether(const MirrorRec& f, uint64_t src, uint64_t dst) {           // :27-38
@@ -42,11 +40,11 @@ VC_HD bool mf_ip(const MirrorRec& f, const MirrorItem& it) {                    
     if (!mf_ether(f, it.mac_src, it.mac_dst)) return false;
     const bool x = f.flags & VC_MF_NET_X, y = f.flags & VC_MF_NET_Y;
     if (!x && !y) return true;
-    const bool xs = x && mf_contains(f.net_x_ip, f.net_x_mask, f.nx_ip_len, f.nx_mask_len, it.ip_src);
-    const bool xd = x && mf_contains(f.net_x_ip, f.net_x_mask, f.nx_ip_len, f.nx_mask_len, it.ip_dst);
+    const bool xs = x && mf_contains(f.net_x, it.ip_src, it.low_src);
+    const bool xd = x && mf_contains(f.net_x, it.ip_dst, it.low_dst);
     if (x && y) {
-        const bool ys = mf_contains(f.net_y_ip, f.net_y_mask, f.ny_ip_len, f.ny_mask_len, it.ip_src);
-        const bool yd = mf_contains(f.net_y_ip, f.net_y_mask, f.ny_ip_len, f.ny_mask_len, it.ip_dst);
+        const bool ys = mf_contains(f.net_y, it.ip_src, it.low_src);
+        const bool yd = mf_contains(f.net_y, it.ip_dst, it.low_dst);
         return (xs && yd) || (ys && xd);
     }
     if (x) return xs || xd;
@@ -82,12 +80,23 @@ VC_HD int mirror_level(const MirrorItem& it) {
     return kLvlApp;
 }
 
+// Filter k through the scalar cache: the loop index is wave-uniform, so
+// reading the record through a constant-address-space pointer puts its
+// fields in SGPRs and every branch on them is a scalar branch.
+VC_HD MirrorRec load_filter(const MirrorImage& img, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) MirrorRec* CRec;
+    return ((CRec)(img.f))[k];
+#else
+    return img.f[k];
+#endif
+}
+
 // checkHelper: union of the mirrors of the matching filters of `origin`.
-// The filter loop is uniform across the wave (scalar loads of the records).
 VC_HD uint64_t mirror_eval(const MirrorImage& img, int32_t origin, const MirrorItem& it, int lvl) {
     uint64_t m = 0;
     for (int k = 0; k < img.n; ++k) {
-        const MirrorRec& f = img.f[k];
+        const MirrorRec f = load_filter(img, k);
         if (f.origin != origin) continue;
         bool hit;
         if (lvl == kLvlEther) hit = mf_ether(f, it.mac_src, it.mac_dst);
@@ -124,6 +133,8 @@ VC_HD MirrorItem mirror_item(const vc_mirror_items& in, int64_t i) {
     it.app = in.app ? in.app[i] : -1;
     it.port_src = in.port_src ? in.port_src[i] : 0;
     it.port_dst = in.port_dst ? in.port_dst[i] : 0;
+    it.low_src = vcn::low_bits_v6v4(it.ip_src);
+    it.low_dst = vcn::low_bits_v6v4(it.ip_dst);
     return it;
 }
 
@@ -146,6 +157,8 @@ VC_HD uint64_t mirror_switch_one(const MirrorImage& img, int32_t origin, const u
         const uint4 d = *reinterpret_cast<const uint4*>(o.dst);
         it.ip_src = v6 ? vcn::Addr{{s.x, s.y, s.z, s.w}, 16} : vcn::Addr{{s.x, 0, 0, 0}, 4};
         it.ip_dst = v6 ? vcn::Addr{{d.x, d.y, d.z, d.w}, 16} : vcn::Addr{{d.x, 0, 0, 0}, 4};
+        it.low_src = vcn::low_bits_v6v4(it.ip_src);
+        it.low_dst = vcn::low_bits_v6v4(it.ip_dst);
         lvl = kLvlIp;
     }
     return mirror_eval(img, origin, it, lvl);
