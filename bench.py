@@ -209,7 +209,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
-                    choices=["c5", "c2", "c3", "c4", "dns", "sni", "parse", "source", "mirror"])
+                    choices=["c5", "c2", "c2host", "c3", "c4", "dns", "sni", "parse", "source",
+                             "mirror"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -480,6 +481,24 @@ def sub_bench(args, clf, dev, rank, world):
         o6 = torch.empty(n - n4, dtype=torch.int32, device=dev)
         fn = lambda: (clf.route_v4(q4, out=o4), clf.route_v6(q6, out=o6))
         per_unit, unit = (8 * 0.85 + 20 * 0.15), "B/lookup (v4 4+4, v6 16+4, 85/15 mix)"
+    elif args.workload == "c2host":
+        # the plain (host-buffer) entry point: H2D copy + kernel + D2H copy
+        # per call, from page-locked buffers (vc_host_register)
+        tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+        a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+        b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+        V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
+        n = 64 << 20
+        proto, src, port = W.gen_acl_queries(tcp, udp, n, W.SEED + 16)
+        out = np.empty(n, np.int32)
+        allow = np.empty(n, np.uint8)
+        bufs = (proto, src, port, out, allow)
+        for x in bufs:
+            V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
+        P = lambda x: C.c_void_p(x.ctypes.data)
+        fn = lambda: V.check(V.lib().vc_acl_classify_v4(clf.h, P(proto), P(src), P(port), n,
+                                                          P(out), P(allow)))
+        per_unit, unit = 12, "B/tuple across PCIe (7 in + 5 out), kernel included"
     elif args.workload == "dns":
         groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
         clf.compile_upstream(groups)

@@ -365,6 +365,15 @@ int vc_mirror_switch(vc_ctx *ctx, int32_t origin, const uint8_t *blob, const uin
                      int64_t n, int layer, uint64_t *out_mirrors);
 
 /* ------------------------------------------------------------------------ */
+/* Host buffers                                                             */
+/* ------------------------------------------------------------------------ */
+/* Page-lock a caller buffer (e.g. a Java direct ByteBuffer, once per buffer,
+ * SURVEY.md §8(b) "Buffers") so the plain entry points' copies run as DMA at
+ * the PCIe rate instead of through driver bounce buffers. */
+int vc_host_register(void *p, int64_t bytes);
+int vc_host_unregister(void *p);
+
+/* ------------------------------------------------------------------------ */
 /* Per-rule hit counters (no reference counterpart)          */
 /* ------------------------------------------------------------------------ */
 #define VC_COUNTERS_ACL    0  /* [tcp rules][udp rules][tcp default][udp default] */

@@ -164,6 +164,8 @@ def lib():
         L.vc_compile_certs.argtypes = [vp, P(C.c_char_p), vp, vp, i32, i32]
         L.vc_cert_choose_dev.argtypes = [vp, vp, vp, vp, i64, vp, vp]
         L.vc_cert_choose.argtypes = [vp, vp, vp, vp, i64, vp]
+        L.vc_host_register.argtypes = [vp, i64]
+        L.vc_host_unregister.argtypes = [vp]
         L.vc_compile_mirror.argtypes = [vp, P(VcMirrorFilter), i32]
         L.vc_mirror_match_dev.argtypes = [vp, i32, P(VcMirrorItems), i64, vp, vp]
         L.vc_mirror_match.argtypes = [vp, i32, P(VcMirrorItems), i64, vp]

@@ -139,28 +139,40 @@ int set_dev(vc_ctx* ctx) {
     return e == hipSuccess ? VC_OK : hip_fail(e, "hipSetDevice");
 }
 
-// Synchronous host-pointer staging for the plain (non _dev) entry points.
+// Synchronous host-pointer staging for the plain (non _dev) entry points:
+// stream-ordered allocations from the context's pool (no hipMalloc /
+// hipFree device synchronisation per call), copies on the context stream,
+// freed in stream order when the call returns.
 struct Staging {
-    std::vector<std::unique_ptr<DevBuf>> bufs;
+    hipMemPool_t pool;
+    hipStream_t s;
+    std::vector<void*> bufs;
     hipError_t err = hipSuccess;
-    void* in(const void* h, size_t bytes, hipStream_t s) {
+    Staging(hipMemPool_t p, hipStream_t st) : pool(p), s(st) {}
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    ~Staging() {
+        for (void* p : bufs) (void)hipFreeAsync(p, s);
+    }
+    void* alloc(size_t bytes) {
+        void* p = nullptr;
+        if (err == hipSuccess)
+            err = pool ? hipMallocFromPoolAsync(&p, std::max<size_t>(bytes, 16), pool, s)
+                       : hipMallocAsync(&p, std::max<size_t>(bytes, 16), s);
+        if (err == hipSuccess) bufs.push_back(p);
+        return p;
+    }
+    void* in(const void* h, size_t bytes, hipStream_t) {
         if (!h) return nullptr;
-        auto b = std::make_unique<DevBuf>();
-        if (err == hipSuccess) err = hipMalloc(&b->p, std::max<size_t>(bytes, 16));
-        if (err == hipSuccess && bytes) err = hipMemcpyAsync(b->p, h, bytes, hipMemcpyHostToDevice, s);
-        void* p = b->p;
-        bufs.push_back(std::move(b));
+        void* p = alloc(bytes);
+        if (err == hipSuccess && bytes) err = hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s);
         return p;
     }
     void* out(const void* h, size_t bytes) {
         if (!h) return nullptr;
-        auto b = std::make_unique<DevBuf>();
-        if (err == hipSuccess) err = hipMalloc(&b->p, std::max<size_t>(bytes, 16));
-        void* p = b->p;
-        bufs.push_back(std::move(b));
-        return p;
+        return alloc(bytes);
     }
-    void back(void* h, const void* d, size_t bytes, hipStream_t s) {
+    void back(void* h, const void* d, size_t bytes, hipStream_t) {
         if (h && d && bytes && err == hipSuccess)
             err = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
     }
@@ -334,7 +346,7 @@ static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* dp = static_cast<uint8_t*>(st.in(proto, size_t(n), s));
     auto* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), s);
@@ -418,7 +430,7 @@ static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t*
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     void* dd = st.in(dst, size_t(n) * (fam == 4 ? 4 : 16), s);
     auto* dout = static_cast<int32_t*>(st.out(out, size_t(n) * 4));
@@ -496,7 +508,7 @@ int vc_hint_search(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_o
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     size_t hb = host_blob ? host_off[n] : 0, ub = uri_blob ? uri_off[n] : 0;
     auto* dhb = static_cast<uint8_t*>(host_blob ? st.in(host_blob, hb, s) : nullptr);
@@ -570,7 +582,7 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* db = static_cast<uint8_t*>(st.in(qblob, qoff[n], s));
     auto* dof = static_cast<uint32_t*>(st.in(qoff, size_t(n + 1) * 4, s));
@@ -630,7 +642,7 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!sni_blob || !sni_off || !out_holder) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* db = static_cast<uint8_t*>(st.in(sni_blob, sni_off[n], s));
     auto* dof = static_cast<uint32_t*>(st.in(sni_off, size_t(n + 1) * 4, s));
@@ -642,6 +654,18 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
     st.back(out_holder, dout, size_t(n) * 4, s);
     hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
     return e == hipSuccess ? VC_OK : hip_fail(e, "cert choose");
+}
+
+int vc_host_register(void* p, int64_t bytes) {
+    if (!p || bytes <= 0) return fail(VC_EINVAL, "bad host buffer");
+    hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterDefault);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hipHostRegister");
+}
+
+int vc_host_unregister(void* p) {
+    if (!p) return fail(VC_EINVAL, "bad host buffer");
+    hipError_t e = hipHostUnregister(p);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hipHostUnregister");
 }
 
 // ---------------------------------------------------------------------------
@@ -686,7 +710,7 @@ int vc_mirror_match(vc_ctx* ctx, int32_t origin, const vc_mirror_items* items, i
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!items || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     const size_t un = size_t(n);
     vc_mirror_items d{};
@@ -730,7 +754,7 @@ int vc_mirror_switch(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uin
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!blob || !off || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
     auto* dof = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
@@ -803,7 +827,7 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t hs = ctx->stream;
     auto* dg = static_cast<int32_t*>(st.in(group, size_t(n) * 4, hs));
     void* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), hs);
@@ -857,7 +881,7 @@ int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!blob || !off || !out) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st;
+    Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
     auto* doff = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
