@@ -149,12 +149,17 @@ class RawEvent:
             h.hipEventCreate.argtypes = [C.c_void_p]
             h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
             h.hipEventElapsedTime.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+            h.hipStreamWaitEvent.argtypes = [C.c_void_p, C.c_void_p, C.c_uint]
             RawEvent._hip = h
         self.h = C.c_void_p()
         assert RawEvent._hip.hipEventCreate(C.byref(self.h)) == 0
 
     def record(self, stream):
         assert RawEvent._hip.hipEventRecord(self.h, C.c_void_p(stream.cuda_stream)) == 0
+
+    def wait(self, stream):
+        """`stream` waits for this event (hipStreamWaitEvent)."""
+        assert RawEvent._hip.hipStreamWaitEvent(C.c_void_p(stream.cuda_stream), self.h, 0) == 0
 
     def elapsed_time(self, other):
         ms = C.c_float()
@@ -221,6 +226,11 @@ def main():
                          "counting passes over the outputs (counters_add)")
     ap.add_argument("--serial", action="store_true",
                     help="ablation: one stream, no overlap between consecutive batches")
+    ap.add_argument("--overlap", choices=["finish", "pipeline"], default="pipeline",
+                    help="what the next batch's hostname-pool pass overlaps: the counter finish "
+                         "passes of this batch (it waits for this batch's pipeline kernel), or "
+                         "the pipeline kernel itself (both are bound by the same random "
+                         "gathers)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -289,7 +299,7 @@ def main():
         s_pipe = s_hint = s_cnt = torch.cuda.current_stream()
     else:
         s_pipe, s_hint, s_cnt = (hip_stream(dev) for _ in range(3))
-    ev_hint, ev_pipe, ev_cnt = {}, {}, {}
+    ev_hint, ev_pipe, ev_cnt, kdone = {}, {}, {}, {}
     timing = []                     # (hint, pipe, count) event pairs of timed steps
     TE = lambda: torch.cuda.Event(enable_timing=True)
 
@@ -297,6 +307,8 @@ def main():
         with torch.cuda.stream(s_hint):
             if j - nbuf in ev_pipe:               # pool buffer no longer read
                 s_hint.wait_event(ev_pipe[j - nbuf])
+            if args.overlap == "finish" and j - 1 in kdone:
+                kdone[j - 1].wait(s_hint)          # after the previous pipeline kernel
             e0, e1 = TE(), TE()
             e0.record()
             V.check(V.lib().vc_hint_search_dev(clf.h, C.c_void_p(pool_blob.data_ptr()),
@@ -326,6 +338,7 @@ def main():
             k2.record(s_pipe)
             e1.record()
             ev_pipe[j] = e1
+            kdone[j] = k1
             rec["pipe"] = (k0, k1)
             rec["pipe_call"] = (k1, k2)
 
@@ -368,7 +381,7 @@ def main():
 
     run(0, args.warmup, False)
     torch.cuda.synchronize()
-    ev_hint.clear(); ev_pipe.clear(); ev_cnt.clear()
+    ev_hint.clear(); ev_pipe.clear(); ev_cnt.clear(); kdone.clear()
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -434,7 +447,9 @@ def main():
                            "parallelism": "dp%d" % world,
                            "schedule": ("serial, one stream" if args.serial else
                                         "2 batches in flight: pool / pipeline / counters on "
-                                        "3 HIP streams")},
+                                        "3 HIP streams; the next pool pass overlaps the %s" %
+                                        ("counter finish" if args.overlap == "finish"
+                                         else "pipeline kernel"))},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()
