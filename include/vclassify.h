@@ -367,9 +367,11 @@ int vc_mirror_switch(vc_ctx *ctx, int32_t origin, const uint8_t *blob, const uin
 /* ------------------------------------------------------------------------ */
 /* Host buffers                                                             */
 /* ------------------------------------------------------------------------ */
-/* Page-lock a caller buffer (e.g. a Java direct ByteBuffer, once per buffer,
- * SURVEY.md §8(b) "Buffers") so the plain entry points' copies run as DMA at
- * the PCIe rate instead of through driver bounce buffers. */
+/* Page-lock and map a caller buffer (e.g. a Java direct ByteBuffer, once per
+ * buffer, SURVEY.md §8(b) "Buffers").  When every buffer of a plain ACL /
+ * route / source call is registered, the kernel reads and writes them across
+ * PCIe directly (zero-copy, both directions at once); otherwise the call
+ * copies through device staging in chunks. */
 int vc_host_register(void *p, int64_t bytes);
 int vc_host_unregister(void *p);
 

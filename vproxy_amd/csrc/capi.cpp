@@ -100,6 +100,7 @@ struct ServerSnap : Snapshot {
 struct vc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t lane[2] = {nullptr, nullptr};   // chunked host-buffer calls (host_chunks)
     hipMemPool_t pool = nullptr;   // scratch of the counter passes
     int num_cus = 256;
     std::atomic<bool> counters_on{false};
@@ -203,7 +204,11 @@ int vc_create(int device, vc_ctx** out) {
     c->device = device;
     c->num_cus = prop.multiProcessorCount;
     if ((e = hipSetDevice(device)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->lane[0], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->lane[1], hipStreamNonBlocking)) != hipSuccess) {
+        for (hipStream_t s : {c->stream, c->lane[0], c->lane[1]})
+            if (s) (void)hipStreamDestroy(s);
         delete c;
         return hip_fail(e, "stream create");
     }
@@ -216,6 +221,8 @@ int vc_create(int device, vc_ctx** out) {
     props.location.id = device;
     if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
+        (void)hipStreamDestroy(c->lane[0]);
+        (void)hipStreamDestroy(c->lane[1]);
         delete c;
         return hip_fail(e, "mem pool create");
     }
@@ -239,6 +246,10 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->certs.reset();
     ctx->mirror.reset();
     (void)hipStreamDestroy(ctx->stream);
+    for (hipStream_t s : ctx->lane) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
     if (ctx->pool) {
         // batches may still run on callers' streams: their scratch is freed
         // in stream order, so wait for the device before the pool goes
@@ -341,25 +352,76 @@ int vc_acl_classify_v6_dev(vc_ctx* ctx, const uint8_t* proto, const uint8_t* src
     return acl_dev(ctx, 6, proto, src6, port, n, out_idx, out_allow, stream);
 }
 
+// Host-buffer batches of fixed-size items in chunks: chunk k's upload,
+// kernel and download are ordered on lane k % 2, so one chunk's H2D copy,
+// the next chunk's kernel and the previous chunk's D2H copy overlap (PCIe is
+// full duplex).  Each chunk's staging is freed in stream order right after
+// its download is enqueued, so the pool reuses it for chunk k + 2.
+constexpr int64_t kHostChunk = int64_t(4) << 20;
+
+// Device address of a page-locked, mapped host buffer (vc_host_register),
+// or null for ordinary pageable memory.  Kernels then read their inputs and
+// write their outputs across PCIe directly (both directions at once).
+static void* mapped(const void* h) {
+    if (!h) return nullptr;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, h) != hipSuccess) {
+        (void)hipGetLastError();                 // pageable memory: clear the error
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    return a.devicePointer;
+}
+
+extern "C++" {
+template <class Body>   // int body(Staging&, int64_t lo, int64_t cnt, hipStream_t)
+static int host_chunks(vc_ctx* ctx, int64_t n, const char* what, Body body) {
+    int rc = VC_OK;
+    for (int64_t lo = 0, k = 0; lo < n && rc == VC_OK; lo += kHostChunk, ++k) {
+        hipStream_t s = ctx->lane[k & 1];
+        Staging st(ctx->pool, s);
+        rc = body(st, lo, std::min(kHostChunk, n - lo), s);
+        if (rc == VC_OK && st.err != hipSuccess) rc = hip_fail(st.err, what);
+    }
+    const hipError_t e0 = hipStreamSynchronize(ctx->lane[0]);
+    const hipError_t e1 = hipStreamSynchronize(ctx->lane[1]);
+    if (rc != VC_OK) return rc;
+    const hipError_t e = e0 != hipSuccess ? e0 : e1;
+    return e == hipSuccess ? VC_OK : hip_fail(e, what);
+}
+}  // extern "C++"
+
 static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
                     const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow) {
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    auto* dp = static_cast<uint8_t*>(st.in(proto, size_t(n), s));
-    auto* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), s);
-    auto* dq = static_cast<uint16_t*>(st.in(port, size_t(n) * 2, s));
-    auto* di = static_cast<int32_t*>(st.out(out_idx, size_t(n) * 4));
-    auto* da = static_cast<uint8_t*>(st.out(out_allow, size_t(n)));
-    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
-    rc = acl_dev(ctx, fam, dp, ds, dq, n, di, da, s);
-    if (rc) return rc;
-    st.back(out_idx, di, size_t(n) * 4, s);
-    st.back(out_allow, da, size_t(n), s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "ACL classify");
+    if (!proto || !src || !port || !out_idx) return fail(VC_EINVAL, "bad batch arguments");
+    const size_t sw = fam == 4 ? 4 : 16;
+    void *mp = mapped(proto), *ms = mapped(src), *mq = mapped(port), *mi = mapped(out_idx);
+    void* ma = mapped(out_allow);
+    if (mp && ms && mq && mi && (!out_allow || ma)) {            // zero-copy
+        rc = acl_dev(ctx, fam, static_cast<uint8_t*>(mp), ms, static_cast<uint16_t*>(mq), n,
+                     static_cast<int32_t*>(mi), static_cast<uint8_t*>(ma), ctx->stream);
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        return e == hipSuccess ? VC_OK : hip_fail(e, "ACL classify");
+    }
+    return host_chunks(ctx, n, "ACL classify", [&](Staging& st, int64_t lo, int64_t c,
+                                                   hipStream_t s) {
+        const size_t u = size_t(lo), m = size_t(c);
+        auto* dp = static_cast<uint8_t*>(st.in(proto + u, m, s));
+        auto* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw, s);
+        auto* dq = static_cast<uint16_t*>(st.in(port + u, m * 2, s));
+        auto* di = static_cast<int32_t*>(st.out(out_idx, m * 4));
+        auto* da = static_cast<uint8_t*>(st.out(out_allow, m));
+        if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
+        int r = acl_dev(ctx, fam, dp, ds, dq, c, di, da, s);
+        if (r) return r;
+        st.back(out_idx + u, di, m * 4, s);
+        if (out_allow) st.back(out_allow + u, da, m, s);
+        return VC_OK;
+    });
 }
 
 int vc_acl_classify_v4(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
@@ -430,16 +492,26 @@ static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t*
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    void* dd = st.in(dst, size_t(n) * (fam == 4 ? 4 : 16), s);
-    auto* dout = static_cast<int32_t*>(st.out(out, size_t(n) * 4));
-    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
-    rc = route_dev(ctx, fam, dd, n, dout, s);
-    if (rc) return rc;
-    st.back(out, dout, size_t(n) * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "route lookup");
+    if (!dst || !out) return fail(VC_EINVAL, "bad batch arguments");
+    const size_t sw = fam == 4 ? 4 : 16;
+    void *md = mapped(dst), *mo = mapped(out);
+    if (md && mo) {                                              // zero-copy
+        rc = route_dev(ctx, fam, md, n, static_cast<int32_t*>(mo), ctx->stream);
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        return e == hipSuccess ? VC_OK : hip_fail(e, "route lookup");
+    }
+    return host_chunks(ctx, n, "route lookup", [&](Staging& st, int64_t lo, int64_t c,
+                                                   hipStream_t s) {
+        const size_t u = size_t(lo), m = size_t(c);
+        void* dd = st.in(static_cast<const uint8_t*>(dst) + u * sw, m * sw, s);
+        auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
+        if (st.err != hipSuccess) return VC_OK;
+        int r = route_dev(ctx, fam, dd, c, dout, s);
+        if (r) return r;
+        st.back(out + u, dout, m * 4, s);
+        return VC_OK;
+    });
 }
 
 int vc_route_lookup_v4(vc_ctx* ctx, const uint32_t* dst4, int64_t n, int32_t* out) {
@@ -658,7 +730,7 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
 
 int vc_host_register(void* p, int64_t bytes) {
     if (!p || bytes <= 0) return fail(VC_EINVAL, "bad host buffer");
-    hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterDefault);
+    hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterMapped);
     return e == hipSuccess ? VC_OK : hip_fail(e, "hipHostRegister");
 }
 
@@ -827,17 +899,28 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t hs = ctx->stream;
-    auto* dg = static_cast<int32_t*>(st.in(group, size_t(n) * 4, hs));
-    void* ds = st.in(src, size_t(n) * (fam == 4 ? 4 : 16), hs);
-    auto* dout = static_cast<int32_t*>(st.out(out, size_t(n) * 4));
-    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
-    rc = source_dev(ctx, fam, dg, ds, n, view, dout, hs);
-    if (rc) return rc;
-    st.back(out, dout, size_t(n) * 4, hs);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(hs);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "source select");
+    if (!group || !src || !out) return fail(VC_EINVAL, "bad batch arguments");
+    const size_t sw = fam == 4 ? 4 : 16;
+    void *mg = mapped(group), *ms = mapped(src), *mo = mapped(out);
+    if (mg && ms && mo) {                                        // zero-copy
+        rc = source_dev(ctx, fam, static_cast<int32_t*>(mg), ms, n, view,
+                        static_cast<int32_t*>(mo), ctx->stream);
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        return e == hipSuccess ? VC_OK : hip_fail(e, "source select");
+    }
+    return host_chunks(ctx, n, "source select", [&](Staging& st, int64_t lo, int64_t c,
+                                                    hipStream_t s) {
+        const size_t u = size_t(lo), m = size_t(c);
+        auto* dg = static_cast<int32_t*>(st.in(group + u, m * 4, s));
+        void* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw, s);
+        auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
+        if (st.err != hipSuccess) return VC_OK;
+        int r = source_dev(ctx, fam, dg, ds, c, view, dout, s);
+        if (r) return r;
+        st.back(out + u, dout, m * 4, s);
+        return VC_OK;
+    });
 }
 
 int vc_source_select_v4_dev(vc_ctx* ctx, const int32_t* group, const uint32_t* src4, int64_t n,
