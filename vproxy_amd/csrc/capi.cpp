@@ -322,14 +322,16 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
     return VC_OK;
 }
 
+// `pin`: the snapshot a chunked host call took once for all its chunks
+// (a call classifies against the tables it started with).
 static int acl_dev(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
                    const uint16_t* port, int64_t n, int32_t* out_idx, uint8_t* out_allow,
-                   void* stream) {
+                   void* stream, std::shared_ptr<const AclSnap> pin = nullptr) {
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!proto || !src || !port || !out_idx)))
         return fail(VC_EINVAL, "bad batch arguments");
-    auto s = ctx->get(ctx->acl);
+    auto s = pin ? pin : ctx->get(ctx->acl);
     if (!s) return fail(VC_ESTATE, "no SecurityGroup compiled");
     unsigned long long* cnt = ctx->counters_on ? s->counters : nullptr;
     hipError_t e = fam == 4
@@ -407,6 +409,7 @@ static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
         hipError_t e = hipStreamSynchronize(ctx->stream);
         return e == hipSuccess ? VC_OK : hip_fail(e, "ACL classify");
     }
+    const auto pin = ctx->get(ctx->acl);
     return host_chunks(ctx, n, "ACL classify", [&](Staging& st, int64_t lo, int64_t c,
                                                    hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
@@ -416,7 +419,7 @@ static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
         auto* di = static_cast<int32_t*>(st.out(out_idx, m * 4));
         auto* da = static_cast<uint8_t*>(st.out(out_allow, m));
         if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
-        int r = acl_dev(ctx, fam, dp, ds, dq, c, di, da, s);
+        int r = acl_dev(ctx, fam, dp, ds, dq, c, di, da, s, pin);
         if (r) return r;
         st.back(out_idx + u, di, m * 4, s);
         if (out_allow) st.back(out_allow + u, da, m, s);
@@ -462,11 +465,12 @@ int vc_compile_routes(vc_ctx* ctx, const vc_net* v4, int n4, const vc_net* v6, i
     return VC_OK;
 }
 
-static int route_dev(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t* out, void* stream) {
+static int route_dev(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t* out, void* stream,
+                     std::shared_ptr<const RouteSnap> pin = nullptr) {
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!dst || !out))) return fail(VC_EINVAL, "bad batch arguments");
-    auto s = ctx->get(ctx->route);
+    auto s = pin ? pin : ctx->get(ctx->route);
     if (!s) return fail(VC_ESTATE, "no RouteTable compiled");
     unsigned long long* cnt = ctx->counters_on ? s->counters : nullptr;
     const int64_t nn = int64_t(s->n4) + s->n6;
@@ -501,13 +505,14 @@ static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t*
         hipError_t e = hipStreamSynchronize(ctx->stream);
         return e == hipSuccess ? VC_OK : hip_fail(e, "route lookup");
     }
+    const auto pin = ctx->get(ctx->route);
     return host_chunks(ctx, n, "route lookup", [&](Staging& st, int64_t lo, int64_t c,
                                                    hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
         void* dd = st.in(static_cast<const uint8_t*>(dst) + u * sw, m * sw, s);
         auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
         if (st.err != hipSuccess) return VC_OK;
-        int r = route_dev(ctx, fam, dd, c, dout, s);
+        int r = route_dev(ctx, fam, dd, c, dout, s, pin);
         if (r) return r;
         st.back(out + u, dout, m * 4, s);
         return VC_OK;
@@ -880,7 +885,8 @@ int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers
 }
 
 static int source_dev(vc_ctx* ctx, int fam, const int32_t* group, const void* src, int64_t n,
-                      int view, int32_t* out, void* stream) {
+                      int view, int32_t* out, void* stream,
+                      std::shared_ptr<const ServerSnap> pin = nullptr) {
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!group || !src || !out))) return fail(VC_EINVAL, "bad batch arguments");
@@ -888,7 +894,7 @@ static int source_dev(vc_ctx* ctx, int fam, const int32_t* group, const void* sr
         return fail(VC_EINVAL, "view must be VC_SOURCE_ALL, _IPV4 or _IPV6");
     if (fam == 6 && (reinterpret_cast<uintptr_t>(src) & 15))
         return fail(VC_EINVAL, "IPv6 addresses must be 16-byte aligned");
-    auto s = ctx->get(ctx->servers);
+    auto s = pin ? pin : ctx->get(ctx->servers);
     if (!s) return fail(VC_ESTATE, "no servers compiled");
     hipError_t e = vc::launch_source(ctx->cfg(stream), s->img, group, src, fam, n, view, out);
     return e == hipSuccess ? VC_OK : hip_fail(e, "source launch");
@@ -909,6 +915,7 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
         hipError_t e = hipStreamSynchronize(ctx->stream);
         return e == hipSuccess ? VC_OK : hip_fail(e, "source select");
     }
+    const auto pin = ctx->get(ctx->servers);
     return host_chunks(ctx, n, "source select", [&](Staging& st, int64_t lo, int64_t c,
                                                     hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
@@ -916,7 +923,7 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
         void* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw, s);
         auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
         if (st.err != hipSuccess) return VC_OK;
-        int r = source_dev(ctx, fam, dg, ds, c, view, dout, s);
+        int r = source_dev(ctx, fam, dg, ds, c, view, dout, s, pin);
         if (r) return r;
         st.back(out + u, dout, m * 4, s);
         return VC_OK;
