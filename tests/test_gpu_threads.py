@@ -55,7 +55,9 @@ def test_concurrent_classify_and_recompile():
         t.start()
     for i in range(12):
         compile_(i % 2)
-    while len(calls) < 6 and not errors:         # classify calls overlapped the recompiles
+    for _ in range(400):                          # classify calls overlapped the recompiles
+        if len(calls) >= 6 or errors:
+            break
         compile_(len(calls) % 2)
     stop.set()
     for t in threads:

@@ -190,6 +190,55 @@ __global__ __launch_bounds__(kBlock) void route_v4_kernel_scalar(
         route_emit(trie_v4(nodes, rb, dst[i]), out + i);
 }
 
+// 4 IPv6 lookups per lane: the trie walk is a chain of dependent gathers
+// (root, then one 8-bit stride per level down to /48 or /64), so four
+// independent walks advance level by level together to keep four gathers in
+// flight per lane.
+__global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
+    const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
+    int32_t* __restrict__ out) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    const int64_t n4 = n >> 2;
+    const uint32_t root = 1u << rb;
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
+        uint64_t hi[4], lo[4];
+        uint32_t e[4];
+        int bits[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v6_key(reinterpret_cast<const uint4*>(dst6)[4 * g + k], &hi[k], &lo[k]);
+            bits[k] = rb;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = nodes[hi[k] >> (64 - rb)];
+        for (;;) {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (e[k] & VC_PTR) {
+                    const uint32_t sub = bits[k] < 64 ? uint32_t(hi[k] >> (56 - bits[k])) & 255u
+                                                      : uint32_t(lo[k] >> (120 - bits[k])) & 255u;
+                    e[k] = nodes[root + (e[k] & ~VC_PTR) * 256u + sub];
+                    bits[k] += 8;
+                    any = true;
+                }
+            }
+            if (!any) break;
+        }
+        int4 o;
+        int32_t* op = reinterpret_cast<int32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) route_emit(e[k], op + k);
+        reinterpret_cast<int4*>(out)[g] = o;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const int64_t i = (n4 << 2) + threadIdx.x;
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(dst6)[i], &hi, &lo);
+        route_emit(trie_v6(nodes, rb, hi, lo), out + i);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void route_v6_kernel(
     const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
     int32_t* __restrict__ out) {
@@ -502,8 +551,12 @@ hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t
                            int64_t none_at) {
     if (n <= 0) return hipSuccess;
     if (!aligned(dst6, 16)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vcd::route_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
-                       c.stream, t.nodes, t.root_bits, dst6, n, out);
+    if (aligned(out, 16))
+        hipLaunchKernelGGL(vcd::route_v6_kernel_x4, dim3(grid_for(c, (n + 3) / 4, 8)),
+                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.root_bits, dst6, n, out);
+    else
+        hipLaunchKernelGGL(vcd::route_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
+                           c.stream, t.nodes, t.root_bits, dst6, n, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, t.n_rules, rule_base, none_at, 0,
