@@ -4,6 +4,9 @@
 // items per lane per step (16-byte address loads, 4-byte proto loads, 8-byte
 // port loads, 16-byte index stores); the ACL interval boundaries are staged
 // in LDS once per workgroup of a grid-stride (persistent-style) launch.
+#include <map>
+#include <mutex>
+
 #include "acl_dev.h"
 #include "launch.h"
 #include "route_dev.h"
@@ -461,6 +464,26 @@ namespace {
 // LDS budget for the staged v4 ACL boundaries (words); above it the kernel
 // searches the boundaries in global memory (L2-resident).
 constexpr int kLdsWords = 30 * 1024;
+
+}  // namespace
+
+int resident_per_cu(const void* kernel, int block, size_t shmem) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, size_t>, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({kernel, shmem});
+    if (it != cache.end()) return it->second;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, shmem) != hipSuccess ||
+        per_cu < 1) {
+        (void)hipGetLastError();
+        per_cu = 1;
+    }
+    cache[{kernel, shmem}] = per_cu;
+    return per_cu;
+}
+
+namespace {
 
 int grid_for(const LaunchCfg& c, int64_t work_items, int blocks_per_cu) {
     int64_t want = (work_items + vcd::kBlock - 1) / vcd::kBlock;

@@ -131,14 +131,16 @@ namespace vc {
 hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
                         const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out) {
     if (n <= 0) return hipSuccess;
-    int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    int64_t cap = int64_t(c.num_cus) * 8;
-    int grid = int(want < cap ? want : cap);
+    const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
     if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::cert_kernel<true>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::cert_kernel<true>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<true>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            certs, blob, off, null, n, out);
     else
-        hipLaunchKernelGGL(vcd::cert_kernel<false>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::cert_kernel<false>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<false>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            certs, blob, off, null, n, out);
     return hipGetLastError();
 }
@@ -148,15 +150,17 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                        const uint8_t* uri_blob, const uint32_t* uri_off, const uint8_t* uri_null,
                        int64_t n, int32_t* out, unsigned long long* counters) {
     if (n <= 0) return hipSuccess;
-    int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    int64_t cap = int64_t(c.num_cus) * 8;
-    int grid = int(want < cap ? want : cap);
+    const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
     if (host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::hint_kernel<true>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::hint_kernel<true>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out);
     else
-        hipLaunchKernelGGL(vcd::hint_kernel<false>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::hint_kernel<false>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<false>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out);
     hipError_t e = hipGetLastError();
@@ -169,14 +173,16 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
                       const uint8_t* qblob, const uint32_t* qoff, int64_t n, uint8_t* kind,
                       int32_t* value, unsigned long long* group_counters) {
     if (n <= 0) return hipSuccess;
-    int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    int64_t cap = int64_t(c.num_cus) * 8;
-    int grid = int(want < cap ? want : cap);
+    const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
     if ((reinterpret_cast<uintptr_t>(qblob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::dns_kernel<true>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::dns_kernel<true>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<true>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value);
     else
-        hipLaunchKernelGGL(vcd::dns_kernel<false>, dim3(grid), dim3(vcd::kHintBlock), 0, c.stream,
+        hipLaunchKernelGGL(vcd::dns_kernel<false>,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<false>), vcd::kHintBlock, 0, want)),
+                           dim3(vcd::kHintBlock), 0, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !group_counters) return e;

@@ -20,6 +20,20 @@ struct LaunchCfg {
     hipMemPool_t pool = nullptr;   // scratch pool (stream-ordered), null = device default
 };
 
+// Workgroups per CU that can be resident at once for `kernel` (occupancy
+// query, cached per kernel).
+int resident_per_cu(const void* kernel, int block, size_t shmem);
+
+// Grid of a grid-stride kernel: as many workgroups as fit the device at
+// once (every workgroup starts in the first round; a larger grid leaves a
+// partial second round), and no more than the work needs.
+inline int resident_grid(const LaunchCfg& c, const void* kernel, int block, size_t shmem,
+                         int64_t want_blocks) {
+    const int64_t cap = int64_t(c.num_cus) * resident_per_cu(kernel, block, shmem);
+    if (want_blocks < 1) want_blocks = 1;
+    return int(want_blocks < cap ? want_blocks : cap);
+}
+
 // Stream-ordered scratch allocation from the context's pool.
 inline hipError_t scratch_alloc(const LaunchCfg& c, void** p, size_t bytes) {
     return c.pool ? hipMallocFromPoolAsync(p, bytes, c.pool, c.stream)

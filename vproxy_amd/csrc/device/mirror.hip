@@ -59,17 +59,17 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
 namespace vc {
 
 namespace {
-int mirror_grid(const LaunchCfg& c, int64_t n) {
-    int64_t want = (n + vcd::kMirrorBlock - 1) / vcd::kMirrorBlock;
-    const int64_t cap = int64_t(c.num_cus) * 8;
-    return int(want < cap ? want : cap);
+template <class K>
+int mirror_grid(const LaunchCfg& c, K kernel, int64_t n) {
+    return resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kMirrorBlock, 0,
+                         (n + vcd::kMirrorBlock - 1) / vcd::kMirrorBlock);
 }
 }  // namespace
 
 hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
                                const vc_mirror_items& in, int64_t n, uint64_t* out) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vcd::mirror_match_kernel, dim3(mirror_grid(c, n)),
+    hipLaunchKernelGGL(vcd::mirror_match_kernel, dim3(mirror_grid(c, vcd::mirror_match_kernel, n)),
                        dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, in, n, out);
     return hipGetLastError();
 }
@@ -79,11 +79,13 @@ hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int3
                                 uint64_t* out) {
     if (n <= 0) return hipSuccess;
     if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::mirror_switch_kernel<true>, dim3(mirror_grid(c, n)),
+        hipLaunchKernelGGL(vcd::mirror_switch_kernel<true>,
+                           dim3(mirror_grid(c, vcd::mirror_switch_kernel<true>, n)),
                            dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
                            out);
     else
-        hipLaunchKernelGGL(vcd::mirror_switch_kernel<false>, dim3(mirror_grid(c, n)),
+        hipLaunchKernelGGL(vcd::mirror_switch_kernel<false>,
+                           dim3(mirror_grid(c, vcd::mirror_switch_kernel<false>, n)),
                            dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
                            out);
     return hipGetLastError();

@@ -77,9 +77,11 @@ hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_
                           int layer, const vc_pkt_out& out) {
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kPktBlock - 1) / vcd::kPktBlock;
-    const int64_t cap = int64_t(c.num_cus) * 8;
-    const int grid = int(want < cap ? want : cap);
-    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
+    const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
+    const void* k = stage ? reinterpret_cast<const void*>(vcd::packet_kernel<true>)
+                          : reinterpret_cast<const void*>(vcd::packet_kernel<false>);
+    const int grid = resident_grid(c, k, vcd::kPktBlock, 0, want);
+    if (stage)
         hipLaunchKernelGGL(vcd::packet_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
                            blob, off, n, layer, out);
     else

@@ -78,9 +78,11 @@ hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32
                          const void* src, int family, int64_t n, int view, int32_t* out) {
     if (n <= 0) return hipSuccess;
     const int vi = view == VC_SOURCE_IPV4 ? 1 : (view == VC_SOURCE_IPV6 ? 2 : 0);
-    int64_t want = (n + vcd::kSelBlock - 1) / vcd::kSelBlock;
-    const int64_t cap = int64_t(c.num_cus) * 8;
-    const int grid = int(want < cap ? want : cap);
+    const int64_t want = (n + vcd::kSelBlock - 1) / vcd::kSelBlock;
+    const int grid = resident_grid(c, family == 4
+                                          ? reinterpret_cast<const void*>(vcd::source_v4_kernel)
+                                          : reinterpret_cast<const void*>(vcd::source_v6_kernel),
+                                   vcd::kSelBlock, 0, want);
     if (family == 4)
         hipLaunchKernelGGL(vcd::source_v4_kernel, dim3(grid), dim3(vcd::kSelBlock), 0, c.stream, img,
                            group, static_cast<const uint32_t*>(src), n, vi, out);
