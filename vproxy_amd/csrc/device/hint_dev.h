@@ -233,14 +233,26 @@ VC_HD uint32_t rec_word(const Rec& r, int j) {       // j < 12, unrolled callers
     return k[j];
 }
 
+// True on the device when any active lane of the wave has p (a wave vote,
+// so an unrolled loop can stop at the wave's longest key).
+VC_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(p) != 0;
+#else
+    return p;
+#endif
+}
+
 // record key == query bytes [st, st + n)?
 template <class Src>
 VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n) {
     if ((r.m.x & ~VC_REC_HAS_PM) != uint32_t(n)) return false;
     uint32_t diff = 0;
 #pragma unroll
-    for (int j = 0; j < VC_REC_INLINE / 4; ++j)
+    for (int j = 0; j < VC_REC_INLINE / 4; ++j) {
+        if (!wave_any(4 * j < n)) break;          // no lane's key reaches word j
         if (4 * j < n) diff |= q.word(st + 4 * j, st, st + n) ^ rec_word(r, j);
+    }
     if (diff) return false;
     if (n > VC_REC_INLINE) {      // long key: the rest from the blob copy
         const uint32_t* kw = reinterpret_cast<const uint32_t*>(blob + r.m.w);
@@ -465,10 +477,17 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         uint4 g[kProbes];
 #pragma unroll
         for (int k = 0; k < kProbes; ++k)    // all first tag groups in flight together
-            g[k] = k <= np ? tag_group(t.tags, t.mask, h[k]) : make_uint4(0, 0, 0, 0);
+            g[k] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < kProbes; ++k)
-            if (group_hits(g[k], h[k] | 1u)) hits |= 1u << k;
+        for (int k = 0; k < kProbes; ++k) {
+            if (!wave_any(k <= np)) break;    // no lane has a k-th suffix
+            if (k <= np) g[k] = tag_group(t.tags, t.mask, h[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kProbes; ++k) {
+            if (!wave_any(k <= np)) break;
+            if (k <= np && group_hits(g[k], h[k] | 1u)) hits |= 1u << k;
+        }
     }
     uint32_t best = VC_NONE;
     while (hits) {
