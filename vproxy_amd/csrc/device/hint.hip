@@ -20,9 +20,14 @@ constexpr int kHintBlock = 256;
 constexpr int kWaves = kHintBlock / 64;
 constexpr uint32_t kStageBytes = 4096;   // per wave: 64 names of up to 64 B on average
 constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
+// Minimum waves per SIMD for hint_kernel: 5 holds it at 96 VGPRs (no spills);
+// unbounded it takes 97, which rounds to 104 and leaves 4 waves per SIMD.
+#ifndef VC_HINT_MINW
+#define VC_HINT_MINW 5
+#endif
 
 template <bool kStage>
-__global__ __launch_bounds__(kHintBlock) void hint_kernel(
+__global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
     const uint8_t* __restrict__ uri_blob, const uint32_t* __restrict__ uri_off,
