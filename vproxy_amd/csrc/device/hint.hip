@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
 }
 
 template <bool kStage>
-__global__ __launch_bounds__(kHintBlock) void dns_kernel(
+__global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
     int32_t* __restrict__ value) {
