@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: M classifications/s (ACL + route + host) per BASELINE.json.
 
-Default workload (`--workload c5`, SURVEY.md §8(d) C5, per-GPU shard, weak
-scaling): every rank holds the replicated tables
+Default workload (`--workload c5`, SURVEY.md §8(d) C5, weak scaling): every
+rank holds the replicated tables
     SecurityGroup   10k rules with port ranges (C2 generator)
     RouteTable      ~1M IPv4 + 200k IPv6 prefixes inserted shortest-first (C3)
     Upstream        100k hint-host groups (C4), hostname pool of 16M
-and classifies, per step, 125M IPv4 packets resident in HBM:
+and, per step, classifies its shard of one seeded global batch of
+N = packets_per_gpu x world IPv4 packets (dist.shard: contiguous slices; the
+packet generator is index-addressable, so rank r's slice is the same packets
+whatever the world size), resident in HBM:
     1. the hostname pool once (Upstream.searchForGroup per hostname)
     2. the fused pipeline kernel per packet: SecurityGroup.allow(src, dport)
        -> RouteTable.lookup(dst) -> pool group of the packet's host id
-    3. per-rule hit counters (ACL, route, group), RCCL all-reduce when N > 1.
+    3. per-rule hit counters (ACL, route, group), one RCCL all-reduce per
+       batch when N > 1 (or with --dist on one GPU).
 A "classification" is one packet through all three.  Inputs are synthetic
 and generated on the device; nothing is cached between steps.
 
-Other workloads (c2, c3, c4) time one classifier alone for DESIGN.md.
+Other workloads (c1, c2, c2host, c3, c4, mix, ...) time one classifier alone
+for DESIGN.md / BASELINE.md, each with its own roofline and CPU baseline.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
@@ -25,6 +30,7 @@ import json
 import os
 import sys
 import time
+import types
 
 import numpy as np
 import torch
@@ -34,11 +40,12 @@ sys.path.insert(0, ROOT)
 
 import vproxy_amd as V  # noqa: E402
 from vproxy_amd import workloads as W  # noqa: E402
-from vproxy_amd.dist import HitCounterBucket  # noqa: E402
+from vproxy_amd.dist import HitCounterBucket, shard  # noqa: E402
 
 METRIC = "M classifications/sec (ACL+LPM+host) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 PROFILES = os.path.join(ROOT, "profiles")
+PACKET_SEED = 1234
 
 
 def log(*a):
@@ -47,45 +54,80 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------
-# device-side synthetic inputs
+# index-addressable synthetic packets (torch, any device)
 # ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _s64(c):
+    c &= _M64
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+_GOLD, _C1, _C2 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+
+def _lsr(x, k):
+    """logical right shift of an int64 tensor"""
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def hash_u32(idx, seed, stream):
+    """splitmix64 finaliser of (item index, seed, stream) -> uint32 in an
+    int64 tensor.  Item i's fields depend on i only, so any slice of the
+    global batch can be generated on its own (sharding)."""
+    x = idx * _GOLD + _s64(seed * 0x100000001B3 + stream * 0xD6E8FEB86659FD93)
+    x = (x ^ _lsr(x, 30)) * _C1
+    x = (x ^ _lsr(x, 27)) * _C2
+    return (x ^ _lsr(x, 31)) & 0xFFFFFFFF
+
+
+def below(u, m):
+    """uint32 u -> uniform integer in [0, m) (m a python int or int64 tensor < 2^31)"""
+    return (u * m) >> 32
+
+
 def dev_u32(x):
     """int64 tensor holding uint32 values -> int32 tensor with the same bits."""
     x = x & 0xFFFFFFFF
     return torch.where(x >= 2**31, x - 2**32, x).to(torch.int32)
 
 
-def gen_packets(n, tcp, udp, net, plen, pool_n, seed, dev):
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    ri = lambda lo, hi, k: torch.randint(lo, hi, (k,), generator=g, device=dev, dtype=torch.int64)
-    proto = torch.where(ri(0, 2, n) == 0, 6, 17).to(torch.uint8)
-    src = ri(0, 2**32, n)
-    port = ri(0, 65536, n)
-    pick = ri(0, 2, n) == 0
-    # half the packets hit a rule of their protocol (network + port range)
-    for p, rules in ((6, tcp), (17, udp)):
+def gen_packets(lo, n, t, pool_n, seed=PACKET_SEED, dev="cpu"):
+    """Items [lo, lo + n) of the seeded global packet batch: proto (50/50
+    TCP/UDP), src, dst, dport, host id.  Half the packets hit a random ACL
+    rule of their protocol (network + port range); 90 % of destinations lie
+    inside a random route prefix; host ids are uniform over the pool.
+    Returns (proto u8, src i32, dst i32, dport i16, host_id i32) tensors
+    (uint32 bits in the signed types)."""
+    idx = torch.arange(lo, lo + n, device=dev, dtype=torch.int64)
+    h = lambda s: hash_u32(idx, seed, s)
+    proto = torch.where((h(1) & 1) == 0, 6, 17).to(torch.uint8)
+    src = h(2)
+    port = h(3) & 0xFFFF
+    pick = (h(4) & 1) == 0
+    for p, rules in ((6, t.tcp), (17, t.udp)):
+        if len(rules) == 0:
+            continue
         ip, mk = W.rule_v4_fields(rules)
         ipd = torch.from_numpy(ip.astype(np.int64)).to(dev)
         mkd = torch.from_numpy(mk.astype(np.int64)).to(dev)
-        lo = torch.from_numpy(rules["min_port"].astype(np.int64)).to(dev)
-        hi = torch.from_numpy(rules["max_port"].astype(np.int64)).to(dev)
-        r = ri(0, len(rules), n)
+        plo = torch.from_numpy(rules["min_port"].astype(np.int64)).to(dev)
+        phi = torch.from_numpy(rules["max_port"].astype(np.int64)).to(dev)
+        r = below(h(5 + p), len(rules))
         sel = pick & (proto == p)
         src = torch.where(sel, ipd[r] | (src & (~mkd[r] & 0xFFFFFFFF)), src)
-        span = hi[r] - lo[r] + 1
-        port = torch.where(sel, lo[r] + (ri(0, 2**31, n) % span), port)
-        del r, span
-    # 90 % of destinations inside a route prefix
-    netd = torch.from_numpy(net.astype(np.int64)).to(dev)
-    mkd = torch.from_numpy(W._mask32(plen).astype(np.int64)).to(dev)
-    r = ri(0, len(net), n)
-    dst = ri(0, 2**32, n)
-    dst = torch.where(ri(0, 10, n) < 9, netd[r] | (dst & (~mkd[r] & 0xFFFFFFFF)), dst)
-    hid = ri(0, pool_n, n)
-    out = (proto, dev_u32(src), dev_u32(dst), port.to(torch.int32).to(torch.int16),
-           hid.to(torch.int32))
-    return out
+        port = torch.where(sel, plo[r] + below(h(40 + p), phi[r] - plo[r] + 1), port)
+        del r, sel
+    netd = torch.from_numpy(t.net.astype(np.int64)).to(dev)
+    mkd = torch.from_numpy(W._mask32(t.plen).astype(np.int64)).to(dev)
+    r = below(h(30), len(t.net))
+    dst = h(31)
+    dst = torch.where(below(h(32), 10) < 9, netd[r] | (dst & (~mkd[r] & 0xFFFFFFFF)), dst)
+    del r
+    hid = below(h(33), pool_n)
+    return (proto, dev_u32(src), dev_u32(dst), port.to(torch.int32).to(torch.int16),
+            hid.to(torch.int32))
 
 
 def gather_strings_dev(blob, off, idx, dev):
@@ -106,37 +148,42 @@ def gather_strings_dev(blob, off, idx, dev):
 
 
 # ---------------------------------------------------------------------------
-# CPU baseline (oracle, test-infrastructure C restatement of the Java scans)
+# C5 tables (replicated on every rank; also built by tests/test_gpu_c5.py)
 # ---------------------------------------------------------------------------
-def cpu_baseline_c5(tcp, udp, v4_list, groups, names_blob, names_off, seed, threads,
-                    budget_s=12.0):
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ffi as O
-    og = O.Groups(groups)
+def c5_rule_tables(acl_rules=10000, v4=1_000_000, v6=200_000, groups=100_000):
+    """Host-side C5 rule lists (no device): the SecurityGroup lists, the
+    route prefixes, the Upstream groups and the hostname source."""
+    t = types.SimpleNamespace()
+    t.tcp, t.udp = W.gen_sg_rules(acl_rules, W.SEED + 2, p_range=0.3)
+    t.net, t.plen = W.gen_v4_prefixes(v4, W.SEED + 3)
+    t.hi, t.lo, t.p6 = W.gen_v6_prefixes(v6, W.SEED + 4)
+    t.groups, t.ghosts = W.gen_groups(groups, W.SEED + 5)
+    names = W.gen_hostnames(t.ghosts, 1 << 20, W.SEED + 6)           # distinct pool source
+    t.nblob, t.noff = W.pack(names)
+    return t
 
-    def run(n):
-        proto, src, port = W.gen_acl_queries(tcp, udp, n, seed)
-        dst = W.v4_lookups(v4_ip, v4_plen, n, seed + 1)
-        hid = np.random.default_rng(seed + 2).integers(0, len(names_off) - 1, n)
-        sub_blob, sub_off = W.pack([bytes(names_blob[names_off[i]:names_off[i + 1]]) for i in hid])
-        t0 = time.perf_counter()
-        O.sg_batch_v4_np(tcp, udp, False, proto, src, port, nthreads=threads)
-        O.rt_batch_v4_np(v4_list, dst, nthreads=threads)
-        O.hint_batch_np(og, sub_blob, sub_off, None, nthreads=threads)
-        return time.perf_counter() - t0
 
-    v4_ip = v4_list["ip"][:, :4].copy().view(">u4").reshape(-1).astype(np.uint32)
-    v4_plen = np.array([bin(int(x)).count("1") for x in
-                        v4_list["mask"][:, :4].copy().view(">u4").reshape(-1)])
-    probe = max(threads * 4, 64)
-    t = run(probe)
-    n = int(min(65536, max(probe, probe * budget_s / max(t, 1e-6))))
-    t = run(n)
-    return {"value": n / t / 1e6, "unit": "M classifications/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d packets of the same C5 workload (ACL 10k rules + RouteTable %d IPv4 "
-                      "rules + Upstream %d groups), oracle linear scans as the Java code does "
-                      "them, %d threads, %.1f s" % (n, len(v4_list), len(groups), threads, t)}
+def c5_tables(clf, dev, pool_n=16 << 20, **kw):
+    """Compile the C5 tables into `clf` exactly as the benchmark does and
+    build the device hostname pool (same on every rank)."""
+    t = c5_rule_tables(**kw)
+    a, na, ka = W.as_ctypes(t.tcp, V._lib.VcAclRule)
+    b, nb, kb = W.as_ctypes(t.udp, V._lib.VcAclRule)
+    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
+    rt = V.RouteTable()
+    allnets = np.concatenate([W.v4_nets(t.net, t.plen), W.v6_nets(t.hi, t.lo, t.p6)])
+    arr, n_all, keep = W.as_ctypes(allnets, V._lib.VcNet)
+    rt.add_rules("bgp", arr, n=n_all)
+    clf.compile_route_table(rt)
+    a4, t.n4 = rt.rules_raw(4)
+    a6, t.n6 = rt.rules_raw(6)
+    t.v4_list = np.frombuffer(bytes(a4)[:t.n4 * 40], W.NET_DT)
+    t.v6_list = np.frombuffer(bytes(a6)[:t.n6 * 40], W.NET_DT)
+    clf.compile_upstream(t.groups)
+    t.pool_n = pool_n
+    t.pidx = np.random.default_rng(W.SEED + 7).integers(0, len(t.noff) - 1, pool_n)
+    t.pool_blob, t.pool_off, t.pool_bytes = gather_strings_dev(t.nblob, t.noff, t.pidx, dev)
+    return t
 
 
 class RawEvent:
@@ -150,6 +197,7 @@ class RawEvent:
             h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
             h.hipEventElapsedTime.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
             h.hipStreamWaitEvent.argtypes = [C.c_void_p, C.c_void_p, C.c_uint]
+            h.hipEventDestroy.argtypes = [C.c_void_p]
             RawEvent._hip = h
         self.h = C.c_void_p()
         assert RawEvent._hip.hipEventCreate(C.byref(self.h)) == 0
@@ -179,6 +227,220 @@ def hip_stream(dev):
     return torch.cuda.ExternalStream(h.value, device=dev)
 
 
+class C5Steps:
+    """The C5 step schedule on one rank.
+
+    Step j = hint(j): classify the hostname pool; pipe(j): the fused
+    pipeline kernel over this rank's packets (it counts ACL hits and
+    route/group buckets; the library finishes the two large counter spaces
+    on the counting stream); counters(j): when `bucket`, copy the library's
+    three counter arrays into one int64 bucket (device-to-device on the
+    counting stream) and all-reduce it (RCCL).  Two batches in flight:
+    outputs and pool results are double-buffered, so batch j+1's pool pass
+    and pipeline overlap batch j's counter finish.  Every step still does
+    all of its work between the caller's synchronisations.
+    """
+
+    def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
+                 finish="stream"):
+        self.clf, self.t, self.dev = clf, t, dev
+        self.proto, self.src, self.dst, self.dport, self.hid = packets
+        self.B = len(self.src)
+        self.serial = serial
+        self.count = counters != "none"
+        self.fused = counters == "fused"
+        self.finish = finish
+        self.nbuf = 1 if serial else 2
+        pool_out = torch.empty(t.pool_n, dtype=torch.int32, device=dev)
+        self.pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(self.nbuf - 1)]
+        self.outsb = [tuple(torch.empty(self.B, dtype=torch.int32, device=dev)
+                            for _ in range(3)) + (None,) for _ in range(self.nbuf)]
+        clf.counters_enable(False)
+        self.csrc = [clf.counters_device(k)
+                     for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
+        self.bucket = HitCounterBucket([n for _, n in self.csrc], dev) if bucket else None
+        if serial:
+            self.s_pipe = self.s_hint = self.s_cnt = torch.cuda.current_stream()
+        else:
+            self.s_pipe, self.s_hint, self.s_cnt = (hip_stream(dev) for _ in range(3))
+        self.ev_hint, self.ev_pipe, self.ev_cnt, self.kdone = {}, {}, {}, {}
+        self.timing = []
+
+    def _hint(self, j, rec):
+        TE = lambda: torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(self.s_hint):
+            if j - self.nbuf in self.ev_pipe:          # pool buffer no longer read
+                self.s_hint.wait_event(self.ev_pipe[j - self.nbuf])
+            e0, e1 = TE(), TE()
+            e0.record()
+            t = self.t
+            V.check(V.lib().vc_hint_search_dev(
+                self.clf.h, C.c_void_p(t.pool_blob.data_ptr()), C.c_void_p(t.pool_off.data_ptr()),
+                None, None, None, None, None, t.pool_n,
+                C.c_void_p(self.pools[j % self.nbuf].data_ptr()),
+                C.c_void_p(self.s_hint.cuda_stream)))
+            e1.record()
+            self.ev_hint[j] = e1
+            rec["hint"] = (e0, e1)
+
+    def _pipe(self, j, rec):
+        TE = lambda: torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(self.s_pipe):
+            self.s_pipe.wait_event(self.ev_hint[j])
+            if j - self.nbuf in self.ev_cnt:           # output buffers counted
+                self.s_pipe.wait_event(self.ev_cnt[j - self.nbuf])
+            k0, k1 = RawEvent(), RawEvent()            # the classify kernel alone
+            k0.record(self.s_pipe)
+            if self.fused:                             # count packets only, not the pool pass
+                self.clf.counters_enable(True)
+            cs = self.s_cnt if (self.fused and self.finish == "stream" and not self.serial) \
+                else None
+            self.clf.pipeline_v4(self.proto, self.src, self.dst, self.dport, self.hid,
+                                 self.pools[j % self.nbuf], outs=self.outsb[j % self.nbuf],
+                                 kernel_done_event=k1.h.value, count_stream=cs)
+            if self.fused:
+                self.clf.counters_enable(False)
+            e1 = TE()
+            e1.record()
+            self.ev_pipe[j] = e1
+            self.kdone[j] = k1
+            rec["pipe"] = (k0, k1)
+
+    def _counters(self, j, rec):
+        outs = self.outsb[j % self.nbuf]
+        with torch.cuda.stream(self.s_cnt):
+            self.s_cnt.wait_event(self.ev_pipe[j])     # also covers a finish on s_pipe
+            k2 = RawEvent()
+            k2.record(self.s_cnt)
+            if self.count and not self.fused:
+                self.clf.counters_add(V.COUNTERS_ACL, outs[0], aux=self.proto)
+                self.clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
+                self.clf.counters_add(V.COUNTERS_GROUP, outs[2])
+            k3 = RawEvent()
+            k3.record(self.s_cnt)
+            if self.bucket is not None:                # one RCCL all-reduce per batch
+                for i, cs in enumerate(self.csrc):
+                    self.bucket.fill(i, cs)
+                self.bucket.reduce()
+            done = torch.cuda.Event()
+            done.record()
+            self.ev_cnt[j] = done
+            rec["count"] = (self.kdone[j], k3)         # kernel end -> counters complete
+
+    def run(self, first, k, timed):
+        """Steps first .. first+k-1.  The hostname pool of the next step is
+        issued before this step's counters, so it overlaps this step's
+        pipeline."""
+        if k <= 0:
+            return
+        recs = [dict() for _ in range(k)]
+        self._hint(first, recs[0])
+        for i in range(k):
+            j = first + i
+            self._pipe(j, recs[i])
+            if i + 1 < k:
+                self._hint(j + 1, recs[i + 1])
+            self._counters(j, recs[i])
+        if timed:
+            self.timing.extend(recs)
+
+    def reset_events(self):
+        self.ev_hint.clear()
+        self.ev_pipe.clear()
+        self.ev_cnt.clear()
+        self.kdone.clear()
+
+    def span(self, key):
+        return float(np.mean([r[key][0].elapsed_time(r[key][1]) for r in self.timing]))
+
+
+def max_over_ranks(x, dev):
+    """MAX of a float over the process group (the step time the job sees)."""
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (oracle, test-infrastructure C restatement of the Java scans)
+# ---------------------------------------------------------------------------
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return {"nproc": os.cpu_count(), "affinity": avail, "cpu_model": model,
+            "threads_all": max(1, min(share, avail, 64))}
+
+
+def cpu_rates(run, unit, budget_s, what, note=None):
+    """Time `run(n, threads) -> seconds` on a bounded sample: all-core (the
+    box's CPU share) and 1 core, each sized to about `budget_s` seconds."""
+    info = cpu_info()
+    res = {}
+    for threads in (info["threads_all"], 1):
+        probe = max(threads * 4, 64)
+        t = run(probe, threads)
+        n = int(max(probe, probe * budget_s / max(t, 1e-6)))
+        t = run(n, threads)
+        res[threads] = (n, t)
+    na, ta = res[info["threads_all"]]
+    n1, t1 = res[1]
+    out = {"value": na / ta / 1e6, "unit": unit, "cores": info["threads_all"], "kind": "port",
+           "sample": "%s; all-core: %d items in %.1f s on %d threads; 1 core: %d items in %.1f s"
+                     % (what, na, ta, info["threads_all"], n1, t1),
+           "one_core": {"value": n1 / t1 / 1e6, "cores": 1},
+           "nproc": info["nproc"], "cpu_model": info["cpu_model"]}
+    if note:
+        out["note"] = note
+    return out
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    return O
+
+
+def cpu_baseline_c5(t, budget_s=8.0):
+    O = _oracle()
+    og = O.Groups(t.groups)
+    names_blob, names_off = t.nblob, t.noff
+
+    def run(n, threads):
+        proto, src, dst, dport, hid = (x.numpy() for x in gen_packets(0, n, t, t.pool_n))
+        src, dst = src.view(np.uint32), dst.view(np.uint32)
+        dport = dport.view(np.uint16)
+        names = [bytes(names_blob[names_off[i]:names_off[i + 1]]) for i in t.pidx[hid]]
+        sub_blob, sub_off = W.pack(names)
+        t0 = time.perf_counter()
+        O.sg_batch_v4_np(t.tcp, t.udp, False, proto, src, dport, nthreads=threads)
+        O.rt_batch_v4_np(t.v4_list, dst, nthreads=threads)
+        O.hint_batch_np(og, sub_blob, sub_off, None, nthreads=threads)
+        return time.perf_counter() - t0
+
+    return cpu_rates(run, "M classifications/s", budget_s,
+                     "the first packets of the same seeded C5 batch (ACL %d rules + RouteTable "
+                     "%d IPv4 rules + Upstream %d groups), oracle linear scans as the Java code "
+                     "does them" % (len(t.tcp) + len(t.udp), len(t.v4_list), len(t.groups)),
+                     note="the CPU leg runs Upstream.searchForGroup for every packet, as the "
+                          "Java path does per connection; the GPU classifies each hostname of "
+                          "the 16M pool once per step and gathers the result per packet. The "
+                          "restatement skips Java's per-call allocations, so it is faster than "
+                          "the reference itself.")
+
+
 def gather_ceiling(table_mb=64):
     """Measured random 4-byte gather rate (G gathers/s) from a table of
     `table_mb`, two independent gathers per item (tools/gather_probe.hip,
@@ -197,14 +459,16 @@ def gather_ceiling(table_mb=64):
 def load_traffic(workload, kernel):
     """Per-launch HBM-side bytes of `kernel` from the committed PMC passes
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench)."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench),
+    and the commit the passes were taken at."""
     p = os.path.join(PROFILES, "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d[workload]["kernels"][kernel]["traffic_bytes"]
+        w = d[workload]
+        return w["kernels"][kernel]["traffic_bytes"], w.get("commit")
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 # ---------------------------------------------------------------------------
@@ -214,23 +478,22 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
-                    choices=["c5", "c2", "c2host", "c3", "c4", "dns", "sni", "parse", "source",
-                             "mirror"])
+                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "sni", "parse",
+                             "source", "mirror", "mix", "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-counters", action="store_true", help="ablation: skip hit counters")
-    ap.add_argument("--counters", choices=["fused", "passes"], default="fused",
+    ap.add_argument("--counters", choices=["fused", "passes", "none"], default="fused",
                     help="fused: the pipeline kernel counts ACL hits and route/group buckets "
                          "itself and the library finishes the large spaces; passes: separate "
-                         "counting passes over the outputs (counters_add)")
+                         "counting passes over the outputs (counters_add); none: ablation")
+    ap.add_argument("--finish", choices=["stream", "inline"], default="stream",
+                    help="where the library's counter finish runs: on the counting stream "
+                         "(overlapping the next batch) or inline after the pipeline kernel")
     ap.add_argument("--serial", action="store_true",
                     help="ablation: one stream, no overlap between consecutive batches")
-    ap.add_argument("--overlap", choices=["finish", "pipeline"], default="pipeline",
-                    help="what the next batch's hostname-pool pass overlaps: the counter finish "
-                         "passes of this batch (it waits for this batch's pipeline kernel), or "
-                         "the pipeline kernel itself (both are bound by the same random "
-                         "gathers)")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the process group and the counter all-reduce even at N = 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -240,8 +503,13 @@ def main():
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
     clf = V.Classifier(local)
 
@@ -249,159 +517,38 @@ def main():
         return sub_bench(args, clf, dev, rank, world)
 
     t_setup = time.time()
-    # ---- replicated tables (same seeds on every rank) ----
-    tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
-    a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
-    b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
-    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
-    net, plen = W.gen_v4_prefixes(1_000_000, W.SEED + 3)
-    hi, lo, p6 = W.gen_v6_prefixes(200_000, W.SEED + 4)
-    rt = V.RouteTable()
-    allnets = np.concatenate([W.v4_nets(net, plen), W.v6_nets(hi, lo, p6)])
-    arr, n_all, keep = W.as_ctypes(allnets, V._lib.VcNet)
-    rt.add_rules("bgp", arr, n=n_all)
-    clf.compile_route_table(rt)
-    a4, n4 = rt.rules_raw(4)
-    v4_list = np.frombuffer(bytes(a4)[:n4 * 40], W.NET_DT)
-    groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
-    clf.compile_upstream(groups)
-    names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)            # distinct pool source
-    nblob, noff = W.pack(names)
-    pidx = np.random.default_rng(W.SEED + 7 + rank).integers(0, len(names), args.pool)
-    pool_blob, pool_off, pool_bytes = gather_strings_dev(nblob, noff, pidx, dev)
-    pool_out = torch.empty(args.pool, dtype=torch.int32, device=dev)
+    t = c5_tables(clf, dev, args.pool)
     log("tables built in %.1fs (acl %d+%d, routes %d+%d, groups %d, pool %d names %.0f MB)" % (
-        time.time() - t_setup, len(tcp), len(udp), n4, len(hi), len(groups), args.pool,
-        pool_bytes / 1e6))
-
-    B = args.packets
-    proto, src, dst, dport, hid = gen_packets(B, tcp, udp, net, plen, args.pool,
-                                              1234 + rank, dev)
-    # Two batches in flight: outputs and pool results are double-buffered so
-    # batch j's hit counters (and batch j+1's hostname pool) run on their own
-    # streams while batch j+1's pipeline runs.  Every step still does all of
-    # its work inside the timed region.
-    nbuf = 1 if args.serial else 2
-    pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(nbuf - 1)]
-    outsb = [tuple(torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)) + (None,)
-             for _ in range(nbuf)]
+        time.time() - t_setup, len(t.tcp), len(t.udp), t.n4, t.n6, len(t.groups), args.pool,
+        t.pool_bytes / 1e6))
+    # this rank's shard of the global batch (weak scaling: N = packets x world)
+    lo, hi = shard(args.packets * world, rank, world)
+    packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
+    steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
+                    counters=args.counters, finish=args.finish)
     torch.cuda.synchronize()
-    log("packets generated (%d per GPU), setup %.1fs" % (B, time.time() - t_setup))
+    log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
+        hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
 
-    # Hit counters: the library's histogram passes over each batch's outputs,
-    # scheduled explicitly (counters_add) on the counting stream.
-    count = not args.no_counters
-    fused = count and args.counters == "fused"
-    clf.counters_enable(False)
-    csrc = [clf.counters_device(k) for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
-    bucket = HitCounterBucket([n for _, n in csrc], dev) if world > 1 else None
-    if args.serial:
-        s_pipe = s_hint = s_cnt = torch.cuda.current_stream()
-    else:
-        s_pipe, s_hint, s_cnt = (hip_stream(dev) for _ in range(3))
-    ev_hint, ev_pipe, ev_cnt, kdone = {}, {}, {}, {}
-    timing = []                     # (hint, pipe, count) event pairs of timed steps
-    TE = lambda: torch.cuda.Event(enable_timing=True)
-
-    def hint(j, rec):
-        with torch.cuda.stream(s_hint):
-            if j - nbuf in ev_pipe:               # pool buffer no longer read
-                s_hint.wait_event(ev_pipe[j - nbuf])
-            if args.overlap == "finish" and j - 1 in kdone:
-                kdone[j - 1].wait(s_hint)          # after the previous pipeline kernel
-            e0, e1 = TE(), TE()
-            e0.record()
-            V.check(V.lib().vc_hint_search_dev(clf.h, C.c_void_p(pool_blob.data_ptr()),
-                                               C.c_void_p(pool_off.data_ptr()), None, None, None,
-                                               None, None, args.pool,
-                                               C.c_void_p(pools[j % nbuf].data_ptr()),
-                                               C.c_void_p(s_hint.cuda_stream)))
-            e1.record()
-            ev_hint[j] = e1
-            rec["hint"] = (e0, e1)
-
-    def pipe(j, rec):
-        with torch.cuda.stream(s_pipe):
-            s_pipe.wait_event(ev_hint[j])
-            if j - nbuf in ev_cnt:                # output buffers counted
-                s_pipe.wait_event(ev_cnt[j - nbuf])
-            k0, k1 = RawEvent(), RawEvent()       # the classify kernel alone
-            e1 = TE()
-            k0.record(s_pipe)
-            if fused:                              # count packets only, not the pool pass
-                clf.counters_enable(True)
-            clf.pipeline_v4(proto, src, dst, dport, hid, pools[j % nbuf], outs=outsb[j % nbuf],
-                            kernel_done_event=k1.h.value)
-            if fused:
-                clf.counters_enable(False)
-            k2 = RawEvent()                       # + in-library counter passes (fused)
-            k2.record(s_pipe)
-            e1.record()
-            ev_pipe[j] = e1
-            kdone[j] = k1
-            rec["pipe"] = (k0, k1)
-            rec["pipe_call"] = (k1, k2)
-
-    def counters(j, rec):
-        outs = outsb[j % nbuf]
-        with torch.cuda.stream(s_cnt):
-            s_cnt.wait_event(ev_pipe[j])
-            e0, e1 = TE(), TE()
-            e0.record()
-            if count and not fused:
-                clf.counters_add(V.COUNTERS_ACL, outs[0], aux=proto)
-                clf.counters_add(V.COUNTERS_ROUTE, outs[1], family=4)
-                clf.counters_add(V.COUNTERS_GROUP, outs[2])
-            e1.record()
-            if bucket is not None:                # one RCCL all-reduce per batch
-                for i, cs in enumerate(csrc):
-                    bucket.fill(i, cs)
-                bucket.reduce()
-            done = torch.cuda.Event()
-            done.record()
-            ev_cnt[j] = done
-            rec["count"] = (e0, e1)
-
-    def run(first, k, timed):
-        """Steps first .. first+k-1; step j = hint(j), pipe(j), counters(j).
-        The hostname pool of the next step is issued before this step's
-        counters, so it overlaps this step's pipeline."""
-        if k <= 0:
-            return
-        recs = [dict() for _ in range(k)]
-        hint(first, recs[0])
-        for i in range(k):
-            j = first + i
-            pipe(j, recs[i])
-            if i + 1 < k:
-                hint(j + 1, recs[i + 1])
-            counters(j, recs[i])
-        if timed:
-            timing.extend(recs)
-
-    run(0, args.warmup, False)
+    steps.run(0, args.warmup, False)
     torch.cuda.synchronize()
-    ev_hint.clear(); ev_pipe.clear(); ev_cnt.clear(); kdone.clear()
-    if world > 1:
-        import torch.distributed as dist
+    steps.reset_events()
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.warmup, args.steps, True)
+    steps.run(args.warmup, args.steps, True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if use_dist:
+        elapsed = max_over_ranks(elapsed, dev)
 
-    span = lambda key: float(np.mean([r[key][0].elapsed_time(r[key][1]) for r in timing]))
-    hint_ms, pipe_ms = span("hint"), span("pipe")
-    count_ms = span("pipe_call") if fused else span("count")
-    total = float(B) * world * args.steps
+    hint_ms, pipe_ms, count_ms = steps.span("hint"), steps.span("pipe"), steps.span("count")
+    B = hi - lo
+    total = float(args.packets) * world * args.steps
     value = total / elapsed / 1e6
     # roofline of the dominant kernel, algorithmic bytes only (SURVEY.md §8(d))
     if pipe_ms >= hint_ms:
@@ -409,7 +556,7 @@ def main():
         unit_desc = "27 B/packet (proto 1 + src 4 + dst 4 + dport 2 + host_id 4 in; 3x int32 out)"
     else:
         dom, ms, units = "hint_kernel", hint_ms, args.pool
-        per_unit = (pool_bytes / args.pool) + 4 + 4
+        per_unit = (t.pool_bytes / args.pool) + 4 + 4
         unit_desc = "%.1f B/hostname (avg bytes + 4 offset + 4 out)" % per_unit
     achieved = per_unit * units / (ms / 1e3) / 1e9
     ceil = gather_ceiling()
@@ -420,58 +567,163 @@ def main():
                     "ceiling_G_gathers_per_s": ceil,
                     "frac": round(g_rate / ceil, 4) if ceil else None,
                     "ceiling_source": "tools/gather_probe.hip -> profiles/r01_gather_probe.csv"}
+    traffic, t_commit = load_traffic("c5", dom)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic("c5", dom),
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+                              "WRITE_SIZE per launch, taken at commit %s)" % t_commit,
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
             "gather_bound": gather_bound,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
                                 "pipeline_v4_kernel": round(pipe_ms, 4),
-                                "hit_counter_passes": round(count_ms, 4),
+                                "kernel_end_to_counters_done": round(count_ms, 4),
                                 "counting": ("in the pipeline kernel (ACL + route/group "
-                                             "buckets) + library passes for the large spaces"
-                                             if fused else "separate passes")}}
+                                             "buckets) + library finish passes on the %s" %
+                                             ("counting stream" if args.finish == "stream"
+                                              else "pipeline stream")
+                                             if steps.fused else args.counters)}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline_c5(tcp, udp, v4_list, groups, nblob, noff, 99, threads)
+        cpu = cpu_baseline_c5(t)
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "M classifications/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u32",
                 "data": "synthetic (seeded, generated on device)",
-                "config": {"workload": "C5 combined ACL->route->host pipeline, per-GPU shard",
-                           "acl_rules": int(len(tcp) + len(udp)), "routes_v4": int(n4),
-                           "routes_v6": int(len(hi)), "groups": len(groups),
-                           "hostname_pool": args.pool, "packets_per_gpu_per_step": B,
+                "config": {"workload": "C5 combined ACL->route->host pipeline, per-GPU shard of "
+                                       "a seeded global batch",
+                           "acl_rules": int(len(t.tcp) + len(t.udp)), "routes_v4": int(t.n4),
+                           "routes_v6": int(t.n6), "groups": len(t.groups),
+                           "hostname_pool": args.pool, "packets_per_gpu_per_step": args.packets,
+                           "global_batch": args.packets * world,
                            "parallelism": "dp%d" % world,
                            "schedule": ("serial, one stream" if args.serial else
-                                        "2 batches in flight: pool / pipeline / counters on "
-                                        "3 HIP streams; the next pool pass overlaps the %s" %
-                                        ("counter finish" if args.overlap == "finish"
-                                         else "pipeline kernel"))},
+                                        "2 batches in flight: pool / pipeline / counters on 3 "
+                                        "HIP streams")},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
-def sub_bench(args, clf, dev, rank, world):
-    """Single-classifier benchmarks (DESIGN.md numbers), not the headline."""
-    res = {}
+# ---------------------------------------------------------------------------
+# sub-benchmarks (DESIGN.md / BASELINE.md numbers, not the headline)
+# ---------------------------------------------------------------------------
+def _time(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
     ev = []
-    if args.workload == "c2":
-        tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return el, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def sub_bench(args, clf, dev, rank, world):
+    """Single-classifier benchmarks.  Each line carries `roofline` (its
+    dominant kernel's algorithmic bytes over its event-timed duration) and,
+    unless --no-cpu-baseline, the oracle's all-core and 1-core rates on a
+    sample of the same workload."""
+    O = None if args.no_cpu_baseline else _oracle()
+    cpu = None
+    extra = {}
+    S = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if args.workload in ("c1", "c2", "c2host"):
+        if args.workload == "c1":
+            # C1 plumbing: 64 rules + Table default 10/8 + 255 random-order CIDRs, 1M tuples
+            tcp, udp = W.gen_sg_rules(64, W.SEED + 1, p_range=0.5, weighted=False)
+            net, plen = W.gen_v4_prefixes(255, W.SEED + 31, dist=((8, 30, 1.0),))
+            rt = V.RouteTable("10.0.0.0/8", None, 1)
+            perm = np.random.default_rng(W.SEED + 32).permutation(len(net))
+            for i in perm:
+                s = "%d.%d.%d.%d/%d" % (net[i] >> 24, (net[i] >> 16) & 255, (net[i] >> 8) & 255,
+                                        net[i] & 255, plen[i])
+                try:
+                    rt.add_rule("r%d" % i, s)
+                except V.VcError:
+                    pass                             # XException of RouteTable.addRule
+            clf.compile_route_table(rt)
+            a4, n4 = rt.rules_raw(4)
+            rlist = np.frombuffer(bytes(a4)[:n4 * 40], W.NET_DT)
+            n = 1 << 20
+        else:
+            tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+            n = 64 << 20
         a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
         b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
         V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
-        n = 64 << 20
-        net, plen = W.gen_v4_prefixes(1000, 1)
-        proto, src, dst, dport, hid = gen_packets(n, tcp, udp, net, plen, 1, 5 + rank, dev)
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        fn = lambda: clf.acl_v4(proto, src, dport, out_idx=out, want_allow=False)
-        per_unit, unit = 11, "B/tuple (7 in + 4 out)"
+        proto, src, port = W.gen_acl_queries(tcp, udp, n, W.SEED + 16)
+        if args.workload == "c2host":
+            # the plain (host-buffer) entry point over registered buffers
+            out = np.empty(n, np.int32)
+            allow = np.empty(n, np.uint8)
+            for x in (proto, src, port, out, allow):
+                V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
+            P = lambda x: C.c_void_p(x.ctypes.data)
+            fn = lambda: V.check(V.lib().vc_acl_classify_v4(clf.h, P(proto), P(src), P(port), n,
+                                                              P(out), P(allow)))
+            per_unit, unit, kern = 12, "B/tuple across PCIe (7 in + 5 out), kernel included", \
+                "acl_v4_kernel (zero-copy over PCIe)"
+        else:
+            d = [torch.from_numpy(x).to(dev) for x in (proto, src, port)]
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            if args.workload == "c1":
+                dst = W.v4_lookups(net, plen, n, W.SEED + 17)
+                dd = torch.from_numpy(dst).to(dev)
+                ro = torch.empty(n, dtype=torch.int32, device=dev)
+                fn = lambda: (clf.acl_v4(*d, out_idx=out, want_allow=False),
+                              clf.route_v4(dd, out=ro))
+                per_unit, unit, kern = 19, "B/tuple (ACL 7 in + 4 out, route 4 in + 4 out)", \
+                    "acl_v4_kernel + route_v4_kernel"
+                # end to end from host buffers (pageable: staged copies)
+                hsrc = (proto, src, port, dst)
+
+                def e2e():
+                    clf.acl_v4(*hsrc[:3], want_allow=False)
+                    clf.route_v4(hsrc[3])
+                e2e()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    e2e()
+                extra["end_to_end_host_buffers_M_per_s"] = round(
+                    n * 5 / (time.perf_counter() - t0) / 1e6, 1)
+                extra["end_to_end_note"] = ("vc_acl_classify_v4 + vc_route_lookup_v4 on pageable "
+                                            "host arrays: H2D + kernel + D2H, synchronous")
+            else:
+                fn = lambda: clf.acl_v4(*d, out_idx=out, want_allow=False)
+                per_unit, unit, kern = 11, "B/tuple (7 in + 4 out)", "acl_v4_kernel"
+        if O is not None:
+            def run(k, threads):
+                t0 = time.perf_counter()
+                O.sg_batch_v4_np(tcp, udp, False, proto[:k], src[:k], port[:k], nthreads=threads)
+                if args.workload == "c1":
+                    O.rt_batch_v4_np(rlist, dst[:k], nthreads=threads)
+                return time.perf_counter() - t0
+            if args.workload == "c1":
+                cpu = {}
+                info = cpu_info()
+                for th in (info["threads_all"], 1):     # C1 runs in full
+                    tt = run(n, th)
+                    cpu[th] = n / tt / 1e6
+                cpu = {"value": cpu[info["threads_all"]], "unit": "M items/s",
+                       "cores": info["threads_all"], "kind": "port",
+                       "sample": "the full C1 batch (%d tuples, ACL + route), oracle linear "
+                                 "scans" % n,
+                       "one_core": {"value": cpu[1], "cores": 1}, "nproc": info["nproc"],
+                       "cpu_model": info["cpu_model"]}
+            else:
+                cpu = cpu_rates(run, "M items/s", 4.0, "first tuples of the C2 batch, oracle "
+                                "first-match scan over 10k rules")
     elif args.workload == "c3":
         net, plen = W.gen_v4_prefixes(1_000_000, W.SEED + 3)
         hi, lo, p6 = W.gen_v6_prefixes(200_000, W.SEED + 4)
@@ -491,47 +743,90 @@ def sub_bench(args, clf, dev, rank, world):
         q4 = dev_u32(torch.where(torch.rand(n4, generator=g, device=dev) < 0.9,
                                  netd[r] | (q & (~mkd[r] & 0xFFFFFFFF)), q))
         del r, q
-        q6 = torch.from_numpy(W.v6_lookups(hi, lo, p6, n - n4, 8 + rank)).to(dev)
+        q6h = W.v6_lookups(hi, lo, p6, n - n4, 8 + rank)
+        q6 = torch.from_numpy(q6h).to(dev)
         o4 = torch.empty(n4, dtype=torch.int32, device=dev)
         o6 = torch.empty(n - n4, dtype=torch.int32, device=dev)
         fn = lambda: (clf.route_v4(q4, out=o4), clf.route_v6(q6, out=o6))
         per_unit, unit = (8 * 0.85 + 20 * 0.15), "B/lookup (v4 4+4, v6 16+4, 85/15 mix)"
-    elif args.workload == "c2host":
-        # the plain (host-buffer) entry point: H2D copy + kernel + D2H copy
-        # per call, from page-locked buffers (vc_host_register)
-        tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
-        a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
-        b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
-        V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
-        n = 64 << 20
-        proto, src, port = W.gen_acl_queries(tcp, udp, n, W.SEED + 16)
-        out = np.empty(n, np.int32)
-        allow = np.empty(n, np.uint8)
-        bufs = (proto, src, port, out, allow)
-        for x in bufs:
-            V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
-        P = lambda x: C.c_void_p(x.ctypes.data)
-        fn = lambda: V.check(V.lib().vc_acl_classify_v4(clf.h, P(proto), P(src), P(port), n,
-                                                          P(out), P(allow)))
-        per_unit, unit = 12, "B/tuple across PCIe (7 in + 5 out), kernel included"
-    elif args.workload == "dns":
+        kern = "route_v4_kernel + route_v6_kernel_x4"
+        # the split, each family timed alone
+        e4, ms4 = _time(lambda: clf.route_v4(q4, out=o4), 3, 1)
+        e6, ms6 = _time(lambda: clf.route_v6(q6, out=o6), 3, 1)
+        extra["v4_ms"], extra["v6_ms"] = round(ms4, 4), round(ms6, 4)
+        extra["v4_G_per_s"] = round(n4 / ms4 / 1e6, 2)
+        extra["v6_G_per_s"] = round((n - n4) / ms6 / 1e6, 2)
+        if O is not None:
+            a4, k4 = rt.rules_raw(4)
+            a6, k6 = rt.rules_raw(6)
+            v4l = np.frombuffer(bytes(a4)[:k4 * 40], W.NET_DT)
+            v6l = np.frombuffer(bytes(a6)[:k6 * 40], W.NET_DT)
+            q4h = W.v4_lookups(net, plen, 1 << 16, W.SEED + 33)
+
+            def run(k, threads):
+                k4_ = max(1, int(k * 0.85))
+                t0 = time.perf_counter()
+                O.rt_batch_v4_np(v4l, q4h[:k4_], nthreads=threads)
+                O.rt_batch_v6_np(v6l, q6h[:max(1, k - k4_)], nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 4.0, "85/15 v4/v6 lookups of the C3 workload, "
+                            "oracle first-match scans over the RouteTable lists")
+    elif args.workload in ("c4", "dns"):
         groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
         clf.compile_upstream(groups)
-        hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
-                           for i in range(50_000))
-        clf.compile_hosts_text(hosts)
-        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+        dns = args.workload == "dns"
+        if dns:
+            hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
+                              for i in range(50_000))
+            clf.compile_hosts_text(hosts)
+            names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+        else:
+            names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
         nblob, noff = W.pack(names)
         n = 16 << 20
-        pidx = np.random.default_rng(W.SEED + 8).integers(0, len(names), n)
+        pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
         blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
-        kind = torch.empty(n, dtype=torch.uint8, device=dev)
-        val = torch.empty(n, dtype=torch.int32, device=dev)
-        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        fn = lambda: V.check(V.lib().vc_dns_classify_dev(
-            clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n,
-            C.c_void_p(kind.data_ptr()), C.c_void_p(val.data_ptr()), s()))
-        per_unit, unit = nbytes / n + 9, "B/qname (bytes + 4 offset + 1 kind + 4 value)"
+        if dns:
+            kind = torch.empty(n, dtype=torch.uint8, device=dev)
+            val = torch.empty(n, dtype=torch.int32, device=dev)
+            fn = lambda: V.check(V.lib().vc_dns_classify_dev(
+                clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n,
+                C.c_void_p(kind.data_ptr()), C.c_void_p(val.data_ptr()), S()))
+            per_unit, unit, kern = nbytes / n + 9, "B/qname (bytes + 4 offset + 1 kind + 4 " \
+                                                   "value)", "dns_kernel"
+        else:
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            fn = lambda: V.check(V.lib().vc_hint_search_dev(
+                clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, None, None,
+                None, None, n, C.c_void_p(out.data_ptr()), S()))
+            per_unit, unit, kern = nbytes / n + 8, "B/hostname (bytes + 4 offset + 4 out)", \
+                "hint_kernel"
+        if O is not None:
+            og = O.Groups(groups)
+            oh = O.Hosts(O.hosts_parse(hosts)[0]) if dns else None
+
+            def run(k, threads):
+                sub = [names[i] for i in pidx[:k]]
+                if dns:
+                    t0 = time.perf_counter()
+                    for q in sub:
+                        O.dns_classify(oh, og, q)
+                    return (time.perf_counter() - t0) / max(1, threads) * threads
+                sb, so = W.pack(sub)
+                t0 = time.perf_counter()
+                O.hint_batch_np(og, sb, so, None, nthreads=threads)
+                return time.perf_counter() - t0
+            if dns:
+                info = cpu_info()
+                k = 2000
+                tt = run(k, 1)
+                cpu = {"value": k / tt / 1e6, "unit": "M items/s", "cores": 1, "kind": "port",
+                       "sample": "%d qnames of the DNS workload, oracle hosts lookup + "
+                                 "searchForGroup scan over 100k groups, 1 thread" % k,
+                       "nproc": info["nproc"], "cpu_model": info["cpu_model"]}
+            else:
+                cpu = cpu_rates(run, "M items/s", 4.0, "hostnames of the C4 pool, oracle "
+                                "searchForGroup scan over 100k groups")
     elif args.workload == "sni":
         _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
         holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]
@@ -542,18 +837,16 @@ def sub_bench(args, clf, dev, rank, world):
         pidx = np.random.default_rng(W.SEED + 11).integers(0, len(names), n)
         blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
-        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
         fn = lambda: V.check(V.lib().vc_cert_choose_dev(
             clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, n,
-            C.c_void_p(out.data_ptr()), s()))
-        per_unit, unit = nbytes / n + 8, "B/SNI (bytes + 4 offset + 4 out)"
+            C.c_void_p(out.data_ptr()), S()))
+        per_unit, unit, kern = nbytes / n + 8, "B/SNI (bytes + 4 offset + 4 out)", "cert_kernel"
     elif args.workload in ("parse", "mirror"):
         frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
         fblob, foff = W.pack(frames)
         n = 32 << 20
         pidx = np.random.default_rng(W.SEED + 13).integers(0, len(frames), n)
         blob, off, nbytes = gather_strings_dev(fblob, foff, pidx, dev)
-        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
         if args.workload == "parse":
             res = {k: torch.empty((n, w) if w > 1 else (n,), dtype={"u8": torch.uint8,
                    "u16": torch.int16, "u32": torch.int32}[t], device=dev)
@@ -561,11 +854,11 @@ def sub_bench(args, clf, dev, rank, world):
             o = V._lib.VcPktOut(**{k: v.data_ptr() for k, v in res.items()})
             fn = lambda: V.check(V.lib().vc_parse_packets_dev(
                 clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, 0,
-                C.byref(o), s()))
+                C.byref(o), S()))
             per_unit = nbytes / n + 4 + 54
             unit = "B/frame (frame bytes + 4 offset in; 54 B of SoA fields out)"
+            kern = "packet_kernel"
         else:
-            from vproxy_amd.mirror import MirrorFilters  # noqa: F401
             filters = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
                         "network2": "10.0.0.0/8"} for i in range(16)] + \
                       [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}]
@@ -574,9 +867,10 @@ def sub_bench(args, clf, dev, rank, world):
             oid = mf.id_of("switch", create=False)
             fn = lambda: V.check(V.lib().vc_mirror_switch_dev(
                 clf.h, oid, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, 0,
-                C.c_void_p(out.data_ptr()), s()))
+                C.c_void_p(out.data_ptr()), S()))
             per_unit = nbytes / n + 4 + 8
             unit = "B/frame (frame bytes + 4 offset in; 8 B mirror set out), 17 filters"
+            kern = "mirror_switch_kernel"
     elif args.workload == "source":
         rng = np.random.default_rng(W.SEED + 14)
         groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
@@ -588,47 +882,29 @@ def sub_bench(args, clf, dev, rank, world):
         grp = torch.randint(0, len(groups), (n,), generator=g, device=dev, dtype=torch.int32)
         src = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, device=dev, dtype=torch.int32)
         out = torch.empty(n, dtype=torch.int32, device=dev)
-        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
         fn = lambda: V.check(V.lib().vc_source_select_v4_dev(
             clf.h, C.c_void_p(grp.data_ptr()), C.c_void_p(src.data_ptr()), n, 0,
-            C.c_void_p(out.data_ptr()), s()))
-        per_unit, unit = 12, "B/item (group 4 + v4 source 4 in, 4 out)"
-    else:  # c4
-        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
-        clf.compile_upstream(groups)
-        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
-        nblob, noff = W.pack(names)
-        n = 16 << 20
-        pidx = np.random.default_rng(W.SEED + 7).integers(0, len(names), n)
-        blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        fn = lambda: V.check(V.lib().vc_hint_search_dev(
-            clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, None, None,
-            None, None, n, C.c_void_p(out.data_ptr()), s()))
-        per_unit, unit = nbytes / n + 8, "B/hostname (bytes + 4 offset + 4 out)"
-    for _ in range(args.warmup):
-        fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        fn()
-        e1.record()
-        ev.append((e0, e1))
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+            C.c_void_p(out.data_ptr()), S()))
+        per_unit, unit, kern = 12, "B/item (group 4 + v4 source 4 in, 4 out)", "source_v4_kernel"
+    else:
+        return mix_bench(args, clf, dev, rank, O)
+    el, ms = _time(fn, args.steps, args.warmup)
     gbs = per_unit * n / (ms / 1e3) / 1e9
     res = {"workload": args.workload, "items": n, "ms_per_step": round(el / args.steps * 1e3, 3),
            "kernel_ms": round(ms, 4), "M_items_per_s": round(n / (ms / 1e3) / 1e6, 1),
-           "algorithmic_GBps": round(gbs, 2), "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 5),
-           "bytes_per_item": unit}
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "kernel": kern,
+                        "algorithmic_bytes": unit},
+           "cpu_baseline": cpu}
+    res.update(extra)
     if rank == 0:
         print(json.dumps(res), flush=True)
     clf.close()
+
+
+def mix_bench(args, clf, dev, rank, O):
+    """Placeholder until the mixed-family pipeline lands."""
+    raise SystemExit("workload %s not available" % args.workload)
 
 
 if __name__ == "__main__":

@@ -218,6 +218,52 @@ int vc_pipeline_v4_dev_ex(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src
                           int32_t *out_route, int32_t *out_group, uint8_t *out_allow, void *stream,
                           void *kernel_done_event);
 
+/* The general pipeline: IPv4 and IPv6 packets in one batch, as the vswitch
+ * drain loop (core/src/main/java/vswitch/Switch.java:744-776) hands them to
+ * L3.route (core/src/main/java/vswitch/stack/L3.java:423-444).  Every array
+ * has n entries in packet order (the layout vc_parse_packets writes); the
+ * fields a packet's family does not use are ignored. */
+typedef struct vc_packets {
+    const uint8_t *family;        /* 4 or 6 per packet: whether the packet's IP objects are
+                                     IPv4 or IPv6 instances -- RouteTable.lookup's `instanceof
+                                     IPv4` dispatch (RouteTable.java:44-58), so an IPv4-mapped
+                                     ::ffff:a.b.c.d address is family 6 and goes to rulesV6 and
+                                     the v6 ACL projection.  NULL = every packet IPv4 */
+    const uint8_t *proto;         /* VC_PROTO_TCP selects tcpRules */
+    const uint32_t *src4, *dst4;  /* IPv4 packets, IP.ipv4Bytes2Int order */
+    const uint8_t *src6, *dst6;   /* IPv6 packets, 16 bytes each, 16-byte aligned; may be NULL
+                                     only when family is NULL */
+    const uint16_t *dport;        /* SecurityGroup.allow's port */
+    const uint32_t *host_id;      /* index into the classified hostname pool (pool_group, from
+                                     vc_hint_search); NULL = no hostname stage (group -1, the
+                                     group counters untouched) */
+} vc_packets;
+
+typedef struct vc_pipeline_out {
+    int32_t *acl;                 /* SecurityGroup.allow: first matching rule index, -1 = default */
+    int32_t *route;               /* RouteTable.lookup: index in rulesV4 (family 4) or rulesV6
+                                     (family 6), -1 = null */
+    int32_t *group;               /* pool_group[host_id]; -1 for host_id >= n_pool */
+    uint8_t *allow;               /* optional: the boolean SecurityGroup.allow returns */
+} vc_pipeline_out;
+
+/* Device pointers, asynchronous on `stream`.  With counters enabled the
+ * classify kernel counts the ACL hits and the route/group buckets itself;
+ * the passes that finish the large counter spaces run on `count_stream`
+ * (ordered after the kernel) when it is not NULL -- so a caller's next batch
+ * can overlap them -- else on `stream`.  kernel_done_event (a hipEvent_t,
+ * optional) is recorded on `stream` right after the classify kernel. */
+int vc_pipeline_dev(vc_ctx *ctx, const vc_packets *in, int64_t n, const int32_t *pool_group,
+                    int64_t n_pool, const vc_pipeline_out *out, void *stream, void *count_stream,
+                    void *kernel_done_event);
+/* Host pointers (every array in `in` and `out`, and pool_group), synchronous.
+ * Zero-copy when every array is inside a vc_host_register'ed buffer (the
+ * kernel reads and writes across PCIe directly); otherwise the batch is
+ * staged through device memory in chunks on two streams.  All chunks
+ * classify against the snapshots current when the call started. */
+int vc_pipeline(vc_ctx *ctx, const vc_packets *in, int64_t n, const int32_t *pool_group,
+                int64_t n_pool, const vc_pipeline_out *out);
+
 /* ------------------------------------------------------------------------ */
 /* Server choice after the group match, method == source:                    */
 /* base/src/main/java/vproxybase/component/svrgroup/ServerGroup.java         */
@@ -238,7 +284,9 @@ typedef struct {
 int vc_compile_servers(vc_ctx *ctx, const vc_server *servers, const int32_t *group_off,
                        int n_groups);
 /* Health-check result changed: healthy[i] for every server (same indexing
- * as vc_compile_servers).  Takes effect for batches issued afterwards. */
+ * as vc_compile_servers).  Publishes a new snapshot (copy-on-write): batches
+ * issued afterwards see it, a batch already in flight -- every chunk of a
+ * chunked host call included -- keeps the health it started with. */
 int vc_servers_set_health(vc_ctx *ctx, const uint8_t *healthy, int64_t n_servers);
 #define VC_SOURCE_ALL   0   /* ServerGroup.next(source)      :422-434 */
 #define VC_SOURCE_IPV4  4   /* ServerGroup.nextIPv4(source)  :436-448 */

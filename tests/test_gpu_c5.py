@@ -1,0 +1,339 @@
+"""GPU tier: the headline C5 configuration exactly as bench.py runs it.
+
+The tables are built by bench.c5_tables (10k ACL rules, 980,848 + 200,000
+routes shortest-first, 100k groups, a 16M-name pool) and the packets by
+bench.gen_packets (the sharded global batch's generator).  The fused
+pipeline runs with the in-kernel hit counters on, over 16M device-resident
+packets, once from aligned arrays (the vector kernel) and once offset by
+one packet (the one-packet-per-lane kernel).  Checks: oracle samples of the
+ACL (SecurityGroup.java:30-45), route (RouteTable.java:44-59) and pool
+group (Upstream.java:187-198) results; whole-batch properties; and counters
+equal to exact histograms of the outputs.
+
+Also here: DNS at C4 scale (100k groups + 50k hosts), counters fed values
+outside the counter space, and the bench's N > 1 schedule (HitCounterBucket
+fill from the library's device counters on the counting stream + an RCCL
+all-reduce) run as a world-size-1 process group on one GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench as B
+import oracle_ffi as O
+import vproxy_amd as V
+from vproxy_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def c5():
+    import torch
+    clf = V.Classifier(0)
+    dev = torch.device("cuda", 0)
+    t = B.c5_tables(clf, dev, 16 << 20)
+    yield clf, t, dev
+    clf.close()
+
+
+def _rule_arrays(rules, dev):
+    import torch
+    ip, mk = W.rule_v4_fields(rules)
+    T = lambda x: torch.from_numpy(np.asarray(x).astype(np.int64)).to(dev)
+    return T(ip), T(mk), T(rules["min_port"]), T(rules["max_port"]), T(rules["allow"])
+
+
+def _check_batch(clf, t, dev, pkts, outs, pool, check_counters=True):
+    """Oracle samples + whole-batch properties + exact counters of one
+    pipeline call whose outputs are `outs`."""
+    import torch
+    proto, src, dst, dport, hid = pkts
+    acl, route, grp, allow = outs
+    n = len(src)
+    u32 = lambda x: x.to(torch.int64) & 0xFFFFFFFF
+    # group = pool[host_id], whole batch
+    assert torch.equal(grp, pool[hid.long()])
+    # whole-batch ACL properties: the index names a rule of the packet's
+    # protocol that contains src and whose port range holds dport; allow is
+    # that rule's bit (defaultAllow = false otherwise)
+    s64, d64, p64 = u32(src), u32(dst), dport.to(torch.int64) & 0xFFFF
+    is_tcp = proto == 6
+    for lst, sel in ((t.tcp, is_tcp), (t.udp, ~is_tcp)):
+        ip, mk, lo, hi, al = _rule_arrays(lst, dev)
+        a = acl[sel].long()
+        assert bool((a < len(lst)).all())
+        h = a >= 0
+        r = a[h]
+        assert bool(((s64[sel][h] & mk[r]) == ip[r]).all())
+        pp = p64[sel][h]
+        assert bool(((pp >= lo[r]) & (pp <= hi[r])).all())
+        assert bool((allow[sel][h].long() == al[r]).all())
+        assert bool((allow[sel][~h] == 0).all())
+    # route: the rule's prefix contains dst; 90 % of dsts were drawn inside one
+    rip = torch.from_numpy(t.v4_list["ip"][:, :4].copy().view(">u4").reshape(-1)
+                           .astype(np.int64)).to(dev)
+    rmk = torch.from_numpy(t.v4_list["mask"][:, :4].copy().view(">u4").reshape(-1)
+                           .astype(np.int64)).to(dev)
+    rr = route.long()
+    h = rr >= 0
+    assert bool(((d64[h] & rmk[rr[h]]) == rip[rr[h]]).all())
+    assert float(h.float().mean()) > 0.85
+    # oracle samples
+    rng = np.random.default_rng(n)
+    s = rng.integers(0, n, 20000)
+    hs = lambda x: x.cpu().numpy()[s]
+    want, wv = O.sg_batch_v4_np(t.tcp, t.udp, False, hs(proto), hs(src).view(np.uint32),
+                                hs(dport).view(np.uint16), nthreads=THREADS)
+    np.testing.assert_array_equal(hs(acl), want)
+    np.testing.assert_array_equal(hs(allow), wv)
+    s = s[:3000]
+    np.testing.assert_array_equal(route.cpu().numpy()[s],
+                                  O.rt_batch_v4_np(t.v4_list, dst.cpu().numpy()[s].view(np.uint32),
+                                                   nthreads=THREADS))
+    if not check_counters:
+        return
+    nt, nu = len(t.tcp), len(t.udp)
+    a = acl.long()
+    bins = torch.where(a >= 0, torch.where(is_tcp, a, nt + a),
+                       torch.where(is_tcp, nt + nu, nt + nu + 1))
+    exp = torch.bincount(bins, minlength=nt + nu + 2).cpu().numpy().astype(np.uint64)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ACL), exp)
+    nn = t.n4 + t.n6
+    exp = torch.bincount(torch.where(rr >= 0, rr, nn), minlength=nn + 2).cpu().numpy()
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE), exp.astype(np.uint64))
+    ng = len(t.groups)
+    g = grp.long()
+    exp = torch.bincount(torch.where(g >= 0, g, ng), minlength=ng + 1).cpu().numpy()
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp.astype(np.uint64))
+
+
+def test_c5_bench_tables_and_pool(c5):
+    """The bench's tables are the C5 sizes, and the classified pool matches
+    the oracle on a sample."""
+    import torch
+    clf, t, dev = c5
+    assert len(t.tcp) + len(t.udp) == 10000
+    assert t.n4 == 980848 and t.n6 == 200000
+    assert len(t.groups) == 100000 and t.pool_n == 16 << 20
+    pool = clf.hint_search((t.pool_blob, t.pool_off, None))
+    torch.cuda.synchronize()
+    s = np.random.default_rng(9).integers(0, t.pool_n, 1500)
+    names = [bytes(t.nblob[t.noff[i]:t.noff[i + 1]]) for i in t.pidx[s]]
+    blob, off = W.pack(names)
+    want = O.hint_batch_np(O.Groups(t.groups), blob, off, None, nthreads=THREADS)
+    np.testing.assert_array_equal(pool.cpu().numpy()[s], want)
+    assert (pool >= 0).float().mean() > 0.5
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_c5_pipeline_fused_counters(c5, offset):
+    """16M packets of the bench's global batch through the fused pipeline
+    with counters on: aligned (vector kernel) and offset by one (scalar)."""
+    import torch
+    clf, t, dev = c5
+    pool = clf.hint_search((t.pool_blob, t.pool_off, None))
+    n = 16 << 20
+    pk = B.gen_packets(0, n + 1, t, t.pool_n, dev=dev)
+    pk = tuple(x[offset:offset + n] for x in pk)
+    if offset:
+        assert pk[1].data_ptr() % 16 != 0
+    torch.cuda.synchronize()
+    clf.counters_enable(True)
+    clf.counters_reset()
+    outs = clf.pipeline_v4(*pk, pool, want_allow=True)
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    _check_batch(clf, t, dev, pk, outs, pool)
+
+
+def test_c5_pipeline_count_stream(c5):
+    """The counter finish on a separate stream (the bench schedule) gives
+    the same counters."""
+    import torch
+    clf, t, dev = c5
+    pool = clf.hint_search((t.pool_blob, t.pool_off, None))
+    n = 8 << 20
+    pk = B.gen_packets(5 << 20, n, t, t.pool_n, dev=dev)
+    s_cnt = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    clf.counters_enable(True)
+    clf.counters_reset()
+    outs = clf.pipeline_v4(*pk, pool, want_allow=True, count_stream=s_cnt)
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    _check_batch(clf, t, dev, pk, outs, pool)
+
+
+def test_generator_device_equals_host(c5):
+    """bench.gen_packets is index-addressable and device-independent."""
+    import torch
+    clf, t, dev = c5
+    a = B.gen_packets(123456, 100000, t, t.pool_n, dev=dev)
+    b = B.gen_packets(123456, 100000, t, t.pool_n, dev="cpu")
+    for x, y in zip(a, b):
+        assert torch.equal(x.cpu(), y)
+
+
+def test_dns_c4_scale():
+    """DNSServer classification at C4 scale: 100k groups + 50k hosts-file
+    names (the bench's DNS workload), oracle sample + group counters."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+        clf.compile_upstream(groups)
+        text = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
+                         for i in range(50_000))
+        clf.compile_hosts_text(text)
+        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+        names[::50] = [b"h%d.hosts.local." % i for i in range(0, len(names[::50]))]
+        names[7::97] = [b"h%d.hosts.local" % i for i in range(0, len(names[7::97]))]
+        names[3::211] = [b"1.2.3.%d." % (i & 255) for i in range(len(names[3::211]))]
+        blob, off = W.pack(names)
+        bd = torch.from_numpy(blob).cuda()
+        od = torch.from_numpy(off.astype(np.int32)).cuda()
+        clf.counters_enable(True)
+        clf.counters_reset()
+        kind, val = clf.dns_classify((bd, od))
+        torch.cuda.synchronize()
+        clf.counters_enable(False)
+        kind, val = kind.cpu().numpy(), val.cpu().numpy()
+        oh = O.Hosts(O.hosts_parse(text)[0])
+        og = O.Groups(groups)
+        s = np.random.default_rng(4).integers(0, len(names), 1200)
+        want = [O.dns_classify(oh, og, names[i]) for i in s]
+        assert [(int(kind[i]), int(val[i])) for i in s] == want
+        assert set(np.unique(kind)) >= {V.DNS_HOSTS, V.DNS_GROUP, V.DNS_IP_LITERAL}
+        g = val[kind == V.DNS_GROUP]
+        exp = np.bincount(g, minlength=len(groups) + 1).astype(np.uint64)
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp)
+    finally:
+        clf.close()
+
+
+def test_counters_values_outside_the_space():
+    """A counter space above 65,536 bins (the bucketed path) fed values at or
+    past its size -- e.g. a hostname pool classified against an older, larger
+    Upstream -- counts only the in-range values and never faults; the fused
+    pipeline agrees."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        ng = 70_000
+        groups = [({}, {"host": "g%d.example" % i}) for i in range(ng)]
+        clf.compile_upstream(groups)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3)
+        n = (4 << 20) + 3
+        out = torch.randint(-1, 3 * ng, (n,), generator=g, device="cuda", dtype=torch.int32)
+        out[::1000] = 2**31 - 1
+        clf.counters_enable(True)
+        clf.counters_reset()
+        clf.counters_add(V.COUNTERS_GROUP, out)
+        torch.cuda.synchronize()
+        o = out.long()
+        keep = (o >= 0) & (o < ng)
+        exp = torch.bincount(o[keep], minlength=ng + 1)
+        exp[ng] = int((o < 0).sum())
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP),
+                                      exp.cpu().numpy().astype(np.uint64))
+        # the pipeline's in-kernel group buckets, pool values past n_groups
+        tcp, udp = W.gen_sg_rules(100, 1)
+        a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+        b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+        V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
+        net, plen = W.gen_v4_prefixes(200_000, 2)
+        nets = W.v4_nets(net, plen)
+        ra, rn, rk = W.as_ctypes(nets, V._lib.VcNet)
+        clf.compile_routes_raw(ra, rn, (V._lib.VcNet * 1)(), 0)
+        pool = torch.randint(-1, 2 * ng, (1 << 20,), generator=g, device="cuda",
+                             dtype=torch.int32)
+        m = 8 << 20
+        T = lambda x: torch.from_numpy(x).cuda()
+        proto, src, port = W.gen_acl_queries(tcp, udp, m, 5)
+        dst = W.v4_lookups(net, plen, m, 6)
+        hid = torch.randint(0, 1 << 20, (m,), generator=g, device="cuda", dtype=torch.int32)
+        clf.counters_reset()
+        clf.counters_enable(True)
+        acl, route, grp, _ = clf.pipeline_v4(T(proto), T(src), T(dst), T(port), hid, pool)
+        torch.cuda.synchronize()
+        clf.counters_enable(False)
+        assert torch.equal(grp, pool[hid.long()])
+        o = grp.long()
+        keep = (o >= 0) & (o < ng)
+        exp = torch.bincount(o[keep], minlength=ng + 1)
+        exp[ng] = int((o < 0).sum())
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP),
+                                      exp.cpu().numpy().astype(np.uint64))
+        r = route.long()
+        exp = torch.bincount(torch.where(r >= 0, r, len(nets)), minlength=len(nets) + 2)
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE),
+                                      exp.cpu().numpy().astype(np.uint64))
+    finally:
+        clf.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("serial,finish", [(False, "stream"), (False, "inline"), (True, "inline")])
+def test_bench_schedule_with_rccl_bucket(serial, finish):
+    """bench.C5Steps with the counter bucket on: HitCounterBucket.fill copies
+    the library's device counters (vc_counters_device) device-to-device on
+    the counting stream, then one RCCL all-reduce (world size 1 on this
+    box); the elapsed-time MAX all-reduce of bench.main.  After W + K steps
+    over the same packets the bucket equals vc_counters_read and (W + K) x
+    the histograms of one step's outputs."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    clf = V.Classifier(0)
+    try:
+        t = B.c5_tables(clf, dev, 1 << 20, acl_rules=2000, v4=150_000, v6=20_000,
+                        groups=70_000)
+        lo, hi = B.shard(4_000_003, 0, 1)
+        pk = B.gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
+        steps = B.C5Steps(clf, t, pk, dev, bucket=True, serial=serial, finish=finish)
+        clf.counters_reset()
+        steps.run(0, 1, False)
+        torch.cuda.synchronize()
+        steps.reset_events()
+        steps.run(1, 2, True)
+        torch.cuda.synchronize()
+        el = B.max_over_ranks(1.5, dev)
+        assert el == 1.5
+        views = [v.cpu().numpy().view(np.uint64) for v in steps.bucket.views]
+        for k, v in zip((V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP), views):
+            np.testing.assert_array_equal(v, clf.counters_read(k))
+        acl, route, grp, _ = steps.outsb[0]
+        nt, nu = len(t.tcp), len(t.udp)
+        is_tcp = pk[0] == 6
+        a = acl.long()
+        bins = torch.where(a >= 0, torch.where(is_tcp, a, nt + a),
+                           torch.where(is_tcp, nt + nu, nt + nu + 1))
+        exp = 3 * torch.bincount(bins, minlength=nt + nu + 2)
+        np.testing.assert_array_equal(views[0], exp.cpu().numpy().astype(np.uint64))
+        r = route.long()
+        nn = t.n4 + t.n6
+        exp = 3 * torch.bincount(torch.where(r >= 0, r, nn), minlength=nn + 2)
+        np.testing.assert_array_equal(views[1], exp.cpu().numpy().astype(np.uint64))
+        g = grp.long()
+        ng = len(t.groups)
+        exp = 3 * torch.bincount(torch.where(g >= 0, g, ng), minlength=ng + 1)
+        np.testing.assert_array_equal(views[2], exp.cpu().numpy().astype(np.uint64))
+        assert steps.span("pipe") > 0
+    finally:
+        clf.close()
+        dist.destroy_process_group()

@@ -3,11 +3,13 @@
 The data path has no collective: each rank classifies its own shard of a
 seeded global batch.  Here the oracle stands in for the per-rank kernels
 (CPU tier, no GPU), and the test checks the host logic bench.py uses on
-the GPU box: the shard split, the single-bucket counter layout and the
-all-reduce, against the hit counters of the whole batch on one rank.
+the GPU box: bench.gen_packets' index-addressable global batch, the shard
+split, the single-bucket counter layout and the all-reduce, against the hit
+counters of the whole batch on one rank.
 """
 import os
 import socket
+import types
 
 import numpy as np
 import pytest
@@ -15,6 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+import bench as B
 import oracle_ffi as O
 from vproxy_amd import workloads as W
 from vproxy_amd.dist import HitCounterBucket, shard
@@ -53,10 +56,26 @@ def _counters(tcp, udp, nets, proto, src, port, dst):
     return [torch.from_numpy(ca.astype(np.int64)), torch.from_numpy(cr.astype(np.int64))]
 
 
-def _batch(tcp, udp, net, plen, n):
-    proto, src, port = W.gen_acl_queries(tcp, udp, n, 73)
-    dst = W.v4_lookups(net, plen, n, 74)
-    return proto, src, port, dst
+def _batch(tcp, udp, net, plen, n, lo=0):
+    """Items [lo, lo + n) of the seeded global batch (bench.gen_packets)."""
+    t = types.SimpleNamespace(tcp=tcp, udp=udp, net=net, plen=plen)
+    proto, src, dst, port, _ = (x.numpy() for x in B.gen_packets(lo, n, t, 1000, seed=73))
+    return proto, src.view(np.uint32), port.view(np.uint16), dst.view(np.uint32)
+
+
+def test_global_batch_is_shardable():
+    """Rank r's slice generated on its own equals the same slice of the
+    whole batch, for every world size (bench.py generates only its shard)."""
+    tcp, udp, net, plen, nets = _tables()
+    n = 10007
+    whole = _batch(tcp, udp, net, plen, n)
+    assert (whole[0] == 6).mean() > 0.4 and (whole[0] == 17).mean() > 0.4
+    for world in (2, 3, 8):
+        for r in range(world):
+            lo, hi = shard(n, r, world)
+            part = _batch(tcp, udp, net, plen, hi - lo, lo)
+            for a, b in zip(part, whole):
+                np.testing.assert_array_equal(a, b[lo:hi])
 
 
 def _worker(rank, world, port, n, q):
@@ -65,9 +84,9 @@ def _worker(rank, world, port, n, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         tcp, udp, net, plen, nets = _tables()                 # replicated tables
-        proto, src, dport, dst = _batch(tcp, udp, net, plen, n)
         lo, hi = shard(n, rank, world)
-        mine = _counters(tcp, udp, nets, proto[lo:hi], src[lo:hi], dport[lo:hi], dst[lo:hi])
+        proto, src, dport, dst = _batch(tcp, udp, net, plen, hi - lo, lo)   # this rank's shard
+        mine = _counters(tcp, udp, nets, proto, src, dport, dst)
         b = HitCounterBucket([t.numel() for t in mine], "cpu")
         for i, t in enumerate(mine):
             b.fill(i, t)

@@ -45,6 +45,15 @@ class VcPktOut(C.Structure):
                 ("dst6", C.c_void_p), ("sport", C.c_void_p), ("dport", C.c_void_p)]
 
 
+class VcPackets(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("family", "proto", "src4", "dst4", "src6", "dst6",
+                                          "dport", "host_id")]
+
+
+class VcPipelineOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("acl", "route", "group", "allow")]
+
+
 class VcServer(C.Structure):
     _fields_ = [("ip", C.c_uint8 * 16), ("ip_len", C.c_int32), ("port", C.c_int32),
                 ("weight", C.c_int32), ("healthy", C.c_int32)]
@@ -155,6 +164,9 @@ def lib():
         L.vc_pipeline_v4_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
         L.vc_pipeline_v4_dev_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                             vp, vp]
+        L.vc_pipeline_dev.argtypes = [vp, P(VcPackets), i64, vp, i64, P(VcPipelineOut), vp, vp,
+                                      vp]
+        L.vc_pipeline.argtypes = [vp, P(VcPackets), i64, vp, i64, P(VcPipelineOut)]
         L.vc_compile_servers.argtypes = [vp, P(VcServer), vp, i32]
         L.vc_servers_set_health.argtypes = [vp, vp, i64]
         for f in ("vc_source_select_v4_dev", "vc_source_select_v6_dev"):

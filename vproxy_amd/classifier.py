@@ -499,24 +499,60 @@ class Classifier:
         return kind, val
 
     def pipeline_v4(self, proto, src4, dst4, dport, host_id, pool_group, outs=None,
-                    want_allow=False, kernel_done_event=None):
-        """Combined ACL -> route -> host pipeline on device tensors.
+                    want_allow=False, kernel_done_event=None, count_stream=None):
+        """Combined ACL -> route -> host pipeline on device tensors (IPv4).
         kernel_done_event: optional raw hipEvent_t (int) recorded right after
-        the classify kernel, before any hit-counter passes."""
-        import torch
-        n = len(src4)
-        if outs is None:
-            dev = src4.device
-            outs = (torch.empty(n, dtype=torch.int32, device=dev),
-                    torch.empty(n, dtype=torch.int32, device=dev),
-                    torch.empty(n, dtype=torch.int32, device=dev),
-                    torch.empty(n, dtype=torch.uint8, device=dev) if want_allow else None)
+        the classify kernel; count_stream: optional torch stream the
+        hit-counter finish passes run on (after the kernel)."""
+        return self.pipeline(proto, src4, dst4, dport, host_id, pool_group, outs=outs,
+                             want_allow=want_allow, kernel_done_event=kernel_done_event,
+                             count_stream=count_stream)
+
+    def pipeline(self, proto, src4, dst4, dport, host_id=None, pool_group=None, family=None,
+                 src6=None, dst6=None, outs=None, want_allow=False, kernel_done_event=None,
+                 count_stream=None):
+        """vc_pipeline(_dev): per packet SecurityGroup.allow(proto, src, dport)
+        -> RouteTable.lookup(dst) (rulesV4 or rulesV6 by `family`, 4 or 6)
+        -> pool_group[host_id].  torch CUDA tensors run on the device
+        (asynchronous, torch's current stream); numpy arrays take the host
+        entry point (synchronous, PCIe included).  src6/dst6: n x 16 bytes.
+        Returns (acl, route, group, allow)."""
+        n = len(proto)
+        dev = _is_dev(proto)
+        if dev:
+            import torch
+            mk = lambda dt: torch.empty(n, dtype=dt, device=proto.device)
+            if outs is None:
+                outs = (mk(torch.int32), mk(torch.int32), mk(torch.int32),
+                        mk(torch.uint8) if want_allow else None)
+        else:
+            conv = lambda x, dt: None if x is None else np.ascontiguousarray(x, dt)
+            proto, src4, dst4 = conv(proto, np.uint8), conv(src4, np.uint32), conv(dst4, np.uint32)
+            dport, host_id = conv(dport, np.uint16), conv(host_id, np.uint32)
+            pool_group, family = conv(pool_group, np.int32), conv(family, np.uint8)
+            src6, dst6 = conv(src6, np.uint8), conv(dst6, np.uint8)
+            if outs is None:
+                outs = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32),
+                        np.empty(n, np.uint8) if want_allow else None)
+        keep = (proto, src4, dst4, dport, host_id, pool_group, family, src6, dst6)
+        pk = _lib.VcPackets(*[x.value if x is not None else None for x in
+                              (_ptr(family), _ptr(proto), _ptr(src4), _ptr(dst4), _ptr(src6),
+                               _ptr(dst6), _ptr(dport), _ptr(host_id))])
         a, r, g, al = outs
-        check(lib().vc_pipeline_v4_dev_ex(self.h, _ptr(proto), _ptr(src4), _ptr(dst4),
-                                          _ptr(dport), _ptr(host_id), _ptr(pool_group),
-                                          len(pool_group), n, _ptr(a), _ptr(r), _ptr(g), _ptr(al),
-                                          _stream(), C.c_void_p(kernel_done_event)
-                                          if kernel_done_event else None))
+        po = _lib.VcPipelineOut(*[x.value if x is not None else None for x in
+                                  (_ptr(a), _ptr(r), _ptr(g), _ptr(al))])
+        n_pool = len(pool_group) if pool_group is not None else 0
+        if dev:
+            check(lib().vc_pipeline_dev(self.h, C.byref(pk), n, _ptr(pool_group), n_pool,
+                                        C.byref(po), _stream(),
+                                        C.c_void_p(count_stream.cuda_stream)
+                                        if count_stream is not None else None,
+                                        C.c_void_p(kernel_done_event)
+                                        if kernel_done_event else None))
+        else:
+            check(lib().vc_pipeline(self.h, C.byref(pk), n, _ptr(pool_group), n_pool,
+                                    C.byref(po)))
+        del keep
         return outs
 
     # ---------------- header extraction ----------------

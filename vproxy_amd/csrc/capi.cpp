@@ -4,6 +4,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -92,7 +93,11 @@ struct MirrorSnap : Snapshot {
 };
 struct ServerSnap : Snapshot {
     ServerImage img{};
-    uint8_t* healthy = nullptr;    // device copy, updated in place (vc_servers_set_health)
+    // A health update publishes a new snapshot that owns a fresh healthy[]
+    // and shares the compiled lists of the snapshot vc_compile_servers made
+    // (kept alive through `lists`), so a batch keeps one health view for all
+    // of its chunks.
+    std::shared_ptr<const ServerSnap> lists;
 };
 
 }  // namespace
@@ -361,17 +366,36 @@ int vc_acl_classify_v6_dev(vc_ctx* ctx, const uint8_t* proto, const uint8_t* src
 // its download is enqueued, so the pool reuses it for chunk k + 2.
 constexpr int64_t kHostChunk = int64_t(4) << 20;
 
-// Device address of a page-locked, mapped host buffer (vc_host_register),
-// or null for ordinary pageable memory.  Kernels then read their inputs and
-// write their outputs across PCIe directly (both directions at once).
-static void* mapped(const void* h) {
+// Buffers registered through vc_host_register: base -> length.  A zero-copy
+// call needs every array's whole extent [p, p + bytes) inside one of them; a
+// short registration (or one made by someone else, whose extent we do not
+// know) falls back to chunked staging instead of faulting on the device.
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, size_t> g_reg;
+
+// Device address of `bytes` bytes at h inside a page-locked, mapped host
+// buffer (vc_host_register), or null -- ordinary pageable memory, a range
+// the registration does not cover, or a device address that is not
+// `align`-aligned (IPv6 arrays are read as 16-byte words).  Kernels then read
+// their inputs and write their outputs across PCIe directly (both directions
+// at once).
+static void* mapped(const void* h, size_t bytes, uintptr_t align = 1) {
     if (!h) return nullptr;
+    {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(h);
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.upper_bound(p);
+        if (it == g_reg.begin()) return nullptr;
+        --it;
+        if (p - it->first > it->second || bytes > it->second - (p - it->first)) return nullptr;
+    }
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, h) != hipSuccess) {
-        (void)hipGetLastError();                 // pageable memory: clear the error
+        (void)hipGetLastError();
         return nullptr;
     }
     if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    if (reinterpret_cast<uintptr_t>(a.devicePointer) & (align - 1)) return nullptr;
     return a.devicePointer;
 }
 
@@ -399,9 +423,9 @@ static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!proto || !src || !port || !out_idx) return fail(VC_EINVAL, "bad batch arguments");
-    const size_t sw = fam == 4 ? 4 : 16;
-    void *mp = mapped(proto), *ms = mapped(src), *mq = mapped(port), *mi = mapped(out_idx);
-    void* ma = mapped(out_allow);
+    const size_t sw = fam == 4 ? 4 : 16, un = size_t(n);
+    void *mp = mapped(proto, un), *ms = mapped(src, un * sw, sw), *mq = mapped(port, un * 2);
+    void *mi = mapped(out_idx, un * 4), *ma = mapped(out_allow, un);
     if (mp && ms && mq && mi && (!out_allow || ma)) {            // zero-copy
         rc = acl_dev(ctx, fam, static_cast<uint8_t*>(mp), ms, static_cast<uint16_t*>(mq), n,
                      static_cast<int32_t*>(mi), static_cast<uint8_t*>(ma), ctx->stream);
@@ -498,7 +522,7 @@ static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t*
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!dst || !out) return fail(VC_EINVAL, "bad batch arguments");
     const size_t sw = fam == 4 ? 4 : 16;
-    void *md = mapped(dst), *mo = mapped(out);
+    void *md = mapped(dst, size_t(n) * sw, sw), *mo = mapped(out, size_t(n) * 4);
     if (md && mo) {                                              // zero-copy
         rc = route_dev(ctx, fam, md, n, static_cast<int32_t*>(mo), ctx->stream);
         if (rc) return rc;
@@ -585,6 +609,8 @@ int vc_hint_search(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_o
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!out_group || (host_blob && !host_off) || (uri_blob && !uri_off))
+        return fail(VC_EINVAL, "bad batch arguments");
     Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     size_t hb = host_blob ? host_off[n] : 0, ub = uri_blob ? uri_off[n] : 0;
@@ -659,6 +685,7 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
     int rc = set_dev(ctx);
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!qblob || !qoff || !out_kind || !out_value) return fail(VC_EINVAL, "bad batch arguments");
     Staging st(ctx->pool, ctx->stream);
     hipStream_t s = ctx->stream;
     auto* db = static_cast<uint8_t*>(st.in(qblob, qoff[n], s));
@@ -736,11 +763,18 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
 int vc_host_register(void* p, int64_t bytes) {
     if (!p || bytes <= 0) return fail(VC_EINVAL, "bad host buffer");
     hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterMapped);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "hipHostRegister");
+    if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[reinterpret_cast<uintptr_t>(p)] = size_t(bytes);
+    return VC_OK;
 }
 
 int vc_host_unregister(void* p) {
     if (!p) return fail(VC_EINVAL, "bad host buffer");
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.erase(reinterpret_cast<uintptr_t>(p));
+    }
     hipError_t e = hipHostUnregister(p);
     return e == hipSuccess ? VC_OK : hip_fail(e, "hipHostUnregister");
 }
@@ -859,8 +893,7 @@ int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* gro
     hipError_t e = hipSuccess;
     s->img.view_off = s->upload(b.view_off, &e);
     s->img.order = s->upload(b.order, &e);
-    s->healthy = const_cast<uint8_t*>(s->upload(b.healthy, &e));
-    s->img.healthy = s->healthy;
+    s->img.healthy = s->upload(b.healthy, &e);
     s->img.group_base = s->upload(b.group_base, &e);
     s->img.n_groups = b.n_groups;
     s->img.n_servers = b.n_servers;
@@ -872,16 +905,22 @@ int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* gro
 int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers) {
     int rc = set_dev(ctx);
     if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = ctx->get(ctx->servers);
     if (!s) return fail(VC_ESTATE, "no servers compiled");
     if (n_servers != s->img.n_servers || (n_servers > 0 && !healthy))
         return fail(VC_EINVAL, "health array does not match the compiled servers");
     std::vector<uint8_t> h(healthy, healthy + n_servers);
     for (auto& x : h) x = x ? 1 : 0;
-    hipError_t e = n_servers ? hipMemcpy(s->healthy, h.data(), size_t(n_servers),
-                                         hipMemcpyHostToDevice)
-                             : hipSuccess;
-    return e == hipSuccess ? VC_OK : hip_fail(e, "health upload");
+    // copy-on-write: batches in flight keep the snapshot (and health) they pinned
+    auto ns = std::make_shared<ServerSnap>();
+    ns->img = s->img;
+    ns->lists = s->lists ? s->lists : s;
+    hipError_t e = hipSuccess;
+    ns->img.healthy = ns->upload(h, &e);
+    if (e != hipSuccess) return hip_fail(e, "health upload");
+    ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(ns)));
+    return VC_OK;
 }
 
 static int source_dev(vc_ctx* ctx, int fam, const int32_t* group, const void* src, int64_t n,
@@ -906,8 +945,8 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!group || !src || !out) return fail(VC_EINVAL, "bad batch arguments");
-    const size_t sw = fam == 4 ? 4 : 16;
-    void *mg = mapped(group), *ms = mapped(src), *mo = mapped(out);
+    const size_t sw = fam == 4 ? 4 : 16, un = size_t(n);
+    void *mg = mapped(group, un * 4), *ms = mapped(src, un * sw, sw), *mo = mapped(out, un * 4);
     if (mg && ms && mo) {                                        // zero-copy
         rc = source_dev(ctx, fam, static_cast<int32_t*>(mg), ms, n, view,
                         static_cast<int32_t*>(mo), ctx->stream);
@@ -1025,25 +1064,137 @@ int vc_pipeline_v4_dev_ex(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src
                           const int32_t* pool_group, int64_t n_pool, int64_t n, int32_t* out_acl,
                           int32_t* out_route, int32_t* out_group, uint8_t* out_allow, void* stream,
                           void* kernel_done_event) {
+    if (n > 0 && !host_id) return fail(VC_EINVAL, "bad batch arguments");
+    const vc_packets in{nullptr, proto, src4, dst4, nullptr, nullptr, dport, host_id};
+    const vc_pipeline_out out{out_acl, out_route, out_group, out_allow};
+    return vc_pipeline_dev(ctx, &in, n, pool_group, n_pool, &out, stream, nullptr,
+                           kernel_done_event);
+}
+
+namespace {
+struct PipePins {                  // the snapshots one pipeline call classifies against
+    std::shared_ptr<const AclSnap> a;
+    std::shared_ptr<const RouteSnap> r;
+    std::shared_ptr<const HintSnap> h;
+};
+}  // namespace
+
+static int pipeline_check(const vc_packets* in, int64_t n, const int32_t* pool_group,
+                          int64_t n_pool, const vc_pipeline_out* out) {
+    if (n < 0 || n_pool < 0 || !in || !out) return fail(VC_EINVAL, "bad batch arguments");
+    if (n == 0) return VC_OK;
+    if (!in->proto || !in->src4 || !in->dst4 || !in->dport || !out->acl || !out->route ||
+        !out->group || (in->host_id && n_pool > 0 && !pool_group))
+        return fail(VC_EINVAL, "bad batch arguments");
+    if (in->family && (!in->src6 || !in->dst6))
+        return fail(VC_EINVAL, "a batch with a family array needs src6 and dst6");
+    return VC_OK;
+}
+
+static int pipeline_dev(vc_ctx* ctx, const vc_packets& in, int64_t n, const int32_t* pool_group,
+                        int64_t n_pool, const vc_pipeline_out& out, void* stream,
+                        void* count_stream, void* kernel_done, const PipePins& pin) {
+    if ((in.src6 && (reinterpret_cast<uintptr_t>(in.src6) & 15)) ||
+        (in.dst6 && (reinterpret_cast<uintptr_t>(in.dst6) & 15)))
+        return fail(VC_EINVAL, "src6 / dst6 must be 16-byte aligned");
+    if (!pin.a || !pin.r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
+    const bool on = ctx->counters_on;
+    vc::PipeArgs p{in.family, in.proto, in.src4, in.dst4, in.src6, in.dst6, in.dport, in.host_id,
+                   pool_group, in.host_id ? n_pool : 0, n, out.acl, out.route, out.group,
+                   out.allow};
+    vc::PipeCounters cnt{on ? pin.a->counters : nullptr, on ? pin.r->counters : nullptr,
+                         on && pin.h && in.host_id ? pin.h->counters : nullptr,
+                         pin.h ? pin.h->img.n_groups : 0};
+    hipError_t e = vc::launch_pipeline(ctx->cfg(stream), pin.a->img, pin.r->img, pin.r->n4,
+                                       pin.r->n6, p, cnt, static_cast<hipEvent_t>(kernel_done),
+                                       static_cast<hipStream_t>(count_stream));
+    return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");
+}
+
+int vc_pipeline_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,
+                    int64_t n_pool, const vc_pipeline_out* out, void* stream, void* count_stream,
+                    void* kernel_done_event) {
     int rc = set_dev(ctx);
     if (rc) return rc;
-    if (n < 0 || n_pool < 0 || (n > 0 && (!proto || !src4 || !dst4 || !dport || !host_id ||
-                                          (n_pool > 0 && !pool_group) ||
-                            !out_acl || !out_route || !out_group)))
-        return fail(VC_EINVAL, "bad batch arguments");
-    auto a = ctx->get(ctx->acl);
-    auto r = ctx->get(ctx->route);
-    auto h = ctx->get(ctx->hint);
-    if (!a || !r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
-    const bool on = ctx->counters_on;
-    const int32_t ng = h ? h->img.n_groups : 0;
-    hipError_t e = vc::launch_pipeline_v4(
-        ctx->cfg(stream), a->img, r->img.fam[0], proto, src4, dst4, dport, host_id, pool_group,
-        n_pool, n,
-        out_acl, out_route, out_group, out_allow, on ? a->counters : nullptr,
-        on ? r->counters : nullptr, int64_t(r->n4) + r->n6, on && h ? h->counters : nullptr, ng,
-        static_cast<hipEvent_t>(kernel_done_event));
-    return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");
+    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
+    const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
+    return pipeline_dev(ctx, *in, n, pool_group, n_pool, *out, stream, count_stream,
+                        kernel_done_event, pin);
+}
+
+int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,
+                int64_t n_pool, const vc_pipeline_out* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
+    if (n == 0) return VC_OK;
+    const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
+    if (!pin.a || !pin.r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
+    const size_t un = size_t(n);
+    const bool six = in->family != nullptr;
+    const size_t pool_bytes = in->host_id ? size_t(n_pool) * 4 : 0;
+    // zero-copy when every array lies inside a registered buffer
+    vc_packets m{};
+    vc_pipeline_out mo{};
+    bool zc = true;
+    auto map = [&](const void* h, size_t bytes, uintptr_t al) -> void* {
+        if (!h || !bytes) return nullptr;
+        void* d = mapped(h, bytes, al);
+        if (!d) zc = false;
+        return d;
+    };
+    m.family = static_cast<const uint8_t*>(map(in->family, un, 1));
+    m.proto = static_cast<const uint8_t*>(map(in->proto, un, 1));
+    m.src4 = static_cast<const uint32_t*>(map(in->src4, un * 4, 4));
+    m.dst4 = static_cast<const uint32_t*>(map(in->dst4, un * 4, 4));
+    m.src6 = static_cast<const uint8_t*>(map(six ? in->src6 : nullptr, un * 16, 16));
+    m.dst6 = static_cast<const uint8_t*>(map(six ? in->dst6 : nullptr, un * 16, 16));
+    m.dport = static_cast<const uint16_t*>(map(in->dport, un * 2, 2));
+    m.host_id = static_cast<const uint32_t*>(map(in->host_id, un * 4, 4));
+    const auto* mpool = static_cast<const int32_t*>(map(pool_bytes ? pool_group : nullptr,
+                                                        pool_bytes, 4));
+    mo.acl = static_cast<int32_t*>(map(out->acl, un * 4, 4));
+    mo.route = static_cast<int32_t*>(map(out->route, un * 4, 4));
+    mo.group = static_cast<int32_t*>(map(out->group, un * 4, 4));
+    mo.allow = static_cast<uint8_t*>(map(out->allow, un, 1));
+    if (zc) {
+        rc = pipeline_dev(ctx, m, n, mpool, n_pool, mo, ctx->stream, nullptr, nullptr, pin);
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline");
+    }
+    // chunked staging; the hostname pool results are uploaded once
+    Staging pst(ctx->pool, ctx->stream);
+    const int32_t* dpool = pool_bytes
+        ? static_cast<const int32_t*>(pst.in(pool_group, pool_bytes, ctx->stream)) : nullptr;
+    if (pst.err == hipSuccess) pst.err = hipStreamSynchronize(ctx->stream);
+    if (pst.err != hipSuccess) return hip_fail(pst.err, "pool upload");
+    return host_chunks(ctx, n, "pipeline", [&](Staging& st, int64_t lo, int64_t c, hipStream_t s) {
+        const size_t u = size_t(lo), k = size_t(c);
+        vc_packets d{};
+        vc_pipeline_out o{};
+        d.family = six ? static_cast<const uint8_t*>(st.in(in->family + u, k, s)) : nullptr;
+        d.proto = static_cast<const uint8_t*>(st.in(in->proto + u, k, s));
+        d.src4 = static_cast<const uint32_t*>(st.in(in->src4 + u, k * 4, s));
+        d.dst4 = static_cast<const uint32_t*>(st.in(in->dst4 + u, k * 4, s));
+        d.src6 = six ? static_cast<const uint8_t*>(st.in(in->src6 + u * 16, k * 16, s)) : nullptr;
+        d.dst6 = six ? static_cast<const uint8_t*>(st.in(in->dst6 + u * 16, k * 16, s)) : nullptr;
+        d.dport = static_cast<const uint16_t*>(st.in(in->dport + u, k * 2, s));
+        d.host_id = in->host_id ? static_cast<const uint32_t*>(st.in(in->host_id + u, k * 4, s))
+                                : nullptr;
+        o.acl = static_cast<int32_t*>(st.out(out->acl, k * 4));
+        o.route = static_cast<int32_t*>(st.out(out->route, k * 4));
+        o.group = static_cast<int32_t*>(st.out(out->group, k * 4));
+        o.allow = static_cast<uint8_t*>(st.out(out->allow, k));
+        if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
+        int r = pipeline_dev(ctx, d, c, dpool, n_pool, o, s, nullptr, nullptr, pin);
+        if (r) return r;
+        st.back(out->acl + u, o.acl, k * 4, s);
+        st.back(out->route + u, o.route, k * 4, s);
+        st.back(out->group + u, o.group, k * 4, s);
+        if (out->allow) st.back(out->allow + u, o.allow, k, s);
+        return VC_OK;
+    });
 }
 
 // ---------------------------------------------------------------------------

@@ -266,19 +266,45 @@ __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, u
     return e;
 }
 
-// In-kernel hit counting of the pipeline (launch_pipeline_v4): the ACL
+__device__ __forceinline__ uint32_t route6_chase(const uint32_t* nodes, int rb, uint32_t e,
+                                                 uint64_t hi, uint64_t lo) {
+    int bits = rb;
+    const uint32_t root = 1u << rb;
+    while (e & VC_PTR) {
+        const uint32_t sub = bits < 64 ? uint32_t(hi >> (56 - bits)) & 255u
+                                       : uint32_t(lo >> (120 - bits)) & 255u;
+        e = nodes[root + (e & ~VC_PTR) * 256u + sub];
+        bits += 8;
+    }
+    return e;
+}
+
+// SecurityGroup.allow on one IPv6 source: the protocol list's v6 projection
+// (128-bit interval search in L2-resident global memory).
+__device__ __forceinline__ uint32_t acl_v6_one(const AclImage& img, bool tcp, uint4 w,
+                                               uint32_t port) {
+    const AclFamilyImage& f = tcp ? img.fam[0][1] : img.fam[1][1];
+    uint64_t hi, lo;
+    v6_key(w, &hi, &lo);
+    const int j = bsearch_u128(f.bounds6, f.nb, hi, lo);
+    return port_lookup(f.pieces, load_desc(f.desc, j), port);
+}
+
+// In-kernel hit counting of the pipeline (launch_pipeline): the ACL
 // histogram in LDS next to the staged boundaries, and per-workgroup bucket
 // counts of the route and group outputs -- the first pass of the large
 // counter-space histogram (counters.hip), which then only scans, scatters
 // and histograms.  The kernel is bound by its table gathers, so the LDS
 // atomics ride along for free and two passes over the outputs disappear.
+// Route values are counted in the combined space [v4 rules][v6 rules].
 struct PipeCount {
     unsigned long long* acl;       // ACL counters, or null: not counted here
     int32_t acl_bins;              // n_tcp + n_udp (LDS words)
     int32_t n_tcp;
     uint32_t* rcounts;             // route bucket counts [bucket * grid + block], or null
     int32_t r_nbk;
-    unsigned long long* route;     // route counters (null bin at route_none_at)
+    int32_t n4;                    // v6 route index r counts as n4 + r
+    unsigned long long* route;     // route counters (v4 null at route_none_at, v6 null next)
     int64_t route_none_at;
     uint32_t* gcounts;             // group bucket counts, or null
     int32_t g_nbk;
@@ -288,35 +314,102 @@ struct PipeCount {
 };
 
 struct PipeTally {                 // per-thread null counts
-    uint32_t acl_tcp = 0, acl_udp = 0, route = 0, group = 0;
+    uint32_t acl_tcp = 0, acl_udp = 0, route = 0, route6 = 0, group = 0;
 };
 
 __device__ __forceinline__ void pipe_count(const PipeCount& pc, uint32_t* ah, uint32_t* rc,
-                                           uint32_t* gc, bool tcp, uint32_t v, int32_t r,
-                                           int32_t g, PipeTally* t) {
+                                           uint32_t* gc, bool tcp, uint32_t v, bool v6,
+                                           int32_t r, int32_t g, PipeTally* t) {
     if (pc.acl) {
         if (v != VC_NONE) atomicAdd(&ah[tcp ? v : uint32_t(pc.n_tcp) + v], 1u);
         else if (tcp) ++t->acl_tcp;
         else ++t->acl_udp;
     }
     if (pc.rcounts) {
-        if (r >= 0) atomicAdd(&rc[r >> pc.bw_shift], 1u);
+        if (r >= 0) atomicAdd(&rc[(v6 ? r + pc.n4 : r) >> pc.bw_shift], 1u);
+        else if (v6) ++t->route6;
         else ++t->route;
     }
     if (pc.gcounts) {
-        if (g >= 0) atomicAdd(&gc[g >> pc.bw_shift], 1u);
-        else ++t->group;
+        // pool results at or past n_groups (a pool classified against an
+        // older Upstream snapshot) are not counted, as in counters.hip
+        if (g >= 0) {
+            if (g < pc.n_groups) atomicAdd(&gc[g >> pc.bw_shift], 1u);
+        } else {
+            ++t->group;
+        }
     }
 }
 
-// One packet through ACL -> route -> pool group (scalar form, also the tail).
+// Flush of the in-kernel counts (every thread of the workgroup calls it).
+__device__ __forceinline__ void pipe_count_flush(const PipeCount& pc, uint32_t* ah, uint32_t* rc,
+                                                 uint32_t* gc, uint32_t* tally,
+                                                 const PipeTally& t) {
+    if (t.acl_tcp) atomicAdd(&tally[0], t.acl_tcp);
+    if (t.acl_udp) atomicAdd(&tally[1], t.acl_udp);
+    if (t.route) atomicAdd(&tally[2], t.route);
+    if (t.group) atomicAdd(&tally[3], t.group);
+    if (t.route6) atomicAdd(&tally[4], t.route6);
+    __syncthreads();
+    if (pc.acl) {
+        for (int k = threadIdx.x; k < pc.acl_bins; k += blockDim.x)
+            if (ah[k]) atomicAdd(pc.acl + k, (unsigned long long)ah[k]);
+        if (threadIdx.x == 0) {                   // [tcp default][udp default]
+            if (tally[0]) atomicAdd(pc.acl + pc.acl_bins, (unsigned long long)tally[0]);
+            if (tally[1]) atomicAdd(pc.acl + pc.acl_bins + 1, (unsigned long long)tally[1]);
+        }
+    }
+    if (pc.rcounts) {
+        for (int k = threadIdx.x; k < pc.r_nbk; k += blockDim.x)
+            pc.rcounts[int64_t(k) * gridDim.x + blockIdx.x] = rc[k];
+        if (threadIdx.x == 0 && tally[2])
+            atomicAdd(pc.route + pc.route_none_at, (unsigned long long)tally[2]);
+        if (threadIdx.x == 0 && tally[4])
+            atomicAdd(pc.route + pc.route_none_at + 1, (unsigned long long)tally[4]);
+    }
+    if (pc.gcounts) {
+        for (int k = threadIdx.x; k < pc.g_nbk; k += blockDim.x)
+            pc.gcounts[int64_t(k) * gridDim.x + blockIdx.x] = gc[k];
+        if (threadIdx.x == 0 && tally[3])
+            atomicAdd(pc.group + pc.n_groups, (unsigned long long)tally[3]);
+    }
+}
+
+// LDS layout of a pipeline workgroup: staged v4 ACL boundaries, then the
+// ACL histogram, route bucket counts and group bucket counts.
+struct PipeLds {
+    uint32_t* ah;
+    uint32_t* rc;
+    uint32_t* gc;
+};
+
+template <bool kLds, bool kCount>
+__device__ __forceinline__ PipeLds pipe_lds_setup(const AclImage& img, const PipeCount& pc,
+                                                  uint32_t* lds, uint32_t* tally) {
+    const int words = kLds ? img.fam[0][0].nb + img.fam[1][0].nb : 0;
+    PipeLds L;
+    L.ah = lds + words;
+    L.rc = L.ah + (pc.acl ? pc.acl_bins : 0);
+    L.gc = L.rc + (pc.rcounts ? pc.r_nbk : 0);
+    if (kCount) {
+        const int cw = (pc.acl ? pc.acl_bins : 0) + (pc.rcounts ? pc.r_nbk : 0) +
+                       (pc.gcounts ? pc.g_nbk : 0);
+        for (int k = threadIdx.x; k < cw; k += blockDim.x) L.ah[k] = 0;
+        if (threadIdx.x < 5) tally[threadIdx.x] = 0;
+    }
+    if (kLds) stage_bounds(img, lds);
+    else if (kCount) __syncthreads();
+    return L;
+}
+
+// One IPv4 packet through ACL -> route -> pool group (scalar form, also the tail).
 template <bool kCount>
 __device__ __forceinline__ void pipeline_one(
     const AclImage& img, const AclV4Ctx& a, const uint32_t* nodes, int rb, const uint8_t* proto,
     const uint32_t* src, const uint32_t* dst, const uint16_t* dport, const uint32_t* host_id,
     const int32_t* pool_group, int64_t n_pool, int64_t i, int32_t* out_acl, int32_t* out_route,
-    int32_t* out_group, uint8_t* out_allow, const PipeCount& pc, uint32_t* ah, uint32_t* rc,
-    uint32_t* gc, PipeTally* t) {
+    int32_t* out_group, uint8_t* out_allow, const PipeCount& pc, const PipeLds& L,
+    PipeTally* t) {
     const uint32_t d = dst[i];
     const uint32_t e = nodes[d >> (32 - rb)];
     const uint32_t h = host_id[i];
@@ -327,7 +420,7 @@ __device__ __forceinline__ void pipeline_one(
     const int32_t r = out_index(route_chase(nodes, rb, e, d));
     out_route[i] = r;
     out_group[i] = grp;
-    if (kCount) pipe_count(pc, ah, rc, gc, tcp, v, r, grp, t);
+    if (kCount) pipe_count(pc, L.ah, L.rc, L.gc, tcp, v, false, r, grp, t);
 }
 
 // Contiguous slice [lo, hi) of n items owned by this workgroup, on 4-item
@@ -353,19 +446,8 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     int32_t* __restrict__ out_acl, int32_t* __restrict__ out_route,
     int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow, PipeCount pc) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int words = kLds ? img.fam[0][0].nb + img.fam[1][0].nb : 0;
-    uint32_t* ah = lds + words;                                  // ACL histogram
-    uint32_t* rc = ah + (pc.acl ? pc.acl_bins : 0);             // route bucket counts
-    uint32_t* gc = rc + (pc.rcounts ? pc.r_nbk : 0);            // group bucket counts
-    __shared__ uint32_t tally[4];
-    if (kCount) {
-        const int cw = (pc.acl ? pc.acl_bins : 0) + (pc.rcounts ? pc.r_nbk : 0) +
-                       (pc.gcounts ? pc.g_nbk : 0);
-        for (int k = threadIdx.x; k < cw; k += blockDim.x) ah[k] = 0;
-        if (threadIdx.x < 4) tally[threadIdx.x] = 0;
-    }
-    if (kLds) stage_bounds(img, lds);
-    else if (kCount) __syncthreads();
+    __shared__ uint32_t tally[5];
+    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally);
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
     int64_t lo, hi;
     pipe_slice(n, &lo, &hi);
@@ -373,8 +455,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     if (!kVec) {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
             pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
-                                 n_pool, i, out_acl, out_route, out_group, out_allow, pc, ah, rc,
-                                 gc, &t);
+                                 n_pool, i, out_acl, out_route, out_group, out_allow, pc, L, &t);
     } else {
         for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
             const int64_t g = i >> 2;
@@ -417,7 +498,8 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
             if (out_allow) reinterpret_cast<uint32_t*>(out_allow)[g] = al;
             if (kCount) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) pipe_count(pc, ah, rc, gc, tcp[k], v[k], pr_[k], grp[k], &t);
+                for (int k = 0; k < 4; ++k)
+                    pipe_count(pc, L.ah, L.rc, L.gc, tcp[k], v[k], false, pr_[k], grp[k], &t);
             }
         }
         // last partial group of 4 (only the final slice, when n % 4 != 0)
@@ -425,34 +507,157 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
         if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
             pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
                                  n_pool, tail + threadIdx.x, out_acl, out_route, out_group,
-                                 out_allow, pc, ah, rc, gc, &t);
+                                 out_allow, pc, L, &t);
     }
-    if (!kCount) return;
-    if (t.acl_tcp) atomicAdd(&tally[0], t.acl_tcp);
-    if (t.acl_udp) atomicAdd(&tally[1], t.acl_udp);
-    if (t.route) atomicAdd(&tally[2], t.route);
-    if (t.group) atomicAdd(&tally[3], t.group);
-    __syncthreads();
-    if (pc.acl) {
-        for (int k = threadIdx.x; k < pc.acl_bins; k += blockDim.x)
-            if (ah[k]) atomicAdd(pc.acl + k, (unsigned long long)ah[k]);
-        if (threadIdx.x == 0) {                   // [tcp default][udp default]
-            if (tally[0]) atomicAdd(pc.acl + pc.acl_bins, (unsigned long long)tally[0]);
-            if (tally[1]) atomicAdd(pc.acl + pc.acl_bins + 1, (unsigned long long)tally[1]);
+    if (kCount) pipe_count_flush(pc, L.ah, L.rc, L.gc, tally, t);
+}
+
+// ---------------------------------------------------------------------------
+// Mixed-family pipeline: per packet, `family` (4 or 6) is the `instanceof
+// IPv4` dispatch of RouteTable.lookup (RouteTable.java:44-58) and of the
+// caller's IP object: an IPv4 packet runs the v4 ACL projection and rulesV4,
+// an IPv6 packet (IPv4-mapped ones included) the v6 ACL projection and
+// rulesV6.  host_id may be absent (no hostname stage: group -1).
+// ---------------------------------------------------------------------------
+struct PipeIn {
+    const uint8_t* family;         // null: every packet IPv4
+    const uint8_t* proto;
+    const uint32_t* src4;
+    const uint32_t* dst4;
+    const uint8_t* src6;           // 16 bytes per packet, 16-byte aligned
+    const uint8_t* dst6;
+    const uint16_t* dport;
+    const uint32_t* host_id;       // null: no hostnames
+    const int32_t* pool_group;
+    int64_t n_pool;
+};
+
+struct PipeOut {
+    int32_t* acl;
+    int32_t* route;
+    int32_t* group;
+    uint8_t* allow;
+};
+
+struct PipeTries {
+    const uint32_t* n4;
+    const uint32_t* n6;
+    int32_t rb4, rb6;
+};
+
+template <bool kCount>
+__device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx& a,
+                                             const PipeTries& tr, const PipeIn& in, int64_t i,
+                                             const PipeOut& out, const PipeCount& pc,
+                                             const PipeLds& L, PipeTally* t) {
+    const bool v6 = in.family && in.family[i] == 6;
+    const bool tcp = in.proto[i] == VC_PROTO_TCP;
+    const uint32_t port = in.dport[i];
+    int32_t grp = -1;
+    if (in.host_id) {
+        const uint32_t h = in.host_id[i];
+        grp = int64_t(h) < in.n_pool ? in.pool_group[h] : -1;
+    }
+    uint32_t v, e;
+    if (v6) {
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(in.dst6)[i], &hi, &lo);
+        e = route6_chase(tr.n6, tr.rb6, tr.n6[hi >> (64 - tr.rb6)], hi, lo);
+        v = acl_v6_one(img, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
+    } else {
+        const uint32_t d = in.dst4[i];
+        e = route_chase(tr.n4, tr.rb4, tr.n4[d >> (32 - tr.rb4)], d);
+        v = acl_v4_one(a, tcp, in.src4[i], port);
+    }
+    acl_emit(img, tcp, v, out.allow ? out.allow + i : nullptr, out.acl + i);
+    const int32_t r = out_index(e);
+    out.route[i] = r;
+    out.group[i] = grp;
+    if (kCount) pipe_count(pc, L.ah, L.rc, L.gc, tcp, v, v6, r, grp, t);
+}
+
+template <bool kLds, bool kVec, bool kCount>
+__global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, PipeTries tr,
+                                                                   PipeIn in, int64_t n,
+                                                                   PipeOut out, PipeCount pc) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t tally[5];
+    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    int64_t lo, hi;
+    pipe_slice(n, &lo, &hi);
+    PipeTally t;
+    if (!kVec) {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+            pipe_mix_one<kCount>(img, a, tr, in, i, out, pc, L, &t);
+    } else {
+        for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
+            const int64_t g = i >> 2;
+            const uint32_t fm = in.family ? reinterpret_cast<const uint32_t*>(in.family)[g]
+                                          : 0x04040404u;
+            const uint32_t pr = reinterpret_cast<const uint32_t*>(in.proto)[g];
+            const uint2 pt = reinterpret_cast<const uint2*>(in.dport)[g];
+            const uint4 d4 = reinterpret_cast<const uint4*>(in.dst4)[g];
+            const uint4 s4 = reinterpret_cast<const uint4*>(in.src4)[g];
+            const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
+            const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
+            const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
+            bool v6[4], tcp[4];
+            uint64_t dh[4], dl[4];
+            uint32_t e[4];
+            int32_t grp[4] = {-1, -1, -1, -1};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v6[k] = ((fm >> (8 * k)) & 0xFFu) == 6;
+                tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+                dh[k] = dl[k] = 0;
+                if (v6[k]) {
+                    v6_key(reinterpret_cast<const uint4*>(in.dst6)[i + k], &dh[k], &dl[k]);
+                    e[k] = tr.n6[dh[k] >> (64 - tr.rb6)];
+                } else {
+                    e[k] = tr.n4[d[k] >> (32 - tr.rb4)];
+                }
+            }
+            if (in.host_id) {
+                const uint4 h4 = reinterpret_cast<const uint4*>(in.host_id)[g];
+                const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    grp[k] = int64_t(h[k]) < in.n_pool ? in.pool_group[h[k]] : -1;
+            }
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[k] = v6[k] ? acl_v6_one(img, tcp[k], reinterpret_cast<const uint4*>(in.src6)[i + k],
+                                          po[k])
+                             : acl_v4_one(a, tcp[k], sk[k], po[k]);
+            int4 oa, orr;
+            uint32_t al = 0;
+            int32_t* pa = reinterpret_cast<int32_t*>(&oa);
+            int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint8_t b = 0;
+                acl_emit(img, tcp[k], v[k], out.allow ? &b : nullptr, pa + k);
+                al |= uint32_t(b) << (8 * k);
+                pr_[k] = out_index(v6[k] ? route6_chase(tr.n6, tr.rb6, e[k], dh[k], dl[k])
+                                         : route_chase(tr.n4, tr.rb4, e[k], d[k]));
+            }
+            reinterpret_cast<int4*>(out.acl)[g] = oa;
+            reinterpret_cast<int4*>(out.route)[g] = orr;
+            reinterpret_cast<int4*>(out.group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+            if (out.allow) reinterpret_cast<uint32_t*>(out.allow)[g] = al;
+            if (kCount) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    pipe_count(pc, L.ah, L.rc, L.gc, tcp[k], v[k], v6[k], pr_[k], grp[k], &t);
+            }
         }
+        const int64_t tail = hi & ~int64_t(3);
+        if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
+            pipe_mix_one<kCount>(img, a, tr, in, tail + threadIdx.x, out, pc, L, &t);
     }
-    if (pc.rcounts) {
-        for (int k = threadIdx.x; k < pc.r_nbk; k += blockDim.x)
-            pc.rcounts[int64_t(k) * gridDim.x + blockIdx.x] = rc[k];
-        if (threadIdx.x == 0 && tally[2])
-            atomicAdd(pc.route + pc.route_none_at, (unsigned long long)tally[2]);
-    }
-    if (pc.gcounts) {
-        for (int k = threadIdx.x; k < pc.g_nbk; k += blockDim.x)
-            pc.gcounts[int64_t(k) * gridDim.x + blockIdx.x] = gc[k];
-        if (threadIdx.x == 0 && tally[3])
-            atomicAdd(pc.group + pc.n_groups, (unsigned long long)tally[3]);
-    }
+    if (kCount) pipe_count_flush(pc, L.ah, L.rc, L.gc, tally, t);
 }
 
 }  // namespace vcd
@@ -586,22 +791,21 @@ hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t
                        counters);
 }
 
-hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
-                              const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
-                              const uint16_t* dport, const uint32_t* host_id,
-                              const int32_t* pool_group, int64_t n_pool, int64_t n,
-                              int32_t* out_acl,
-                              int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
-                              unsigned long long* acl_cnt, unsigned long long* route_cnt,
-                              int64_t route_none_at, unsigned long long* group_cnt,
-                              int32_t n_groups, hipEvent_t kernel_done) {
+hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteImage& route,
+                           int32_t n4, int32_t n6, const PipeArgs& p, const PipeCounters& cnt,
+                           hipEvent_t kernel_done, hipStream_t count_stream) {
+    const int64_t n = p.n;
     if (n <= 0) return kernel_done ? hipEventRecord(kernel_done, c.stream) : hipSuccess;
+    // the tuned C5 kernel: IPv4 packets with hostnames; everything else
+    // (per-packet family, no hostname stage) runs the mixed kernel
+    const bool mix = p.family != nullptr || p.host_id == nullptr;
     const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
     const bool lds = words <= kLdsWords;
-    const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(dst4, 16) &&
-                     aligned(dport, 8) && aligned(host_id, 16) && aligned(out_acl, 16) &&
-                     aligned(out_route, 16) && aligned(out_group, 16) &&
-                     (!out_allow || aligned(out_allow, 4));
+    bool vec = aligned(p.proto, 4) && aligned(p.src4, 16) && aligned(p.dst4, 16) &&
+               aligned(p.dport, 8) && aligned(p.host_id, 16) && aligned(p.out_acl, 16) &&
+               aligned(p.out_route, 16) && aligned(p.out_group, 16) &&
+               (!p.out_allow || aligned(p.out_allow, 4));
+    if (mix) vec = vec && aligned(p.family, 4);
     int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
     const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
     // In-kernel counting where it fits the workgroup's LDS; the rest is
@@ -610,83 +814,126 @@ hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const Tri
     size_t shmem = lds ? size_t(words) * 4 : 0;
     vcd::PipeCount pc{};
     pc.bw_shift = big_hist_bucket_shift();
+    pc.n4 = n4;
+    const int64_t route_nval = int64_t(n4) + n6;     // combined [v4 rules][v6 rules]
     BigHist rh, gh;
     hipError_t e = hipSuccess;
     const int32_t acl_bins = acl.n_tcp + acl.n_udp;
-    if (acl_cnt && shmem + size_t(acl_bins) * 4 <= kLdsMax) {
-        pc.acl = acl_cnt;
+    if (cnt.acl && shmem + size_t(acl_bins) * 4 <= kLdsMax) {
+        pc.acl = cnt.acl;
         pc.acl_bins = acl_bins;
         pc.n_tcp = acl.n_tcp;
         shmem += size_t(acl_bins) * 4;
     }
-    if (route_cnt && big_hist_applies(n, r4.n_rules)) {
-        e = big_hist_begin(c, n, r4.n_rules, grid, &rh);
+    if (cnt.route && big_hist_applies(n, route_nval)) {
+        e = big_hist_begin(c, n, route_nval, grid, &rh);
         if (e == hipSuccess && shmem + size_t(rh.nbk) * 4 <= kLdsMax) {
             pc.rcounts = rh.counts;
             pc.r_nbk = rh.nbk;
-            pc.route = route_cnt;
-            pc.route_none_at = route_none_at;
+            pc.route = cnt.route;
+            pc.route_none_at = route_nval;
             shmem += size_t(rh.nbk) * 4;
         }
     }
-    if (e == hipSuccess && group_cnt && big_hist_applies(n, n_groups)) {
-        e = big_hist_begin(c, n, n_groups, grid, &gh);
+    if (e == hipSuccess && cnt.group && big_hist_applies(n, cnt.n_groups)) {
+        e = big_hist_begin(c, n, cnt.n_groups, grid, &gh);
         if (e == hipSuccess && shmem + size_t(gh.nbk) * 4 <= kLdsMax) {
             pc.gcounts = gh.counts;
             pc.g_nbk = gh.nbk;
-            pc.group = group_cnt;
-            pc.n_groups = n_groups;
+            pc.group = cnt.group;
+            pc.n_groups = cnt.n_groups;
             shmem += size_t(gh.nbk) * 4;
         }
     }
-    const bool cnt = pc.acl || pc.rcounts || pc.gcounts;
+    const bool count = pc.acl || pc.rcounts || pc.gcounts;
     if (e == hipSuccess) {
+        const TrieImage& r4 = route.fam[0];
 #define VC_PIPE(L, V, K)                                                                           \
     do {                                                                                           \
         if (shmem > 64 * 1024) e = allow_lds(vcd::pipeline_v4_kernel<L, V, K>, kLdsMax);           \
         if (e != hipSuccess) break;                                                                \
         hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V, K>), dim3(grid),                         \
                            dim3(vcd::kPipeBlock), shmem, c.stream, acl, r4.nodes, r4.root_bits,   \
-                           proto, src4, dst4, dport, host_id, pool_group, n_pool, n, out_acl,      \
-                           out_route, out_group, out_allow, pc);                                   \
+                           p.proto, p.src4, p.dst4, p.dport, p.host_id, p.pool_group, p.n_pool,    \
+                           n, p.out_acl, p.out_route, p.out_group, p.out_allow, pc);               \
     } while (0)
-        if (cnt) {
-            if (lds && vec) VC_PIPE(true, true, true);
-            else if (lds) VC_PIPE(true, false, true);
-            else if (vec) VC_PIPE(false, true, true);
-            else VC_PIPE(false, false, true);
+#define VC_MIX(L, V, K)                                                                            \
+    do {                                                                                           \
+        if (shmem > 64 * 1024) e = allow_lds(vcd::pipeline_mix_kernel<L, V, K>, kLdsMax);          \
+        if (e != hipSuccess) break;                                                                \
+        hipLaunchKernelGGL((vcd::pipeline_mix_kernel<L, V, K>), dim3(grid),                        \
+                           dim3(vcd::kPipeBlock), shmem, c.stream, acl, tr, in, n, out, pc);       \
+    } while (0)
+        if (!mix) {
+            if (count) {
+                if (lds && vec) VC_PIPE(true, true, true);
+                else if (lds) VC_PIPE(true, false, true);
+                else if (vec) VC_PIPE(false, true, true);
+                else VC_PIPE(false, false, true);
+            } else {
+                if (lds && vec) VC_PIPE(true, true, false);
+                else if (lds) VC_PIPE(true, false, false);
+                else if (vec) VC_PIPE(false, true, false);
+                else VC_PIPE(false, false, false);
+            }
         } else {
-            if (lds && vec) VC_PIPE(true, true, false);
-            else if (lds) VC_PIPE(true, false, false);
-            else if (vec) VC_PIPE(false, true, false);
-            else VC_PIPE(false, false, false);
+            const vcd::PipeTries tr{route.fam[0].nodes, route.fam[1].nodes, route.fam[0].root_bits,
+                                    route.fam[1].root_bits};
+            const vcd::PipeIn in{p.family, p.proto, p.src4, p.dst4, p.src6, p.dst6,
+                                 p.dport, p.host_id, p.pool_group, p.n_pool};
+            const vcd::PipeOut out{p.out_acl, p.out_route, p.out_group, p.out_allow};
+            if (count) {
+                if (lds && vec) VC_MIX(true, true, true);
+                else if (lds) VC_MIX(true, false, true);
+                else if (vec) VC_MIX(false, true, true);
+                else VC_MIX(false, false, true);
+            } else {
+                if (lds && vec) VC_MIX(true, true, false);
+                else if (lds) VC_MIX(true, false, false);
+                else if (vec) VC_MIX(false, true, false);
+                else VC_MIX(false, false, false);
+            }
         }
 #undef VC_PIPE
+#undef VC_MIX
         if (e == hipSuccess) e = hipGetLastError();
         if (e == hipSuccess && kernel_done) e = hipEventRecord(kernel_done, c.stream);
     }
-    // second halves of the in-kernel counts, and whatever was not counted inside
+    // The second halves of the in-kernel counts, and whatever was not
+    // counted inside, run on the counting stream when one is given (after
+    // the kernel), so they overlap the caller's next batch.
+    LaunchCfg cf = c;
+    if (count_stream && count_stream != c.stream && (rh.counts || gh.counts || cnt.acl ||
+                                                     cnt.route || cnt.group)) {
+        hipEvent_t ev = nullptr;
+        hipError_t e2 = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventRecord(ev, c.stream);
+        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(count_stream, ev, 0);
+        if (ev) (void)hipEventDestroy(ev);
+        if (e2 == hipSuccess) cf.stream = count_stream;
+        else if (e == hipSuccess) e = e2;
+    }
     if (rh.counts) {
-        const hipError_t e2 = big_hist_finish(c, &rh, VC_HIST_PLAIN, out_route, nullptr, n, 0,
-                                              r4.n_rules, 0, route_cnt,
+        const hipError_t e2 = big_hist_finish(cf, &rh, VC_HIST_ROUTE, p.out_route, p.family, n, n4,
+                                              route_nval, 0, cnt.route,
                                               e == hipSuccess && pc.rcounts != nullptr);
         if (e == hipSuccess) e = e2;
     }
     if (gh.counts) {
-        const hipError_t e2 = big_hist_finish(c, &gh, VC_HIST_PLAIN, out_group, nullptr, n, 0,
-                                              n_groups, 0, group_cnt,
+        const hipError_t e2 = big_hist_finish(cf, &gh, VC_HIST_PLAIN, p.out_group, nullptr, n, 0,
+                                              cnt.n_groups, 0, cnt.group,
                                               e == hipSuccess && pc.gcounts != nullptr);
         if (e == hipSuccess) e = e2;
     }
-    if (e == hipSuccess && acl_cnt && !pc.acl)
-        e = launch_hist(c, VC_HIST_ACL, out_acl, proto, n, acl_bins, 0, acl_bins, acl.n_tcp,
-                        acl_cnt);
-    if (e == hipSuccess && route_cnt && !pc.rcounts)
-        e = launch_hist(c, VC_HIST_PLAIN, out_route, nullptr, n, r4.n_rules, 0, route_none_at, 0,
-                        route_cnt);
-    if (e == hipSuccess && group_cnt && !pc.gcounts)
-        e = launch_hist(c, VC_HIST_PLAIN, out_group, nullptr, n, n_groups, 0, n_groups, 0,
-                        group_cnt);
+    if (e == hipSuccess && cnt.acl && !pc.acl)
+        e = launch_hist(cf, VC_HIST_ACL, p.out_acl, p.proto, n, acl_bins, 0, acl_bins, acl.n_tcp,
+                        cnt.acl);
+    if (e == hipSuccess && cnt.route && !pc.rcounts)
+        e = launch_hist(cf, VC_HIST_ROUTE, p.out_route, p.family, n, route_nval, 0, route_nval,
+                        n4, cnt.route);
+    if (e == hipSuccess && cnt.group && !pc.gcounts)
+        e = launch_hist(cf, VC_HIST_PLAIN, p.out_group, nullptr, n, cnt.n_groups, 0,
+                        cnt.n_groups, 0, cnt.group);
     return e;
 }
 

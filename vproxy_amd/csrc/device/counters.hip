@@ -43,6 +43,11 @@ __device__ __forceinline__ Item item_of(int mode, int32_t v, uint8_t a, int32_t 
         if (v < 0) return Item{-1, tcp};
         return Item{tcp ? int64_t(v) : int64_t(nt) + v, false};
     }
+    if (mode == VC_HIST_ROUTE) {                 // aux = family; v6 rules follow the nt v4 rules
+        const bool v4 = a != 6;
+        if (v < 0) return Item{-1, v4};
+        return Item{v4 ? int64_t(v) : int64_t(nt) + v, false};
+    }
     if (mode == VC_HIST_DNS && a != VC_DNS_GROUP) return Item{-2, false};   // not counted
     return Item{v < 0 ? -1 : int64_t(v), false};
 }
@@ -90,7 +95,8 @@ struct Run {
 
 __device__ __forceinline__ void flush_nulls(int mode, uint32_t n_tcp, uint32_t n_other,
                                             int64_t null_bin, unsigned long long* cnt) {
-    // ACL: [tcp default, udp default] at null_bin, null_bin + 1
+    // ACL: [tcp default, udp default] at null_bin, null_bin + 1; ROUTE:
+    // [v4 null, v6 null] there (n_tcp counts the first bin's nulls)
     __shared__ uint32_t nulls[2];
     if (threadIdx.x < 2) nulls[threadIdx.x] = 0;
     __syncthreads();
@@ -98,7 +104,7 @@ __device__ __forceinline__ void flush_nulls(int mode, uint32_t n_tcp, uint32_t n
     if (n_other) atomicAdd(&nulls[1], n_other);
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (mode == VC_HIST_ACL) {
+        if (mode == VC_HIST_ACL || mode == VC_HIST_ROUTE) {
             if (nulls[0]) atomicAdd(cnt + null_bin, (unsigned long long)nulls[0]);
             if (nulls[1]) atomicAdd(cnt + null_bin + 1, (unsigned long long)nulls[1]);
         } else if (nulls[1]) {
@@ -305,8 +311,13 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
                 for (int k = 0; k < 4; ++k) it[k] = i + k < hi ? load1(mode, idx, aux, i + k, nt)
                                                                 : Item{-2, false};
             }
+            // values past the counter space (v / kBW >= nbk: a caller-supplied
+            // output classified against another snapshot) are not counted --
+            // bucket_count_kernel drops the same values through Run's range
+            // check, so both passes agree on every bucket's length
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[q + k] = it[k].v >= 0 ? int32_t(it[k].v) : -1;
+            for (int k = 0; k < 4; ++k)
+                v[q + k] = it[k].v >= 0 && it[k].v / kBW < nbk ? int32_t(it[k].v) : -1;
         }
 #pragma unroll
         for (int q = 0; q < kPer; ++q)

@@ -13,6 +13,7 @@ namespace vc {
 #define VC_HIST_PLAIN 0   // v >= 0 -> base + v, v < 0 -> null_bin
 #define VC_HIST_ACL 1     // aux = proto: tcp v -> v, udp v -> nt + v, -1 -> null_bin (+1 udp)
 #define VC_HIST_DNS 2     // aux = kind: counted only where kind == VC_DNS_GROUP
+#define VC_HIST_ROUTE 3   // aux = family: v4 v -> v, v6 v -> nt + v; -1 -> null_bin (+1 for v6)
 
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
@@ -69,15 +70,40 @@ hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32
 hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
                                 const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                                 uint64_t* out);
-hipError_t launch_pipeline_v4(const LaunchCfg& c, const AclImage& acl, const TrieImage& r4,
-                              const uint8_t* proto, const uint32_t* src4, const uint32_t* dst4,
-                              const uint16_t* dport, const uint32_t* host_id,
-                              const int32_t* pool_group, int64_t n_pool, int64_t n,
-                              int32_t* out_acl,
-                              int32_t* out_route, int32_t* out_group, uint8_t* out_allow,
-                              unsigned long long* acl_cnt, unsigned long long* route_cnt,
-                              int64_t route_none_at, unsigned long long* group_cnt,
-                              int32_t n_groups, hipEvent_t kernel_done = nullptr);
+// Combined ACL -> route -> host pipeline (classify.hip).  Device pointers;
+// family null = every packet IPv4, host_id null = no hostname stage.
+struct PipeArgs {
+    const uint8_t* family;
+    const uint8_t* proto;
+    const uint32_t* src4;
+    const uint32_t* dst4;
+    const uint8_t* src6;           // 16-byte aligned
+    const uint8_t* dst6;
+    const uint16_t* dport;
+    const uint32_t* host_id;
+    const int32_t* pool_group;
+    int64_t n_pool;
+    int64_t n;
+    int32_t* out_acl;
+    int32_t* out_route;
+    int32_t* out_group;
+    uint8_t* out_allow;
+};
+// Counter arrays of the pinned snapshots (null = not counted): ACL
+// [tcp][udp][tcp default][udp default], route [v4][v6][v4 null][v6 null],
+// group [handles][null].
+struct PipeCounters {
+    unsigned long long* acl;
+    unsigned long long* route;
+    unsigned long long* group;
+    int32_t n_groups;
+};
+// kernel_done (optional) is recorded right after the classify kernel; the
+// counter finish passes run on count_stream (after the kernel) when it is
+// given, else on c.stream.
+hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteImage& route,
+                           int32_t n4, int32_t n6, const PipeArgs& p, const PipeCounters& cnt,
+                           hipEvent_t kernel_done, hipStream_t count_stream);
 
 // ServerGroup source hashing (select.hip); family 4: src = uint32 v4 keys,
 // 6: 16-byte addresses (16-byte aligned); view = VC_SOURCE_*.
