@@ -265,6 +265,7 @@ class C5Steps:
             self.s_pipe, self.s_hint, self.s_cnt = (hip_stream(dev) for _ in range(3))
         self.ev_hint, self.ev_pipe, self.ev_cnt, self.kdone = {}, {}, {}, {}
         self.timing = []
+        self.host_ms = {"hint": 0.0, "pipe": 0.0, "counters": 0.0}   # host time issuing
 
     def _hint(self, j, rec):
         TE = lambda: torch.cuda.Event(enable_timing=True)
@@ -334,13 +335,22 @@ class C5Steps:
         if k <= 0:
             return
         recs = [dict() for _ in range(k)]
+        T = time.perf_counter
+        t = T()
         self._hint(first, recs[0])
+        self.host_ms["hint"] += (T() - t) * 1e3
         for i in range(k):
             j = first + i
+            t = T()
             self._pipe(j, recs[i])
+            self.host_ms["pipe"] += (T() - t) * 1e3
+            t = T()
             if i + 1 < k:
                 self._hint(j + 1, recs[i + 1])
+            self.host_ms["hint"] += (T() - t) * 1e3
+            t = T()
             self._counters(j, recs[i])
+            self.host_ms["counters"] += (T() - t) * 1e3
         if timed:
             self.timing.extend(recs)
 
@@ -547,6 +557,8 @@ def main():
         elapsed = max_over_ranks(elapsed, dev)
 
     hint_ms, pipe_ms, count_ms = steps.span("hint"), steps.span("pipe"), steps.span("count")
+    log("host ms issuing over %d steps: %s" % (args.warmup + args.steps, {
+        k: round(v, 2) for k, v in steps.host_ms.items()}))
     B = hi - lo
     total = float(args.packets) * world * args.steps
     value = total / elapsed / 1e6

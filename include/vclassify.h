@@ -22,6 +22,20 @@
  *  - Strings are packed in a byte blob with uint32 offsets (n+1 entries, item
  *    i = blob[off[i], off[i+1])); an optional uint8 `null` array marks Java
  *    null items (NULL pointer = no null items).
+ *  - String encoding: every Java String crosses the boundary as its UTF-8
+ *    bytes (String.getBytes(UTF_8); an unpaired surrogate, which that call
+ *    would replace by '?', must be sent as its 3-byte WTF-8 form).  That
+ *    covers annotations (hint-host / hint-uri), hosts-file keys, Host / SNI /
+ *    URI hint strings and certificate names.  equals / startsWith / endsWith
+ *    on these bytes agree with Java's on the strings, and the one length Java
+ *    scores -- Hint.matchLevel's uriLevel = uri.length() + 1
+ *    (base/src/main/java/vproxybase/processor/Hint.java:146-150) -- is taken
+ *    in UTF-16 units of the annotation, so non-ASCII URIs score as in Java.
+ *    The exception is DNS: qnames are the wire bytes Formatter.parseDomainName
+ *    produces (base/.../dns/Formatter.java:225-257 makes one char per byte,
+ *    ISO-8859-1): a qname byte 0xE9 is the char U+00E9 and matches the
+ *    annotation bytes C3 A9, as in Java.  vc_compile_hosts_text reads the hosts file as UTF-8, as
+ *    Resolver.getHosts' InputStreamReader does with a UTF-8 default charset.
  *  - Rule tables are compiled into immutable snapshots and published
  *    atomically; concurrent classify calls keep using the snapshot they
  *    started with (threads: SURVEY.md §8(b) "Threading").

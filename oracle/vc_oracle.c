@@ -727,6 +727,20 @@ vo_hint vo_hint_of(const char *host, int host_len, int port, const char *uri, in
     return h;
 }
 
+/* String.length() of the Java string whose UTF-8 bytes (WTF-8 for unpaired
+ * surrogates: the boundary's string encoding, include/vclassify.h) are s:
+ * one UTF-16 unit per code point, two for a supplementary code point. */
+static int j_length(const char *s, int n)
+{
+    int u = 0;
+    for (int i = 0; i < n; ++i) {
+        unsigned char c = (unsigned char)s[i];
+        if ((c & 0xC0) != 0x80) ++u;
+        if (c >= 0xF0) ++u;
+    }
+    return u;
+}
+
 /* Hint.matchLevel -- Hint.java:100-160 */
 int vo_match_level(const vo_hint *h, const vo_annos *a, int na)
 {
@@ -756,9 +770,9 @@ int vo_match_level(const vo_hint *h, const vo_annos *a, int na)
     int uri_level = 0;
     if (au != NULL && h->uri != NULL) {
         if (j_equals(h->uri, h->uri_len, au, aun)) {
-            uri_level = h->uri_len + 1;
+            uri_level = j_length(h->uri, h->uri_len) + 1;    /* this.uri.length() + 1 */
         } else if (j_starts_with(h->uri, h->uri_len, au, aun)) {
-            uri_level = aun + 1;
+            uri_level = j_length(au, aun) + 1;               /* annoUri.length() + 1 */
         } else if (j_equals(au, aun, "*", 1)) {
             uri_level = 1;
         }
@@ -820,8 +834,33 @@ static int hosts_get(const vo_hosts *hs, const char *k, int kn)
 }
 
 int vo_dns_classify(const vo_hosts *hosts, const vo_group *g, int ng,
-                    const char *qname, int qlen, int32_t *value)
+                    const char *qwire, int qwlen, int32_t *value)
 {
+    /* Formatter.parseDomainName (Formatter.java:225-257) builds the qname
+     * with (char) b per wire byte -- ISO-8859-1.  Strings here are the UTF-8
+     * bytes of the Java strings, so bytes >= 0x80 become two bytes. */
+    char qbuf[1024];
+    const char *qname = qwire;
+    int qlen = qwlen, ascii = 1;
+    for (int i = 0; i < qwlen; ++i)
+        if ((unsigned char)qwire[i] >= 0x80) ascii = 0;
+    if (!ascii) {
+        if (qwlen > 512) {            /* no wire name is this long (the library's limit) */
+            *value = 0;
+            return VO_DNS_RECURSIVE;
+        }
+        qlen = 0;
+        for (int i = 0; i < qwlen; ++i) {
+            unsigned char c = (unsigned char)qwire[i];
+            if (c < 0x80) {
+                qbuf[qlen++] = (char)c;
+            } else {
+                qbuf[qlen++] = (char)(0xC0 | (c >> 6));
+                qbuf[qlen++] = (char)(0x80 | (c & 0x3F));
+            }
+        }
+        qname = qbuf;
+    }
     int hv = hosts_get(hosts, qname, qlen);                  /* :127 */
     if (hv >= 0) {
         *value = hv;

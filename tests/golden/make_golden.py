@@ -183,6 +183,21 @@ def kats():
          "queries": [[{"uri": "/a/b/c"}, 2], [{"uri": "/a/"}, 1], [{"uri": "/z"}, 0],
                      [{"host": "x.com", "uri": "/a"}, 3], [{"host": "y.com", "uri": "/a"}, 1],
                      [{"uri": "/a?q=1"}, 1]]},
+        {"source": "Hint.java:146-157: uriLevel is String.length() + 1 -- UTF-16 units, not the "
+                   "UTF-8 bytes strings cross the boundary in; capped at 1023.  By units group 0 "
+                   "scores 602 and group 1 1023 (wins); by bytes both would cap at 1023 and the "
+                   "tie would go to group 0",
+         "groups": [[{}, {"uri": "/" + "\u00e9" * 600}],
+                    [{}, {"uri": "/" + "\u00e9" * 600 + "a" * 430}]],
+         "queries": [[{"uri": "/" + "\u00e9" * 600 + "a" * 430 + "/x"}, 1],
+                     [{"uri": "/" + "\u00e9" * 600}, 0]]},
+        {"source": "Hint.java:130-140: non-ASCII hosts compare as Java strings (UTF-8 bytes here); "
+                   "a supplementary character is one code point",
+         "groups": [[{}, {"host": "caf\u00e9.com"}], [{}, {"host": "\U0001f600.example"}],
+                    [{}, {"host": "com", "uri": "/\U0001f600"}]],
+         "queries": [[{"host": "caf\u00e9.com"}, 0], [{"host": "www.caf\u00e9.com:80"}, 0],
+                     [{"host": "a.\U0001f600.example"}, 1], [{"host": "cafe.com"}, 2],
+                     [{"host": "x.com", "uri": "/\U0001f600/y"}, 2]]},
     ]
     dns = [  # CI.java:632-697 dnsServer + SURVEY.md Appendix B DNS flow (DNSServer.java:116-166)
         {"source": "CI.java:632-697 dnsServer; Appendix B DNS",
@@ -195,6 +210,21 @@ def kats():
                      ["::1.", 3, 6],
                      ["x.vproxy.local.", 4, 0],
                      ["nothing.org.", 5, 0]]},
+    ]
+    # DNS qnames as wire bytes (hex): Formatter.parseDomainName (Formatter.java:225-257)
+    # makes one char per byte ((char) b, ISO-8859-1); annotations and hosts-file keys
+    # are Java strings (UTF-8 across the boundary, Resolver reads the file in UTF-8)
+    dns_wire = [
+        {"source": "Formatter.java:225-257 (char) b + DNSServer.java:116-166",
+         "groups": [[{}, {"host": "caf\u00e9.com"}], [{}, {"host": "b.com"}]],
+         "hosts": [["h\u00f4te.local.", 7], ["h\u00f4te.local", 7]],
+         "queries": [[b"caf\xe9.com.".hex(), 2, 0],            # U+00E9 == the annotation's char
+                     [b"x.caf\xe9.com.".hex(), 2, 0],
+                     [b"caf\xc3\xa9.com.".hex(), 5, 0],        # UTF-8 on the wire: "caf\u00c3\u00a9"
+                     [b"h\xf4te.local.".hex(), 1, 7],
+                     [b"b.com.".hex(), 2, 1],
+                     [b"\xff.vproxy.local.".hex(), 4, 0],
+                     [b"\xe9\xe9.1.2.3.".hex(), 5, 0]]},
     ]
     # SecurityGroup scenarios: a list of steps (TestTcpLB.java:640-674, CI.java:1071-1197)
     lb, s5 = 7005, 7006
@@ -229,7 +259,8 @@ def kats():
     ]
     dump("kats.json", {"mask_match": [{"expect": e, "input": i, "net": n}
                                       for e, i, n in mask_match],
-                       "hints": hints, "dns": dns, "security_group": sg})
+                       "hints": hints, "dns": dns, "dns_wire": dns_wire,
+                       "security_group": sg})
 
 
 if __name__ == "__main__":

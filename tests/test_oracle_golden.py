@@ -99,6 +99,29 @@ def test_dns_kats():
             assert O.dns_classify(h, g, q) == (kind, value), (case["source"], q)
 
 
+def test_dns_wire_kats():
+    """qnames as wire bytes: ISO-8859-1 chars (Formatter.java:225-257) against
+    UTF-8 annotations / hosts keys."""
+    for case in load("kats.json")["dns_wire"]:
+        g = O.Groups(case["groups"])
+        h = O.Hosts(case["hosts"])
+        for q, kind, value in case["queries"]:
+            assert O.dns_classify(h, g, bytes.fromhex(q)) == (kind, value), (case["source"], q)
+
+
+def test_match_level_counts_utf16_units():
+    """Hint.matchLevel's uriLevel = String.length() + 1 (Hint.java:146-150):
+    "/\u00e9" is 2 units (3 UTF-8 bytes), "/\U0001f600" 3 units (a surrogate
+    pair; 5 bytes)."""
+    for uri, units in (("/\u00e9", 2), ("/\U0001f600", 3), ("/a\u00e9\U0001f600b", 6)):
+        ub = uri.encode()
+        annos = (O.VoAnnos * 1)()
+        annos[0].uri, annos[0].uri_len = ub, len(ub)
+        for q in (uri, uri + "/tail"):
+            h, keep = O.hint_of(None, 0, q)
+            assert O.lib().vo_match_level(O.C.byref(h), annos, 1) == units + 1, (uri, q)
+
+
 def test_security_group_scenarios():
     for case in load("kats.json")["security_group"]:
         tcp, udp, dflt = [], [], True

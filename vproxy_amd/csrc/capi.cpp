@@ -107,6 +107,9 @@ struct vc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t lane[2] = {nullptr, nullptr};   // chunked host-buffer calls (host_chunks)
     hipMemPool_t pool = nullptr;   // scratch of the counter passes
+    hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
+    std::mutex handoff_mu;
+    vc::ScratchRing scratch;       // counter-pass scratch, reused across calls
     int num_cus = 256;
     std::atomic<bool> counters_on{false};
     std::mutex compile_mu;   // serialises compiles; classify never takes it
@@ -133,6 +136,8 @@ struct vc_ctx {
         c.num_cus = num_cus;
         c.stream = static_cast<hipStream_t>(s);
         c.pool = pool;
+        c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
+        c.scratch = const_cast<vc::ScratchRing*>(&scratch);
         return c;
     }
 };
@@ -217,14 +222,19 @@ int vc_create(int device, vc_ctx** out) {
         delete c;
         return hip_fail(e, "stream create");
     }
-    // Scratch pool of the counter passes: calls may come on several streams
-    // at once, so a block freed on one stream is never handed to another
-    // without a stream-order dependency; memory stays cached between calls.
+    // Staging pool of the host-buffer entry points: calls may come on several
+    // streams at once, so a block freed on one stream is never handed to
+    // another without a stream-order dependency; memory stays cached.
     hipMemPoolProps props{};
     props.allocType = hipMemAllocationTypePinned;
     props.location.type = hipMemLocationTypeDevice;
     props.location.id = device;
-    if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess) {
+    if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming)) != hipSuccess ||
+        (e = c->scratch.init()) != hipSuccess) {
+        c->scratch.destroy();
+        if (c->handoff) (void)hipEventDestroy(c->handoff);
+        if (c->pool) (void)hipMemPoolDestroy(c->pool);
         (void)hipStreamDestroy(c->stream);
         (void)hipStreamDestroy(c->lane[0]);
         (void)hipStreamDestroy(c->lane[1]);
@@ -261,6 +271,9 @@ void vc_destroy(vc_ctx* ctx) {
         (void)hipDeviceSynchronize();
         (void)hipMemPoolDestroy(ctx->pool);
     }
+    (void)hipDeviceSynchronize();
+    if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
+    ctx->scratch.destroy();
     delete ctx;
 }
 

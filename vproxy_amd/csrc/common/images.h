@@ -109,10 +109,12 @@ struct PortMin {                   // per host key: min index per distinct hint-
 struct GroupRec {                  // merged annotations of one ServerGroupHandle
     int32_t host_len;              // -1 = null
     uint32_t host_off;
-    int32_t uri_len;               // -1 = null
+    int32_t uri_len;               // -1 = null (bytes)
     uint32_t uri_off;
     int32_t port;                  // 0 = absent
     int32_t any;                   // 0 when H, P and U are all absent (level is always 0)
+    int32_t uri_units;             // U.length(): UTF-16 code units of the UTF-8 bytes
+    int32_t pad;
 };
 
 struct HintImage {

@@ -385,6 +385,19 @@ uint32_t HostTableBuilt::insert(const std::string& k, int32_t a, int32_t b,
     return s;
 }
 
+// String.length() of the Java string whose UTF-8 (WTF-8 for unpaired
+// surrogates) bytes are s: one UTF-16 unit per code point, two for a
+// supplementary one (a 4-byte sequence) -- the uriLevel of Hint.matchLevel
+// (Hint.java:146-150) counts these, not bytes.
+static int32_t utf16_units(const uint8_t* s, int n) {
+    int32_t u = 0;
+    for (int i = 0; i < n; ++i) {
+        if ((s[i] & 0xC0) != 0x80) ++u;        // every byte that starts a code point
+        if (s[i] >= 0xF0) ++u;                  // 4-byte sequence: a surrogate pair
+    }
+    return u;
+}
+
 int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
     *out = HintBuilt{};
     out->n_groups = n;
@@ -395,7 +408,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
     };
     std::map<std::string, KeyAcc> hostk, urik;
     std::vector<std::string> host_order, uri_order;
-    out->groups.reserve(size_t(n) * 6);
+    out->groups.reserve(size_t(n) * 8);
     for (int g = 0; g < n; ++g) {
         // Hint.matchLevel merge (Hint.java:108-118): first non-null host,
         // first non-zero port, first non-null uri over [handle, group].
@@ -407,10 +420,14 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
             if (!U && a->uri) { U = a->uri; Un = a->uri_len; }
         }
         if ((H && Hn < 0) || (U && Un < 0)) return VC_EINVAL;
-        int32_t rec[6] = {-1, 0, -1, 0, P, (H || P != 0 || U) ? 1 : 0};
+        int32_t rec[8] = {-1, 0, -1, 0, P, (H || P != 0 || U) ? 1 : 0, 0, 0};
         if (H) { rec[0] = Hn; rec[1] = static_cast<int32_t>(append_blob(&out->blob, H, Hn)); }
-        if (U) { rec[2] = Un; rec[3] = static_cast<int32_t>(append_blob(&out->blob, U, Un)); }
-        out->groups.insert(out->groups.end(), rec, rec + 6);
+        if (U) {
+            rec[2] = Un;
+            rec[3] = static_cast<int32_t>(append_blob(&out->blob, U, Un));
+            rec[6] = utf16_units(reinterpret_cast<const uint8_t*>(U), Un);
+        }
+        out->groups.insert(out->groups.end(), rec, rec + 8);
         if (H) {
             std::string k(H, Hn);
             auto it = hostk.find(k);

@@ -67,7 +67,7 @@ struct HintBuilt {
     std::vector<uint32_t> uri_tags;
     std::vector<uint32_t> lists;
     std::vector<int32_t> port_mins;      // (port, idx) pairs
-    std::vector<int32_t> groups;         // 6 words per GroupRec
+    std::vector<int32_t> groups;         // 8 words per GroupRec
     int32_t n_groups = 0;
     int32_t wildcard_slot = -1, uri_star_slot = -1, has_uri_keys = 0;
 };

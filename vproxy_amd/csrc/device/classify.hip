@@ -819,15 +819,26 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     BigHist rh, gh;
     hipError_t e = hipSuccess;
     const int32_t acl_bins = acl.n_tcp + acl.n_udp;
+    // one scratch lease for both large counter spaces, released on the
+    // stream the finish passes run on
+    const bool r_big = cnt.route && big_hist_applies(n, route_nval);
+    const bool g_big = cnt.group && big_hist_applies(n, cnt.n_groups);
+    const size_t rbytes = r_big ? big_hist_bytes(n, route_nval, grid) : 0;
+    const size_t gbytes = g_big ? big_hist_bytes(n, cnt.n_groups, grid) : 0;
+    int slot = -1;
+    uint8_t* scratch = nullptr;
+    if (rbytes + gbytes)
+        e = c.scratch ? c.scratch->acquire(rbytes + gbytes, c.stream, &slot, &scratch)
+                      : hipErrorInvalidValue;
     if (cnt.acl && shmem + size_t(acl_bins) * 4 <= kLdsMax) {
         pc.acl = cnt.acl;
         pc.acl_bins = acl_bins;
         pc.n_tcp = acl.n_tcp;
         shmem += size_t(acl_bins) * 4;
     }
-    if (cnt.route && big_hist_applies(n, route_nval)) {
-        e = big_hist_begin(c, n, route_nval, grid, &rh);
-        if (e == hipSuccess && shmem + size_t(rh.nbk) * 4 <= kLdsMax) {
+    if (r_big && e == hipSuccess) {
+        big_hist_begin(scratch, n, route_nval, grid, &rh);
+        if (shmem + size_t(rh.nbk) * 4 <= kLdsMax) {
             pc.rcounts = rh.counts;
             pc.r_nbk = rh.nbk;
             pc.route = cnt.route;
@@ -835,9 +846,9 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
             shmem += size_t(rh.nbk) * 4;
         }
     }
-    if (e == hipSuccess && cnt.group && big_hist_applies(n, cnt.n_groups)) {
-        e = big_hist_begin(c, n, cnt.n_groups, grid, &gh);
-        if (e == hipSuccess && shmem + size_t(gh.nbk) * 4 <= kLdsMax) {
+    if (g_big && e == hipSuccess) {
+        big_hist_begin(scratch + rbytes, n, cnt.n_groups, grid, &gh);
+        if (shmem + size_t(gh.nbk) * 4 <= kLdsMax) {
             pc.gcounts = gh.counts;
             pc.g_nbk = gh.nbk;
             pc.group = cnt.group;
@@ -905,11 +916,8 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     LaunchCfg cf = c;
     if (count_stream && count_stream != c.stream && (rh.counts || gh.counts || cnt.acl ||
                                                      cnt.route || cnt.group)) {
-        hipEvent_t ev = nullptr;
-        hipError_t e2 = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e2 == hipSuccess) e2 = hipEventRecord(ev, c.stream);
-        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(count_stream, ev, 0);
-        if (ev) (void)hipEventDestroy(ev);
+        const hipError_t e2 = c.handoff.ev ? c.handoff(c.stream, count_stream)
+                                           : hipErrorInvalidValue;
         if (e2 == hipSuccess) cf.stream = count_stream;
         else if (e == hipSuccess) e = e2;
     }
@@ -923,6 +931,10 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
         const hipError_t e2 = big_hist_finish(cf, &gh, VC_HIST_PLAIN, p.out_group, nullptr, n, 0,
                                               cnt.n_groups, 0, cnt.group,
                                               e == hipSuccess && pc.gcounts != nullptr);
+        if (e == hipSuccess) e = e2;
+    }
+    if (slot >= 0) {
+        const hipError_t e2 = c.scratch->release(slot, cf.stream);
         if (e == hipSuccess) e = e2;
     }
     if (e == hipSuccess && cnt.acl && !pc.acl)

@@ -179,8 +179,8 @@ __global__ __launch_bounds__(kHistBlock) void hist_kernel(
 template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
-    int32_t nt, int nbk, uint32_t* __restrict__ counts, unsigned long long* __restrict__ cnt,
-    int64_t null_bin) {
+    int32_t nt, int nbk, int64_t nval, uint32_t* __restrict__ counts,
+    unsigned long long* __restrict__ cnt, int64_t null_bin) {
     extern __shared__ uint32_t c[];            // nbk words
     for (int k = threadIdx.x; k < nbk; k += blockDim.x) c[k] = 0;
     __syncthreads();
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
         }
         for (int k = 0; k < m; ++k) {
             count_null(it[k], &ntc, &noth);
-            if (it[k].v >= 0) run.add(it[k].v / kBW, c, 0, nbk);
+            if (it[k].v >= 0 && it[k].v < nval) run.add(it[k].v / kBW, c, 0, nbk);
         }
     }
     run.flush(c, 0, nbk);
@@ -281,7 +281,8 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scan_kernel(
 template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
-    int32_t nt, int nbk, const uint32_t* __restrict__ offsets, uint16_t* __restrict__ tmp) {
+    int32_t nt, int nbk, int64_t nval, const uint32_t* __restrict__ offsets,
+    uint16_t* __restrict__ tmp) {
     // LDS sized by the bucket count, so the kernel can share a CU with the
     // classify kernels of the next batch
     extern __shared__ uint32_t dyn[];
@@ -311,13 +312,14 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
                 for (int k = 0; k < 4; ++k) it[k] = i + k < hi ? load1(mode, idx, aux, i + k, nt)
                                                                 : Item{-2, false};
             }
-            // values past the counter space (v / kBW >= nbk: a caller-supplied
-            // output classified against another snapshot) are not counted --
-            // bucket_count_kernel drops the same values through Run's range
-            // check, so both passes agree on every bucket's length
+            // values at or past the counter space (a caller-supplied output
+            // classified against another snapshot) are not counted -- the
+            // bucket counts (bucket_count_kernel, or the pipeline kernel's
+            // pipe_count) drop exactly the same values, so every bucket's run
+            // has the length its offsets reserve
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                v[q + k] = it[k].v >= 0 && it[k].v / kBW < nbk ? int32_t(it[k].v) : -1;
+                v[q + k] = it[k].v >= 0 && it[k].v < nval ? int32_t(it[k].v) : -1;
         }
 #pragma unroll
         for (int q = 0; q < kPer; ++q)
@@ -442,21 +444,27 @@ hipError_t launch_hist(const LaunchCfg& c, int mode, const int32_t* idx, const u
     const int64_t max_blk = (n + 65535) / 65536;
     if (nblk > max_blk) nblk = int(max_blk < 1 ? 1 : max_blk);
     BigHist h;
-    hipError_t e = big_hist_begin(c, n, nval, nblk, &h);
+    int slot = -1;
+    uint8_t* scratch = nullptr;
+    hipError_t e = c.scratch ? c.scratch->acquire(big_hist_bytes(n, nval, nblk), c.stream, &slot,
+                                                  &scratch)
+                             : hipErrorInvalidValue;
     if (e == hipSuccess) {
+        big_hist_begin(scratch, n, nval, nblk, &h);
         if (vec)
             hipLaunchKernelGGL(vcd::bucket_count_kernel<true>, dim3(nblk), dim3(vcd::kHistBlock),
-                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, h.counts,
-                               counters, null_bin);
+                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, nval,
+                               h.counts, counters, null_bin);
         else
             hipLaunchKernelGGL(vcd::bucket_count_kernel<false>, dim3(nblk), dim3(vcd::kHistBlock),
-                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, h.counts,
-                               counters, null_bin);
+                               size_t(h.nbk) * 4, c.stream, mode, idx, aux, n, nt, h.nbk, nval,
+                               h.counts, counters, null_bin);
         e = hipGetLastError();
     }
     const hipError_t e2 = big_hist_finish(c, &h, mode, idx, aux, n, nt, nval, base, counters,
                                           e == hipSuccess);
-    return e != hipSuccess ? e : e2;
+    const hipError_t e3 = slot >= 0 ? c.scratch->release(slot, c.stream) : hipSuccess;
+    return e != hipSuccess ? e : e2 != hipSuccess ? e2 : e3;
 }
 
 bool big_hist_applies(int64_t n, int64_t nval) {
@@ -467,19 +475,96 @@ bool big_hist_applies(int64_t n, int64_t nval) {
 
 int big_hist_bucket_shift() { return 13; }   // log2(kBW)
 
-hipError_t big_hist_begin(const LaunchCfg& c, int64_t n, int64_t nval, int nblk, BigHist* h) {
+namespace {
+size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+}  // namespace
+
+size_t big_hist_bytes(int64_t n, int64_t nval, int nblk) {
+    const int64_t nbk = (nval + vcd::kBW - 1) / vcd::kBW;
+    const int64_t m = nbk * nblk;
+    return up256(size_t(m) * 4) + up256(size_t(m + 1) * 4) + up256(size_t(nbk + 1) * 4) +
+           up256(size_t(n > 0 ? n : 1) * 2);
+}
+
+void big_hist_begin(uint8_t* scratch, int64_t n, int64_t nval, int nblk, BigHist* h) {
     static_assert(vcd::kBW == 8192, "big_hist_bucket_shift");
     *h = BigHist{};
     h->nbk = int((nval + vcd::kBW - 1) / vcd::kBW);
     h->nblk = nblk;
     const int64_t m = int64_t(h->nbk) * nblk;
-    hipError_t e = scratch_alloc(c, reinterpret_cast<void**>(&h->counts), size_t(m) * 4);
-    if (e == hipSuccess)
-        e = scratch_alloc(c, reinterpret_cast<void**>(&h->offsets), size_t(m + 1) * 4);
-    if (e == hipSuccess)
-        e = scratch_alloc(c, reinterpret_cast<void**>(&h->seg_off), size_t(h->nbk + 1) * 4);
-    if (e == hipSuccess)
-        e = scratch_alloc(c, reinterpret_cast<void**>(&h->tmp), size_t(n > 0 ? n : 1) * 2);
+    uint8_t* p = scratch;
+    h->counts = reinterpret_cast<uint32_t*>(p);
+    p += up256(size_t(m) * 4);
+    h->offsets = reinterpret_cast<uint32_t*>(p);
+    p += up256(size_t(m + 1) * 4);
+    h->seg_off = reinterpret_cast<uint32_t*>(p);
+    p += up256(size_t(h->nbk + 1) * 4);
+    h->tmp = reinterpret_cast<uint16_t*>(p);
+}
+
+hipError_t ScratchRing::init() {
+    for (Slot& s : slots_) {
+        hipError_t e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+void ScratchRing::destroy() {
+    for (Slot& s : slots_) {
+        if (s.p) (void)hipFree(s.p);
+        if (s.ev) (void)hipEventDestroy(s.ev);
+        s = Slot{};
+    }
+}
+
+hipError_t ScratchRing::acquire(size_t bytes, hipStream_t st, int* slot, uint8_t** base) {
+    int k = -1;
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            for (int i = 0; i < kSlots && k < 0; ++i) {
+                const int j = (next_ + i) % kSlots;
+                if (!slots_[j].busy) k = j;
+            }
+            if (k >= 0) break;
+            cv_.wait(lk);                      // more concurrent calls than arenas
+        }
+        slots_[k].busy = true;
+        next_ = (k + 1) % kSlots;
+    }
+    Slot& s = slots_[k];
+    hipError_t e = hipSuccess;
+    if (s.cap < bytes) {                       // grow: only while batch sizes still grow
+        if (s.used) e = hipEventSynchronize(s.ev);
+        if (e == hipSuccess && s.p) e = hipFree(s.p);
+        s.p = nullptr;
+        s.cap = 0;
+        const size_t cap = up256(bytes + bytes / 4);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.p), cap);
+        if (e == hipSuccess) s.cap = cap;
+        else s.p = nullptr;
+    } else if (s.used) {
+        e = hipStreamWaitEvent(st, s.ev, 0);
+    }
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(mu_);
+        s.busy = false;
+        cv_.notify_one();
+        return e;
+    }
+    *slot = k;
+    *base = s.p;
+    return hipSuccess;
+}
+
+hipError_t ScratchRing::release(int slot, hipStream_t st) {
+    Slot& s = slots_[slot];
+    const hipError_t e = hipEventRecord(s.ev, st);
+    std::lock_guard<std::mutex> lk(mu_);
+    s.used = s.used || e == hipSuccess;
+    s.busy = false;
+    cv_.notify_one();
     return e;
 }
 
@@ -497,21 +582,17 @@ hipError_t big_hist_finish(const LaunchCfg& c, BigHist* h, int mode, const int32
                            h->counts, h->offsets, m, nbk, nblk, h->seg_off);
         if (vec)
             hipLaunchKernelGGL(vcd::bucket_scatter_kernel<true>, dim3(nblk), dim3(vcd::kHistBlock),
-                               size_t(nbk) * 12, c.stream, mode, idx, aux, n, nt, nbk, h->offsets,
-                               h->tmp);
+                               size_t(nbk) * 12, c.stream, mode, idx, aux, n, nt, nbk, nval,
+                               h->offsets, h->tmp);
         else
             hipLaunchKernelGGL(vcd::bucket_scatter_kernel<false>, dim3(nblk),
                                dim3(vcd::kHistBlock), size_t(nbk) * 12, c.stream, mode, idx, aux,
-                               n, nt, nbk, h->offsets, h->tmp);
+                               n, nt, nbk, nval, h->offsets, h->tmp);
         hipLaunchKernelGGL(vcd::bucket_hist_kernel, dim3(unsigned(max_segs)), dim3(vcd::kHistBlock),
                            0, c.stream, h->tmp, h->offsets, h->seg_off, nblk, nbk, nval, base,
                            counters);
         e = hipGetLastError();
     }
-    if (h->counts) (void)hipFreeAsync(h->counts, c.stream);
-    if (h->offsets) (void)hipFreeAsync(h->offsets, c.stream);
-    if (h->seg_off) (void)hipFreeAsync(h->seg_off, c.stream);
-    if (h->tmp) (void)hipFreeAsync(h->tmp, c.stream);
     *h = BigHist{};
     return e;
 }

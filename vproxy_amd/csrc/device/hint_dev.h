@@ -554,8 +554,8 @@ VC_HDN int uri_probe(const HintImage& img, uint32_t h, const uint8_t* p, int n, 
 
 // Hint.matchLevel for one merged group (Hint.java:100-160)
 VC_HDN int match_level(const HintImage& img, uint32_t g, DStr host, int port, DStr uri) {
-    const int32_t* r = reinterpret_cast<const int32_t*>(img.groups) + 6 * g;
-    const int32_t Hn = r[0], Un = r[2], P = r[4];
+    const int32_t* r = reinterpret_cast<const int32_t*>(img.groups) + 8 * g;
+    const int32_t Hn = r[0], Un = r[2], P = r[4], Uu = r[6];
     if (!r[5]) return 0;
     if (port != 0 && P != 0 && port != P) return 0;
     const uint8_t* H = img.blob + uint32_t(r[1]);
@@ -569,8 +569,9 @@ VC_HDN int match_level(const HintImage& img, uint32_t g, DStr host, int port, DS
     }
     int ul = 0;
     if (Un >= 0 && uri.n >= 0) {
-        if (uri.n == Un && bytes_eq(uri.p, U, Un)) ul = uri.n + 1;
-        else if (uri.n >= Un && bytes_eq(uri.p, U, Un)) ul = Un + 1;
+        // uri.length() == U.length() when equal: both levels are U's UTF-16
+        // length + 1 (strings are UTF-8 here, Java counts UTF-16 units)
+        if (uri.n >= Un && bytes_eq(uri.p, U, Un)) ul = Uu + 1;
         else if (Un == 1 && U[0] == '*') ul = 1;
     }
     if (ul > 1023) ul = 1023;
@@ -643,12 +644,12 @@ VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,
     return hint_general(img, host, port, uri);
 }
 
-// DNSServer.handleRequest classification (DNSServer.java:116-166) on the
-// query name bytes (trailing dot included, Formatter.parseDomainName).
+// DNSServer.handleRequest classification (DNSServer.java:116-166) on a
+// query name in the boundary's string encoding (UTF-8), trailing dot
+// included.
 template <class Src>
-VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
-                   const Src& q,
-                                        int qn, uint8_t* kind, int32_t* value) {
+VC_HD void dns_flow(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
+                    const Src& q, int qn, uint8_t* kind, int32_t* value) {
     // (1) hosts.get(qname) on the raw qname (trailing dot kept), :127
     if (hosts.n > 0) {
         Rec r;
@@ -677,6 +678,44 @@ VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImag
         *kind = internal ? VC_DNS_INTERNAL : VC_DNS_RECURSIVE;   // (6) :164
         *value = 0;
     }
+}
+
+// Formatter.parseDomainName (Formatter.java:225-257) turns each wire byte
+// into a char with (char) b: the qname string is ISO-8859-1.  Annotations
+// and hosts keys arrive as UTF-8, so a qname byte >= 0x80 is the two UTF-8
+// bytes of U+0080..U+00FF; the rare non-ASCII qname is transcoded into a
+// private buffer and classified from there.  Wire names are at most 255
+// bytes; a non-ASCII name over 512 bytes is reported as recursive.
+VC_HDN __noinline__ void dns_latin1(const HostsImage& hosts, const HintImage* slow_img,
+                                    const uint8_t* qp, int qn, uint8_t* kind, int32_t* value) {
+    uint8_t buf[1024];
+    if (qn > 512) {
+        *kind = VC_DNS_RECURSIVE;
+        *value = 0;
+        return;
+    }
+    int n = 0;
+    for (int i = 0; i < qn; ++i) {
+        const uint8_t c = qp[i];
+        if (c < 0x80) {
+            buf[n++] = c;
+        } else {
+            buf[n++] = uint8_t(0xC0 | (c >> 6));
+            buf[n++] = uint8_t(0x80 | (c & 0x3F));
+        }
+    }
+    dns_flow(hosts, *slow_img, slow_img, PtrSrc{buf}, n, kind, value);
+}
+
+// DNSServer classification on the wire bytes of a query name
+// (Formatter.parseDomainName output, trailing dot included).
+template <class Src>
+VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
+                   const Src& q, int qn, uint8_t* kind, int32_t* value) {
+    uint32_t hi = 0;
+    for (int pos = 0; pos < qn; pos += 4) hi |= q.word(pos, 0, qn);
+    if (hi & 0x80808080u) dns_latin1(hosts, slow_img, q.ptr(), qn, kind, value);
+    else dns_flow(hosts, img, slow_img, q, qn, kind, value);
 }
 
 // SSLContextHolder.choose(sni) (SSLContextHolder.java:51-79) over the

@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <mutex>
+
 #include "../common/images.h"
 #include "vclassify.h"
 
@@ -15,10 +18,56 @@ namespace vc {
 #define VC_HIST_DNS 2     // aux = kind: counted only where kind == VC_DNS_GROUP
 #define VC_HIST_ROUTE 3   // aux = family: v4 v -> v, v6 v -> nt + v; -1 -> null_bin (+1 for v6)
 
+// A context-owned event for handing work from the caller's stream to a
+// second one (record + wait under the mutex).  One event re-recorded per
+// call: creating and destroying an event per call made hipEventDestroy wait
+// for the pending record, which blocked the host until the kernel ended.
+struct Handoff {
+    hipEvent_t ev = nullptr;
+    std::mutex* mu = nullptr;
+    // `to` waits for everything issued on `from` so far
+    hipError_t operator()(hipStream_t from, hipStream_t to) const {
+        std::lock_guard<std::mutex> lk(*mu);
+        hipError_t e = hipEventRecord(ev, from);
+        return e == hipSuccess ? hipStreamWaitEvent(to, ev, 0) : e;
+    }
+};
+
+// Device scratch owned by a context and reused across calls: a few arenas,
+// each ordered by an event recorded where its last user finished with it.
+// A lease makes the caller's stream wait (in stream order, not on the host)
+// for the arena's previous user; releasing records the event on the stream
+// that used it last.  Replaces stream-ordered pool allocations, whose
+// hipFreeAsync blocked the calling thread for milliseconds on this runtime
+// (profiles/r02_hip_api_free_async.txt).
+class ScratchRing {
+public:
+    static constexpr int kSlots = 4;
+    hipError_t init();
+    void destroy();           // after the device is idle
+    hipError_t acquire(size_t bytes, hipStream_t s, int* slot, uint8_t** base);
+    hipError_t release(int slot, hipStream_t s);
+
+private:
+    struct Slot {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool busy = false;
+        bool used = false;
+    };
+    std::mutex mu_;
+    std::condition_variable cv_;
+    Slot slots_[kSlots];
+    int next_ = 0;
+};
+
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
     hipStream_t stream = nullptr;
-    hipMemPool_t pool = nullptr;   // scratch pool (stream-ordered), null = device default
+    hipMemPool_t pool = nullptr;   // staging pool of the host entry points
+    Handoff handoff;
+    ScratchRing* scratch = nullptr;   // counter-pass scratch (required by the launchers)
 };
 
 // Workgroups per CU that can be resident at once for `kernel` (occupancy
@@ -35,11 +84,6 @@ inline int resident_grid(const LaunchCfg& c, const void* kernel, int block, size
     return int(want_blocks < cap ? want_blocks : cap);
 }
 
-// Stream-ordered scratch allocation from the context's pool.
-inline hipError_t scratch_alloc(const LaunchCfg& c, void** p, size_t bytes) {
-    return c.pool ? hipMallocFromPoolAsync(p, bytes, c.pool, c.stream)
-                  : hipMallocAsync(p, bytes, c.stream);
-}
 
 hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t* proto,
                          const uint32_t* src4, const uint16_t* port, int64_t n, int32_t* out,
@@ -117,9 +161,9 @@ hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_
 
 // Large counter spaces (counters.hip): bucket partition + per-bucket LDS
 // histograms, split so a producer kernel (the pipeline) can supply the
-// per-workgroup bucket counts itself: begin (allocate), producer writes
-// counts[bucket * nblk + block] over pipe_slice() slices of nblk
-// workgroups, finish (scan, scatter, histogram, free).
+// per-workgroup bucket counts itself: begin (carve the arrays out of leased
+// scratch), producer writes counts[bucket * nblk + block] over pipe_slice()
+// slices of nblk workgroups, finish (scan, scatter, histogram).
 struct BigHist {
     int nbk = 0, nblk = 0;
     uint32_t* counts = nullptr;
@@ -129,7 +173,8 @@ struct BigHist {
 };
 bool big_hist_applies(int64_t n, int64_t nval);
 int big_hist_bucket_shift();
-hipError_t big_hist_begin(const LaunchCfg& c, int64_t n, int64_t nval, int nblk, BigHist* h);
+size_t big_hist_bytes(int64_t n, int64_t nval, int nblk);
+void big_hist_begin(uint8_t* scratch, int64_t n, int64_t nval, int nblk, BigHist* h);
 hipError_t big_hist_finish(const LaunchCfg& c, BigHist* h, int mode, const int32_t* idx,
                            const uint8_t* aux, int64_t n, int32_t nt, int64_t nval, int64_t base,
                            unsigned long long* counters, bool run);
