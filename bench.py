@@ -235,14 +235,14 @@ class C5Steps:
     route/group buckets; the library finishes the two large counter spaces
     on the counting stream); counters(j): when `bucket`, copy the library's
     three counter arrays into one int64 bucket (device-to-device on the
-    counting stream) and all-reduce it (RCCL).  Two batches in flight:
-    outputs and pool results are double-buffered, so batch j+1's pool pass
-    and pipeline overlap batch j's counter finish.  Every step still does
-    all of its work between the caller's synchronisations.
+    counting stream) and all-reduce it (RCCL).  `inflight` batches in
+    flight: outputs and pool results have that many buffers, so batch j+1's
+    pool pass and pipeline kernel overlap batch j's counter finish.  Every
+    step still does all of its work between the caller's synchronisations.
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream"):
+                 finish="stream", inflight=2):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -250,7 +250,7 @@ class C5Steps:
         self.count = counters != "none"
         self.fused = counters == "fused"
         self.finish = finish
-        self.nbuf = 1 if serial else 2
+        self.nbuf = 1 if serial else max(1, inflight)
         pool_out = torch.empty(t.pool_n, dtype=torch.int32, device=dev)
         self.pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(self.nbuf - 1)]
         self.outsb = [tuple(torch.empty(self.B, dtype=torch.int32, device=dev)
@@ -502,6 +502,8 @@ def main():
                          "(overlapping the next batch) or inline after the pipeline kernel")
     ap.add_argument("--serial", action="store_true",
                     help="ablation: one stream, no overlap between consecutive batches")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (output and pool buffers)")
     ap.add_argument("--dist", action="store_true",
                     help="use the process group and the counter all-reduce even at N = 1")
     args = ap.parse_args()
@@ -535,7 +537,7 @@ def main():
     lo, hi = shard(args.packets * world, rank, world)
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
     steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
-                    counters=args.counters, finish=args.finish)
+                    counters=args.counters, finish=args.finish, inflight=args.inflight)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
@@ -611,8 +613,9 @@ def main():
                            "global_batch": args.packets * world,
                            "parallelism": "dp%d" % world,
                            "schedule": ("serial, one stream" if args.serial else
-                                        "2 batches in flight: pool / pipeline / counters on 3 "
-                                        "HIP streams")},
+                                        "%d batches in flight: pool / pipeline / counters on 3 "
+                                        "HIP streams, counter finish on the counters stream"
+                                        % args.inflight)},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()

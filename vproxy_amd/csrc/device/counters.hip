@@ -18,6 +18,8 @@
 // Null results (no rule / default) are counted in registers and added once
 // per workgroup; a thread collapses runs of equal values before touching
 // LDS, which keeps hot bins off a single LDS address.
+#include <vector>
+
 #include "dev_common.h"
 #include "launch.h"
 
@@ -535,15 +537,39 @@ hipError_t ScratchRing::acquire(size_t bytes, hipStream_t st, int* slot, uint8_t
     }
     Slot& s = slots_[k];
     hipError_t e = hipSuccess;
-    if (s.cap < bytes) {                       // grow: only while batch sizes still grow
-        if (s.used) e = hipEventSynchronize(s.ev);
-        if (e == hipSuccess && s.p) e = hipFree(s.p);
-        s.p = nullptr;
-        s.cap = 0;
+    if (s.cap < bytes) {
+        // Grow every idle arena to the new size at once (a batch larger
+        // than any before): one host stall here instead of one per arena
+        // on the next few calls, which would land in the caller's stream of
+        // batches as bubbles.
         const size_t cap = up256(bytes + bytes / 4);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.p), cap);
-        if (e == hipSuccess) s.cap = cap;
-        else s.p = nullptr;
+        std::vector<int> grow{k};
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (int j = 0; j < kSlots; ++j)
+                if (j != k && !slots_[j].busy && slots_[j].cap < cap) {
+                    slots_[j].busy = true;
+                    grow.push_back(j);
+                }
+        }
+        for (int j : grow) {
+            Slot& g = slots_[j];
+            hipError_t eg = g.used ? hipEventSynchronize(g.ev) : hipSuccess;
+            if (eg == hipSuccess && g.p) eg = hipFree(g.p);
+            g.p = nullptr;
+            g.cap = 0;
+            if (eg == hipSuccess) eg = hipMalloc(reinterpret_cast<void**>(&g.p), cap);
+            if (eg == hipSuccess) g.cap = cap;
+            else g.p = nullptr;
+            g.used = false;
+            if (j == k) e = eg;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (int j : grow)
+                if (j != k) slots_[j].busy = false;
+        }
+        cv_.notify_all();
     } else if (s.used) {
         e = hipStreamWaitEvent(st, s.ev, 0);
     }
