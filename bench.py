@@ -917,9 +917,131 @@ def sub_bench(args, clf, dev, rank, world):
     clf.close()
 
 
+def _be_bytes(x, n):
+    """int64 tensor of 64-bit values -> uint8 [n, 8] big-endian bytes."""
+    return x.contiguous().view(torch.uint8).view(n, 8).flip(1)
+
+
+def gen_mixed(lo, n, t, pool_n, v6_frac=0.15, seed=PACKET_SEED + 1, dev="cpu"):
+    """Items [lo, lo + n) of a seeded mixed-family batch for vc_pipeline:
+    gen_packets' IPv4 fields plus a family (v6_frac IPv6), IPv6 sources
+    (half IPv4-mapped ::ffff:a.b.c.d forms of the IPv4 source, so the v4
+    rules' v6 projections match them) and IPv6 destinations (90 % inside a
+    random rulesV6 prefix).  Index-addressable like gen_packets."""
+    proto, src, dst, dport, hid = gen_packets(lo, n, t, pool_n, seed=seed, dev=dev)
+    idx = torch.arange(lo, lo + n, device=dev, dtype=torch.int64)
+    h = lambda s: hash_u32(idx, seed, s)
+    fam = torch.where(below(h(60), 1 << 20) < int(v6_frac * (1 << 20)), 6, 4).to(torch.uint8)
+    # sources: ::ffff:src4 or a random 2001:db8::/32 address
+    s_hi = (h(61) << 32) | h(62)
+    s_hi = torch.where((h(63) & 1) == 0, torch.zeros_like(s_hi),
+                       (s_hi & 0xFFFFFFFF) | (0x20010DB8 << 32))
+    s_lo = torch.where(s_hi == 0, (0xFFFF << 32) | (src.to(torch.int64) & 0xFFFFFFFF),
+                       (h(64) << 32) | h(65))
+    # destinations: 90 % inside a random IPv6 route prefix
+    hi_t = torch.from_numpy(t.hi.view(np.int64)).to(dev)
+    p6 = torch.from_numpy(t.p6.astype(np.int64)).to(dev)
+    r = below(h(66), len(t.hi))
+    q = (h(67) << 32) | h(68)
+    keep = torch.where(p6[r] >= 64, torch.full_like(q, -1),
+                       (torch.full_like(q, -1) << (64 - torch.clamp(p6[r], max=63))))
+    d_hi = torch.where(below(h(69), 10) < 9, (hi_t[r] & keep) | (q & ~keep), q)
+    d_lo = (h(70) << 32) | h(71)
+    src6 = torch.cat([_be_bytes(s_hi, n), _be_bytes(s_lo, n)], 1).contiguous()
+    dst6 = torch.cat([_be_bytes(d_hi, n), _be_bytes(d_lo, n)], 1).contiguous()
+    return fam, proto, src, dst, src6, dst6, dport, hid
+
+
 def mix_bench(args, clf, dev, rank, O):
-    """Placeholder until the mixed-family pipeline lands."""
-    raise SystemExit("workload %s not available" % args.workload)
+    """The general pipeline (vc_pipeline_dev / vc_pipeline) on the C5 tables
+    over a mixed batch: 85 % IPv4 / 15 % IPv6 packets as in C3, per-packet
+    family dispatch (RouteTable.java:44-58).  `mix`: device-resident
+    packets, fused counters with the finish on a second stream; `mixhost`:
+    the host entry point over registered (zero-copy) host buffers."""
+    t = c5_tables(clf, dev, args.pool)
+    n = args.packets if args.workload == "mix" else 32 << 20
+    fam, proto, src, dst, src6, dst6, dport, hid = gen_mixed(0, n, t, t.pool_n, dev=dev)
+    pool = clf.hint_search((t.pool_blob, t.pool_off, None))
+    torch.cuda.synchronize()
+    n6 = int((fam == 6).sum())
+    extra = {"ipv6_packets": n6, "ipv4_packets": n - n6}
+    per_unit = ((n - n6) * 28 + n6 * 52) / n
+    unit = ("B/packet: IPv4 28 (family 1 + proto 1 + src 4 + dst 4 + dport 2 + host_id 4 in, 3x "
+            "int32 out), IPv6 52 (family 1 + proto 1 + src 16 + dst 16 + dport 2 + host_id 4 "
+            "in, 3x int32 out); %.1f at this mix" % ((n - n6) * 28 / n + n6 * 52 / n))
+    if args.workload == "mix":
+        outs = tuple(torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3)) + (None,)
+        s_cnt = hip_stream(dev)
+        clf.counters_enable(True)
+        fn = lambda: clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=src6,
+                                  dst6=dst6, outs=outs, count_stream=s_cnt)
+        kern = "pipeline_mix_kernel (+ counter finish on a second stream)"
+
+        def fin():
+            torch.cuda.current_stream().wait_stream(s_cnt)
+    else:
+        hs = [x.cpu().numpy() for x in (fam, proto, src, dst, src6, dst6, dport, hid)]
+        hs[2], hs[3] = hs[2].view(np.uint32), hs[3].view(np.uint32)
+        hs[6], hs[7] = hs[6].view(np.uint16), hs[7].view(np.uint32)
+        hpool = pool.cpu().numpy()
+        houts = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32), None)
+        reg = hs + [hpool] + list(houts[:3])
+        for x in reg:
+            V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
+        fn = lambda: clf.pipeline(hs[1], hs[2], hs[3], hs[6], hs[7], hpool, family=hs[0],
+                                  src6=hs[4], dst6=hs[5], outs=houts)
+        kern = "pipeline_mix_kernel over PCIe (zero-copy), synchronous"
+        fin = None
+    for _ in range(args.warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        if fin:
+            fin()
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if args.workload == "mixhost":
+        ms = el / args.steps * 1e3
+    gbs = per_unit * n / (ms / 1e3) / 1e9
+    cpu = None
+    if O is not None:
+        og = O.Groups(t.groups)
+
+        def run(k, threads):
+            x = [v[:k].cpu().numpy() for v in (fam, proto, src, dst, src6, dst6, dport, hid)]
+            six = x[0] == 6
+            names = [bytes(t.nblob[t.noff[i]:t.noff[i + 1]]) for i in t.pidx[x[7]]]
+            sb, so = W.pack(names)
+            t0 = time.perf_counter()
+            O.sg_batch_v4_np(t.tcp, t.udp, False, x[1][~six], x[2][~six].view(np.uint32),
+                             x[6][~six].view(np.uint16), nthreads=threads)
+            O.sg_batch_v6_np(t.tcp, t.udp, False, x[1][six], x[4][six], x[6][six].view(np.uint16),
+                             nthreads=threads)
+            O.rt_batch_v4_np(t.v4_list, x[3][~six].view(np.uint32), nthreads=threads)
+            O.rt_batch_v6_np(t.v6_list, x[5][six], nthreads=threads)
+            O.hint_batch_np(og, sb, so, None, nthreads=threads)
+            return time.perf_counter() - t0
+        cpu = cpu_rates(run, "M classifications/s", 4.0, "the first packets of the mixed batch, "
+                        "oracle linear scans (v4 / v6 SecurityGroup lists, rulesV4 / rulesV6, "
+                        "searchForGroup per packet)")
+    res = {"workload": args.workload, "items": n, "ms_per_step": round(el / args.steps * 1e3, 3),
+           "kernel_ms": round(ms, 4), "M_items_per_s": round(n / (ms / 1e3) / 1e6, 1),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "kernel": kern,
+                        "algorithmic_bytes": unit},
+           "cpu_baseline": cpu}
+    res.update(extra)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    clf.close()
 
 
 if __name__ == "__main__":

@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--workload", default="c5")
     ap.add_argument("--kernels", default="pipeline_v4_kernel,hint_kernel")
+    ap.add_argument("--l2", default=None, help="rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum output")
+    ap.add_argument("--commit", default=None, help="git commit the passes were taken at")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     stats = _find(a.stats, "*kernel_stats.csv")
@@ -73,6 +75,10 @@ def main():
             avg_ns[kname(row["Name"])] = float(row["AverageNs"])
     fetch = counter_avg(a.fetch, "FETCH_SIZE")
     write = counter_avg(a.write, "WRITE_SIZE")
+    l2 = {}
+    if a.l2:
+        hits, miss = counter_avg(a.l2, "TCC_HIT_sum"), counter_avg(a.l2, "TCC_MISS_sum")
+        l2 = {k: (hits[k][1], miss[k][1]) for k in hits if k in miss}
     out = {}
     for k in a.kernels.split(","):
         if k not in fetch or k not in write:
@@ -84,13 +90,15 @@ def main():
                   "fetch_bytes_x2": 2 * fr, "write_bytes": wr, "traffic_bytes": traffic,
                   "avg_ns_kernel_trace": ns,
                   "traffic_GBps": traffic / ns if ns else None}
+        if k in l2:
+            out[k]["tcc_hit"], out[k]["tcc_miss"] = l2[k]
     path = os.path.join(prof, "pmc_traffic.json")
     try:
         with open(path) as f:
             allw = json.load(f)
     except (OSError, ValueError):
         allw = {}
-    allw[a.workload] = {"tag": a.tag, "kernels": out,
+    allw[a.workload] = {"tag": a.tag, "commit": a.commit, "kernels": out,
                         "note": "per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024, read side x2 "
                                 "per MI355X_MICROARCH.md §HBM (gfx950 half-count)"}
     with open(path, "w") as f:

@@ -4,6 +4,7 @@
 // items per lane per step (16-byte address loads, 4-byte proto loads, 8-byte
 // port loads, 16-byte index stores); the ACL interval boundaries are staged
 // in LDS once per workgroup of a grid-stride (persistent-style) launch.
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -131,20 +132,70 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
 }
 
 // ---------------------------------------------------------------------------
-// ACL on IPv6 sources (128-bit interval search in global memory)
+// ACL on IPv6 sources: 128-bit interval search, two levels.  Every
+// (1 << shift)-th boundary of both protocol lists is staged in LDS as a
+// fence; the search runs over the fences in LDS, then over one block of
+// 1 << shift boundaries in global memory (L2-resident): shift dependent
+// global loads instead of log2(nb) (~15 at 10k rules).
 // ---------------------------------------------------------------------------
+struct AclV6Ctx {
+    const uint64_t* f[2];          // LDS fences, (hi, lo) pairs
+    const uint64_t* b[2];          // global boundaries
+    const uint32_t* desc[2];
+    const uint32_t* pieces[2];
+    int nf[2], nb[2];
+    int shift;
+};
+
+__device__ __forceinline__ int fence_count(int nb, int shift) {
+    return (nb + (1 << shift) - 1) >> shift;
+}
+
+// Stages the fences of both lists at lds (16-byte aligned); the caller syncs.
+__device__ __forceinline__ AclV6Ctx stage_fences(const AclImage& img, uint64_t* lds, int shift) {
+    AclV6Ctx a;
+    a.shift = shift;
+    int off = 0;
+    for (int l = 0; l < 2; ++l) {
+        const AclFamilyImage& f = img.fam[l][1];
+        a.nb[l] = f.nb;
+        a.nf[l] = fence_count(f.nb, shift);
+        a.b[l] = f.bounds6;
+        a.desc[l] = f.desc;
+        a.pieces[l] = f.pieces;
+        a.f[l] = lds + 2 * off;
+        for (int k = threadIdx.x; k < a.nf[l]; k += blockDim.x)
+            reinterpret_cast<ulonglong2*>(lds)[off + k] =
+                reinterpret_cast<const ulonglong2*>(f.bounds6)[int64_t(k) << shift];
+        off += a.nf[l];
+    }
+    return a;
+}
+
+__device__ __forceinline__ uint32_t acl_v6_fenced(const AclV6Ctx& a, bool tcp, uint4 w,
+                                                  uint32_t port) {
+    const int l = tcp ? 0 : 1;
+    uint64_t hi, lo;
+    v6_key(w, &hi, &lo);
+    const int k = bsearch_u128(a.f[l], a.nf[l], hi, lo);
+    const int base = k << a.shift;
+    const int rest = a.nb[l] - base;
+    const int len = rest < (1 << a.shift) ? rest : (1 << a.shift);
+    const int j = base + bsearch_u128(a.b[l] + 2 * int64_t(base), len, hi, lo);
+    return port_lookup(a.pieces[l], load_desc(a.desc[l], j), port);
+}
+
 __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
-    AclImage img, const uint8_t* __restrict__ proto, const uint8_t* __restrict__ src6,
-    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
-    uint8_t* __restrict__ allow) {
+    AclImage img, int shift, const uint8_t* __restrict__ proto,
+    const uint8_t* __restrict__ src6, const uint16_t* __restrict__ port, int64_t n,
+    int32_t* __restrict__ out, uint8_t* __restrict__ allow) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t fences[];
+    const AclV6Ctx a = stage_fences(img, fences, shift);
+    __syncthreads();
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
-        const AclFamilyImage& f = t ? img.fam[0][1] : img.fam[1][1];
-        uint64_t hi, lo;
-        v6_key(reinterpret_cast<const uint4*>(src6)[i], &hi, &lo);
-        const int j = bsearch_u128(f.bounds6, f.nb, hi, lo);
-        const uint32_t v = port_lookup(f.pieces, load_desc(f.desc, j), port[i]);
+        const uint32_t v = acl_v6_fenced(a, t, reinterpret_cast<const uint4*>(src6)[i], port[i]);
         acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
@@ -277,17 +328,6 @@ __device__ __forceinline__ uint32_t route6_chase(const uint32_t* nodes, int rb, 
         bits += 8;
     }
     return e;
-}
-
-// SecurityGroup.allow on one IPv6 source: the protocol list's v6 projection
-// (128-bit interval search in L2-resident global memory).
-__device__ __forceinline__ uint32_t acl_v6_one(const AclImage& img, bool tcp, uint4 w,
-                                               uint32_t port) {
-    const AclFamilyImage& f = tcp ? img.fam[0][1] : img.fam[1][1];
-    uint64_t hi, lo;
-    v6_key(w, &hi, &lo);
-    const int j = bsearch_u128(f.bounds6, f.nb, hi, lo);
-    return port_lookup(f.pieces, load_desc(f.desc, j), port);
 }
 
 // In-kernel hit counting of the pipeline (launch_pipeline): the ACL
@@ -547,9 +587,10 @@ struct PipeTries {
 
 template <bool kCount>
 __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx& a,
-                                             const PipeTries& tr, const PipeIn& in, int64_t i,
-                                             const PipeOut& out, const PipeCount& pc,
-                                             const PipeLds& L, PipeTally* t) {
+                                             const AclV6Ctx& a6, const PipeTries& tr,
+                                             const PipeIn& in, int64_t i, const PipeOut& out,
+                                             const PipeCount& pc, const PipeLds& L,
+                                             PipeTally* t) {
     const bool v6 = in.family && in.family[i] == 6;
     const bool tcp = in.proto[i] == VC_PROTO_TCP;
     const uint32_t port = in.dport[i];
@@ -563,7 +604,7 @@ __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.dst6)[i], &hi, &lo);
         e = route6_chase(tr.n6, tr.rb6, tr.n6[hi >> (64 - tr.rb6)], hi, lo);
-        v = acl_v6_one(img, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
+        v = acl_v6_fenced(a6, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
     } else {
         const uint32_t d = in.dst4[i];
         e = route_chase(tr.n4, tr.rb4, tr.n4[d >> (32 - tr.rb4)], d);
@@ -576,86 +617,145 @@ __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx
     if (kCount) pipe_count(pc, L.ah, L.rc, L.gc, tcp, v, v6, r, grp, t);
 }
 
+constexpr int kPipeWaves = kPipeBlock / 64;
+
+// Cross-lane LDS exchange inside one wave (no workgroup barrier needed).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The vector path keeps IPv4 and IPv6 packets from diverging: a wave's 256
+// packets (4 per lane) are classified by family with a ballot, the IPv6
+// ones are queued in LDS and spread over all 64 lanes (one round per 64
+// IPv6 packets), their results handed back through LDS, and only then does
+// every lane finish its IPv4 packets.  Without it every wave ran the IPv6
+// path (ACL search + trie walk) once per packet slot whenever any of its
+// lanes had an IPv6 packet there -- i.e. always, at a 15 % IPv6 mix.
 template <bool kLds, bool kVec, bool kCount>
 __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, PipeTries tr,
                                                                    PipeIn in, int64_t n,
-                                                                   PipeOut out, PipeCount pc) {
+                                                                   PipeOut out, PipeCount pc,
+                                                                   int fshift, int fence_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t tally[5];
+    __shared__ uint8_t q6[kPipeWaves][256];        // queued IPv6 packets: lane * 4 + slot
+    __shared__ uint32_t r6[kPipeWaves][64][2];     // per round: ACL value, route entry
+    const AclV6Ctx a6 = stage_fences(img, reinterpret_cast<uint64_t*>(lds + fence_words), fshift);
     const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally);
+    __syncthreads();
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
     int64_t lo, hi;
     pipe_slice(n, &lo, &hi);
     PipeTally t;
     if (!kVec) {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-            pipe_mix_one<kCount>(img, a, tr, in, i, out, pc, L, &t);
+            pipe_mix_one<kCount>(img, a, a6, tr, in, i, out, pc, L, &t);
     } else {
-        for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
+        const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+        const uint64_t below_me = (uint64_t(1) << lane) - 1;
+        const int64_t per_iter = 4 * int64_t(blockDim.x);
+        const int64_t iters = (hi - lo + per_iter - 1) / per_iter;    // uniform
+        for (int64_t it = 0; it < iters; ++it) {
+            const int64_t i = lo + it * per_iter + 4 * int64_t(threadIdx.x);
+            const bool act = i + 3 < hi;
             const int64_t g = i >> 2;
-            const uint32_t fm = in.family ? reinterpret_cast<const uint32_t*>(in.family)[g]
-                                          : 0x04040404u;
-            const uint32_t pr = reinterpret_cast<const uint32_t*>(in.proto)[g];
-            const uint2 pt = reinterpret_cast<const uint2*>(in.dport)[g];
-            const uint4 d4 = reinterpret_cast<const uint4*>(in.dst4)[g];
-            const uint4 s4 = reinterpret_cast<const uint4*>(in.src4)[g];
+            uint32_t fm = 0x04040404u, pr = 0;
+            uint2 pt = make_uint2(0, 0);
+            uint4 d4 = make_uint4(0, 0, 0, 0), s4 = d4;
+            if (act) {
+                if (in.family) fm = reinterpret_cast<const uint32_t*>(in.family)[g];
+                pr = reinterpret_cast<const uint32_t*>(in.proto)[g];
+                pt = reinterpret_cast<const uint2*>(in.dport)[g];
+                d4 = reinterpret_cast<const uint4*>(in.dst4)[g];
+                s4 = reinterpret_cast<const uint4*>(in.src4)[g];
+            }
             const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
             const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
             const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
             bool v6[4], tcp[4];
-            uint64_t dh[4], dl[4];
-            uint32_t e[4];
+            uint32_t e[4], v[4];
             int32_t grp[4] = {-1, -1, -1, -1};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                v6[k] = ((fm >> (8 * k)) & 0xFFu) == 6;
+                v6[k] = act && ((fm >> (8 * k)) & 0xFFu) == 6;
                 tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-                dh[k] = dl[k] = 0;
-                if (v6[k]) {
-                    v6_key(reinterpret_cast<const uint4*>(in.dst6)[i + k], &dh[k], &dl[k]);
-                    e[k] = tr.n6[dh[k] >> (64 - tr.rb6)];
-                } else {
-                    e[k] = tr.n4[d[k] >> (32 - tr.rb4)];
-                }
+                e[k] = act && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
+                v[k] = VC_NONE;
             }
-            if (in.host_id) {
+            if (act && in.host_id) {
                 const uint4 h4 = reinterpret_cast<const uint4*>(in.host_id)[g];
                 const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     grp[k] = int64_t(h[k]) < in.n_pool ? in.pool_group[h[k]] : -1;
             }
-            uint32_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v[k] = v6[k] ? acl_v6_one(img, tcp[k], reinterpret_cast<const uint4*>(in.src6)[i + k],
-                                          po[k])
-                             : acl_v4_one(a, tcp[k], sk[k], po[k]);
-            int4 oa, orr;
-            uint32_t al = 0;
-            int32_t* pa = reinterpret_cast<int32_t*>(&oa);
-            int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
+            // queue this wave's IPv6 packets (slot-major, then lane order)
+            int pos[4];
+            int total = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                uint8_t b = 0;
-                acl_emit(img, tcp[k], v[k], out.allow ? &b : nullptr, pa + k);
-                al |= uint32_t(b) << (8 * k);
-                pr_[k] = out_index(v6[k] ? route6_chase(tr.n6, tr.rb6, e[k], dh[k], dl[k])
-                                         : route_chase(tr.n4, tr.rb4, e[k], d[k]));
+                const uint64_t m = __ballot(v6[k]);
+                pos[k] = total + __popcll(m & below_me);
+                total += __popcll(m);
+                if (v6[k]) q6[w][pos[k]] = uint8_t(lane * 4 + k);
             }
-            reinterpret_cast<int4*>(out.acl)[g] = oa;
-            reinterpret_cast<int4*>(out.route)[g] = orr;
-            reinterpret_cast<int4*>(out.group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
-            if (out.allow) reinterpret_cast<uint32_t*>(out.allow)[g] = al;
-            if (kCount) {
+            if (total) {                                  // wave-uniform
+                wave_sync();
+                const int64_t wbase = lo + it * per_iter + 256 * int64_t(w);
+                for (int r0 = 0; r0 < total; r0 += 64) {
+                    if (r0 + lane < total) {
+                        const int64_t gi = wbase + q6[w][r0 + lane];
+                        const bool t6 = in.proto[gi] == VC_PROTO_TCP;
+                        uint64_t hh, ll;
+                        v6_key(reinterpret_cast<const uint4*>(in.dst6)[gi], &hh, &ll);
+                        const uint32_t root = tr.n6[hh >> (64 - tr.rb6)];
+                        const uint32_t vv = acl_v6_fenced(a6, t6,
+                                                          reinterpret_cast<const uint4*>(in.src6)[gi],
+                                                          in.dport[gi]);
+                        r6[w][lane][1] = route6_chase(tr.n6, tr.rb6, root, hh, ll);
+                        r6[w][lane][0] = vv;
+                    }
+                    wave_sync();
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (v6[k] && pos[k] >= r0 && pos[k] < r0 + 64) {
+                            v[k] = r6[w][pos[k] - r0][0];
+                            e[k] = r6[w][pos[k] - r0][1];
+                        }
+                    wave_sync();
+                }
+            }
+            if (act) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    pipe_count(pc, L.ah, L.rc, L.gc, tcp[k], v[k], v6[k], pr_[k], grp[k], &t);
+                    if (!v6[k]) v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+                int4 oa, orr;
+                uint32_t al = 0;
+                int32_t* pa = reinterpret_cast<int32_t*>(&oa);
+                int32_t* pr_ = reinterpret_cast<int32_t*>(&orr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint8_t b = 0;
+                    acl_emit(img, tcp[k], v[k], out.allow ? &b : nullptr, pa + k);
+                    al |= uint32_t(b) << (8 * k);
+                    pr_[k] = out_index(v6[k] ? e[k] : route_chase(tr.n4, tr.rb4, e[k], d[k]));
+                }
+                reinterpret_cast<int4*>(out.acl)[g] = oa;
+                reinterpret_cast<int4*>(out.route)[g] = orr;
+                reinterpret_cast<int4*>(out.group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+                if (out.allow) reinterpret_cast<uint32_t*>(out.allow)[g] = al;
+                if (kCount) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        pipe_count(pc, L.ah, L.rc, L.gc, tcp[k], v[k], v6[k], pr_[k], grp[k], &t);
+                }
             }
         }
         const int64_t tail = hi & ~int64_t(3);
         if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
-            pipe_mix_one<kCount>(img, a, tr, in, tail + threadIdx.x, out, pc, L, &t);
+            pipe_mix_one<kCount>(img, a, a6, tr, in, tail + threadIdx.x, out, pc, L, &t);
     }
     if (kCount) pipe_count_flush(pc, L.ah, L.rc, L.gc, tally, t);
 }
@@ -669,6 +769,8 @@ namespace {
 // LDS budget for the staged v4 ACL boundaries (words); above it the kernel
 // searches the boundaries in global memory (L2-resident).
 constexpr int kLdsWords = 30 * 1024;
+
+int vcd_fences(int nb, int shift) { return (nb + (1 << shift) - 1) >> shift; }
 
 }  // namespace
 
@@ -698,6 +800,23 @@ int grid_for(const LaunchCfg& c, int64_t work_items, int blocks_per_cu) {
 }
 
 bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+// LDS budget of the IPv6 ACL fences: blocks of at least 16 boundaries
+constexpr size_t kFenceBytes = 40 * 1024;
+
+int v6_fence_shift(const AclImage& img) {
+    int shift = 4;
+    auto bytes = [&](int s) {
+        return size_t(vcd_fences(img.fam[0][1].nb, s) + vcd_fences(img.fam[1][1].nb, s)) * 16;
+    };
+    while (bytes(shift) > kFenceBytes && shift < 30) ++shift;
+    return shift;
+}
+
+size_t v6_fence_bytes(const AclImage& img, int shift) {
+    return std::max<size_t>(16, size_t(vcd_fences(img.fam[0][1].nb, shift) +
+                                       vcd_fences(img.fam[1][1].nb, shift)) * 16);
+}
 
 // Dynamic LDS beyond 64 KiB must be opted into per kernel.  Keyed by the
 // kernel's address: template instances share a function-pointer type.
@@ -750,8 +869,12 @@ hipError_t launch_acl_v6(const LaunchCfg& c, const AclImage& img, const uint8_t*
                          uint8_t* allow, unsigned long long* counters) {
     if (n <= 0) return hipSuccess;
     if (!aligned(src6, 16)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vcd::acl_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
-                       c.stream, img, proto, src6, port, n, out, allow);
+    const int shift = v6_fence_shift(img);
+    const size_t shmem = v6_fence_bytes(img, shift);
+    if (shmem > 64 * 1024)
+        if (hipError_t e = allow_lds(vcd::acl_v6_kernel, shmem)) return e;
+    hipLaunchKernelGGL(vcd::acl_v6_kernel, dim3(grid_for(c, n, 4)), dim3(vcd::kBlock), shmem,
+                       c.stream, img, shift, proto, src6, port, n, out, allow);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_ACL, out, proto, n, int64_t(img.n_tcp) + img.n_udp, 0,
@@ -799,8 +922,16 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     // the tuned C5 kernel: IPv4 packets with hostnames; everything else
     // (per-packet family, no hostname stage) runs the mixed kernel
     const bool mix = p.family != nullptr || p.host_id == nullptr;
+    // LDS: the mixed kernel always stages the IPv6 ACL fences (and holds its
+    // per-wave IPv6 queues statically); the v4 boundaries and the in-kernel
+    // counts take what is left
+    constexpr size_t kLdsMax = 160 * 1024 - 256;
+    constexpr size_t kMixStatic = 13 * 1024;
+    const int fshift = mix ? v6_fence_shift(acl) : 0;
+    const size_t fbytes = mix ? v6_fence_bytes(acl, fshift) : 0;
+    const size_t lds_max = mix ? kLdsMax - kMixStatic - fbytes : kLdsMax;
     const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
-    const bool lds = words <= kLdsWords;
+    const bool lds = words <= kLdsWords && size_t(words) * 4 <= lds_max;
     bool vec = aligned(p.proto, 4) && aligned(p.src4, 16) && aligned(p.dst4, 16) &&
                aligned(p.dport, 8) && aligned(p.host_id, 16) && aligned(p.out_acl, 16) &&
                aligned(p.out_route, 16) && aligned(p.out_group, 16) &&
@@ -810,7 +941,6 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
     // In-kernel counting where it fits the workgroup's LDS; the rest is
     // counted by separate passes over the outputs afterwards.
-    constexpr size_t kLdsMax = 160 * 1024 - 256;
     size_t shmem = lds ? size_t(words) * 4 : 0;
     vcd::PipeCount pc{};
     pc.bw_shift = big_hist_bucket_shift();
@@ -830,7 +960,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     if (rbytes + gbytes)
         e = c.scratch ? c.scratch->acquire(rbytes + gbytes, c.stream, &slot, &scratch)
                       : hipErrorInvalidValue;
-    if (cnt.acl && shmem + size_t(acl_bins) * 4 <= kLdsMax) {
+    if (cnt.acl && shmem + size_t(acl_bins) * 4 <= lds_max) {
         pc.acl = cnt.acl;
         pc.acl_bins = acl_bins;
         pc.n_tcp = acl.n_tcp;
@@ -838,7 +968,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     }
     if (r_big && e == hipSuccess) {
         big_hist_begin(scratch, n, route_nval, grid, &rh);
-        if (shmem + size_t(rh.nbk) * 4 <= kLdsMax) {
+        if (shmem + size_t(rh.nbk) * 4 <= lds_max) {
             pc.rcounts = rh.counts;
             pc.r_nbk = rh.nbk;
             pc.route = cnt.route;
@@ -848,7 +978,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     }
     if (g_big && e == hipSuccess) {
         big_hist_begin(scratch + rbytes, n, cnt.n_groups, grid, &gh);
-        if (shmem + size_t(gh.nbk) * 4 <= kLdsMax) {
+        if (shmem + size_t(gh.nbk) * 4 <= lds_max) {
             pc.gcounts = gh.counts;
             pc.g_nbk = gh.nbk;
             pc.group = cnt.group;
@@ -857,6 +987,8 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
         }
     }
     const bool count = pc.acl || pc.rcounts || pc.gcounts;
+    const int fence_words = int((shmem / 4 + 3) & ~size_t(3));
+    if (mix) shmem = size_t(fence_words) * 4 + fbytes;
     if (e == hipSuccess) {
         const TrieImage& r4 = route.fam[0];
 #define VC_PIPE(L, V, K)                                                                           \
@@ -870,10 +1002,12 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     } while (0)
 #define VC_MIX(L, V, K)                                                                            \
     do {                                                                                           \
-        if (shmem > 64 * 1024) e = allow_lds(vcd::pipeline_mix_kernel<L, V, K>, kLdsMax);          \
+        if (shmem > 64 * 1024)                                                                     \
+            e = allow_lds(vcd::pipeline_mix_kernel<L, V, K>, kLdsMax - kMixStatic);                \
         if (e != hipSuccess) break;                                                                \
         hipLaunchKernelGGL((vcd::pipeline_mix_kernel<L, V, K>), dim3(grid),                        \
-                           dim3(vcd::kPipeBlock), shmem, c.stream, acl, tr, in, n, out, pc);       \
+                           dim3(vcd::kPipeBlock), shmem, c.stream, acl, tr, in, n, out, pc,        \
+                           fshift, fence_words);                                                   \
     } while (0)
         if (!mix) {
             if (count) {
