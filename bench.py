@@ -489,7 +489,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
                     choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "sni", "parse",
-                             "source", "mirror", "mix", "mixhost"])
+                             "switch", "source", "mirror", "mix", "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -856,7 +856,7 @@ def sub_bench(args, clf, dev, rank, world):
             clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, n,
             C.c_void_p(out.data_ptr()), S()))
         per_unit, unit, kern = nbytes / n + 8, "B/SNI (bytes + 4 offset + 4 out)", "cert_kernel"
-    elif args.workload in ("parse", "mirror"):
+    elif args.workload in ("parse", "mirror", "switch"):
         frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
         fblob, foff = W.pack(frames)
         n = 32 << 20
@@ -873,6 +873,25 @@ def sub_bench(args, clf, dev, rank, world):
             per_unit = nbytes / n + 4 + 54
             unit = "B/frame (frame bytes + 4 offset in; 54 B of SoA fields out)"
             kern = "packet_kernel"
+        elif args.workload == "switch":
+            # parse + bare-VXLAN ACL on the sender + inner route, one kernel,
+            # over the C5 SecurityGroup and route tables; only the route
+            # index and the verdict leave the kernel
+            t = c5_tables(clf, dev, 1 << 20)
+            g = torch.Generator(device=dev)
+            g.manual_seed(19)
+            r4 = dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
+            out_route = torch.empty(n, dtype=torch.int32, device=dev)
+            out_allow = torch.empty(n, dtype=torch.uint8, device=dev)
+            none = V._lib.VcPktOut()
+            fn = lambda: V.check(V.lib().vc_switch_classify_dev(
+                clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, 0, None,
+                C.c_void_p(r4.data_ptr()), None, 4789, C.byref(none), None,
+                C.c_void_p(out_allow.data_ptr()), C.c_void_p(out_route.data_ptr()), S()))
+            per_unit = nbytes / n + 4 + 4 + 5
+            unit = ("B/datagram (frame bytes + 4 offset + 4 sender in; 4 route + 1 verdict out), "
+                    "10k-rule SecurityGroup, 980,848 + 200,000 routes")
+            kern = "switch_kernel"
         else:
             filters = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
                         "network2": "10.0.0.0/8"} for i in range(16)] + \

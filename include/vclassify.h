@@ -375,6 +375,27 @@ int vc_parse_packets_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, 
 int vc_parse_packets(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n, int layer,
                      const vc_pkt_out *out);
 
+/* Switch.PacketHandler.readable's per-datagram classification in one pass
+ * (core/src/main/java/vswitch/Switch.java:679-700,744-776): for datagram i
+ * from sender remote[i],
+ *   out_allow[i] / out_acl[i] = bareVXLanAccess.allow(Protocol.UDP, remote,
+ *       bind_port) -- the compiled SecurityGroup's UDP list (index, -1 =
+ *       defaultAllow decided);
+ *   `out` = VXLanPacket.from(payload) etc., as vc_parse_packets;
+ *   out_route[i] = RouteTable.lookup(inner dst) (L3.java:423-444): an index
+ *       in rulesV4 (inner IPv4) or rulesV6 (inner IPv6), -1 when none
+ *       matches, the datagram is denied, or it does not parse into an IP
+ *       packet.
+ * The switch's further per-packet decisions (remote-switch ifaces, MAC
+ * checks, synthetic IPs, hop limit) stay with the caller.  remote_family:
+ * 4/6 per datagram (NULL = all IPv4); remote4 / remote6 (16-byte aligned)
+ * as in vc_packets.  Any vc_pkt_out pointer and out_acl / out_allow may be
+ * NULL; out_route is required.  Device pointers. */
+int vc_switch_classify_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
+                           int layer, const uint8_t *remote_family, const uint32_t *remote4,
+                           const uint8_t *remote6, int bind_port, const vc_pkt_out *out,
+                           int32_t *out_acl, uint8_t *out_allow, int32_t *out_route, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Traffic-mirror filters (vmirror/FilterConfig.java:27-94, Mirror.java)   */
 /* ------------------------------------------------------------------------ */

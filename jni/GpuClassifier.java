@@ -1,0 +1,93 @@
+package vproxy.component.secure;
+
+import java.io.IOException;
+import java.nio.ByteBuffer;
+
+/**
+ * JNI face of libvclassify (include/vclassify.h), selected with
+ * -Dclassifier=gpu and loaded the way vfd/posix/PosixFDs.java:12-21 loads
+ * vfdposix.  Every batch is a set of direct ByteBuffers (native byte order,
+ * SoA, n items); results are indices into the live Java lists, -1 = null /
+ * default, so callers map them back exactly as SecurityGroup.allow,
+ * RouteTable.lookup and Upstream.searchForGroup would have returned them.
+ * Strings are UTF-8 (include/vclassify.h "String encoding").
+ * Native side: jni/vproxy_component_secure_GpuClassifier.c.
+ */
+public final class GpuClassifier {
+    static {
+        try {
+            System.loadLibrary("vclassify_jni");
+        } catch (UnsatisfiedLinkError e) {
+            System.out.println("vclassify_jni not found, requires libvclassify_jni.so and "
+                + "libvclassify.so on java.library.path");
+            e.printStackTrace(System.out);
+            System.exit(1);
+        }
+    }
+
+    private GpuClassifier() {
+    }
+
+    public static native long create(int device) throws IOException;
+    public static native void destroy(long ctx);
+    /** Page-lock and map a long-lived direct buffer once: calls on it become zero-copy. */
+    public static native void registerBuffer(ByteBuffer buf) throws IOException;
+    public static native void unregisterBuffer(ByteBuffer buf) throws IOException;
+
+    /** tcp / udp: packed vc_acl_rule[] (52 B each) in SecurityGroup list order. */
+    public static native void compileAcl(long ctx, ByteBuffer tcp, int nTcp, ByteBuffer udp, int nUdp,
+                                         boolean defaultAllow) throws IOException;
+    public static native void classifyAclV4(long ctx, ByteBuffer proto, ByteBuffer src4, ByteBuffer port,
+                                            int n, ByteBuffer outIdx, ByteBuffer outAllow) throws IOException;
+    public static native void classifyAclV6(long ctx, ByteBuffer proto, ByteBuffer src6, ByteBuffer port,
+                                            int n, ByteBuffer outIdx, ByteBuffer outAllow) throws IOException;
+
+    /** v4 / v6: packed vc_net[] (40 B each) of rulesV4 / rulesV6 in list order. */
+    public static native void compileRoutes(long ctx, ByteBuffer v4, int n4, ByteBuffer v6, int n6)
+        throws IOException;
+    public static native void lookupRouteV4(long ctx, ByteBuffer dst4, int n, ByteBuffer out) throws IOException;
+    public static native void lookupRouteV6(long ctx, ByteBuffer dst6, int n, ByteBuffer out) throws IOException;
+
+    /** groups: packed vc_group_annos[] whose string slots hold offsets into `strings` (-1 = null). */
+    public static native void compileUpstream(long ctx, ByteBuffer groups, int n, ByteBuffer strings)
+        throws IOException;
+    public static native void searchHints(long ctx, ByteBuffer hostBlob, ByteBuffer hostOff, ByteBuffer hostNull,
+                                          ByteBuffer port, ByteBuffer uriBlob, ByteBuffer uriOff,
+                                          ByteBuffer uriNull, int n, ByteBuffer outGroup) throws IOException;
+    public static native void compileHostsText(long ctx, ByteBuffer text, int len) throws IOException;
+    /** qnames as Formatter.parseDomainName's wire bytes (blob + n + 1 int offsets). */
+    public static native void classifyDns(long ctx, ByteBuffer qBlob, ByteBuffer qOff, int n,
+                                          ByteBuffer outKind, ByteBuffer outValue) throws IOException;
+
+    /** A Switch drain-loop batch: family (4/6), proto, src4, dst4, src6, dst6, dport, host ids. */
+    public static native void pipeline(long ctx, ByteBuffer family, ByteBuffer proto, ByteBuffer src4,
+                                       ByteBuffer dst4, ByteBuffer src6, ByteBuffer dst6, ByteBuffer dport,
+                                       ByteBuffer hostId, ByteBuffer poolGroup, int nPool, int n,
+                                       ByteBuffer outAcl, ByteBuffer outRoute, ByteBuffer outGroup,
+                                       ByteBuffer outAllow) throws IOException;
+
+    /** servers: packed vc_server[] (32 B each) per group; groupOff: n + 1 ints. */
+    public static native void compileServers(long ctx, ByteBuffer servers, ByteBuffer groupOff, int nGroups)
+        throws IOException;
+    public static native void setServerHealth(long ctx, ByteBuffer healthy, int nServers) throws IOException;
+    /** view 0 = next(source), 4 = nextIPv4, 6 = nextIPv6; out: index in the group's server list or -1. */
+    public static native void selectSourceV4(long ctx, ByteBuffer group, ByteBuffer src4, int n, int view,
+                                             ByteBuffer outServer) throws IOException;
+
+    /** frames: blob + n + 1 int offsets; out: 12 direct buffers in vc_pkt_out order (null = skip). */
+    public static native void parsePackets(long ctx, ByteBuffer blob, ByteBuffer off, int n, int layer,
+                                           ByteBuffer[] out) throws IOException;
+
+    public static native void compileCerts(long ctx, ByteBuffer names, ByteBuffer off, ByteBuffer holder,
+                                           int nNames, int nHolders) throws IOException;
+    public static native void chooseCerts(long ctx, ByteBuffer sni, ByteBuffer off, ByteBuffer isNull, int n,
+                                          ByteBuffer outHolder) throws IOException;
+
+    public static native void compileMirror(long ctx, ByteBuffer filters, int n) throws IOException;
+    public static native void mirrorSwitch(long ctx, int origin, ByteBuffer blob, ByteBuffer off, int n,
+                                           int layer, ByteBuffer outMirrors) throws IOException;
+
+    public static native void enableCounters(long ctx, boolean on) throws IOException;
+    /** GlobalInspection-style text of the per-rule hit counters. */
+    public static native String countersPrometheus(long ctx, String extraLabels) throws IOException;
+}

@@ -1,0 +1,116 @@
+"""GPU tier: vc_switch_classify_dev -- the vswitch's per-datagram chain in
+one kernel, against the oracle's restatements of each step:
+
+    bareVXLanAccess.allow(Protocol.UDP, remote, vxlanBindingAddress.port)
+        core/src/main/java/vswitch/Switch.java:679 -> SecurityGroup.java:30-45
+    VXLanPacket.from / EthernetPacket / Ipv4Packet / Ipv6Packet ...
+        Switch.java:681-684 -> base/src/main/java/vpacket/*.java
+    RouteTable.lookup(inner dst)
+        core/src/main/java/vswitch/stack/L3.java:423-444 -> RouteTable.java:44-59
+
+Frames are the parse-chain cases of tests/cases.py (every layer, malformed
+and truncated shapes); senders are IPv4 and IPv6 (incl. IPv4-mapped).
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import vproxy_amd as V
+from vproxy_amd import workloads as W
+
+from cases import gen_frames
+
+pytestmark = pytest.mark.gpu
+BIND_PORT = 4789
+
+
+def _rules(rng):
+    udp = [("10.0.0.0/8", 4789, 4789, True), ("10.1.0.0/16", 0, 65535, False),
+           ("192.168.0.0/16", 4000, 5000, True), ("::ffff:172.16.0.0/108", 0, 65535, True),
+           ("2001:db8::/32", 4789, 4789, False), ("2001:db8:1::/48", 0, 65535, True),
+           ("0.0.0.0/0", 1, 100, True)]
+    tcp = [("0.0.0.0/0", 0, 65535, True)]
+    from cases import rule_row
+    return (np.concatenate([rule_row(*r) for r in tcp]),
+            np.concatenate([rule_row(*r) for r in udp]))
+
+
+def _remotes(rng, n):
+    fam = np.where(rng.random(n) < 0.7, 4, 6).astype(np.uint8)
+    base = rng.choice(np.array([0x0A000000, 0x0A010000, 0xC0A80000, 0xAC100000, 0x08080000],
+                               np.uint64), n)
+    r4 = (base | rng.integers(0, 1 << 16, n).astype(np.uint64)).astype(np.uint32)
+    r6 = np.zeros((n, 16), np.uint8)
+    k = rng.integers(0, 3, n)
+    r6[k == 0, 10:12] = 0xFF                         # ::ffff:a.b.c.d
+    r6[k == 0, 12:] = W.v4_to_bytes(r4)[k == 0]
+    r6[k >= 1, :4] = [0x20, 0x01, 0x0D, 0xB8]
+    r6[k == 2, 4:6] = [0, 1]
+    r6[:, 14:] = rng.integers(0, 256, (n, 2))
+    return fam, r4, r6
+
+
+@pytest.mark.parametrize("dflt", [False, True])
+def test_switch_classify_vs_oracle(dflt):
+    import torch
+    rng = np.random.default_rng(17)
+    clf = V.Classifier(0)
+    try:
+        tcp, udp = _rules(rng)
+        a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+        b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+        V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1 if dflt else 0))
+        plen = rng.integers(1, 20, 3000)
+        net = rng.integers(0, 2**32, 3000, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+        key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
+        _, first = np.unique(key, return_index=True)
+        nets4 = W.v4_nets(net[np.sort(first)], plen[np.sort(first)])
+        rng.shuffle(nets4)
+        hi = rng.integers(0, 2**64, 2000, dtype=np.uint64)
+        p6 = rng.integers(1, 24, 2000)
+        hi &= np.where(p6 >= 64, np.uint64(2**64 - 1),
+                       np.uint64(2**64 - 1) << (64 - p6).astype(np.uint64))
+        keyh = np.stack([hi.view(np.int64), p6], 1)
+        _, f6 = np.unique(keyh, axis=0, return_index=True)
+        nets6 = W.v6_nets(hi[np.sort(f6)], np.zeros(len(f6), np.uint64), p6[np.sort(f6)])
+        ra, rn, rk = W.as_ctypes(nets4, V._lib.VcNet)
+        rb, rbn, rbk = W.as_ctypes(nets6, V._lib.VcNet)
+        clf.compile_routes_raw(ra, rn, rb, rbn)
+        frames = gen_frames(rng, 30011)
+        n = len(frames)
+        fam, r4, r6 = _remotes(rng, n)
+        blob, off = W.pack(frames)
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        res, acl, allow, route = clf.switch_classify(
+            (T(blob), T(off.astype(np.int32))), T(r4.view(np.int32)), BIND_PORT, remote6=T(r6),
+            remote_family=T(fam))
+        torch.cuda.synchronize()
+        acl, allow, route = acl.cpu().numpy(), allow.cpu().numpy(), route.cpu().numpy()
+        l3 = res["l3"].cpu().numpy()
+        status = res["status"].cpu().numpy()
+        # the bare-VXLAN ACL on the sender (UDP list, bind port)
+        proto = np.full(n, 17, np.uint8)
+        ports = np.full(n, BIND_PORT, np.uint16)
+        w4, a4 = O.sg_batch_v4_np(tcp, udp, dflt, proto, r4, ports)
+        r6m = np.ascontiguousarray(r6)
+        w6, a6 = O.sg_batch_v6_np(tcp, udp, dflt, proto, r6m, ports)
+        six = fam == 6
+        np.testing.assert_array_equal(acl, np.where(six, w6, w4))
+        np.testing.assert_array_equal(allow, np.where(six, a6, a4))
+        assert 0.1 < allow.mean() < 0.9
+        # the parse, then the inner route for allowed IP packets
+        want = np.full(n, -1, np.int32)
+        for i, f in enumerate(frames):
+            p = O.parse_packet(f, V.LAYER_VXLAN)
+            assert (p["status"], p["l3"]) == (int(status[i]), int(l3[i])), i
+            if not allow[i] or p["status"] != 0 or p["l3"] not in (4, 6):
+                continue
+            dst = bytes.fromhex(p["dst"])
+            if p["l3"] == 4:
+                want[i] = O.rt_batch_v4_np(nets4, np.frombuffer(dst, ">u4").astype(np.uint32))[0]
+            else:
+                want[i] = O.rt_batch_v6_np(nets6, np.frombuffer(dst, np.uint8).reshape(1, 16))[0]
+        np.testing.assert_array_equal(route, want)
+        assert (route >= 0).sum() > 1000
+    finally:
+        clf.close()

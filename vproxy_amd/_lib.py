@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvclassify.so")
+# VCLASSIFY_LIB: another in-tree build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("VCLASSIFY_LIB") or os.path.join(HERE, "libvclassify.so")
 
 VC_OK, VC_EINVAL, VC_EEXIST, VC_ENOTFOUND, VC_EXEXC, VC_EDEVICE, VC_ENOMEM, VC_ESTATE = \
     0, -1, -2, -3, -4, -5, -6, -7
@@ -185,6 +186,8 @@ def lib():
         L.vc_mirror_switch.argtypes = [vp, i32, vp, vp, i64, i32, vp]
         L.vc_parse_packets_dev.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut), vp]
         L.vc_parse_packets.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut)]
+        L.vc_switch_classify_dev.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, i32, P(VcPktOut),
+                                             vp, vp, vp, vp]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

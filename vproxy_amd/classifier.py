@@ -588,6 +588,31 @@ class Classifier:
         check(lib().vc_parse_packets(self.h, _ptr(blob), _ptr(off), n, int(layer), C.byref(o)))
         return res
 
+    def switch_classify(self, frames, remote4, bind_port, remote6=None, remote_family=None,
+                        layer=0):
+        """Switch.PacketHandler.readable per datagram in one kernel
+        (vc_switch_classify_dev): bareVXLanAccess.allow(UDP, remote,
+        bind_port), the VXLAN parse and RouteTable.lookup(inner dst).
+        frames: (blob, off) torch CUDA tensors; remote4 int32 tensor,
+        remote6 [n, 16] uint8, remote_family uint8 (4/6).  Returns
+        (parse fields dict, acl, allow, route)."""
+        import torch
+        blob, off = frames
+        n = len(off) - 1
+        dev = blob.device
+        tdt = {"u8": torch.uint8, "u16": torch.int16, "u32": torch.int32}
+        res = {k: torch.empty((n, w) if w > 1 else (n,), dtype=tdt[t], device=dev)
+               for k, w, t in self._PKT_FIELDS}
+        o = VcPktOut(**{k: v.data_ptr() for k, v in res.items()})
+        acl = torch.empty(n, dtype=torch.int32, device=dev)
+        allow = torch.empty(n, dtype=torch.uint8, device=dev)
+        route = torch.empty(n, dtype=torch.int32, device=dev)
+        check(lib().vc_switch_classify_dev(self.h, _ptr(blob), _ptr(off), n, int(layer),
+                                           _ptr(remote_family), _ptr(remote4), _ptr(remote6),
+                                           int(bind_port), C.byref(o), _ptr(acl), _ptr(allow),
+                                           _ptr(route), _stream()))
+        return res, acl, allow, route
+
     # ---------------- ServerGroup source hashing ----------------
     def compile_servers(self, groups):
         """Server lists per group (see server_array)."""

@@ -1017,6 +1017,33 @@ int vc_parse_packets_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, 
     return e == hipSuccess ? VC_OK : hip_fail(e, "packet launch");
 }
 
+int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
+                           int layer, const uint8_t* remote_family, const uint32_t* remote4,
+                           const uint8_t* remote6, int bind_port, const vc_pkt_out* out,
+                           int32_t* out_acl, uint8_t* out_allow, int32_t* out_route,
+                           void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!blob || !off || !out_route || !remote4 ||
+                            (remote_family && !remote6))))
+        return fail(VC_EINVAL, "bad batch arguments");
+    if (layer != VC_LAYER_VXLAN && layer != VC_LAYER_ETHER && layer != VC_LAYER_IPV4 &&
+        layer != VC_LAYER_IPV6)
+        return fail(VC_EINVAL, "layer must be VC_LAYER_VXLAN, _ETHER, _IPV4 or _IPV6");
+    const vc_pkt_out none{};
+    const vc_pkt_out& o = out ? *out : none;
+    if ((reinterpret_cast<uintptr_t>(o.src6) & 15) || (reinterpret_cast<uintptr_t>(o.dst6) & 15) ||
+        (reinterpret_cast<uintptr_t>(remote6) & 15))
+        return fail(VC_EINVAL, "src6 / dst6 / remote6 must be 16-byte aligned");
+    auto a = ctx->get(ctx->acl);
+    auto r = ctx->get(ctx->route);
+    if (!a || !r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
+    hipError_t e = vc::launch_switch(ctx->cfg(stream), a->img, r->img, blob, off, n, layer, o,
+                                     remote_family, remote4, remote6, bind_port, out_acl,
+                                     out_allow, out_route);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "switch launch");
+}
+
 int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                      const vc_pkt_out* out) {
     int rc = set_dev(ctx);

@@ -12,6 +12,10 @@
 #include "launch.h"
 #include "route_dev.h"
 
+#ifndef VC_PIPE_NT
+#define VC_PIPE_NT 0
+#endif
+
 namespace vcd {
 
 constexpr int kBlock = 512;
@@ -307,6 +311,50 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel(
 // ---------------------------------------------------------------------------
 // Combined pipeline (C5): ACL(src, dport) -> route(dst) -> pool group gather
 // ---------------------------------------------------------------------------
+// The packet SoA streams are read and the outputs written once; with
+// VC_PIPE_NT they carry the nontemporal hint so they do not displace the
+// gathered tables (route root, pool results) from the caches.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint4 stream_ld(const uint4* p) {
+#if VC_PIPE_NT
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint2 stream_ld(const uint2* p) {
+#if VC_PIPE_NT
+    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+    return make_uint2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint32_t stream_ld(const uint32_t* p) {
+#if VC_PIPE_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stream_st(int4* p, int4 v) {
+#if VC_PIPE_NT
+    u32x4 w = {uint32_t(v.x), uint32_t(v.y), uint32_t(v.z), uint32_t(v.w)};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void stream_st(uint32_t* p, uint32_t v) {
+#if VC_PIPE_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, uint32_t e,
                                                 uint32_t d) {
     int shift = 32 - rb;
@@ -499,11 +547,11 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     } else {
         for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
             const int64_t g = i >> 2;
-            const uint4 d4 = reinterpret_cast<const uint4*>(dst)[g];
-            const uint4 h4 = reinterpret_cast<const uint4*>(host_id)[g];
-            const uint4 s4 = reinterpret_cast<const uint4*>(src)[g];
-            const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
-            const uint2 pt = reinterpret_cast<const uint2*>(dport)[g];
+            const uint4 d4 = stream_ld(reinterpret_cast<const uint4*>(dst) + g);
+            const uint4 h4 = stream_ld(reinterpret_cast<const uint4*>(host_id) + g);
+            const uint4 s4 = stream_ld(reinterpret_cast<const uint4*>(src) + g);
+            const uint32_t pr = stream_ld(reinterpret_cast<const uint32_t*>(proto) + g);
+            const uint2 pt = stream_ld(reinterpret_cast<const uint2*>(dport) + g);
             const uint32_t d[4] = {d4.x, d4.y, d4.z, d4.w};
             const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
             const uint32_t sk[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -532,10 +580,10 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
                 al |= uint32_t(b) << (8 * k);
                 pr_[k] = out_index(route_chase(nodes, rb, e[k], d[k]));
             }
-            reinterpret_cast<int4*>(out_acl)[g] = oa;
-            reinterpret_cast<int4*>(out_route)[g] = orr;
-            reinterpret_cast<int4*>(out_group)[g] = make_int4(grp[0], grp[1], grp[2], grp[3]);
-            if (out_allow) reinterpret_cast<uint32_t*>(out_allow)[g] = al;
+            stream_st(reinterpret_cast<int4*>(out_acl) + g, oa);
+            stream_st(reinterpret_cast<int4*>(out_route) + g, orr);
+            stream_st(reinterpret_cast<int4*>(out_group) + g, make_int4(grp[0], grp[1], grp[2], grp[3]));
+            if (out_allow) stream_st(reinterpret_cast<uint32_t*>(out_allow) + g, al);
             if (kCount) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)

@@ -215,6 +215,19 @@ __global__ __launch_bounds__(kHistBlock) void bucket_count_kernel(
         counts[int64_t(k) * gridDim.x + blockIdx.x] = c[k];
 }
 
+// Exclusive prefix sum over one wave's 64 lanes (no LDS, no barrier).
+__device__ __forceinline__ uint32_t wave_scan_excl(uint32_t v, uint32_t* total) {
+    const int lane = int(threadIdx.x & 63);
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
 // (2) one workgroup: exclusive scan of counts (bucket-major, m entries) ->
 // offsets[0..m]; then the segment table seg_off[0..nbk] (segments of at
 // most kSeg items per bucket, prefix-summed).
@@ -327,23 +340,47 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
         for (int q = 0; q < kPer; ++q)
             r[q] = v[q] >= 0 ? atomicAdd(&tcnt[v[q] / kBW], 1u) : 0u;
         __syncthreads();
-        // exclusive scan of tcnt over the buckets: 4 per thread, then block scan
-        uint32_t c4[4], s4 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int bk = threadIdx.x * 4 + k;
-            c4[k] = bk < nbk ? tcnt[bk] : 0u;
-            s4 += c4[k];
-        }
+        // exclusive scan of tcnt over the buckets, 4 per lane: one wave
+        // when there are at most 256 buckets (every counter space of the
+        // benchmark), else the whole workgroup
         uint32_t total;
-        uint32_t st = block_scan_excl(s4, part, &total);
+        if (nbk <= 256) {
+            if (threadIdx.x < 64) {
+                uint32_t c4[4], s4 = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int bk = threadIdx.x * 4 + k;
-            if (bk < nbk) tst[bk] = st;
-            st += c4[k];
+                for (int k = 0; k < 4; ++k) {
+                    const int bk = threadIdx.x * 4 + k;
+                    c4[k] = bk < nbk ? tcnt[bk] : 0u;
+                    s4 += c4[k];
+                }
+                uint32_t st = wave_scan_excl(s4, &total);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int bk = threadIdx.x * 4 + k;
+                    if (bk < nbk) tst[bk] = st;
+                    st += c4[k];
+                }
+                if (threadIdx.x == 0) part[0] = total;
+            }
+            __syncthreads();
+            total = part[0];
+        } else {
+            uint32_t c4[4], s4 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int bk = threadIdx.x * 4 + k;
+                c4[k] = bk < nbk ? tcnt[bk] : 0u;
+                s4 += c4[k];
+            }
+            uint32_t st = block_scan_excl(s4, part, &total);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int bk = threadIdx.x * 4 + k;
+                if (bk < nbk) tst[bk] = st;
+                st += c4[k];
+            }
+            __syncthreads();
         }
-        __syncthreads();
 #pragma unroll
         for (int q = 0; q < kPer; ++q)
             if (v[q] >= 0) sorted[tst[v[q] / kBW] + r[q]] = v[q];
@@ -388,8 +425,27 @@ __global__ __launch_bounds__(kHistBlock) void bucket_hist_kernel(
     const uint32_t s1 = s0 + kSeg < b1 ? s0 + kSeg : b1;
     const int64_t lo_bin = int64_t(b) * kBW;
     Run run;
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += blockDim.x)
-        run.add(lo_bin + tmp[i], h, lo_bin, kBW);
+    // 8 bins per lane per 16-byte load over the segment's aligned middle
+    const uint32_t a0 = (s0 + 7) & ~7u, a1 = s1 & ~7u;
+    if (a0 < a1) {
+        for (uint32_t i = s0 + threadIdx.x; i < a0; i += blockDim.x)
+            run.add(lo_bin + tmp[i], h, lo_bin, kBW);
+        for (uint32_t i = a1 + threadIdx.x; i < s1; i += blockDim.x)
+            run.add(lo_bin + tmp[i], h, lo_bin, kBW);
+        const uint4* t8 = reinterpret_cast<const uint4*>(tmp);
+        for (uint32_t c = (a0 >> 3) + threadIdx.x; c < (a1 >> 3); c += blockDim.x) {
+            const uint4 w = t8[c];
+            const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                run.add(lo_bin + (p[k] & 0xFFFFu), h, lo_bin, kBW);
+                run.add(lo_bin + (p[k] >> 16), h, lo_bin, kBW);
+            }
+        }
+    } else {
+        for (uint32_t i = s0 + threadIdx.x; i < s1; i += blockDim.x)
+            run.add(lo_bin + tmp[i], h, lo_bin, kBW);
+    }
     run.flush(h, lo_bin, kBW);
     __syncthreads();
     for (int k = threadIdx.x; k < kBW && lo_bin + k < nval; k += blockDim.x)

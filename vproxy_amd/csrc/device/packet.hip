@@ -1,6 +1,8 @@
 // packet.hip -- batched header extraction (packet_dev.h): one lane per frame.
+#include "acl_dev.h"
 #include "launch.h"
 #include "packet_dev.h"
+#include "route_dev.h"
 #include "stage.h"
 
 namespace vcd {
@@ -69,9 +71,117 @@ __global__ __launch_bounds__(kPktBlock) void packet_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Switch.PacketHandler.readable's per-datagram chain in one pass
+// (core/src/main/java/vswitch/Switch.java:679-700, 744-776, L3.java:423-444):
+// bareVXLanAccess.allow(UDP, remote, vxlanBindingAddress.port) on the outer
+// sender, VXLanPacket.from on the payload, and RouteTable.lookup(dst) of the
+// inner IPv4/IPv6 packet -- the parse results stay in registers, no SoA
+// round trip through HBM between the three.
+// ---------------------------------------------------------------------------
+struct SwitchIn {
+    const uint8_t* rfam;            // remote family per datagram (4/6), null = all IPv4
+    const uint32_t* r4;
+    const uint8_t* r6;              // 16 bytes per datagram, 16-byte aligned
+    uint32_t bind_port;
+};
+
+struct SwitchOut {
+    int32_t* acl;
+    uint8_t* allow;
+    int32_t* route;
+};
+
+__device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage& rt,
+                                           const SwitchIn& in, int64_t i, const PktOut& o,
+                                           const SwitchOut& so) {
+    // SecurityGroup.allow(Protocol.UDP, remote, port): the UDP list
+    const bool six = in.rfam && in.rfam[i] == 6;
+    uint32_t v;
+    if (six) {
+        const AclFamilyImage& f = acl.fam[1][1];
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
+        v = port_lookup(f.pieces, load_desc(f.desc, bsearch_u128(f.bounds6, f.nb, hi, lo)),
+                        in.bind_port);
+    } else {
+        const AclFamilyImage& f = acl.fam[1][0];
+        v = port_lookup(f.pieces, load_desc(f.desc, bsearch_u32(f.bounds4, f.nb, in.r4[i])),
+                        in.bind_port);
+    }
+    const bool allow = v == VC_NONE ? acl.default_allow != 0 : acl.allow[acl.n_tcp + v] != 0;
+    if (so.acl) so.acl[i] = out_index(v);
+    if (so.allow) so.allow[i] = allow ? 1 : 0;
+    // the inner packet's route, for allowed datagrams that parsed into IP
+    int32_t r = -1;
+    if (allow && o.status == VC_PKT_OK) {
+        if (o.l3 == VC_L3_IPV4) {
+            const uint32_t d = uint32_t(o.dst[0]) << 24 | uint32_t(o.dst[1]) << 16 |
+                               uint32_t(o.dst[2]) << 8 | o.dst[3];
+            r = out_index(trie_v4(rt.fam[0].nodes, rt.fam[0].root_bits, d));
+        } else if (o.l3 == VC_L3_IPV6) {
+            uint64_t hi, lo;
+            v6_key(*reinterpret_cast<const uint4*>(o.dst), &hi, &lo);
+            r = out_index(trie_v6(rt.fam[1].nodes, rt.fam[1].root_bits, hi, lo));
+        }
+    }
+    so.route[i] = r;
+}
+
+template <bool kStage>
+__global__ __launch_bounds__(kPktBlock) void switch_kernel(
+    const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n, int layer,
+    vc_pkt_out out, AclImage acl, RouteImage rt, SwitchIn in, SwitchOut so) {
+    __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
+    for (int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64; base < n; base += wstride) {
+        const int64_t i = base + lane;
+        const int64_t last = base + 64 < n ? base + 64 : n;
+        uint32_t a0 = 0;
+        const bool staged =
+            kStage && stage_wave<kPktStage>(blob, off[base], off[last], stage[w], &a0);
+        if (i < n) {
+            const uint32_t a = off[i], e = off[i + 1];
+            PktOut o;
+            if (staged) {
+                const uint8_t* lp = reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0);
+                parse_packet(lp, int(e - a), layer, &o);
+            } else {
+                parse_packet(blob + a, int(e - a), layer, &o);
+            }
+            store_pkt(out, i, o);
+            switch_one(acl, rt, in, i, o, so);
+        }
+        if (kStage) wave_done();
+    }
+}
+
 }  // namespace vcd
 
 namespace vc {
+
+hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
+                         const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                         const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
+                         const uint8_t* r6, int bind_port, int32_t* out_acl, uint8_t* out_allow,
+                         int32_t* out_route) {
+    if (n <= 0) return hipSuccess;
+    const int64_t want = (n + vcd::kPktBlock - 1) / vcd::kPktBlock;
+    const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
+    const void* k = stage ? reinterpret_cast<const void*>(vcd::switch_kernel<true>)
+                          : reinterpret_cast<const void*>(vcd::switch_kernel<false>);
+    const int grid = resident_grid(c, k, vcd::kPktBlock, 0, want);
+    const vcd::SwitchIn in{rfam, r4, r6, uint32_t(bind_port)};
+    const vcd::SwitchOut so{out_acl, out_allow, out_route};
+    if (stage)
+        hipLaunchKernelGGL(vcd::switch_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
+                           blob, off, n, layer, out, acl, rt, in, so);
+    else
+        hipLaunchKernelGGL(vcd::switch_kernel<false>, dim3(grid), dim3(vcd::kPktBlock), 0,
+                           c.stream, blob, off, n, layer, out, acl, rt, in, so);
+    return hipGetLastError();
+}
 
 hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_t* off, int64_t n,
                           int layer, const vc_pkt_out& out) {
