@@ -395,6 +395,11 @@ int vc_switch_classify_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off
                            int layer, const uint8_t *remote_family, const uint32_t *remote4,
                            const uint8_t *remote6, int bind_port, const vc_pkt_out *out,
                            int32_t *out_acl, uint8_t *out_allow, int32_t *out_route, void *stream);
+/* Host pointers (every array), synchronous. */
+int vc_switch_classify(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n, int layer,
+                       const uint8_t *remote_family, const uint32_t *remote4,
+                       const uint8_t *remote6, int bind_port, const vc_pkt_out *out,
+                       int32_t *out_acl, uint8_t *out_allow, int32_t *out_route);
 
 /* ------------------------------------------------------------------------ */
 /* Traffic-mirror filters (vmirror/FilterConfig.java:27-94, Mirror.java)   */

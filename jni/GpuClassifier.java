@@ -66,6 +66,15 @@ public final class GpuClassifier {
                                        ByteBuffer outAcl, ByteBuffer outRoute, ByteBuffer outGroup,
                                        ByteBuffer outAllow) throws IOException;
 
+    /**
+     * Switch.PacketHandler.readable per datagram: bareVXLanAccess.allow on the sender, the VXLAN
+     * parse (out: 12 buffers in vc_pkt_out order, null = skip) and the inner packet's route.
+     */
+    public static native void switchClassify(long ctx, ByteBuffer blob, ByteBuffer off, int n, int layer,
+                                             ByteBuffer remoteFamily, ByteBuffer remote4, ByteBuffer remote6,
+                                             int bindPort, ByteBuffer[] out, ByteBuffer outAcl,
+                                             ByteBuffer outAllow, ByteBuffer outRoute) throws IOException;
+
     /** servers: packed vc_server[] (32 B each) per group; groupOff: n + 1 ints. */
     public static native void compileServers(long ctx, ByteBuffer servers, ByteBuffer groupOff, int nGroups)
         throws IOException;

@@ -222,6 +222,25 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_parsePackets
     jni_throw(env, vc_parse_packets(CTX(ctx), addr(env, blob), addr(env, off), n, layer, &o));
 }
 
+JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_switchClassify
+  (JNIEnv *env, jclass self, jlong ctx, jobject blob, jobject off, jint n, jint layer,
+   jobject remoteFamily, jobject remote4, jobject remote6, jint bindPort, jobjectArray out,
+   jobject outAcl, jobject outAllow, jobject outRoute) {
+    vc_pkt_out o;
+    void *f[12];
+    int i;
+    (void) self;
+    for (i = 0; i < 12; ++i)
+        f[i] = out ? addr(env, (*env)->GetObjectArrayElement(env, out, i)) : NULL;
+    o.status = f[0]; o.l3 = f[1]; o.l4 = f[2]; o.proto = f[3]; o.vni = f[4];
+    o.ether_type = f[5]; o.src4 = f[6]; o.dst4 = f[7]; o.src6 = f[8]; o.dst6 = f[9];
+    o.sport = f[10]; o.dport = f[11];
+    jni_throw(env, vc_switch_classify(CTX(ctx), addr(env, blob), addr(env, off), n, layer,
+                                      addr(env, remoteFamily), addr(env, remote4),
+                                      addr(env, remote6), bindPort, &o, addr(env, outAcl),
+                                      addr(env, outAllow), addr(env, outRoute)));
+}
+
 /* SSLContextHolder: certificate names (UTF-8 blob + offsets) and holder per name */
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileCerts
   (JNIEnv *env, jclass self, jlong ctx, jobject names, jobject off, jobject holder,

@@ -112,5 +112,16 @@ def test_switch_classify_vs_oracle(dflt):
                 want[i] = O.rt_batch_v6_np(nets6, np.frombuffer(dst, np.uint8).reshape(1, 16))[0]
         np.testing.assert_array_equal(route, want)
         assert (route >= 0).sum() > 1000
+        # the host entry point (vc_switch_classify) gives the same results
+        import ctypes as C
+        P = lambda x: C.c_void_p(x.ctypes.data)
+        h_route, h_acl = np.empty(n, np.int32), np.empty(n, np.int32)
+        h_allow, h_l3 = np.empty(n, np.uint8), np.empty(n, np.uint8)
+        o = V._lib.VcPktOut(l3=h_l3.ctypes.data)
+        V.check(V.lib().vc_switch_classify(clf.h, P(blob), P(off), n, 0, P(fam), P(r4), P(r6m),
+                                           BIND_PORT, C.byref(o), P(h_acl), P(h_allow),
+                                           P(h_route)))
+        for g, w in ((h_route, route), (h_acl, acl), (h_allow, allow), (h_l3, l3)):
+            np.testing.assert_array_equal(g, w)
     finally:
         clf.close()

@@ -188,6 +188,8 @@ def lib():
         L.vc_parse_packets.argtypes = [vp, vp, vp, i64, i32, P(VcPktOut)]
         L.vc_switch_classify_dev.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, i32, P(VcPktOut),
                                              vp, vp, vp, vp]
+        L.vc_switch_classify.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, i32, P(VcPktOut), vp,
+                                         vp, vp]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

@@ -1044,6 +1044,75 @@ int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off
     return e == hipSuccess ? VC_OK : hip_fail(e, "switch launch");
 }
 
+// Device copies of the host arrays of a vc_pkt_out (NULL stays NULL).
+static vc_pkt_out stage_pkt_out(Staging& st, const vc_pkt_out& out, size_t un) {
+    vc_pkt_out d{};
+    d.status = static_cast<uint8_t*>(st.out(out.status, un));
+    d.l3 = static_cast<uint8_t*>(st.out(out.l3, un));
+    d.l4 = static_cast<uint8_t*>(st.out(out.l4, un));
+    d.proto = static_cast<uint8_t*>(st.out(out.proto, un));
+    d.vni = static_cast<uint32_t*>(st.out(out.vni, un * 4));
+    d.ether_type = static_cast<uint16_t*>(st.out(out.ether_type, un * 2));
+    d.src4 = static_cast<uint32_t*>(st.out(out.src4, un * 4));
+    d.dst4 = static_cast<uint32_t*>(st.out(out.dst4, un * 4));
+    d.src6 = static_cast<uint8_t*>(st.out(out.src6, un * 16));
+    d.dst6 = static_cast<uint8_t*>(st.out(out.dst6, un * 16));
+    d.sport = static_cast<uint16_t*>(st.out(out.sport, un * 2));
+    d.dport = static_cast<uint16_t*>(st.out(out.dport, un * 2));
+    return d;
+}
+
+static void back_pkt_out(Staging& st, const vc_pkt_out& out, const vc_pkt_out& d, size_t un,
+                         hipStream_t s) {
+    st.back(out.status, d.status, un, s);
+    st.back(out.l3, d.l3, un, s);
+    st.back(out.l4, d.l4, un, s);
+    st.back(out.proto, d.proto, un, s);
+    st.back(out.vni, d.vni, un * 4, s);
+    st.back(out.ether_type, d.ether_type, un * 2, s);
+    st.back(out.src4, d.src4, un * 4, s);
+    st.back(out.dst4, d.dst4, un * 4, s);
+    st.back(out.src6, d.src6, un * 16, s);
+    st.back(out.dst6, d.dst6, un * 16, s);
+    st.back(out.sport, d.sport, un * 2, s);
+    st.back(out.dport, d.dport, un * 2, s);
+}
+
+int vc_switch_classify(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                       const uint8_t* remote_family, const uint32_t* remote4,
+                       const uint8_t* remote6, int bind_port, const vc_pkt_out* out,
+                       int32_t* out_acl, uint8_t* out_allow, int32_t* out_route) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!blob || !off || !out_route || !remote4 || (remote_family && !remote6))
+        return fail(VC_EINVAL, "bad batch arguments");
+    Staging st(ctx->pool, ctx->stream);
+    hipStream_t s = ctx->stream;
+    const size_t un = size_t(n);
+    const vc_pkt_out none{};
+    const vc_pkt_out& o = out ? *out : none;
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
+    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4, s));
+    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un, s));
+    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4, s));
+    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16, s));
+    const vc_pkt_out d = stage_pkt_out(st, o, un);
+    auto* dacl = static_cast<int32_t*>(st.out(out_acl, un * 4));
+    auto* dal = static_cast<uint8_t*>(st.out(out_allow, un));
+    auto* dr = static_cast<int32_t*>(st.out(out_route, un * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_switch_classify_dev(ctx, db, doff, n, layer, dfam, d4, d6, bind_port, &d, dacl, dal, dr,
+                                s);
+    if (rc) return rc;
+    back_pkt_out(st, o, d, un, s);
+    st.back(out_acl, dacl, un * 4, s);
+    st.back(out_allow, dal, un, s);
+    st.back(out_route, dr, un * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "switch classify");
+}
+
 int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                      const vc_pkt_out* out) {
     int rc = set_dev(ctx);

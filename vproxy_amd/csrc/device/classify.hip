@@ -13,7 +13,7 @@
 #include "route_dev.h"
 
 #ifndef VC_PIPE_NT
-#define VC_PIPE_NT 0
+#define VC_PIPE_NT 1
 #endif
 
 namespace vcd {
