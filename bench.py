@@ -242,7 +242,7 @@ class C5Steps:
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream", inflight=2):
+                 finish="stream", inflight=2, overlap="finish"):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -250,6 +250,7 @@ class C5Steps:
         self.count = counters != "none"
         self.fused = counters == "fused"
         self.finish = finish
+        self.overlap = overlap
         self.nbuf = 1 if serial else max(1, inflight)
         pool_out = torch.empty(t.pool_n, dtype=torch.int32, device=dev)
         self.pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(self.nbuf - 1)]
@@ -272,6 +273,8 @@ class C5Steps:
         with torch.cuda.stream(self.s_hint):
             if j - self.nbuf in self.ev_pipe:          # pool buffer no longer read
                 self.s_hint.wait_event(self.ev_pipe[j - self.nbuf])
+            if self.overlap == "finish" and j - 1 in self.kdone:
+                self.kdone[j - 1].wait(self.s_hint)     # after the previous pipeline kernel
             e0, e1 = TE(), TE()
             e0.record()
             t = self.t
@@ -502,6 +505,10 @@ def main():
                          "(overlapping the next batch) or inline after the pipeline kernel")
     ap.add_argument("--serial", action="store_true",
                     help="ablation: one stream, no overlap between consecutive batches")
+    ap.add_argument("--overlap", choices=["finish", "pipeline"], default="finish",
+                    help="what the next batch's hostname-pool pass runs beside: this batch's "
+                         "counter finish (it waits for this batch's pipeline kernel, which then "
+                         "runs alone) or the pipeline kernel itself")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (output and pool buffers)")
     ap.add_argument("--dist", action="store_true",
@@ -537,7 +544,8 @@ def main():
     lo, hi = shard(args.packets * world, rank, world)
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
     steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
-                    counters=args.counters, finish=args.finish, inflight=args.inflight)
+                    counters=args.counters, finish=args.finish, inflight=args.inflight,
+                    overlap=args.overlap)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
@@ -614,8 +622,10 @@ def main():
                            "parallelism": "dp%d" % world,
                            "schedule": ("serial, one stream" if args.serial else
                                         "%d batches in flight: pool / pipeline / counters on 3 "
-                                        "HIP streams, counter finish on the counters stream"
-                                        % args.inflight)},
+                                        "HIP streams, counter finish on the counters stream, "
+                                        "next pool pass beside the %s" % (
+                                            args.inflight, "counter finish" if
+                                            args.overlap == "finish" else "pipeline kernel"))},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()
