@@ -177,6 +177,21 @@ VC_HD uint32_t keep_mask(int pos, int lo, int hi) {
     return m_lo & m_hi;
 }
 
+// bytes j of a word at `pos` kept iff pos + j >= lo; needs pos > lo - 4
+VC_HD uint32_t lo_mask(int pos, int lo) {
+    return pos >= lo ? ~0u : (~0u << (8 * (lo - pos)));
+}
+
+// the first r bytes of a word; needs r >= 1
+VC_HD uint32_t tail_mask(int r) {
+    return r >= 4 ? ~0u : ((1u << (8 * r)) - 1u);
+}
+
+// Word reads of a source.  word(pos, lo, hi) keeps bytes in [lo, hi).
+// down(pos, lo, hi) is for words that end at or before hi (right-to-left
+// scans) and masks only the low side.  cursor(pos, hi).get(j) is the word
+// at pos + 4j; with LdsSrc its bytes at or past hi are NOT masked, so
+// callers mask with tail_mask.
 struct PtrSrc {
     const uint8_t* p;
     VC_HD const uint8_t* ptr() const { return p; }
@@ -189,6 +204,14 @@ struct PtrSrc {
         }
         return w;
     }
+    // word ending at or before hi, bytes below lo zero (pos > lo - 4)
+    VC_HD uint32_t down(int pos, int lo, int hi) const { return word(pos, lo, hi); }
+    struct Cur {
+        const uint8_t* p;
+        int pos, hi;
+        VC_HD uint32_t get(int j) const { return PtrSrc{p}.word(pos + 4 * j, pos, hi); }
+    };
+    VC_HD Cur cursor(int pos, int hi) const { return Cur{p, pos, hi}; }
 };
 
 // LE word from two aligned words: bytes [sh, sh + 4) of (hi:lo)
@@ -200,10 +223,21 @@ struct LdsSrc {
     const uint32_t* w;            // the wave's LDS stage (dword array)
     int off;                      // byte offset of the name's byte 0 in the stage
     VC_HD const uint8_t* ptr() const { return reinterpret_cast<const uint8_t*>(w) + off; }
-    VC_HD uint32_t word(int pos, int lo, int hi) const {
+    VC_HD uint32_t raw(int pos) const {
         const int a = off + pos;                // >= 0: the stage has a 16-byte apron
-        const uint32_t v = funnel(w[a >> 2], w[(a >> 2) + 1], uint32_t(a & 3));
-        return v & keep_mask(pos, lo, hi);
+        return funnel(w[a >> 2], w[(a >> 2) + 1], uint32_t(a & 3));
+    }
+    VC_HD uint32_t word(int pos, int lo, int hi) const { return raw(pos) & keep_mask(pos, lo, hi); }
+    // a word that ends at or before the key's end: only the low side to mask
+    VC_HD uint32_t down(int pos, int lo, int hi) const { return raw(pos) & lo_mask(pos, lo); }
+    struct Cur {                  // word j at dword p[j], p[j + 1] (immediate offsets)
+        const uint32_t* p;
+        uint32_t sh;
+        VC_HD uint32_t get(int j) const { return funnel(p[j], p[j + 1], sh); }
+    };
+    VC_HD Cur cursor(int pos, int hi) const {
+        const int a = off + pos;
+        return Cur{w + (a >> 2), uint32_t(a & 3)};
     }
 };
 
@@ -248,10 +282,11 @@ template <class Src>
 VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n) {
     if ((r.m.x & ~VC_REC_HAS_PM) != uint32_t(n)) return false;
     uint32_t diff = 0;
+    const auto c = q.cursor(st, st + n);
 #pragma unroll
     for (int j = 0; j < VC_REC_INLINE / 4; ++j) {
         if (!wave_any(4 * j < n)) break;          // no lane's key reaches word j
-        if (4 * j < n) diff |= q.word(st + 4 * j, st, st + n) ^ rec_word(r, j);
+        if (4 * j < n) diff |= (c.get(j) ^ rec_word(r, j)) & tail_mask(n - 4 * j);
     }
     if (diff) return false;
     if (n > VC_REC_INLINE) {      // long key: the rest from the blob copy
@@ -298,12 +333,17 @@ VC_HD uint32_t group_hits(uint4 g, uint32_t want) {
 }
 
 // slot of key [st, st + n) with hash h; -1 if absent.  *out = its record.
+// m0: group_hits of the first tag group when the caller already holds it
+// (host_only_fast loads every probe's first group up front), else ~0u.
 template <class Src>
-VC_HD int host_find(const HostTable& t, uint32_t h, const Src& q, int st, int n, Rec* out) {
+VC_HD int host_find(const HostTable& t, uint32_t h, const Src& q, int st, int n, Rec* out,
+                    uint32_t m0 = ~0u) {
     const uint32_t want = h | 1u;
     uint32_t s = h & t.mask & ~3u;
     for (;;) {
-        uint32_t m = group_hits(gload(reinterpret_cast<const uint4*>(t.tags + s)), want);
+        uint32_t m = m0 != ~0u ? m0
+                               : group_hits(gload(reinterpret_cast<const uint4*>(t.tags + s)), want);
+        m0 = ~0u;
         while (m & 15u) {
             const uint32_t k = __builtin_ctz(m);
             m &= m - 1;
@@ -345,7 +385,7 @@ VC_HD uint32_t pick(const HintImage& img, int slot, const Rec& r, int port) {
 template <class Src>
 VC_HD uint32_t src_khash(const Src& q, int st, int e) {
     uint32_t S = vck::kSeed;
-    for (int pos = e - 4; pos > st - 4; pos -= 4) S = vck::mix(S, q.word(pos, st, e));
+    for (int pos = e - 4; pos > st - 4; pos -= 4) S = vck::mix(S, q.down(pos, st, e));
     return vck::fin(S, uint32_t(e - st));
 }
 
@@ -424,8 +464,9 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
     int e = n, np = 0, nc = 0;
     uint32_t S = vck::kSeed;
     for (int pos = n - 4; pos > -4;) {
-        const uint32_t valid = keep_mask(pos, 0, e);
-        const uint32_t w = q.word(pos, 0, e);
+        // every word read here ends at or before e: only bytes below 0 to drop
+        const uint32_t valid = lo_mask(pos, 0);
+        const uint32_t w = q.down(pos, 0, e);
         const uint32_t cf = vck::byte_eq_flags(w, 0x3A3A3A3Au) & valid;
         if (cf) {                       // restart at the leftmost ':' so far
             nc += __builtin_popcount(cf);
@@ -444,12 +485,15 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             const uint32_t hv = b == 3 ? vck::fin(S, len)
                                        : vck::fin(vck::mix(S, w & (~0u << (8 * (b + 1)))), len);
             ++np;
+            // shift in: [1] = the latest (longest) suffix.  Plain moves under
+            // the lanes-with-a-dot mask, no per-slot compare and select.
 #pragma unroll
-            for (int k = 1; k < kProbes; ++k)
-                if (k == np) {
-                    h[k] = hv;
-                    st[k] = sp;
-                }
+            for (int k = kProbes - 1; k > 1; --k) {
+                h[k] = h[k - 1];
+                st[k] = st[k - 1];
+            }
+            h[1] = hv;
+            st[1] = sp;
         }
         S = vck::mix(S, w);
         pos -= 4;
@@ -459,34 +503,38 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
     st[0] = 0;
     if (nc) {
         // cut at the colon; strip "www." (then the whole host is the suffix
-        // after the dot at 3, recorded last); empty -> null
+        // after the dot at 3, the longest, in [1]); empty -> null
         if (e >= 4 && q.word(0, 0, 4) == 0x2E777777u) {
+            h[0] = h[1];
+            st[0] = 4;
 #pragma unroll
-            for (int k = 1; k < kProbes; ++k)
-                if (k == np) {
-                    h[0] = h[k];
-                    st[0] = 4;
-                }
+            for (int k = 1; k < kProbes - 1; ++k) {
+                h[k] = h[k + 1];
+                st[k] = st[k + 1];
+            }
             np -= 1;
         }
         if (e - st[0] <= 0) return -1;
     }
     const HostTable t = host_table(img);
-    uint32_t hits = 0;
+    // hits: bit k = probe k's first group has a tag match or continues;
+    // tm: its 4 match bits at 4k; cont: bit k = it continues (group_hits bit 4)
+    uint32_t hits = 0, tm = 0, cont = 0;
     {
+        // all first tag groups in flight together; g[k] is read only where
+        // it was loaded (k <= np), so it needs no initial value
         uint4 g[kProbes];
 #pragma unroll
-        for (int k = 0; k < kProbes; ++k)    // all first tag groups in flight together
-            g[k] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < kProbes; ++k) {
-            if (!wave_any(k <= np)) break;    // no lane has a k-th suffix
+        for (int k = 0; k < kProbes; ++k)
             if (k <= np) g[k] = tag_group(t.tags, t.mask, h[k]);
-        }
 #pragma unroll
         for (int k = 0; k < kProbes; ++k) {
-            if (!wave_any(k <= np)) break;
-            if (k <= np && group_hits(g[k], h[k] | 1u)) hits |= 1u << k;
+            if (k <= np) {
+                const uint32_t m = group_hits(g[k], h[k] | 1u);
+                tm |= (m & 15u) << (4 * k);
+                cont |= ((m >> 4) & 1u) << k;
+                hits |= (m != 0u ? 1u : 0u) << k;
+            }
         }
     }
     uint32_t best = VC_NONE;
@@ -501,7 +549,8 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             sk = k == j ? st[j] : sk;
         }
         Rec r;
-        const int slot = host_find(t, hk, q, sk, e - sk, &r);
+        const uint32_t m0 = ((tm >> (4 * k)) & 15u) | (((cont >> k) & 1u) << 4);
+        const int slot = host_find(t, hk, q, sk, e - sk, &r, m0);
         if (slot < 0) continue;
         const uint32_t v = pick(img, slot, r, port);
         if (k == 0) {
