@@ -58,7 +58,7 @@ def acl(tcp, udp, dflt, family, proto, src, port):
 def route(rules, family, keys):
     n = len(keys)
     out = np.empty(n, np.int32)
-    stats = np.zeros(2, np.int32)
+    stats = np.zeros(3, np.int32)     # root bits, nodes, one-prefix records
     rc = lib().ic_route(P(rules), len(rules), family, P(keys), n, P(out), P(stats))
     assert rc == 0, rc
     return out, stats

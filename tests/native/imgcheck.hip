@@ -98,7 +98,8 @@ int ic_route(const vc_net* rules, int nr, int family, const void* keys, int64_t 
     int rc = vc::build_trie(rules, nr, family == 4 ? 0 : 1, &t);
     if (rc) return rc;
     stats[0] = t.root_bits;
-    stats[1] = int32_t((t.nodes.size() - (size_t(1) << t.root_bits)) / 256);
+    stats[1] = t.n_nodes;
+    stats[2] = t.n_records;
     for (int64_t i = 0; i < n; ++i) {
         uint32_t e;
         if (family == 4) {

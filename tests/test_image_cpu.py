@@ -116,6 +116,66 @@ def test_route_v6():
     np.testing.assert_array_equal(got, want)
 
 
+def _flip(q6, bit):
+    """q6 [n,16] with address bit `bit` (0 = most significant) flipped"""
+    out = q6.copy()
+    out[:, bit // 8] ^= np.uint8(0x80 >> (bit % 8))
+    return out
+
+
+def test_route_one_prefix_records():
+    """Root slots holding a single longer prefix compile to one-prefix
+    records (images.h VC_ONE).  Edges: length 64 (the record limit) and 65
+    (nodes), a covering shorter prefix listed before and after the long one
+    (the record's match value is the min), slots with two long prefixes
+    (nodes), and queries one bit inside / outside each prefix."""
+    rng = np.random.default_rng(51)
+    n = 1500
+    plen = rng.choice(np.array([25, 30, 32, 40, 47, 48, 56, 63, 64, 65, 80]), n)
+    hi = rng.integers(0, 2**64, n, dtype=np.uint64)
+    lo = rng.integers(0, 2**64, n, dtype=np.uint64)
+    hm = np.where(plen >= 64, np.uint64(2**64 - 1),
+                  np.uint64(2**64 - 1) << (64 - np.minimum(plen, 64)).astype(np.uint64))
+    lm = np.where(plen > 64, np.uint64(2**64 - 1) << (128 - np.maximum(plen, 65)).astype(np.uint64),
+                  np.uint64(0))
+    hi &= hm
+    lo &= lm
+    hi[:100] = (hi[100:200] & np.uint64(0xFFFFFF0000000000)) | (hi[:100] & np.uint64(0xFFFFFFFFFF))
+    hi[:100] &= hm[:100]                                  # 100 slots with two long prefixes
+    cover_p = rng.integers(16, 24, 300)                   # shorter covering prefixes
+    cover_h = hi[200:500] & (np.uint64(2**64 - 1) << (64 - cover_p).astype(np.uint64))
+    all_hi = np.concatenate([hi, cover_h])
+    all_lo = np.concatenate([lo, np.zeros(300, np.uint64)])
+    all_p = np.concatenate([plen, cover_p])
+    nets = W.v6_nets(all_hi, all_lo, all_p)
+    rng.shuffle(nets)                                     # list order = priority
+    q = W.v6_lookups(all_hi, all_lo, all_p, 20000, 52, inside=1.0)
+    qb = np.concatenate([q] + [_flip(q[:3000], b) for b in (23, 24, 31, 39, 46, 47, 55, 62, 63, 64)])
+    got, stats = IC.route(nets, 6, qb)
+    want = O.rt_batch_v6_np(nets, qb, nthreads=4)
+    np.testing.assert_array_equal(got, want)
+    assert stats[0] == 16 and stats[2] > 500 and stats[1] > 0, stats
+    # 24-bit root: pad the table past 4096 rules with far-away /12s
+    pad = W.v6_nets(np.arange(4000, dtype=np.uint64) << np.uint64(52),
+                    np.zeros(4000, np.uint64), np.full(4000, 12))
+    big = np.concatenate([nets, pad])
+    got, stats = IC.route(big, 6, qb)
+    np.testing.assert_array_equal(got, O.rt_batch_v6_np(big, qb, nthreads=4))
+    assert stats[0] == 24 and stats[2] > 500, stats
+    # IPv4 with a 16-bit root: /17-/32 prefixes alone in their slot
+    p4 = rng.integers(17, 33, 2000)
+    n4 = rng.integers(0, 2**32, 2000, dtype=np.uint64).astype(np.uint32) & W._mask32(p4)
+    c4p = rng.integers(8, 17, 200)
+    c4 = n4[:200] & W._mask32(c4p)
+    v4n = W.v4_nets(np.concatenate([n4, c4]), np.concatenate([p4, c4p]))
+    rng.shuffle(v4n)
+    q4 = W.v4_lookups(np.concatenate([n4, c4]), np.concatenate([p4, c4p]), 20000, 53, inside=1.0)
+    q4 = np.concatenate([q4, q4 ^ np.uint32(1 << 15), q4 ^ np.uint32(1), q4 ^ np.uint32(1 << 8)])
+    got, stats = IC.route(v4n, 4, q4)
+    np.testing.assert_array_equal(got, O.rt_batch_v4_np(v4n, q4, nthreads=4))
+    assert stats[0] == 16 and stats[2] > 1000, stats
+
+
 def test_hint_random():
     groups, hosts, queries = hint_cases_random(np.random.default_rng(41), 800, 20000)
     arr, ng, keep = group_array(groups)

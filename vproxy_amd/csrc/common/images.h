@@ -9,6 +9,8 @@
 
 #define VC_NONE 0x7FFFFFFFu       // "no rule" in a value slot (-> -1 on output)
 #define VC_PTR  0x80000000u       // trie entry: child node pointer flag
+#define VC_ONE  0x40000000u       // with VC_PTR: one-prefix record (RouteImage)
+#define VC_ONE_MAX 0x40000000u    // record ids (16-byte units from the node base)
 
 // ---------------------------------------------------------------------------
 // ACL (SecurityGroup): one image per (protocol list, input family).
@@ -42,6 +44,12 @@ struct AclImage {
 // RouteTable: one multibit stride trie per family (DIR-24-8 for IPv4).
 // Root = 2^root_bits entries, every deeper node 256 entries (8-bit stride).
 // Entry: VC_PTR | node_id  -> child at nodes[(1<<root_bits) + node_id*256]
+//        VC_PTR | VC_ONE | id -> one-prefix record at ((uint4*)nodes)[id]:
+//                             {key bits 0-31, key bits 32-63, match value,
+//                              miss value (24 bits, 0xFFFFFF = none) | len << 24}
+//                             -- the entry's subtree holds one prefix of
+//                             length len <= 64; the answer is the match
+//                             value when the key's top len bits equal it
 //        otherwise value   -> min list index of the prefixes covering this
 //                             entry's address range (VC_NONE if none).
 // "min list index" is RouteTable.lookup's first-match (list order), not LPM.

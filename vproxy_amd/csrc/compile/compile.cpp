@@ -287,12 +287,34 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
         }
         for (auto& t : th) t.join();
     }
-    // 2) longer prefixes in ascending length: walk/create 8-bit nodes; a new
-    //    node inherits its parent entry's value (leaf pushing).
+    // 2) a root slot whose subtree holds exactly one longer prefix P (len <=
+    //    64) gets a one-prefix record instead of a chain of nodes: match ->
+    //    min(P's index, the slot's inherited value), miss -> inherited.  One
+    //    16-byte gather replaces up to five dependent node gathers (IPv6
+    //    /32-/64 prefixes under a 24-bit root).  The miss value is stored in
+    //    24 bits, so records need fewer than 0xFFFFFF rules.
+    std::unordered_map<uint32_t, uint32_t> per_slot;      // root slot -> long prefixes
+    per_slot.reserve(ps.size() - split);
+    for (size_t i = split; i < ps.size(); ++i)
+        ++per_slot[static_cast<uint32_t>(ps[i].key >> (128 - rb))];
+    const bool records_ok = n < 0xFFFFFF;
+    std::vector<uint32_t> rec_words, rec_slots;
+    // 3) the other longer prefixes in ascending length: walk/create 8-bit
+    //    nodes; a new node inherits its parent entry's value (leaf pushing).
     uint32_t n_children = 0;
     for (size_t i = split; i < ps.size(); ++i) {
         const P& p = ps[i];
         size_t entry = static_cast<size_t>(p.key >> (128 - rb));
+        if (records_ok && p.len <= 64 && per_slot[static_cast<uint32_t>(entry)] == 1) {
+            const uint32_t inh = out->nodes[entry];          // a value: no other long prefix here
+            const uint64_t khi = static_cast<uint64_t>(p.key >> 64);
+            rec_words.push_back(static_cast<uint32_t>(khi >> 32));
+            rec_words.push_back(static_cast<uint32_t>(khi));
+            rec_words.push_back(std::min(p.idx, inh));
+            rec_words.push_back((inh == VC_NONE ? 0xFFFFFFu : inh) | (uint32_t(p.len) << 24));
+            rec_slots.push_back(static_cast<uint32_t>(entry));
+            continue;
+        }
         int bits = rb;
         for (;;) {
             uint32_t v = out->nodes[entry];
@@ -318,6 +340,15 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
             bits = nb;
         }
     }
+    out->n_nodes = static_cast<int32_t>(n_children);
+    // records after the nodes (the node array is a multiple of 4 words, so
+    // they are 16-byte aligned); an entry addresses them in 16-byte units
+    const size_t base = out->nodes.size() / 4;
+    if (base + rec_slots.size() > VC_ONE_MAX) return VC_ENOMEM;
+    for (size_t k = 0; k < rec_slots.size(); ++k)
+        out->nodes[rec_slots[k]] = VC_PTR | VC_ONE | static_cast<uint32_t>(base + k);
+    out->nodes.insert(out->nodes.end(), rec_words.begin(), rec_words.end());
+    out->n_records = static_cast<int32_t>(rec_slots.size());
     return VC_OK;
 }
 

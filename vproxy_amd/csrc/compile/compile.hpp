@@ -31,10 +31,12 @@ int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_u
               int default_allow, AclBuilt* out);
 
 struct TrieBuilt {
-    std::vector<uint32_t> nodes;
+    std::vector<uint32_t> nodes;     // root, 256-entry nodes, then one-prefix records
     int32_t root_bits = 16;
     int32_t key_bits = 32;
     int32_t n_rules = 0;
+    int32_t n_nodes = 0;             // 256-entry nodes below the root
+    int32_t n_records = 0;           // one-prefix records (images.h VC_ONE)
 };
 
 // One RouteTable family list (list order = priority) -> stride trie.

@@ -225,7 +225,8 @@ __global__ __launch_bounds__(kBlock) void route_v4_kernel(
             int shift = 32 - rb;
             while (e[k] & VC_PTR) {
                 shift -= 8;
-                e[k] = nodes[(1u << rb) + (e[k] & ~VC_PTR) * 256u + ((key[k] >> shift) & 255u)];
+                e[k] = trie_next(nodes, 1u << rb, e[k], (key[k] >> shift) & 255u,
+                                 uint64_t(key[k]) << 32);
             }
         }
         int4 o;
@@ -274,9 +275,7 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (e[k] & VC_PTR) {
-                    const uint32_t sub = bits[k] < 64 ? uint32_t(hi[k] >> (56 - bits[k])) & 255u
-                                                      : uint32_t(lo[k] >> (120 - bits[k])) & 255u;
-                    e[k] = nodes[root + (e[k] & ~VC_PTR) * 256u + sub];
+                    e[k] = trie_next(nodes, root, e[k], v6_sub(hi[k], lo[k], bits[k]), hi[k]);
                     bits[k] += 8;
                     any = true;
                 }
@@ -360,7 +359,7 @@ __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, u
     int shift = 32 - rb;
     while (e & VC_PTR) {
         shift -= 8;
-        e = nodes[(1u << rb) + (e & ~VC_PTR) * 256u + ((d >> shift) & 255u)];
+        e = trie_next(nodes, 1u << rb, e, (d >> shift) & 255u, uint64_t(d) << 32);
     }
     return e;
 }
@@ -370,9 +369,7 @@ __device__ __forceinline__ uint32_t route6_chase(const uint32_t* nodes, int rb, 
     int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
-        const uint32_t sub = bits < 64 ? uint32_t(hi >> (56 - bits)) & 255u
-                                       : uint32_t(lo >> (120 - bits)) & 255u;
-        e = nodes[root + (e & ~VC_PTR) * 256u + sub];
+        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits), hi);
         bits += 8;
     }
     return e;

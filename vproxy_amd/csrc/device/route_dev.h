@@ -1,13 +1,33 @@
 // route_dev.h -- device side of RouteTable.lookup (RouteTable.java:44-59).
 //
 // Walks the leaf-pushed stride trie: root entry, then at most one 8-bit node
-// per remaining byte of the prefix.  Every entry holds the min list index of
-// the prefixes covering it, so the last entry reached is the answer.
+// per remaining byte of the prefix, or one 16-byte one-prefix record where
+// the subtree holds a single prefix (images.h VC_ONE).  Every entry holds the
+// min list index of the prefixes covering it, so the last entry reached is
+// the answer.
 #pragma once
 
 #include "dev_common.h"
 
 namespace vcd {
+
+// One-prefix record: the key's top bits (hi = key bits 0-63, left-aligned)
+// against the record's prefix.
+VC_HD uint32_t one_match(uint4 r, uint64_t hi) {
+    const uint32_t len = r.w >> 24;                        // rb < len <= 64
+    const uint64_t key = (uint64_t(r.x) << 32) | r.y;
+    const uint32_t miss = r.w & 0xFFFFFFu;
+    if (((hi ^ key) >> (64 - len)) == 0) return r.z;
+    return miss == 0xFFFFFFu ? VC_NONE : miss;
+}
+
+// Next entry below pointer entry e: the child node's entry `sub`, or the
+// record's answer (never a pointer, so the walk ends).
+VC_HD uint32_t trie_next(const uint32_t* nodes, uint32_t root, uint32_t e, uint32_t sub,
+                         uint64_t hi) {
+    if (e & VC_ONE) return one_match(reinterpret_cast<const uint4*>(nodes)[e & ~(VC_PTR | VC_ONE)], hi);
+    return nodes[root + (e & ~VC_PTR) * 256u + sub];
+}
 
 VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
     uint32_t e = nodes[key >> (32 - rb)];
@@ -15,9 +35,13 @@ VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
         shift -= 8;
-        e = nodes[root + (e & ~VC_PTR) * 256u + ((key >> shift) & 255u)];
+        e = trie_next(nodes, root, e, (key >> shift) & 255u, uint64_t(key) << 32);
     }
     return e;
+}
+
+VC_HD uint32_t v6_sub(uint64_t hi, uint64_t lo, int bits) {
+    return bits < 64 ? uint32_t(hi >> (56 - bits)) & 255u : uint32_t(lo >> (120 - bits)) & 255u;
 }
 
 VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo) {
@@ -25,9 +49,7 @@ VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo) 
     int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
-        uint32_t sub = bits < 64 ? uint32_t(hi >> (56 - bits)) & 255u
-                                 : uint32_t(lo >> (120 - bits)) & 255u;
-        e = nodes[root + (e & ~VC_PTR) * 256u + sub];
+        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits), hi);
         bits += 8;
     }
     return e;
