@@ -26,19 +26,33 @@ constexpr int kBlock = 512;
 constexpr int kPipeBlock = 1024;
 
 // ---------------------------------------------------------------------------
-// ACL (SecurityGroup.allow) on IPv4 sources
+// ACL (SecurityGroup.allow) on IPv4 sources.  The boundaries of both lists
+// are staged in LDS; when they exceed the LDS budget, every (1 << shift)-th
+// boundary is staged as a fence and the search finishes in one block of
+// 1 << shift boundaries in global memory (the same two levels as IPv6).
 // ---------------------------------------------------------------------------
 struct AclV4Ctx {
-    const uint32_t* b[2];
+    const uint32_t* f[2];          // LDS: every boundary (shift 0) or the fences
+    const uint32_t* b[2];          // global boundaries
     const uint32_t* desc[2];
     const uint32_t* pieces[2];
-    int nb[2];
+    int nf[2], nb[2];
+    int shift;                     // uniform per launch
 };
+
+__device__ __forceinline__ int fence_count(int nb, int shift) {
+    return (nb + (1 << shift) - 1) >> shift;
+}
 
 __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint32_t key,
                                                uint32_t port) {
     const int l = tcp ? 0 : 1;
-    const int j = bsearch_u32(a.b[l], a.nb[l], key);
+    int j = bsearch_u32(a.f[l], a.nf[l], key);
+    if (a.shift) {
+        const int base = j << a.shift;
+        const int rest = a.nb[l] - base;
+        j = base + bsearch_u32(a.b[l] + base, rest < (1 << a.shift) ? rest : (1 << a.shift), key);
+    }
     const uint2 d = load_desc(a.desc[l], j);
     return port_lookup(a.pieces[l], d, port);
 }
@@ -52,36 +66,49 @@ __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t
     }
 }
 
-__device__ __forceinline__ AclV4Ctx acl_v4_ctx(const AclImage& img, const uint32_t* lds) {
+// lds: the staged boundaries or fences (stage_bounds), or null: one-level
+// search of the global boundaries
+__device__ __forceinline__ AclV4Ctx acl_v4_ctx(const AclImage& img, const uint32_t* lds,
+                                               int shift) {
     AclV4Ctx a;
-    a.nb[0] = img.fam[0][0].nb;
-    a.nb[1] = img.fam[1][0].nb;
-    a.b[0] = lds ? lds : img.fam[0][0].bounds4;
-    a.b[1] = lds ? lds + a.nb[0] : img.fam[1][0].bounds4;
-    a.desc[0] = img.fam[0][0].desc;
-    a.desc[1] = img.fam[1][0].desc;
-    a.pieces[0] = img.fam[0][0].pieces;
-    a.pieces[1] = img.fam[1][0].pieces;
+    a.shift = lds ? shift : 0;
+    int off = 0;
+    for (int l = 0; l < 2; ++l) {
+        const AclFamilyImage& f = img.fam[l][0];
+        a.nb[l] = f.nb;
+        a.nf[l] = fence_count(f.nb, a.shift);
+        a.b[l] = f.bounds4;
+        a.f[l] = lds ? lds + off : f.bounds4;
+        a.desc[l] = f.desc;
+        a.pieces[l] = f.pieces;
+        off += a.nf[l];
+    }
     return a;
 }
 
-__device__ __forceinline__ void stage_bounds(const AclImage& img, uint32_t* lds) {
-    const int nb0 = img.fam[0][0].nb, nb1 = img.fam[1][0].nb;
+// LDS words stage_bounds fills
+__device__ __forceinline__ int staged_words(const AclImage& img, int shift) {
+    return fence_count(img.fam[0][0].nb, shift) + fence_count(img.fam[1][0].nb, shift);
+}
+
+__device__ __forceinline__ void stage_bounds(const AclImage& img, uint32_t* lds, int shift) {
+    const int nf0 = fence_count(img.fam[0][0].nb, shift);
+    const int nf1 = fence_count(img.fam[1][0].nb, shift);
     const uint32_t* b0 = img.fam[0][0].bounds4;
     const uint32_t* b1 = img.fam[1][0].bounds4;
-    for (int k = threadIdx.x; k < nb0; k += blockDim.x) lds[k] = b0[k];
-    for (int k = threadIdx.x; k < nb1; k += blockDim.x) lds[nb0 + k] = b1[k];
+    for (int k = threadIdx.x; k < nf0; k += blockDim.x) lds[k] = b0[int64_t(k) << shift];
+    for (int k = threadIdx.x; k < nf1; k += blockDim.x) lds[nf0 + k] = b1[int64_t(k) << shift];
     __syncthreads();
 }
 
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
-    AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
+    AclImage img, int shift, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
     uint8_t* __restrict__ allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    if (kLds) stage_bounds(img, lds);
-    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    if (kLds) stage_bounds(img, lds, shift);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr, shift);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     const int64_t n4 = n >> 2;
     for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
@@ -121,12 +148,12 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
 // Unaligned-pointer variant: one item per lane.
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
-    AclImage img, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
+    AclImage img, int shift, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
     uint8_t* __restrict__ allow) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    if (kLds) stage_bounds(img, lds);
-    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    if (kLds) stage_bounds(img, lds, shift);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr, shift);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
@@ -150,10 +177,6 @@ struct AclV6Ctx {
     int nf[2], nb[2];
     int shift;
 };
-
-__device__ __forceinline__ int fence_count(int nb, int shift) {
-    return (nb + (1 << shift) - 1) >> shift;
-}
 
 // Stages the fences of both lists at lds (16-byte aligned); the caller syncs.
 __device__ __forceinline__ AclV6Ctx stage_fences(const AclImage& img, uint64_t* lds, int shift) {
@@ -470,8 +493,8 @@ struct PipeLds {
 
 template <bool kLds, bool kCount>
 __device__ __forceinline__ PipeLds pipe_lds_setup(const AclImage& img, const PipeCount& pc,
-                                                  uint32_t* lds, uint32_t* tally) {
-    const int words = kLds ? img.fam[0][0].nb + img.fam[1][0].nb : 0;
+                                                  uint32_t* lds, uint32_t* tally, int shift) {
+    const int words = kLds ? staged_words(img, shift) : 0;
     PipeLds L;
     L.ah = lds + words;
     L.rc = L.ah + (pc.acl ? pc.acl_bins : 0);
@@ -482,7 +505,7 @@ __device__ __forceinline__ PipeLds pipe_lds_setup(const AclImage& img, const Pip
         for (int k = threadIdx.x; k < cw; k += blockDim.x) L.ah[k] = 0;
         if (threadIdx.x < 5) tally[threadIdx.x] = 0;
     }
-    if (kLds) stage_bounds(img, lds);
+    if (kLds) stage_bounds(img, lds, shift);
     else if (kCount) __syncthreads();
     return L;
 }
@@ -529,11 +552,11 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     const uint16_t* __restrict__ dport, const uint32_t* __restrict__ host_id,
     const int32_t* __restrict__ pool_group, int64_t n_pool, int64_t n,
     int32_t* __restrict__ out_acl, int32_t* __restrict__ out_route,
-    int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow, PipeCount pc) {
+    int32_t* __restrict__ out_group, uint8_t* __restrict__ out_allow, PipeCount pc, int shift) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t tally[5];
-    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally);
-    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally, shift);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr, shift);
     int64_t lo, hi;
     pipe_slice(n, &lo, &hi);
     PipeTally t;
@@ -682,15 +705,16 @@ template <bool kLds, bool kVec, bool kCount>
 __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, PipeTries tr,
                                                                    PipeIn in, int64_t n,
                                                                    PipeOut out, PipeCount pc,
-                                                                   int fshift, int fence_words) {
+                                                                   int fshift, int fence_words,
+                                                                   int shift) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t tally[5];
     __shared__ uint8_t q6[kPipeWaves][256];        // queued IPv6 packets: lane * 4 + slot
     __shared__ uint32_t r6[kPipeWaves][64][2];     // per round: ACL value, route entry
     const AclV6Ctx a6 = stage_fences(img, reinterpret_cast<uint64_t*>(lds + fence_words), fshift);
-    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally);
+    const PipeLds L = pipe_lds_setup<kLds, kCount>(img, pc, lds, tally, shift);
     __syncthreads();
-    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr);
+    const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr, shift);
     int64_t lo, hi;
     pipe_slice(n, &lo, &hi);
     PipeTally t;
@@ -811,11 +835,24 @@ namespace vc {
 
 namespace {
 
-// LDS budget for the staged v4 ACL boundaries (words); above it the kernel
-// searches the boundaries in global memory (L2-resident).
+// LDS budget for the staged v4 ACL boundaries (words); above it every
+// (1 << shift)-th boundary is staged as a fence (acl_v4_one).
 constexpr int kLdsWords = 30 * 1024;
 
 int vcd_fences(int nb, int shift) { return (nb + (1 << shift) - 1) >> shift; }
+
+// Smallest fence shift whose staged v4 words fit `words`.
+int v4_fence_shift(const AclImage& img, size_t words) {
+    int shift = 0;
+    while (size_t(vcd_fences(img.fam[0][0].nb, shift) + vcd_fences(img.fam[1][0].nb, shift)) >
+               words && shift < 30)
+        ++shift;
+    return shift;
+}
+
+int v4_staged_words(const AclImage& img, int shift) {
+    return vcd_fences(img.fam[0][0].nb, shift) + vcd_fences(img.fam[1][0].nb, shift);
+}
 
 }  // namespace
 
@@ -877,31 +914,22 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
                          const uint32_t* src4, const uint16_t* port, int64_t n, int32_t* out,
                          uint8_t* allow, unsigned long long* counters) {
     if (n <= 0) return hipSuccess;
-    const int words = img.fam[0][0].nb + img.fam[1][0].nb;
-    const bool lds = words <= kLdsWords;
-    const size_t shmem = lds ? size_t(words) * 4 : 0;
+    const int shift = v4_fence_shift(img, kLdsWords);
+    const int words = v4_staged_words(img, shift);
+    const size_t shmem = size_t(words) * 4;
     const bool vec = aligned(proto, 4) && aligned(src4, 16) && aligned(port, 8) &&
                      aligned(out, 16) && (!allow || aligned(allow, 4));
-    const int per_cu = lds ? (words <= 16 * 1024 ? 4 : 2) : 8;
+    const int per_cu = words <= 16 * 1024 ? 4 : 2;
     if (vec) {
         const int grid = grid_for(c, (n + 3) / 4, per_cu);
-        if (lds) {
-            if (hipError_t e = allow_lds(vcd::acl_v4_kernel<true>)) return e;
-            hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
-                               c.stream, img, proto, src4, port, n, out, allow);
-        } else {
-            hipLaunchKernelGGL(vcd::acl_v4_kernel<false>, dim3(grid), dim3(vcd::kBlock), 0,
-                               c.stream, img, proto, src4, port, n, out, allow);
-        }
+        if (hipError_t e = allow_lds(vcd::acl_v4_kernel<true>)) return e;
+        hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
+                           c.stream, img, shift, proto, src4, port, n, out, allow);
     } else {
         const int grid = grid_for(c, n, per_cu);
-        if (lds) {
-            if (hipError_t e = allow_lds(vcd::acl_v4_kernel_scalar<true>)) return e;
-            hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
-                               shmem, c.stream, img, proto, src4, port, n, out, allow);
-        } else
-            hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<false>, dim3(grid), dim3(vcd::kBlock), 0,
-                               c.stream, img, proto, src4, port, n, out, allow);
+        if (hipError_t e = allow_lds(vcd::acl_v4_kernel_scalar<true>)) return e;
+        hipLaunchKernelGGL(vcd::acl_v4_kernel_scalar<true>, dim3(grid), dim3(vcd::kBlock),
+                           shmem, c.stream, img, shift, proto, src4, port, n, out, allow);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
@@ -975,8 +1003,9 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     const int fshift = mix ? v6_fence_shift(acl) : 0;
     const size_t fbytes = mix ? v6_fence_bytes(acl, fshift) : 0;
     const size_t lds_max = mix ? kLdsMax - kMixStatic - fbytes : kLdsMax;
-    const int words = acl.fam[0][0].nb + acl.fam[1][0].nb;
-    const bool lds = words <= kLdsWords && size_t(words) * 4 <= lds_max;
+    // v4 boundaries (or their fences) always staged; the counts fit after
+    const int shift = v4_fence_shift(acl, std::min<size_t>(kLdsWords, lds_max / 4));
+    const int words = v4_staged_words(acl, shift);
     bool vec = aligned(p.proto, 4) && aligned(p.src4, 16) && aligned(p.dst4, 16) &&
                aligned(p.dport, 8) && aligned(p.host_id, 16) && aligned(p.out_acl, 16) &&
                aligned(p.out_route, 16) && aligned(p.out_group, 16) &&
@@ -986,7 +1015,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
     // In-kernel counting where it fits the workgroup's LDS; the rest is
     // counted by separate passes over the outputs afterwards.
-    size_t shmem = lds ? size_t(words) * 4 : 0;
+    size_t shmem = size_t(words) * 4;
     vcd::PipeCount pc{};
     pc.bw_shift = big_hist_bucket_shift();
     pc.n4 = n4;
@@ -1043,7 +1072,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
         hipLaunchKernelGGL((vcd::pipeline_v4_kernel<L, V, K>), dim3(grid),                         \
                            dim3(vcd::kPipeBlock), shmem, c.stream, acl, r4.nodes, r4.root_bits,   \
                            p.proto, p.src4, p.dst4, p.dport, p.host_id, p.pool_group, p.n_pool,    \
-                           n, p.out_acl, p.out_route, p.out_group, p.out_allow, pc);               \
+                           n, p.out_acl, p.out_route, p.out_group, p.out_allow, pc, shift);        \
     } while (0)
 #define VC_MIX(L, V, K)                                                                            \
     do {                                                                                           \
@@ -1052,19 +1081,15 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
         if (e != hipSuccess) break;                                                                \
         hipLaunchKernelGGL((vcd::pipeline_mix_kernel<L, V, K>), dim3(grid),                        \
                            dim3(vcd::kPipeBlock), shmem, c.stream, acl, tr, in, n, out, pc,        \
-                           fshift, fence_words);                                                   \
+                           fshift, fence_words, shift);                                            \
     } while (0)
         if (!mix) {
             if (count) {
-                if (lds && vec) VC_PIPE(true, true, true);
-                else if (lds) VC_PIPE(true, false, true);
-                else if (vec) VC_PIPE(false, true, true);
-                else VC_PIPE(false, false, true);
+                if (vec) VC_PIPE(true, true, true);
+                else VC_PIPE(true, false, true);
             } else {
-                if (lds && vec) VC_PIPE(true, true, false);
-                else if (lds) VC_PIPE(true, false, false);
-                else if (vec) VC_PIPE(false, true, false);
-                else VC_PIPE(false, false, false);
+                if (vec) VC_PIPE(true, true, false);
+                else VC_PIPE(true, false, false);
             }
         } else {
             const vcd::PipeTries tr{route.fam[0].nodes, route.fam[1].nodes, route.fam[0].root_bits,
@@ -1073,15 +1098,11 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
                                  p.dport, p.host_id, p.pool_group, p.n_pool};
             const vcd::PipeOut out{p.out_acl, p.out_route, p.out_group, p.out_allow};
             if (count) {
-                if (lds && vec) VC_MIX(true, true, true);
-                else if (lds) VC_MIX(true, false, true);
-                else if (vec) VC_MIX(false, true, true);
-                else VC_MIX(false, false, true);
+                if (vec) VC_MIX(true, true, true);
+                else VC_MIX(true, false, true);
             } else {
-                if (lds && vec) VC_MIX(true, true, false);
-                else if (lds) VC_MIX(true, false, false);
-                else if (vec) VC_MIX(false, true, false);
-                else VC_MIX(false, false, false);
+                if (vec) VC_MIX(true, true, false);
+                else VC_MIX(true, false, false);
             }
         }
 #undef VC_PIPE
