@@ -4,9 +4,11 @@
  *
  * Each batched entry point replaces one Java hot-path method (paths relative
  * to the nintha/vproxy tree).  The JNI shim a maintainer would add on the Java
- * side is shown in INTEGRATION.md; it maps 1:1 onto these functions in the
+ * side is jni/vproxy_component_secure_GpuClassifier.c (+ jni/GpuClassifier.java,
+ * walked through in INTEGRATION.md); it maps 1:1 onto these functions in the
  * style of base/src/main/c/vfd_posix_GeneralPosix.c (jlong handles, direct
  * ByteBuffers, status codes mapped to IOException/UnsupportedOperationException).
+ * tests/native/abi_c.c is a plain C99 consumer of this header.
  *
  * Conventions
  *  - Plain C types only.  Every function returns an int status (VC_OK = 0,
@@ -15,8 +17,9 @@
  *    null / "no rule" (the caller maps index -> SecurityGroupRule / RouteRule
  *    / ServerGroupHandle exactly as the Java code would have returned it).
  *  - *_dev functions take DEVICE pointers and a hipStream_t (passed as void*,
- *    NULL = HIP's null stream); they are asynchronous and ordered on it.  The plain variants
- *    take HOST pointers and are synchronous (H2D + kernel + D2H).
+ *    NULL = HIP's null stream); they are asynchronous and ordered on it.  The
+ *    plain variants take HOST pointers and are synchronous (H2D + kernel +
+ *    D2H, or zero-copy over buffers registered with vc_host_register).
  *  - IPv4 addresses are uint32 in IP.ipv4Bytes2Int order (big-endian value,
  *    vfd/IP.java:476-478); IPv6 addresses are 16 raw bytes per item.
  *  - Strings are packed in a byte blob with uint32 offsets (n+1 entries, item
@@ -34,8 +37,9 @@
  *    The exception is DNS: qnames are the wire bytes Formatter.parseDomainName
  *    produces (base/.../dns/Formatter.java:225-257 makes one char per byte,
  *    ISO-8859-1): a qname byte 0xE9 is the char U+00E9 and matches the
- *    annotation bytes C3 A9, as in Java.  vc_compile_hosts_text reads the hosts file as UTF-8, as
- *    Resolver.getHosts' InputStreamReader does with a UTF-8 default charset.
+ *    annotation bytes C3 A9, as in Java.  vc_compile_hosts_text reads the
+ *    hosts file as UTF-8, as Resolver.getHosts' InputStreamReader does with a
+ *    UTF-8 default charset.
  *  - Rule tables are compiled into immutable snapshots and published
  *    atomically; concurrent classify calls keep using the snapshot they
  *    started with (threads: SURVEY.md §8(b) "Threading").
