@@ -397,15 +397,18 @@ def cpu_info():
             "threads_all": max(1, min(share, avail, 64))}
 
 
-def cpu_rates(run, unit, budget_s, what, note=None):
+def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
     """Time `run(n, threads) -> seconds` on a bounded sample: all-core (the
-    box's CPU share) and 1 core, each sized to about `budget_s` seconds."""
+    box's CPU share) and 1 core, each sized to about `budget_s` seconds and
+    at most `cap` items (the sample the caller holds)."""
     info = cpu_info()
     res = {}
     for threads in (info["threads_all"], 1):
         probe = max(threads * 4, 64)
         t = run(probe, threads)
         n = int(max(probe, probe * budget_s / max(t, 1e-6)))
+        if cap:
+            n = min(n, cap)
         t = run(n, threads)
         res[threads] = (n, t)
     na, ta = res[info["threads_all"]]
@@ -418,6 +421,12 @@ def cpu_rates(run, unit, budget_s, what, note=None):
     if note:
         out["note"] = note
     return out
+
+
+def sample_blob(blob, off, idx):
+    """Host blob + uint32 offsets of strings[idx] (a CPU-baseline sample)."""
+    b, o, _ = gather_strings_dev(blob, off, np.asarray(idx), "cpu")
+    return b.numpy(), o.numpy().view(np.uint32)
 
 
 def _oracle():
@@ -831,27 +840,19 @@ def sub_bench(args, clf, dev, rank, world):
             oh = O.Hosts(O.hosts_parse(hosts)[0]) if dns else None
 
             def run(k, threads):
-                sub = [names[i] for i in pidx[:k]]
-                if dns:
-                    t0 = time.perf_counter()
-                    for q in sub:
-                        O.dns_classify(oh, og, q)
-                    return (time.perf_counter() - t0) / max(1, threads) * threads
-                sb, so = W.pack(sub)
+                sb, so = sample_blob(nblob, noff, pidx[:k])
                 t0 = time.perf_counter()
-                O.hint_batch_np(og, sb, so, None, nthreads=threads)
+                if dns:
+                    O.dns_batch_np(oh, og, sb, so, nthreads=threads)
+                else:
+                    O.hint_batch_np(og, sb, so, None, nthreads=threads)
                 return time.perf_counter() - t0
             if dns:
-                info = cpu_info()
-                k = 2000
-                tt = run(k, 1)
-                cpu = {"value": k / tt / 1e6, "unit": "M items/s", "cores": 1, "kind": "port",
-                       "sample": "%d qnames of the DNS workload, oracle hosts lookup + "
-                                 "searchForGroup scan over 100k groups, 1 thread" % k,
-                       "nproc": info["nproc"], "cpu_model": info["cpu_model"]}
+                cpu = cpu_rates(run, "M items/s", 4.0, "qnames of the DNS workload, oracle hosts "
+                                "lookup (50k entries) + searchForGroup scan over 100k groups", cap=n)
             else:
                 cpu = cpu_rates(run, "M items/s", 4.0, "hostnames of the C4 pool, oracle "
-                                "searchForGroup scan over 100k groups")
+                                "searchForGroup scan over 100k groups", cap=n)
     elif args.workload == "sni":
         _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
         holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]
@@ -866,6 +867,16 @@ def sub_bench(args, clf, dev, rank, world):
             clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), None, n,
             C.c_void_p(out.data_ptr()), S()))
         per_unit, unit, kern = nbytes / n + 8, "B/SNI (bytes + 4 offset + 4 out)", "cert_kernel"
+        if O is not None:
+            oc = O.Certs(holders)
+
+            def run(k, threads):
+                sb, so = sample_blob(nblob, noff, pidx[:k])
+                t0 = time.perf_counter()
+                O.cert_batch_np(oc, sb, so, nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 3.0, "SNIs of the workload, oracle "
+                            "SSLContextHolder.choose scan over 100k holders (200k names)", cap=n)
     elif args.workload in ("parse", "mirror", "switch"):
         frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
         fblob, foff = W.pack(frames)
@@ -883,6 +894,14 @@ def sub_bench(args, clf, dev, rank, world):
             per_unit = nbytes / n + 4 + 54
             unit = "B/frame (frame bytes + 4 offset in; 54 B of SoA fields out)"
             kern = "packet_kernel"
+            if O is not None:
+                def run(k, threads):
+                    sb, so = sample_blob(fblob, foff, pidx[:k])
+                    t0 = time.perf_counter()
+                    O.parse_batch_np(sb, so, 0, nthreads=threads)
+                    return time.perf_counter() - t0
+                cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle vpacket "
+                                "parse chain (VXLAN -> Ethernet -> IPv4/IPv6 -> TCP/ICMP)", cap=n)
         elif args.workload == "switch":
             # parse + bare-VXLAN ACL on the sender + inner route, one kernel,
             # over the C5 SecurityGroup and route tables; only the route
@@ -902,6 +921,18 @@ def sub_bench(args, clf, dev, rank, world):
             unit = ("B/datagram (frame bytes + 4 offset + 4 sender in; 4 route + 1 verdict out), "
                     "10k-rule SecurityGroup, 980,848 + 200,000 routes")
             kern = "switch_kernel"
+            if O is not None:
+                r4h = r4[:1 << 20].cpu().numpy().view(np.uint32)
+
+                def run(k, threads):
+                    sb, so = sample_blob(fblob, foff, pidx[:k])
+                    t0 = time.perf_counter()
+                    O.switch_batch_np(t.tcp, t.udp, False, sb, so, r4h[:k], 4789, t.v4_list,
+                                      t.v6_list, nthreads=threads)
+                    return time.perf_counter() - t0
+                cpu = cpu_rates(run, "M items/s", 4.0, "datagrams of the workload, oracle parse + "
+                                "SecurityGroup.allow scan + RouteTable.lookup scan of the inner "
+                                "destination", cap=1 << 20)
         else:
             filters = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
                         "network2": "10.0.0.0/8"} for i in range(16)] + \
@@ -915,6 +946,18 @@ def sub_bench(args, clf, dev, rank, world):
             per_unit = nbytes / n + 4 + 8
             unit = "B/frame (frame bytes + 4 offset in; 8 B mirror set out), 17 filters"
             kern = "mirror_switch_kernel"
+            if O is not None:
+                ids = {}
+                oarr = O.mirror_filters(filters, ids)
+
+                def run(k, threads):
+                    sb, so = sample_blob(fblob, foff, pidx[:k])
+                    t0 = time.perf_counter()
+                    O.mirror_switch_batch_np(oarr, len(filters), ids["switch"], sb, so, 0,
+                                             nthreads=threads)
+                    return time.perf_counter() - t0
+                cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle "
+                                "Mirror.switchPacket over the 17 filters", cap=n)
     elif args.workload == "source":
         rng = np.random.default_rng(W.SEED + 14)
         groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
@@ -930,6 +973,18 @@ def sub_bench(args, clf, dev, rank, world):
             clf.h, C.c_void_p(grp.data_ptr()), C.c_void_p(src.data_ptr()), n, 0,
             C.c_void_p(out.data_ptr()), S()))
         per_unit, unit, kern = 12, "B/item (group 4 + v4 source 4 in, 4 out)", "source_v4_kernel"
+        if O is not None:
+            gh = grp[:1 << 22].cpu().numpy()
+            sh = src[:1 << 22].cpu().numpy().view(np.uint32)
+            osg = O.SourceGroups(groups)
+
+            def run(k, threads):
+                t0 = time.perf_counter()
+                O.source_batch_np(osg, 0, gh[:k], sh[:k], nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 3.0, "clients of the workload, oracle "
+                            "sourceHashGet over each group's sourceReset order (built once per "
+                            "call for all 10k groups, as Java caches it per group)", cap=1 << 22)
     else:
         return mix_bench(args, clf, dev, rank, O)
     el, ms = _time(fn, args.steps, args.warmup)

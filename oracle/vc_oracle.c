@@ -1350,3 +1350,170 @@ uint64_t vo_mirror_switch(const vo_mirror_filter *f, int n, int origin, const ui
     }
     return m;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Batched forms (pthread partitions) -- checkers and bench cpu_baseline     */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const vo_hosts *hosts; const vo_group *g; int ng;
+    const uint8_t *blob; const uint32_t *off; uint8_t *kind; int32_t *value;
+} dns_batch_ctx;
+
+static void dns_range(void *p, int64_t lo, int64_t hi)
+{
+    dns_batch_ctx *c = (dns_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        int32_t v = 0;
+        const int k = vo_dns_classify(c->hosts, c->g, c->ng, (const char *)c->blob + c->off[i],
+                                      (int)(c->off[i + 1] - c->off[i]), &v);
+        c->kind[i] = (uint8_t)k;
+        c->value[i] = v;
+    }
+}
+
+void vo_dns_batch(const vo_hosts *hosts, const vo_group *g, int ng, const uint8_t *blob,
+                  const uint32_t *off, int64_t n, uint8_t *kind, int32_t *value, int nthreads)
+{
+    dns_batch_ctx c = {hosts, g, ng, blob, off, kind, value};
+    parallel_for(n, nthreads, dns_range, &c);
+}
+
+typedef struct { const uint8_t *blob; const uint32_t *off; int layer; vo_pkt *out; } parse_batch_ctx;
+
+static void parse_range(void *p, int64_t lo, int64_t hi)
+{
+    parse_batch_ctx *c = (parse_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i)
+        vo_parse_packet(c->blob + c->off[i], (int)(c->off[i + 1] - c->off[i]), c->layer, &c->out[i]);
+}
+
+void vo_parse_batch(const uint8_t *blob, const uint32_t *off, int64_t n, int layer, vo_pkt *out,
+                    int nthreads)
+{
+    parse_batch_ctx c = {blob, off, layer, out};
+    parallel_for(n, nthreads, parse_range, &c);
+}
+
+typedef struct {
+    const vo_sg_rule *tcp; int ntcp; const vo_sg_rule *udp; int nudp; int dflt;
+    const uint8_t *blob; const uint32_t *off; const uint32_t *remote4; int bind_port;
+    const vo_net *v4; int n4; const vo_net *v6; int n6;
+    int32_t *acl; uint8_t *allow; int32_t *route;
+} switch_batch_ctx;
+
+static void switch_range(void *p, int64_t lo, int64_t hi)
+{
+    switch_batch_ctx *c = (switch_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        const uint32_t r = c->remote4[i];
+        const uint8_t rb[4] = {(uint8_t)(r >> 24), (uint8_t)(r >> 16), (uint8_t)(r >> 8), (uint8_t)r};
+        int verdict = 0;
+        const int a = vo_sg_allow(c->tcp, c->ntcp, c->udp, c->nudp, c->dflt, 17, rb, 4,
+                                  c->bind_port, &verdict);
+        if (c->acl) c->acl[i] = a;
+        if (c->allow) c->allow[i] = (uint8_t)verdict;
+        vo_pkt pk;
+        vo_parse_packet(c->blob + c->off[i], (int)(c->off[i + 1] - c->off[i]), 0, &pk);
+        int32_t rt = -1;
+        if (verdict && pk.status == 0 && (pk.l3 == 4 || pk.l3 == 6))
+            rt = pk.l3 == 4 ? vo_rt_lookup_list(c->v4, c->n4, pk.dst, 4)
+                            : vo_rt_lookup_list(c->v6, c->n6, pk.dst, 16);
+        c->route[i] = rt;
+    }
+}
+
+void vo_switch_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                     int default_allow, const uint8_t *blob, const uint32_t *off, int64_t n,
+                     const uint32_t *remote4, int bind_port, const vo_net *v4, int n4,
+                     const vo_net *v6, int n6, int32_t *acl, uint8_t *allow, int32_t *route,
+                     int nthreads)
+{
+    switch_batch_ctx c = {tcp, ntcp, udp, nudp, default_allow, blob, off, remote4, bind_port,
+                          v4, n4, v6, n6, acl, allow, route};
+    parallel_for(n, nthreads, switch_range, &c);
+}
+
+typedef struct {
+    const char *const *names; const int32_t *lens; const int32_t *holder; int n_names, n_holders;
+    const uint8_t *blob; const uint32_t *off; const uint8_t *sni_null; int32_t *out;
+} cert_batch_ctx;
+
+static void cert_range(void *p, int64_t lo, int64_t hi)
+{
+    cert_batch_ctx *c = (cert_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i)
+        c->out[i] = vo_cert_choose(c->names, c->lens, c->holder, c->n_names, c->n_holders,
+                                   c->blob + c->off[i], (int)(c->off[i + 1] - c->off[i]),
+                                   c->sni_null ? c->sni_null[i] : 0);
+}
+
+void vo_cert_batch(const char *const *names, const int32_t *name_lens, const int32_t *holder,
+                   int n_names, int n_holders, const uint8_t *blob, const uint32_t *off,
+                   const uint8_t *sni_null, int64_t n, int32_t *out, int nthreads)
+{
+    cert_batch_ctx c = {names, name_lens, holder, n_names, n_holders, blob, off, sni_null, out};
+    parallel_for(n, nthreads, cert_range, &c);
+}
+
+typedef struct {
+    const vo_mirror_filter *f; int nf, origin, layer;
+    const uint8_t *blob; const uint32_t *off; uint64_t *out;
+} mirror_batch_ctx;
+
+static void mirror_range(void *p, int64_t lo, int64_t hi)
+{
+    mirror_batch_ctx *c = (mirror_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i)
+        c->out[i] = vo_mirror_switch(c->f, c->nf, c->origin, c->blob + c->off[i],
+                                     (int)(c->off[i + 1] - c->off[i]), c->layer);
+}
+
+void vo_mirror_switch_batch(const vo_mirror_filter *f, int nf, int origin, const uint8_t *blob,
+                            const uint32_t *off, int64_t n, int layer, uint64_t *out, int nthreads)
+{
+    mirror_batch_ctx c = {f, nf, origin, layer, blob, off, out};
+    parallel_for(n, nthreads, mirror_range, &c);
+}
+
+typedef struct {
+    const vo_server *servers; const int32_t *goff; const int32_t *order; const int32_t *size;
+    const int32_t *grp; const uint32_t *src4; int32_t *out;
+} source_batch_ctx;
+
+static void source_range(void *p, int64_t lo, int64_t hi)
+{
+    source_batch_ctx *c = (source_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int g = c->grp[i];
+        const int32_t *ord = c->order + c->goff[g];
+        const int size = c->size[g];
+        const uint32_t s = c->src4[i];
+        const uint8_t sb[4] = {(uint8_t)(s >> 24), (uint8_t)(s >> 16), (uint8_t)(s >> 8), (uint8_t)s};
+        int32_t hash = vo_source_hash(sb, 4);
+        int result = -1;
+        for (int recurse = 0; recurse < size; ++recurse) {      /* ServerGroup.java:480-489 */
+            const int idx = hash % size;
+            if (c->servers[c->goff[g] + ord[idx]].healthy) {
+                result = ord[idx];
+                break;
+            }
+            hash = idx + 1;
+        }
+        c->out[i] = result;
+    }
+}
+
+void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups, int view,
+                     const int32_t *grp, const uint32_t *src4, int64_t n, int32_t *out,
+                     int nthreads)
+{
+    const int total = n_groups > 0 ? goff[n_groups] : 0;
+    int32_t *order = (int32_t *)malloc(sizeof(int32_t) * (size_t)(total > 0 ? total : 1));
+    int32_t *size = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n_groups > 0 ? n_groups : 1));
+    for (int g = 0; g < n_groups; ++g)
+        size[g] = vo_source_list(servers + goff[g], goff[g + 1] - goff[g], view, order + goff[g]);
+    source_batch_ctx c = {servers, goff, order, size, grp, src4, out};
+    parallel_for(n, nthreads, source_range, &c);
+    free(order);
+    free(size);
+}

@@ -228,6 +228,37 @@ uint64_t vo_mirror_switch(const vo_mirror_filter *f, int n, int origin, const ui
 int vo_cert_choose(const char *const *names, const int32_t *name_lens, const int32_t *holder,
                    int n_names, int n_holders, const uint8_t *sni, int sni_len, int sni_null);
 
+/* ---- batched, pthread-partitioned forms of the restatements above (the
+ * GPU tests' checkers and bench.py's cpu_baseline legs); item i of a packed
+ * blob = blob[off[i], off[i+1]) ---- */
+void vo_dns_batch(const vo_hosts *hosts, const vo_group *g, int ng, const uint8_t *blob,
+                  const uint32_t *off, int64_t n, uint8_t *kind, int32_t *value, int nthreads);
+void vo_parse_batch(const uint8_t *blob, const uint32_t *off, int64_t n, int layer, vo_pkt *out,
+                    int nthreads);
+/* Switch.java:679-684 + L3.java:423-444 per datagram: the bare-VXLAN
+ * SecurityGroup check of the IPv4 sender (UDP list, bind port), the VXLAN
+ * parse, and RouteTable.lookup of the inner destination when allowed and
+ * the frame parses to IPv4/IPv6 (else -1).  remote4 in IP.ipv4Bytes2Int order. */
+void vo_switch_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                     int default_allow, const uint8_t *blob, const uint32_t *off, int64_t n,
+                     const uint32_t *remote4, int bind_port, const vo_net *v4, int n4,
+                     const vo_net *v6, int n6, int32_t *acl, uint8_t *allow, int32_t *route,
+                     int nthreads);
+/* SSLContextHolder.choose per SNI (sni_null may be NULL: none null) */
+void vo_cert_batch(const char *const *names, const int32_t *name_lens, const int32_t *holder,
+                   int n_names, int n_holders, const uint8_t *blob, const uint32_t *off,
+                   const uint8_t *sni_null, int64_t n, int32_t *out, int nthreads);
+void vo_mirror_switch_batch(const vo_mirror_filter *f, int nf, int origin, const uint8_t *blob,
+                            const uint32_t *off, int64_t n, int layer, uint64_t *out,
+                            int nthreads);
+/* sourceHashGet per item: group grp[i]'s servers are servers[goff[g], goff[g+1]);
+ * the sourceReset order of every group is built once first (Java caches it
+ * until the next reset); src4 in IP.ipv4Bytes2Int order; out = the index
+ * within the group, or -1. */
+void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups, int view,
+                     const int32_t *grp, const uint32_t *src4, int64_t n, int32_t *out,
+                     int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -127,6 +127,17 @@ def lib():
         L.vo_mirror_switch.restype = C.c_uint64
         L.vo_cert_choose.argtypes = [P(C.c_char_p), i32p, i32p, C.c_int, C.c_int, u8p, C.c_int,
                                      C.c_int]
+        vp, i64 = C.c_void_p, C.c_int64
+        L.vo_dns_batch.argtypes = [P(VoHosts), P(VoGroup), C.c_int, vp, vp, i64, vp, vp, C.c_int]
+        L.vo_parse_batch.argtypes = [vp, vp, i64, C.c_int, P(VoPkt), C.c_int]
+        L.vo_switch_batch.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int, vp, vp,
+                                      i64, vp, C.c_int, P(VoNet), C.c_int, P(VoNet), C.c_int, vp,
+                                      vp, vp, C.c_int]
+        L.vo_cert_batch.argtypes = [P(C.c_char_p), i32p, i32p, C.c_int, C.c_int, vp, vp, vp, i64,
+                                    vp, C.c_int]
+        L.vo_mirror_switch_batch.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int, vp, vp, i64,
+                                             C.c_int, vp, C.c_int]
+        L.vo_source_batch.argtypes = [P(VoServer), vp, C.c_int, C.c_int, vp, vp, i64, vp, C.c_int]
         _lib = L
     return _lib
 
@@ -577,3 +588,80 @@ def mirror_match(arr, n, origin, mac_src, mac_dst, ip_src, ip_dst, transport, po
 
 def mirror_switch(arr, n, origin, frame, layer):
     return int(lib().vo_mirror_switch(arr, n, origin, _u8(bytes(frame)), len(frame), layer))
+
+
+# ---- batched forms (pthread partitions): checkers and bench cpu_baseline ----
+def _u32a(x):
+    return np.ascontiguousarray(x, np.uint32)
+
+
+def dns_batch_np(hosts, groups, blob, off, nthreads=1):
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    h = hosts if isinstance(hosts, Hosts) else Hosts(hosts)
+    n = len(off) - 1
+    kind, value = np.empty(n, np.uint8), np.empty(n, np.int32)
+    lib().vo_dns_batch(C.byref(h.h), g.arr, g.n, _ptr(np.ascontiguousarray(blob, np.uint8)),
+                       _ptr(_u32a(off)), n, _ptr(kind), _ptr(value), nthreads)
+    return kind, value
+
+
+def parse_batch_np(blob, off, layer, nthreads=1):
+    """-> ctypes array of VoPkt, one per frame"""
+    n = len(off) - 1
+    out = (VoPkt * max(1, n))()
+    lib().vo_parse_batch(_ptr(np.ascontiguousarray(blob, np.uint8)), _ptr(_u32a(off)), n, layer,
+                         out, nthreads)
+    return out
+
+
+def switch_batch_np(tcp, udp, dflt, blob, off, remote4, bind_port, v4, v6, nthreads=1):
+    n = len(off) - 1
+    acl, allow, route = np.empty(n, np.int32), np.empty(n, np.uint8), np.empty(n, np.int32)
+    t = tcp if len(tcp) else np.zeros(1, tcp.dtype)
+    u = udp if len(udp) else np.zeros(1, udp.dtype)
+    a4 = v4 if len(v4) else np.zeros(1, v4.dtype)
+    a6 = v6 if len(v6) else np.zeros(1, v6.dtype)
+    lib().vo_switch_batch(_cast(t, VoSgRule), len(tcp), _cast(u, VoSgRule), len(udp),
+                          1 if dflt else 0, _ptr(np.ascontiguousarray(blob, np.uint8)),
+                          _ptr(_u32a(off)), n, _ptr(_u32a(remote4)), bind_port,
+                          _cast(a4, VoNet), len(v4), _cast(a6, VoNet), len(v6), _ptr(acl),
+                          _ptr(allow), _ptr(route), nthreads)
+    return acl, allow, route
+
+
+def cert_batch_np(certs, blob, off, nthreads=1):
+    n = len(off) - 1
+    out = np.empty(n, np.int32)
+    lib().vo_cert_batch(certs.karr, certs.larr, certs.harr, len(certs.names), certs.n_holders,
+                        _ptr(np.ascontiguousarray(blob, np.uint8)), _ptr(_u32a(off)), None, n,
+                        _ptr(out), nthreads)
+    return out
+
+
+def mirror_switch_batch_np(arr, nf, origin, blob, off, layer, nthreads=1):
+    n = len(off) - 1
+    out = np.empty(n, np.uint64)
+    lib().vo_mirror_switch_batch(arr, nf, origin, _ptr(np.ascontiguousarray(blob, np.uint8)),
+                                 _ptr(_u32a(off)), n, layer, _ptr(out), nthreads)
+    return out
+
+
+class SourceGroups:
+    """groups: list of server lists [(ip bytes, port, weight, healthy)], flattened once."""
+
+    def __init__(self, groups):
+        self.arr = servers_arr([s for g in groups for s in g])
+        self.goff = np.zeros(len(groups) + 1, np.int32)
+        self.goff[1:] = np.cumsum([len(g) for g in groups])
+        self.n = len(groups)
+
+
+def source_batch_np(groups, view, grp, src4, nthreads=1):
+    """-> index within the item's group, or -1"""
+    sg = groups if isinstance(groups, SourceGroups) else SourceGroups(groups)
+    n = len(grp)
+    out = np.empty(n, np.int32)
+    lib().vo_source_batch(sg.arr, _ptr(sg.goff), sg.n, view,
+                          _ptr(np.ascontiguousarray(grp, np.int32)), _ptr(_u32a(src4)), n,
+                          _ptr(out), nthreads)
+    return out

@@ -168,6 +168,56 @@ def test_c5_pipeline_count_stream(c5):
     _check_batch(clf, t, dev, pk, outs, pool)
 
 
+def test_mix_bench_batch_vs_oracle(c5):
+    """The `mix` sub-bench exactly as bench.py runs it: 16M packets of
+    bench.gen_mixed (15 % IPv6: IPv4-mapped and 2001:db8:: sources, 90 % of
+    destinations inside a rulesV6 prefix) through vc_pipeline_dev on the C5
+    tables, counter finish on a second stream.  Oracle samples per family
+    (the `instanceof IPv4` dispatch, RouteTable.java:44-58), group =
+    pool[host_id] over the whole batch, exact route counters."""
+    import torch
+    clf, t, dev = c5
+    pool = clf.hint_search((t.pool_blob, t.pool_off, None))
+    n = 16 << 20
+    fam, proto, src, dst, src6, dst6, dport, hid = B.gen_mixed(0, n, t, t.pool_n, dev=dev)
+    s_cnt = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    clf.counters_enable(True)
+    clf.counters_reset()
+    acl, route, grp, allow = clf.pipeline(proto, src, dst, dport, hid, pool, family=fam,
+                                          src6=src6, dst6=dst6, want_allow=True,
+                                          count_stream=s_cnt)
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    assert torch.equal(grp, pool[hid.long()])
+    six = (fam == 6).cpu().numpy()
+    assert 0.13 < six.mean() < 0.17
+    rng = np.random.default_rng(77)
+    h = lambda x: x.cpu().numpy()
+    acl_h, route_h, allow_h = h(acl), h(route), h(allow)
+    proto_h, dport_h = h(proto), h(dport).view(np.uint16)
+    for is6, k in ((False, 8000), (True, 3000)):
+        s = rng.choice(np.nonzero(six == is6)[0], k, replace=False)
+        if is6:
+            want, wv = O.sg_batch_v6_np(t.tcp, t.udp, False, proto_h[s], h(src6)[s], dport_h[s],
+                                        nthreads=THREADS)
+            wr = O.rt_batch_v6_np(t.v6_list, h(dst6)[s][:1500], nthreads=THREADS)
+        else:
+            want, wv = O.sg_batch_v4_np(t.tcp, t.udp, False, proto_h[s], h(src)[s].view(np.uint32),
+                                        dport_h[s], nthreads=THREADS)
+            wr = O.rt_batch_v4_np(t.v4_list, h(dst)[s][:1500].view(np.uint32), nthreads=THREADS)
+        np.testing.assert_array_equal(acl_h[s], want)
+        np.testing.assert_array_equal(allow_h[s], wv)
+        np.testing.assert_array_equal(route_h[s][:1500], wr)
+    assert (route_h[six] >= 0).mean() > 0.8 and (acl_h[six] >= 0).mean() > 0.05
+    nn = t.n4 + t.n6
+    rr = route.long()
+    bins = torch.where(rr >= 0, torch.where(fam == 6, t.n4 + rr, rr),
+                       torch.where(fam == 6, nn + 1, nn))
+    exp = torch.bincount(bins, minlength=nn + 2).cpu().numpy().astype(np.uint64)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE), exp)
+
+
 def test_generator_device_equals_host(c5):
     """bench.gen_packets is index-addressable and device-independent."""
     import torch

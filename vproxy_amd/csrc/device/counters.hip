@@ -29,7 +29,7 @@ constexpr int kHistBlock = 1024;
 constexpr int kHistBins = 32768;      // small path: 128 KiB of LDS per workgroup
 constexpr int kBW = 8192;             // large path: bins per bucket (32 KiB of LDS)
 constexpr int kMaxBuckets = 4096;
-constexpr int kTile = 8192;           // scatter tile: items sorted by bucket in LDS
+constexpr int kTile = 32768;          // scatter tile: items sorted by bucket in LDS (128 KiB)
 constexpr uint32_t kSeg = 256 * 1024; // max items per histogram segment
 
 // Item i -> bin in [0, nval), or -1 for a null result (*udp_or_plain_null
@@ -292,7 +292,11 @@ __global__ __launch_bounds__(kHistBlock) void bucket_scan_kernel(
 
 // (3) scatter each workgroup's slice into bucket-contiguous order, a tile of
 // kTile items at a time sorted by bucket in LDS, so bucket runs are written
-// with consecutive lanes.
+// with consecutive lanes.  The 32K-item tile (128 KiB of LDS) runs as fast
+// alone as 8K ones, but in the C5 schedule, where the next hostname-pool
+// pass runs beside this finish, a scatter workgroup then never shares its
+// CU with pool-pass workgroups: the pool pass takes 1.12 instead of 1.40 ms
+// and the step 6.29 instead of 6.42 ms (profiles/r02_ab_scatter_tile.txt).
 template <bool kVec>
 __global__ __launch_bounds__(kHistBlock) void bucket_scatter_kernel(
     int mode, const int32_t* __restrict__ idx, const uint8_t* __restrict__ aux, int64_t n,
