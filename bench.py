@@ -404,12 +404,16 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
     info = cpu_info()
     res = {}
     for threads in (info["threads_all"], 1):
-        probe = max(threads * 4, 64)
-        t = run(probe, threads)
-        n = int(max(probe, probe * budget_s / max(t, 1e-6)))
-        if cap:
-            n = min(n, cap)
-        t = run(n, threads)
+        # grow the sample until it runs at least half the budget (a short
+        # probe is dominated by thread start-up), or reaches the cap
+        n = max(threads * 4, 64)
+        while True:
+            t = run(n, threads)
+            if t >= 0.5 * budget_s or (cap and n >= cap):
+                break
+            n = int(min(n * 16, max(2 * n, n * budget_s / max(t, 1e-6))))
+            if cap:
+                n = min(n, cap)
         res[threads] = (n, t)
     na, ta = res[info["threads_all"]]
     n1, t1 = res[1]
@@ -901,7 +905,7 @@ def sub_bench(args, clf, dev, rank, world):
                     O.parse_batch_np(sb, so, 0, nthreads=threads)
                     return time.perf_counter() - t0
                 cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle vpacket "
-                                "parse chain (VXLAN -> Ethernet -> IPv4/IPv6 -> TCP/ICMP)", cap=n)
+                                "parse chain (VXLAN -> Ethernet -> IPv4/IPv6 -> TCP/ICMP)", cap=1 << 22)
         elif args.workload == "switch":
             # parse + bare-VXLAN ACL on the sender + inner route, one kernel,
             # over the C5 SecurityGroup and route tables; only the route
@@ -957,7 +961,7 @@ def sub_bench(args, clf, dev, rank, world):
                                              nthreads=threads)
                     return time.perf_counter() - t0
                 cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle "
-                                "Mirror.switchPacket over the 17 filters", cap=n)
+                                "Mirror.switchPacket over the 17 filters", cap=1 << 22)
     elif args.workload == "source":
         rng = np.random.default_rng(W.SEED + 14)
         groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
