@@ -242,7 +242,7 @@ class C5Steps:
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream", inflight=2, overlap="finish"):
+                 finish="stream", inflight=2, overlap="finish", gate=False):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -251,6 +251,7 @@ class C5Steps:
         self.fused = counters == "fused"
         self.finish = finish
         self.overlap = overlap
+        self.gate = gate
         self.nbuf = 1 if serial else max(1, inflight)
         pool_out = torch.empty(t.pool_n, dtype=torch.int32, device=dev)
         self.pools = [pool_out] + [torch.empty_like(pool_out) for _ in range(self.nbuf - 1)]
@@ -293,6 +294,8 @@ class C5Steps:
             self.s_pipe.wait_event(self.ev_hint[j])
             if j - self.nbuf in self.ev_cnt:           # output buffers counted
                 self.s_pipe.wait_event(self.ev_cnt[j - self.nbuf])
+            if self.gate and j - 1 in self.ev_cnt:      # the previous batch's finish done
+                self.s_pipe.wait_event(self.ev_cnt[j - 1])
             k0, k1 = RawEvent(), RawEvent()            # the classify kernel alone
             k0.record(self.s_pipe)
             if self.fused:                             # count packets only, not the pool pass
@@ -522,6 +525,9 @@ def main():
                     help="what the next batch's hostname-pool pass runs beside: this batch's "
                          "counter finish (it waits for this batch's pipeline kernel, which then "
                          "runs alone) or the pipeline kernel itself")
+    ap.add_argument("--gate", action="store_true",
+                    help="the pipeline kernel also waits for the previous batch's counter "
+                         "finish (which then overlaps only the pool pass)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (output and pool buffers)")
     ap.add_argument("--dist", action="store_true",
@@ -558,7 +564,7 @@ def main():
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
     steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
                     counters=args.counters, finish=args.finish, inflight=args.inflight,
-                    overlap=args.overlap)
+                    overlap=args.overlap, gate=args.gate)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))

@@ -110,6 +110,7 @@ struct vc_ctx {
     hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
     std::mutex handoff_mu;
     vc::ScratchRing scratch;       // counter-pass scratch, reused across calls
+    vc::TicketRing tickets;        // work counters of the string kernels
     int num_cus = 256;
     std::atomic<bool> counters_on{false};
     std::mutex compile_mu;   // serialises compiles; classify never takes it
@@ -138,6 +139,7 @@ struct vc_ctx {
         c.pool = pool;
         c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
         c.scratch = const_cast<vc::ScratchRing*>(&scratch);
+        c.tickets = const_cast<vc::TicketRing*>(&tickets);
         return c;
     }
 };
@@ -231,8 +233,9 @@ int vc_create(int device, vc_ctx** out) {
     props.location.id = device;
     if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming)) != hipSuccess ||
-        (e = c->scratch.init()) != hipSuccess) {
+        (e = c->scratch.init()) != hipSuccess || (e = c->tickets.init()) != hipSuccess) {
         c->scratch.destroy();
+        c->tickets.destroy();
         if (c->handoff) (void)hipEventDestroy(c->handoff);
         if (c->pool) (void)hipMemPoolDestroy(c->pool);
         (void)hipStreamDestroy(c->stream);
@@ -274,6 +277,7 @@ void vc_destroy(vc_ctx* ctx) {
     (void)hipDeviceSynchronize();
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     ctx->scratch.destroy();
+    ctx->tickets.destroy();
     delete ctx;
 }
 

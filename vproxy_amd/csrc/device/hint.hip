@@ -26,21 +26,56 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_HINT_MINW 5
 #endif
 
+// The 64-item chunks of a launch, in wave-uniform order: taken kPerTicket
+// at a time from the launch's ticket counter (launch.h TicketRing) or,
+// without one, the static grid-stride sequence.  One ticket per 1024 items
+// keeps the counter's same-address atomics (served one at a time at the
+// memory side) far below the kernel's rate: one ticket per 64-name chunk
+// made the hint pass 3.6x slower.  Every wave takes exactly one
+// out-of-range ticket (its last), so the wave holding ticket
+// ntickets + nwaves - 1 is the last taker of the launch and resets the
+// counter for the slot's next launch.
+constexpr int64_t kPerTicket = 16;
+
+struct Chunks {
+    uint32_t* ticket;
+    int64_t nchunks;
+    __device__ int64_t take() const {
+        uint32_t t = 0;
+        if ((threadIdx.x & 63) == 0) {
+            t = atomicAdd(ticket, 1u);
+            const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+            const uint32_t ntickets = uint32_t((nchunks + kPerTicket - 1) / kPerTicket);
+            if (t == ntickets + nwaves - 1) atomicExch(ticket, 0u);
+        }
+        return int64_t(__shfl(t, 0, 64)) * kPerTicket;
+    }
+    __device__ int64_t first(int w) const {
+        return ticket ? take() : int64_t(blockIdx.x) * kWaves + w;
+    }
+    __device__ int64_t next(int64_t c) const {
+        if (!ticket) return c + int64_t(gridDim.x) * kWaves;
+        return (c + 1) % kPerTicket != 0 && c + 1 < nchunks ? c + 1 : take();
+    }
+};
+
 template <bool kStage>
 __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
     const uint8_t* __restrict__ uri_blob, const uint32_t* __restrict__ uri_off,
-    const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out) {
+    const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out,
+    uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
+    const Chunks ch{ticket, (n + 63) / 64};
     const bool general = uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
-    for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
+    for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
@@ -81,12 +116,13 @@ template <bool kStage>
 __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
-    int32_t* __restrict__ value) {
+    int32_t* __restrict__ value, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
+    const Chunks ch{ticket, (n + 63) / 64};
     HintImage slow_img = img;
-    for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
+    for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
@@ -109,11 +145,13 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
 template <bool kStage>
 __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     CertImage certs, const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off,
-    const uint8_t* __restrict__ null, int64_t n, int32_t* __restrict__ out) {
+    const uint8_t* __restrict__ null, int64_t n, int32_t* __restrict__ out,
+    uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kWaves * 64;
-    for (int64_t base = (int64_t(blockIdx.x) * kWaves + w) * 64; base < n; base += wstride) {
+    const Chunks ch{ticket, (n + 63) / 64};
+    for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
@@ -141,12 +179,12 @@ hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_
         hipLaunchKernelGGL(vcd::cert_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
-                           certs, blob, off, null, n, out);
+                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::cert_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
-                           certs, blob, off, null, n, out);
+                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
     return hipGetLastError();
 }
 
@@ -161,13 +199,13 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out);
+                           n, out, c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::hint_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out);
+                           n, out, c.tickets ? c.tickets->next() : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, img.n_groups, 0, img.n_groups, 0,
@@ -183,12 +221,14 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
         hipLaunchKernelGGL(vcd::dns_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
-                           hosts, hints, qblob, qoff, n, kind, value);
+                           hosts, hints, qblob, qoff, n, kind, value,
+                           c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::dns_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), 0, c.stream,
-                           hosts, hints, qblob, qoff, n, kind, value);
+                           hosts, hints, qblob, qoff, n, kind, value,
+                           c.tickets ? c.tickets->next() : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !group_counters) return e;
     return launch_hist(c, VC_HIST_DNS, value, kind, n, hints.n_groups, 0, hints.n_groups, 0,

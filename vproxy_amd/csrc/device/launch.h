@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 
@@ -62,12 +63,38 @@ private:
     int next_ = 0;
 };
 
+// Work counters of the dynamically scheduled string kernels (hint, DNS,
+// SNI): the waves of a launch take 64-item chunks from one device counter,
+// so workgroups that become resident late -- beside another stream's kernel
+// -- do not hold back a fixed share of the work.  The wave that takes the
+// launch's last ticket resets the counter to zero, so a slot needs no
+// memset before reuse; slots go round-robin (kSlots launches in flight).
+class TicketRing {
+public:
+    static constexpr uint32_t kSlots = 4096;
+    hipError_t init() {
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_), kSlots * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemset(d_, 0, kSlots * sizeof(uint32_t));
+        return e;
+    }
+    void destroy() {            // after the device is idle
+        if (d_) (void)hipFree(d_);
+        d_ = nullptr;
+    }
+    uint32_t* next() { return d_ ? d_ + next_.fetch_add(1) % kSlots : nullptr; }
+
+private:
+    uint32_t* d_ = nullptr;
+    std::atomic<uint32_t> next_{0};
+};
+
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
     hipStream_t stream = nullptr;
     hipMemPool_t pool = nullptr;   // staging pool of the host entry points
     Handoff handoff;
     ScratchRing* scratch = nullptr;   // counter-pass scratch (required by the launchers)
+    TicketRing* tickets = nullptr;    // work counters; null: static grid-stride split
 };
 
 // Workgroups per CU that can be resident at once for `kernel` (occupancy
