@@ -242,7 +242,7 @@ class C5Steps:
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream", inflight=2, overlap="finish", gate=False):
+                 finish="stream", inflight=3, overlap="finish", gate=False):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -528,7 +528,7 @@ def main():
     ap.add_argument("--gate", action="store_true",
                     help="the pipeline kernel also waits for the previous batch's counter "
                          "finish (which then overlaps only the pool pass)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight (output and pool buffers)")
     ap.add_argument("--dist", action="store_true",
                     help="use the process group and the counter all-reduce even at N = 1")
