@@ -280,13 +280,24 @@ VC_HD bool wave_any(bool p) {
 // record key == query bytes [st, st + n)?
 template <class Src>
 VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n) {
-    if ((r.m.x & ~VC_REC_HAS_PM) != uint32_t(n)) return false;
+    // The word masks use rn, the record's length, made opaque after the
+    // check: with n the compiler hoists all twelve masks out of the probe
+    // loop and computes them per hit; only the key's last word needs one.
+    int rn = int(r.m.x & ~VC_REC_HAS_PM);
+    if (rn != n) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(rn));
+#endif
     uint32_t diff = 0;
     const auto c = q.cursor(st, st + n);
 #pragma unroll
     for (int j = 0; j < VC_REC_INLINE / 4; ++j) {
-        if (!wave_any(4 * j < n)) break;          // no lane's key reaches word j
-        if (4 * j < n) diff |= (c.get(j) ^ rec_word(r, j)) & tail_mask(n - 4 * j);
+        if (!wave_any(4 * j < rn)) break;         // no lane's key reaches word j
+        if (4 * j < rn) {
+            uint32_t d = c.get(j) ^ rec_word(r, j);
+            if (4 * j + 4 > rn) d &= tail_mask(rn - 4 * j);
+            diff |= d;
+        }
     }
     if (diff) return false;
     if (n > VC_REC_INLINE) {      // long key: the rest from the blob copy
