@@ -286,6 +286,40 @@ def test_hint_random_vs_oracle(clf):
     np.testing.assert_array_equal(got, want)
 
 
+def test_hint_work_tickets_wrap(clf):
+    """The string kernels take work tickets from a ring of 4096 per-launch
+    device counters (launch.h TicketRing) that each launch's last wave
+    resets: over 4500 launches (every slot reused) of sizes around the
+    64-item chunk and 1024-item ticket edges, on two streams, every result
+    equals the oracle's."""
+    import ctypes as C
+    import torch
+    groups, hosts, queries = hint_cases_random(np.random.default_rng(43), 300, 7000)
+    clf.compile_upstream(groups)
+    og = O.Groups(groups)
+    hs = [q[0] for q in queries if q[0] is not None][:6000]
+    want = np.array([O.search_for_group(og, h, 0, None) for h in hs], np.int32)
+    blob, off, _ = pack_strings(hs)
+    bd = torch.from_numpy(blob).cuda()
+    od = torch.from_numpy(off.astype(np.int32)).cuda()
+    sizes = [1, 63, 64, 65, 1023, 1024, 1025, 3000, 6000]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(4500):
+        n = sizes[k % len(sizes)]
+        s = streams[k % 2]
+        with torch.cuda.stream(s):
+            o = torch.empty(n, dtype=torch.int32, device="cuda")
+            V.check(V.lib().vc_hint_search_dev(
+                clf.h, C.c_void_p(bd.data_ptr()), C.c_void_p(od.data_ptr()), None, None, None,
+                None, None, n, C.c_void_p(o.data_ptr()), C.c_void_p(s.cuda_stream)))
+        if k % 500 == 0 or k >= 4490:
+            outs.append((n, o))
+    torch.cuda.synchronize()
+    for n, o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), want[:n])
+
+
 def test_hint_c4_scale(clf):
     """C4: 100k hint-host groups vs 1M hostnames (16M in the bench);
     oracle-checked sample (each oracle query scans all 100k groups)."""
