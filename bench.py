@@ -430,6 +430,15 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
     return out
 
 
+def end_to_end(fn, items, reps=3):
+    """M items/s of a synchronous host-buffer call (H2D + kernels + D2H)."""
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return round(items * reps / (time.perf_counter() - t0) / 1e6, 1)
+
+
 def sample_blob(blob, off, idx):
     """Host blob + uint32 offsets of strings[idx] (a CPU-baseline sample)."""
     b, o, _ = gather_strings_dev(blob, off, np.asarray(idx), "cpu")
@@ -746,6 +755,10 @@ def sub_bench(args, clf, dev, rank, world):
             else:
                 fn = lambda: clf.acl_v4(*d, out_idx=out, want_allow=False)
                 per_unit, unit, kern = 11, "B/tuple (7 in + 4 out)", "acl_v4_kernel"
+                extra["end_to_end_host_buffers_M_per_s"] = end_to_end(
+                    lambda: clf.acl_v4(proto, src, port, want_allow=True), n)
+                extra["end_to_end_note"] = ("vc_acl_classify_v4 on pageable host arrays (chunked "
+                                            "DMA staging), synchronous; registered buffers: c2host")
         if O is not None:
             def run(k, threads):
                 t0 = time.perf_counter()
@@ -798,6 +811,12 @@ def sub_bench(args, clf, dev, rank, world):
         e4, ms4 = _time(lambda: clf.route_v4(q4, out=o4), 3, 1)
         e6, ms6 = _time(lambda: clf.route_v6(q6, out=o6), 3, 1)
         extra["v4_ms"], extra["v6_ms"] = round(ms4, 4), round(ms6, 4)
+        q4h_all = q4.cpu().numpy().view(np.uint32)
+        extra["end_to_end_host_buffers_M_per_s"] = end_to_end(
+            lambda: (clf.route_v4(q4h_all), clf.route_v6(q6h)), n)
+        extra["end_to_end_note"] = ("vc_route_lookup_v4 + vc_route_lookup_v6 on pageable host "
+                                    "arrays: chunked H2D + kernel + D2H, synchronous")
+        del q4h_all
         extra["v4_G_per_s"] = round(n4 / ms4 / 1e6, 2)
         extra["v6_G_per_s"] = round((n - n4) / ms6 / 1e6, 2)
         if O is not None:
@@ -830,6 +849,19 @@ def sub_bench(args, clf, dev, rank, world):
         n = 16 << 20
         pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
         blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
+        hblob, hoff = blob.cpu().numpy(), off.cpu().numpy().view(np.uint32)
+        P = lambda x: C.c_void_p(x.ctypes.data)
+        if dns:
+            hk, hv = np.empty(n, np.uint8), np.empty(n, np.int32)
+            e2e = lambda: V.check(V.lib().vc_dns_classify(clf.h, P(hblob), P(hoff), n, P(hk), P(hv)))
+        else:
+            ho_ = np.empty(n, np.int32)
+            e2e = lambda: V.check(V.lib().vc_hint_search(clf.h, P(hblob), P(hoff), None, None, None,
+                                                         None, None, n, P(ho_)))
+        extra["end_to_end_host_buffers_M_per_s"] = end_to_end(e2e, n)
+        extra["end_to_end_note"] = ("%s on pageable host arrays (blob + offsets in, results "
+                                    "out): chunked H2D + kernel + D2H, synchronous"
+                                    % ("vc_dns_classify" if dns else "vc_hint_search"))
         if dns:
             kind = torch.empty(n, dtype=torch.uint8, device=dev)
             val = torch.empty(n, dtype=torch.int32, device=dev)
