@@ -37,6 +37,31 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 // counter for the slot's next launch.
 constexpr int64_t kPerTicket = 16;
 
+#if defined(VC_HINT_PROF)
+// Profiling build: phase cycles summed over the waves of every launch
+// (0 stage, 1 scan, 2 tag groups, 3 records, 4 DNS hosts, 5 output), [6] waves.
+__device__ unsigned long long vc_hint_prof[kProfPhases + 1];
+__device__ __forceinline__ void prof_begin() {
+    uint64_t* t = vc_prof_lds + (threadIdx.x >> 6) * (kProfPhases + 1);
+    if ((threadIdx.x & 63) < kProfPhases) t[threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) == 0) t[kProfPhases] = clock64();
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void prof_end() {
+    const uint64_t* t = vc_prof_lds + (threadIdx.x >> 6) * (kProfPhases + 1);
+    const int l = int(threadIdx.x & 63);
+    if (l < kProfPhases) atomicAdd(&vc_hint_prof[l], (unsigned long long)t[l]);
+    if (l == kProfPhases) atomicAdd(&vc_hint_prof[l], 1ull);
+}
+constexpr size_t kProfLds = size_t(kWaves) * (kProfPhases + 1) * 8;
+#define VC_PBEGIN() prof_begin()
+#define VC_PEND() prof_end()
+#else
+constexpr size_t kProfLds = 0;
+#define VC_PBEGIN() ((void)0)
+#define VC_PEND() ((void)0)
+#endif
+
 struct Chunks {
     uint32_t* ticket;
     int64_t nchunks;
@@ -74,6 +99,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // copy so the fast path keeps reading the kernel argument (whose table
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
+    VC_PBEGIN();
     for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
         const int64_t base = c * 64;
         const int64_t i = base + lane;
@@ -81,6 +107,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
         uint32_t a0 = 0;
         const bool staged =
             kStage && host_blob && stage_wave<kStageBytes>(host_blob, host_off[base], host_off[last], stage[w], &a0);
+        VC_PMARK(0);
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
             const bool has_host = host_blob && !(host_null && host_null[i]);
@@ -109,7 +136,9 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             out[i] = r;
         }
         if (kStage) wave_done();
+        VC_PMARK(5);
     }
+    VC_PEND();
 }
 
 template <bool kStage>
@@ -121,12 +150,14 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const Chunks ch{ticket, (n + 63) / 64};
     HintImage slow_img = img;
+    VC_PBEGIN();
     for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
         const int64_t base = c * 64;
         const int64_t i = base + lane;
         const int64_t last = base + 64 < n ? base + 64 : n;
         uint32_t a0 = 0;
         const bool staged = kStage && stage_wave<kStageBytes>(qblob, qoff[base], qoff[last], stage[w], &a0);
+        VC_PMARK(0);
         if (i < n) {
             const uint32_t a = qoff[i], e = qoff[i + 1];
             uint8_t kd;
@@ -139,7 +170,9 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
             value[i] = val;
         }
         if (kStage) wave_done();
+        VC_PMARK(5);
     }
+    VC_PEND();
 }
 
 template <bool kStage>
@@ -197,13 +230,13 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
     if (host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0)
         hipLaunchKernelGGL(vcd::hint_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out, c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::hint_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<false>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out, c.tickets ? c.tickets->next() : nullptr);
     hipError_t e = hipGetLastError();
@@ -220,13 +253,13 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
     if ((reinterpret_cast<uintptr_t>(qblob) & 3) == 0)
         hipLaunchKernelGGL(vcd::dns_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<true>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value,
                            c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::dns_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<false>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value,
                            c.tickets ? c.tickets->next() : nullptr);
     hipError_t e = hipGetLastError();
@@ -236,3 +269,12 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
 }
 
 }  // namespace vc
+
+#if defined(VC_HINT_PROF)
+// Profiling build only: read and clear the phase sums (not in vclassify.h).
+extern "C" int vc_debug_hint_prof(unsigned long long* out) {
+    unsigned long long z[vcd::kProfPhases + 1] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vcd::vc_hint_prof), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(vcd::vc_hint_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -20,6 +20,24 @@
 
 namespace vcd {
 
+// Profiling builds only (-DVC_HINT_PROF, scripts/hint_prof.py): per-wave
+// cycles of the string kernels' phases, accumulated in LDS by every active
+// lane (the clock is wave-uniform, so the lanes store equal values).
+#if defined(VC_HINT_PROF)
+constexpr int kProfPhases = 6;
+extern __shared__ uint64_t vc_prof_lds[];
+__device__ __forceinline__ void prof_mark(int i) {
+    uint64_t* t = vc_prof_lds + (threadIdx.x >> 6) * (kProfPhases + 1);
+    const uint64_t now = clock64();
+    t[i] += now - t[kProfPhases];
+    t[kProfPhases] = now;
+}
+#endif
+#if defined(VC_HINT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define VC_PMARK(i) prof_mark(i)
+#else
+#define VC_PMARK(i) ((void)0)
+#endif
 
 struct DStr {
     const uint8_t* p;
@@ -509,6 +527,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         S = vck::mix(S, w);
         pos -= 4;
     }
+    VC_PMARK(1);
     if (nc >= 2 || np > kMaxSuffix) return host_only_slow(*slow_img, q.ptr(), n, port);
     h[0] = vck::fin(S, uint32_t(e));
     st[0] = 0;
@@ -548,6 +567,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             }
         }
     }
+    VC_PMARK(2);
     uint32_t best = VC_NONE;
     while (hits) {
         const int k = __builtin_ctz(hits);
@@ -570,6 +590,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             best = v < best ? v : best;
         }
     }
+    VC_PMARK(3);
     if (best == VC_NONE) best = wildcard_pick(img, port);
     return best != VC_NONE ? int32_t(best) : -1;
 }
@@ -720,6 +741,7 @@ VC_HD void dns_flow(const HostsImage& hosts, const HintImage& img, const HintIma
             return;
         }
     }
+    VC_PMARK(4);
     // (2) strip one trailing dot, :133-135
     const uint8_t* qp = q.ptr();
     const int dn = (qn > 0 && (q.word(qn - 1, qn - 1, qn) & 0xFFu) == '.') ? qn - 1 : qn;
