@@ -20,10 +20,15 @@ constexpr int kHintBlock = 256;
 constexpr int kWaves = kHintBlock / 64;
 constexpr uint32_t kStageBytes = 4096;   // per wave: 64 names of up to 64 B on average
 constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
-// Minimum waves per SIMD for hint_kernel: 5 holds it at 96 VGPRs (no spills);
-// unbounded it takes 97, which rounds to 104 and leaves 4 waves per SIMD.
+// Minimum waves per SIMD.  hint_kernel: 7 holds it at 72 VGPRs (a few
+// spills around the slow-path calls): C4 0.866 -> 0.817 ms against 5 waves at
+// 96 VGPRs.  dns_kernel: 6 (80 VGPRs); at 7 it spills in the hot path and
+// takes 1.26 ms instead of 1.07 (profiles/r02_ab_hint_occupancy.txt).
 #ifndef VC_HINT_MINW
-#define VC_HINT_MINW 5
+#define VC_HINT_MINW 7
+#endif
+#ifndef VC_DNS_MINW
+#define VC_DNS_MINW 6
 #endif
 
 // The 64-item chunks of a launch, in wave-uniform order: taken kPerTicket
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
 }
 
 template <bool kStage>
-__global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void dns_kernel(
+__global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
     int32_t* __restrict__ value, uint32_t* __restrict__ ticket) {

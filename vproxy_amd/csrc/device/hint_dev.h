@@ -326,6 +326,58 @@ VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n
     return true;
 }
 
+template <class T>
+VC_HD T gload(const T* p);
+
+// Record s's key == query bytes [st, st + n)?  *meta = its meta word on a
+// match.  The meta and the first 32 key bytes are loaded together; the last
+// 16 inline bytes only when some lane's key is longer.
+template <class Src>
+VC_HD bool rec_match(const HostRec* recs, uint32_t s, const uint8_t* blob, const Src& q, int st,
+                     int n, uint4* meta) {
+    const uint4* p = reinterpret_cast<const uint4*>(recs + s);
+    const uint4 m = gload(p), k0 = gload(p + 1), k1 = gload(p + 2);
+    int rn = int(m.x & ~VC_REC_HAS_PM);
+    if (rn != n) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(rn));
+#endif
+    uint32_t diff = 0;
+    const auto c = q.cursor(st, st + n);
+    {
+        const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!wave_any(4 * j < rn)) break;
+            if (4 * j < rn) {
+                uint32_t d = c.get(j) ^ k[j];
+                if (4 * j + 4 > rn) d &= tail_mask(rn - 4 * j);
+                diff |= d;
+            }
+        }
+    }
+    if (wave_any(rn > 32) && rn > 32) {
+        const uint4 k2 = gload(p + 3);
+        const uint32_t k[4] = {k2.x, k2.y, k2.z, k2.w};
+#pragma unroll
+        for (int j = 8; j < 12; ++j) {
+            if (4 * j < rn) {
+                uint32_t d = c.get(j) ^ k[j - 8];
+                if (4 * j + 4 > rn) d &= tail_mask(rn - 4 * j);
+                diff |= d;
+            }
+        }
+    }
+    if (diff) return false;
+    if (n > VC_REC_INLINE) {      // long key: the rest from the blob copy
+        const uint32_t* kw = reinterpret_cast<const uint32_t*>(blob + m.w);
+        for (int j = VC_REC_INLINE / 4; 4 * j < n; ++j)
+            if (q.word(st + 4 * j, st, st + n) != kw[j]) return false;
+    }
+    *meta = m;
+    return true;
+}
+
 // Global-memory load through an explicitly global pointer: table pointers
 // travel inside image structs, where the compiler cannot infer the address
 // space and would emit flat loads.
@@ -376,11 +428,7 @@ VC_HD int host_find(const HostTable& t, uint32_t h, const Src& q, int st, int n,
         while (m & 15u) {
             const uint32_t k = __builtin_ctz(m);
             m &= m - 1;
-            const Rec r = load_rec_g(t.recs, s + k);
-            if (rec_eq(r, t.blob, q, st, n)) {
-                *out = r;
-                return int(s + k);
-            }
+            if (rec_match(t.recs, s + k, t.blob, q, st, n, &out->m)) return int(s + k);
         }
         if (!(m & 16u)) return -1;
         s = (s + 4) & t.mask;
@@ -489,7 +537,7 @@ template <class Src>
 VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
                              int port) {
     uint32_t h[kProbes];
-    int st[kProbes];
+    uint64_t stp = 0;                 // suffix starts, a byte each: [k] at bits 8k
     int e = n, np = 0, nc = 0;
     uint32_t S = vck::kSeed;
     for (int pos = n - 4; pos > -4;) {
@@ -517,34 +565,27 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             // shift in: [1] = the latest (longest) suffix.  Plain moves under
             // the lanes-with-a-dot mask, no per-slot compare and select.
 #pragma unroll
-            for (int k = kProbes - 1; k > 1; --k) {
-                h[k] = h[k - 1];
-                st[k] = st[k - 1];
-            }
+            for (int k = kProbes - 1; k > 1; --k) h[k] = h[k - 1];
             h[1] = hv;
-            st[1] = sp;
+            stp = ((stp & 0xFFFFFFFFFF00ull) << 8) | (uint64_t(sp) << 8);
         }
         S = vck::mix(S, w);
         pos -= 4;
     }
     VC_PMARK(1);
-    if (nc >= 2 || np > kMaxSuffix) return host_only_slow(*slow_img, q.ptr(), n, port);
+    if (nc >= 2 || np > kMaxSuffix || n > 255) return host_only_slow(*slow_img, q.ptr(), n, port);
     h[0] = vck::fin(S, uint32_t(e));
-    st[0] = 0;
     if (nc) {
         // cut at the colon; strip "www." (then the whole host is the suffix
         // after the dot at 3, the longest, in [1]); empty -> null
         if (e >= 4 && q.word(0, 0, 4) == 0x2E777777u) {
             h[0] = h[1];
-            st[0] = 4;
 #pragma unroll
-            for (int k = 1; k < kProbes - 1; ++k) {
-                h[k] = h[k + 1];
-                st[k] = st[k + 1];
-            }
+            for (int k = 1; k < kProbes - 1; ++k) h[k] = h[k + 1];
+            stp = stp >> 8;
             np -= 1;
         }
-        if (e - st[0] <= 0) return -1;
+        if (e - int(stp & 0xFF) <= 0) return -1;
     }
     const HostTable t = host_table(img);
     // hits: bit k = probe k's first group has a tag match or continues;
@@ -573,12 +614,9 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         const int k = __builtin_ctz(hits);
         hits &= hits - 1;
         uint32_t hk = h[0];
-        int sk = st[0];
 #pragma unroll
-        for (int j = 1; j < kProbes; ++j) {
-            hk = k == j ? h[j] : hk;
-            sk = k == j ? st[j] : sk;
-        }
+        for (int j = 1; j < kProbes; ++j) hk = k == j ? h[j] : hk;
+        const int sk = int((stp >> (8 * k)) & 0xFF);
         Rec r;
         const uint32_t m0 = ((tm >> (4 * k)) & 15u) | (((cont >> k) & 1u) << 4);
         const int slot = host_find(t, hk, q, sk, e - sk, &r, m0);
