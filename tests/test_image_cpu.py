@@ -255,6 +255,31 @@ def test_dns_image():
     assert [(int(k), int(v)) for k, v in zip(kind, val)] == want
 
 
+def test_dns_hosts_dot_forms():
+    """The hosts table holds names without one trailing dot (.b tells them
+    apart): a name and the name + "." are distinct keys, first entry wins,
+    and the probe is made on the dotted qname's scan hash, on a colon
+    name's own hash, and before the slow group path (many labels)."""
+    groups, ghosts = W.gen_groups(2000, 75)
+    arr, ng, keep = group_array(groups)
+    pairs = [("a.example.", 1), ("a.example", 2), ("b.example", 3), ("c.example..", 4),
+             ("c.example.", 5), ("a.example.", 9), ("x:1.", 6), ("p.q.r.s.t.u.v.w.", 7),
+             ("", 8), (".", 10), ("\u00e9.example.", 11), (ghosts[0] + ".", 12), (ghosts[1], 13),
+             ("www.y.com:80.", 14), ("e.f::1.", 15)]
+    names = [b"a.example.", b"a.example", b"b.example.", b"b.example", b"c.example..",
+             b"c.example.", b"c.example", b"x:1.", b"x:1", b"p.q.r.s.t.u.v.w.", b"p.q.r.s.t.u.v.w",
+             b".", b"", b"..", b"\xe9.example.", b"\xe9.example", (ghosts[0] + ".").encode(),
+             ghosts[0].encode(), (ghosts[1] + ".").encode(), ghosts[1].encode(),
+             b"www.y.com:80.", b"www.y.com:80", b"e.f::1.", b"e.f::1"]
+    qb, qo = W.pack(names)
+    kind, val = IC.dns(pairs, arr, ng, qb, qo)
+    og = O.Groups(groups)
+    oh = O.Hosts(pairs)
+    want = [O.dns_classify(oh, og, q) for q in names]
+    assert [(int(k), int(v)) for k, v in zip(kind, val)] == want
+    assert sum(1 for k, _ in want if k == 1) >= 12        # VC_DNS_HOSTS hits
+
+
 def test_hint_fast_path_shapes():
     """The kernels' word-at-a-time fast path (plain and LDS-staged sources at
     every alignment, checked inside the harness) vs the oracle on the hard
