@@ -31,6 +31,7 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_DNS_MINW 6
 #endif
 
+
 // The 64-item chunks of a launch, in wave-uniform order: taken kPerTicket
 // at a time from the launch's ticket counter (launch.h TicketRing) or,
 // without one, the static grid-stride sequence.  One ticket per 1024 items
@@ -87,7 +88,44 @@ struct Chunks {
         if (!ticket) return c + int64_t(gridDim.x) * kWaves;
         return (c + 1) % kPerTicket != 0 && c + 1 < nchunks ? c + 1 : take();
     }
+    // c + 1 is this wave's next chunk (same ticket)
+    __device__ bool paired(int64_t c) const {
+        return ticket && (c + 1) % kPerTicket != 0 && c + 1 < nchunks;
+    }
 };
+
+// The chunk loop of the string kernels.  A wave stages its chunk's items
+// (contiguous in the blob) into LDS with one coalesced copy; when the next
+// chunk is also this wave's and both fit the stage, it stages the two
+// together and runs body(c, staged, a0) for each from one copy, halving the
+// dependent offset -> blob load round trips per name.
+template <uint32_t kBytes, bool kPair, class Body>
+__device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_t* blob,
+                                           const uint32_t* off, int64_t n, uint32_t* stage,
+                                           Body body) {
+    for (int64_t c = ch.first(w); c < ch.nchunks;) {
+        const int64_t base = c * 64;
+        const int64_t end1 = base + 64 < n ? base + 64 : n;
+        uint32_t a0 = 0;
+        int nsub = 1;
+        bool staged = false;
+        if (blob) {
+            if (kPair && ch.paired(c)) {
+                const int64_t end2 = base + 128 < n ? base + 128 : n;
+                if (stage_wave<kBytes>(blob, off[base], off[end2], stage, &a0)) {
+                    staged = true;
+                    nsub = 2;
+                }
+            }
+            if (!staged) staged = stage_wave<kBytes>(blob, off[base], off[end1], stage, &a0);
+        }
+        VC_PMARK(0);
+        for (int sub = 0; sub < nsub; ++sub) body(c + sub, staged, a0);
+        wave_done();
+        VC_PMARK(5);
+        c = ch.next(c + nsub - 1);
+    }
+}
 
 template <bool kStage>
 __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
@@ -105,14 +143,9 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
     VC_PBEGIN();
-    for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
-        const int64_t base = c * 64;
-        const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged =
-            kStage && host_blob && stage_wave<kStageBytes>(host_blob, host_off[base], host_off[last], stage[w], &a0);
-        VC_PMARK(0);
+    chunk_loop<kStageBytes, true>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
+                            [&](int64_t c, bool staged, uint32_t a0) {
+        const int64_t i = c * 64 + lane;
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
             const bool has_host = host_blob && !(host_null && host_null[i]);
@@ -140,9 +173,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             }
             out[i] = r;
         }
-        if (kStage) wave_done();
-        VC_PMARK(5);
-    }
+    });
     VC_PEND();
 }
 
@@ -156,6 +187,8 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     const Chunks ch{ticket, (n + 63) / 64};
     HintImage slow_img = img;
     VC_PBEGIN();
+    // one chunk per stage: staging two (chunk_loop) adds live registers
+    // that spill in this kernel's hot path (DNS 1.08 -> 1.21 ms)
     for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
         const int64_t base = c * 64;
         const int64_t i = base + lane;
@@ -188,12 +221,10 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const Chunks ch{ticket, (n + 63) / 64};
-    for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
-        const int64_t base = c * 64;
-        const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged = kStage && stage_wave<kStageBytes>(blob, off[base], off[last], stage[w], &a0);
+    VC_PBEGIN();
+    chunk_loop<kStageBytes, true>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
+                            [&](int64_t c, bool staged, uint32_t a0) {
+        const int64_t i = c * 64 + lane;
         if (i < n) {
             const uint32_t a = off[i], e = off[i + 1];
             const bool is_null = null && null[i];
@@ -201,8 +232,8 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
                                        is_null)
                             : cert_one(certs, PtrSrc{blob + a}, int(e - a), is_null);
         }
-        if (kStage) wave_done();
-    }
+    });
+    VC_PEND();
 }
 
 }  // namespace vcd
@@ -216,12 +247,12 @@ hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_
     if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
         hipLaunchKernelGGL(vcd::cert_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<true>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
     else
         hipLaunchKernelGGL(vcd::cert_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<false>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), 0, c.stream,
+                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
     return hipGetLastError();
 }
