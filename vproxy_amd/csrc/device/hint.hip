@@ -97,30 +97,55 @@ struct Chunks {
 // The chunk loop of the string kernels.  A wave stages its chunk's items
 // (contiguous in the blob) into LDS with one coalesced copy; when the next
 // chunk is also this wave's and both fit the stage, it stages the two
-// together and runs body(c, staged, a0) for each from one copy, halving the
-// dependent offset -> blob load round trips per name.
-template <uint32_t kBytes, bool kPair, class Body>
+// together and runs body(c, staged, a0, a, e) for each from one copy.
+// kPre: every offset the two chunks need (the staged span, and each lane's
+// [a, e)) is loaded together up front, so a pair costs one offset and one
+// blob round trip before its first scan instead of four dependent ones
+// (SNI 0.638 -> 0.624 ms); the hint kernel loads each chunk's [a, e) at its
+// body instead, as the four live offsets spill there (0.81 -> 0.92 ms).
+template <uint32_t kBytes, bool kPair, bool kPre, class Body>
 __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
+    const int lane = int(threadIdx.x & 63);
     for (int64_t c = ch.first(w); c < ch.nchunks;) {
         const int64_t base = c * 64;
-        const int64_t end1 = base + 64 < n ? base + 64 : n;
+        const bool pair = kPair && ch.paired(c);
+        // this lane's [A0, E0) and [A1, E1) in chunks c and c + 1 (clamped
+        // to n past the end), and the spans' ends o1 = off[base + 64],
+        // o2 = off[base + 128]
+        uint32_t A0 = 0, E0 = 0, A1 = 0, E1 = 0, o0 = 0, o1 = 0, o2 = 0;
+        if (off) {
+            const int64_t i0 = base + lane, i1 = i0 + 64;
+            if (kPre) {
+                A0 = off[i0 < n ? i0 : n];
+                E0 = off[i0 + 1 < n ? i0 + 1 : n];
+                A1 = off[i1 < n ? i1 : n];
+                E1 = off[i1 + 1 < n ? i1 + 1 : n];
+            }
+            o0 = off[base];
+            o1 = off[base + 64 < n ? base + 64 : n];
+            o2 = off[base + 128 < n ? base + 128 : n];
+        }
         uint32_t a0 = 0;
         int nsub = 1;
         bool staged = false;
         if (blob) {
-            if (kPair && ch.paired(c)) {
-                const int64_t end2 = base + 128 < n ? base + 128 : n;
-                if (stage_wave<kBytes>(blob, off[base], off[end2], stage, &a0)) {
-                    staged = true;
-                    nsub = 2;
-                }
+            if (pair && stage_wave<kBytes>(blob, o0, o2, stage, &a0)) {
+                staged = true;
+                nsub = 2;
             }
-            if (!staged) staged = stage_wave<kBytes>(blob, off[base], off[end1], stage, &a0);
+            if (!staged) staged = stage_wave<kBytes>(blob, o0, o1, stage, &a0);
         }
         VC_PMARK(0);
-        for (int sub = 0; sub < nsub; ++sub) body(c + sub, staged, a0);
+        for (int sub = 0; sub < nsub; ++sub) {
+            if (!kPre && off) {
+                const int64_t i = base + 64 * sub + lane;
+                A0 = off[i < n ? i : n];
+                E0 = off[i + 1 < n ? i + 1 : n];
+            }
+            body(c + sub, staged, a0, kPre && sub ? A1 : A0, kPre && sub ? E1 : E0);
+        }
         wave_done();
         VC_PMARK(5);
         c = ch.next(c + nsub - 1);
@@ -143,8 +168,8 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
-                            [&](int64_t c, bool staged, uint32_t a0) {
+    chunk_loop<kStageBytes, true, false>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
+                                  [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         const int64_t i = c * 64 + lane;
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
@@ -154,7 +179,6 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             if (!general || !has_uri) {
                 // uri null (or no hint-uri anywhere): host-only levels
                 if (has_host) {
-                    const uint32_t a = host_off[i], e = host_off[i + 1];
                     if (staged)
                         r = host_only_fast(img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
                                            int(e - a), p);
@@ -163,12 +187,9 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
                 }
             } else {
                 DStr h{nullptr, -1}, u{nullptr, -1};
-                if (has_host) {
-                    const uint32_t a = host_off[i], e = host_off[i + 1];
-                    h = DStr{host_blob + a, int(e - a)};
-                }
-                const uint32_t a = uri_off[i], e = uri_off[i + 1];
-                u = DStr{uri_blob + a, int(e - a)};
+                if (has_host) h = DStr{host_blob + a, int(e - a)};
+                const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
+                u = DStr{uri_blob + ua, int(ue - ua)};
                 r = hint_general(slow_img, format_host(h), p, format_uri(u));
             }
             out[i] = r;
@@ -222,11 +243,10 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const Chunks ch{ticket, (n + 63) / 64};
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
-                            [&](int64_t c, bool staged, uint32_t a0) {
+    chunk_loop<kStageBytes, true, true>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
+                                  [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         const int64_t i = c * 64 + lane;
         if (i < n) {
-            const uint32_t a = off[i], e = off[i + 1];
             const bool is_null = null && null[i];
             out[i] = staged ? cert_one(certs, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a),
                                        is_null)
