@@ -215,16 +215,31 @@ class RawEvent:
         return ms.value
 
 
-def hip_stream(dev):
+def hip_stream(dev, cus=None):
     """A fresh non-blocking HIP stream wrapped for torch.  HIP spreads the
     streams a process creates round-robin over its hardware queues; three
     created back to back land on three queues, so the kernels on them can
-    run concurrently (torch's pooled streams shared a queue here)."""
+    run concurrently (torch's pooled streams shared a queue here).  `cus`:
+    the CU ids the stream may use (hipExtStreamCreateWithCUMask); the
+    library sizes its grids to the mask."""
     hip = C.CDLL("libamdhip64.so")
     h = C.c_void_p()
-    rc = hip.hipStreamCreateWithFlags(C.byref(h), C.c_uint(1))      # hipStreamNonBlocking
+    if cus is None:
+        rc = hip.hipStreamCreateWithFlags(C.byref(h), C.c_uint(1))  # hipStreamNonBlocking
+    else:
+        words = (C.c_uint32 * 32)()
+        for cu in cus:
+            words[cu // 32] |= 1 << (cu % 32)
+        rc = hip.hipExtStreamCreateWithCUMask(C.byref(h), C.c_uint32(32), words)
     assert rc == 0, rc
     return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def cu_split(total, k):
+    """k CU ids spread evenly over [0, total), and the rest."""
+    pick = sorted({int(i * total / k) for i in range(k)}) if k > 0 else []
+    rest = [c for c in range(total) if c not in set(pick)]
+    return pick, rest
 
 
 class C5Steps:
@@ -242,7 +257,7 @@ class C5Steps:
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream", inflight=3, overlap="finish", gate=False):
+                 finish="stream", inflight=3, overlap="finish", gate=False, pool_cus=0):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -263,6 +278,14 @@ class C5Steps:
         self.bucket = HitCounterBucket([n for _, n in self.csrc], dev) if bucket else None
         if serial:
             self.s_pipe = self.s_hint = self.s_cnt = torch.cuda.current_stream()
+        elif pool_cus > 0:
+            # the pool pass and the counter finish on pool_cus CUs, the
+            # pipeline kernel on the others
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            small, big = cu_split(ncu, pool_cus)
+            self.s_pipe = hip_stream(dev, big)
+            self.s_hint = hip_stream(dev, small)
+            self.s_cnt = hip_stream(dev, small)
         else:
             self.s_pipe, self.s_hint, self.s_cnt = (hip_stream(dev) for _ in range(3))
         self.ev_hint, self.ev_pipe, self.ev_cnt, self.kdone = {}, {}, {}, {}
@@ -539,6 +562,9 @@ def main():
                          "finish (which then overlaps only the pool pass)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight (output and pool buffers)")
+    ap.add_argument("--pool-cus", type=int, default=0,
+                    help="CU partition: the pool pass and the counter finish on this many CUs "
+                         "(a CU-masked stream), the pipeline kernel on the rest (0: no masks)")
     ap.add_argument("--dist", action="store_true",
                     help="use the process group and the counter all-reduce even at N = 1")
     args = ap.parse_args()
@@ -573,7 +599,7 @@ def main():
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
     steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
                     counters=args.counters, finish=args.finish, inflight=args.inflight,
-                    overlap=args.overlap, gate=args.gate)
+                    overlap=args.overlap, gate=args.gate, pool_cus=args.pool_cus)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
@@ -653,7 +679,9 @@ def main():
                                         "HIP streams, counter finish on the counters stream, "
                                         "next pool pass beside the %s" % (
                                             args.inflight, "counter finish" if
-                                            args.overlap == "finish" else "pipeline kernel"))},
+                                            args.overlap == "finish" else "pipeline kernel") +
+                                        (", pool pass and finish on %d CUs, pipeline on the "
+                                         "rest" % args.pool_cus if args.pool_cus else ""))},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()

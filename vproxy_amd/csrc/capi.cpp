@@ -132,10 +132,19 @@ struct vc_ctx {
     }
     // `s` is the caller's hipStream_t; NULL is HIP's null stream, as in
     // every HIP API (torch's default stream reports itself as 0).
+    // CUs a stream may run on: its CU mask (hipExtStreamCreateWithCUMask),
+    // so grids sized to one resident round fill a partitioned stream's share
+    int stream_cus(hipStream_t s) const {
+        uint32_t m[32] = {};
+        if (hipExtStreamGetCUMask(s, 32, m) != hipSuccess) return num_cus;
+        int k = 0;
+        for (uint32_t w : m) k += __builtin_popcount(w);
+        return k > 0 && k < num_cus ? k : num_cus;
+    }
     vc::LaunchCfg cfg(void* s) const {
         vc::LaunchCfg c;
-        c.num_cus = num_cus;
         c.stream = static_cast<hipStream_t>(s);
+        c.num_cus = stream_cus(c.stream);
         c.pool = pool;
         c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
         c.scratch = const_cast<vc::ScratchRing*>(&scratch);
