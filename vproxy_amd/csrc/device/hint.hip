@@ -27,6 +27,9 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_HINT_MINW
 #define VC_HINT_MINW 7
 #endif
+#ifndef VC_HINT_PRE
+#define VC_HINT_PRE 0
+#endif
 #ifndef VC_DNS_MINW
 #define VC_DNS_MINW 6
 #endif
@@ -98,12 +101,13 @@ struct Chunks {
 // (contiguous in the blob) into LDS with one coalesced copy; when the next
 // chunk is also this wave's and both fit the stage, it stages the two
 // together and runs body(c, staged, a0, a, e) for each from one copy.
-// kPre: every offset the two chunks need (the staged span, and each lane's
-// [a, e)) is loaded together up front, so a pair costs one offset and one
-// blob round trip before its first scan instead of four dependent ones
-// (SNI 0.638 -> 0.624 ms); the hint kernel loads each chunk's [a, e) at its
-// body instead, as the four live offsets spill there (0.81 -> 0.92 ms).
-template <uint32_t kBytes, bool kPair, bool kPre, class Body>
+// kPre 2: every offset the two chunks need (the staged span, and each
+// lane's [a, e)) is loaded together up front, so a pair costs one offset and
+// one blob round trip before its first scan instead of four dependent ones
+// (SNI 0.638 -> 0.624 ms).  kPre 0: each chunk's [a, e) is loaded at its
+// body -- the hint kernel, where live offsets spill (all four up front:
+// 0.81 -> 0.92 ms; the first chunk's only, kPre 1: 0.83 ms).
+template <uint32_t kBytes, bool kPair, int kPre, class Body>
 __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
@@ -117,9 +121,11 @@ __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_
         uint32_t A0 = 0, E0 = 0, A1 = 0, E1 = 0, o0 = 0, o1 = 0, o2 = 0;
         if (off) {
             const int64_t i0 = base + lane, i1 = i0 + 64;
-            if (kPre) {
+            if (kPre >= 1) {
                 A0 = off[i0 < n ? i0 : n];
                 E0 = off[i0 + 1 < n ? i0 + 1 : n];
+            }
+            if (kPre >= 2) {
                 A1 = off[i1 < n ? i1 : n];
                 E1 = off[i1 + 1 < n ? i1 + 1 : n];
             }
@@ -139,12 +145,12 @@ __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_
         }
         VC_PMARK(0);
         for (int sub = 0; sub < nsub; ++sub) {
-            if (!kPre && off) {
+            if (off && (kPre == 0 || (kPre == 1 && sub == 1))) {
                 const int64_t i = base + 64 * sub + lane;
                 A0 = off[i < n ? i : n];
                 E0 = off[i + 1 < n ? i + 1 : n];
             }
-            body(c + sub, staged, a0, kPre && sub ? A1 : A0, kPre && sub ? E1 : E0);
+            body(c + sub, staged, a0, kPre == 2 && sub ? A1 : A0, kPre == 2 && sub ? E1 : E0);
         }
         wave_done();
         VC_PMARK(5);
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true, false>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
+    chunk_loop<kStageBytes, true, VC_HINT_PRE>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
                                   [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         const int64_t i = c * 64 + lane;
         if (i < n) {
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const Chunks ch{ticket, (n + 63) / 64};
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true, true>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
+    chunk_loop<kStageBytes, true, 2>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
                                   [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         const int64_t i = c * 64 + lane;
         if (i < n) {
