@@ -539,7 +539,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
-                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "sni", "parse",
+                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "dnsd", "sni", "parse",
                              "switch", "source", "mirror", "mix", "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
@@ -923,6 +923,80 @@ def sub_bench(args, clf, dev, rank, world):
             else:
                 cpu = cpu_rates(run, "M items/s", 4.0, "hostnames of the C4 pool, oracle "
                                 "searchForGroup scan over 100k groups", cap=n)
+    elif args.workload == "dnsd":
+        # DNSServer's drain loop per datagram: UDP SecurityGroup (10k rules)
+        # -> parsePackets -> handleRequest classification over 100k groups
+        # + 50k hosts; queries of one A / AAAA question, 30 % with an EDNS0
+        # OPT record, from random IPv4 senders
+        from vproxy_amd import dnswire as DW
+        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+        clf.compile_upstream(groups)
+        hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
+                          for i in range(50_000))
+        clf.compile_hosts_text(hosts)
+        tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+        a_, na_, ka_ = W.as_ctypes(tcp, V._lib.VcAclRule)
+        b_, nb_, kb_ = W.as_ctypes(udp, V._lib.VcAclRule)
+        V.check(V.lib().vc_compile_acl(clf.h, a_, na_, b_, nb_, 1))
+        qn = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+        trng = np.random.default_rng(W.SEED + 20)
+        qt = np.where(trng.random(len(qn)) < 0.7, DW.A, DW.AAAA)
+        edns = trng.random(len(qn)) < 0.3
+        dgs = [DW.header(qd=1, ar=int(e), ident=i & 0xFFFF) + DW.question(q, int(t)) +
+               (DW.opt_record() if e else b"") for i, (q, t, e) in enumerate(zip(qn, qt, edns))]
+        dblob, doff = W.pack(dgs)
+        n = 16 << 20
+        pidx = np.random.default_rng(W.SEED + 21).integers(0, len(dgs), n)
+        blob, off, nbytes = gather_strings_dev(dblob, doff, pidx, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(23)
+        r4 = dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
+        rport = torch.randint(1024, 65536, (n,), generator=g, device=dev).to(torch.int16)
+        res = {"status": torch.empty(n, dtype=torch.uint8, device=dev),
+               "acl": torch.empty(n, dtype=torch.int32, device=dev),
+               "nq": torch.empty(n, dtype=torch.uint8, device=dev),
+               "qtype": torch.empty((n, V.DNSD_MAXQ), dtype=torch.int16, device=dev),
+               "kind": torch.empty((n, V.DNSD_MAXQ), dtype=torch.uint8, device=dev),
+               "value": torch.empty((n, V.DNSD_MAXQ), dtype=torch.int32, device=dev)}
+        o = V._lib.VcDnsdOut(**{k_: v_.data_ptr() for k_, v_ in res.items()})
+        fn = lambda: V.check(V.lib().vc_dns_datagrams_dev(
+            clf.h, C.c_void_p(blob.data_ptr()), C.c_void_p(off.data_ptr()), n, None,
+            C.c_void_p(r4.data_ptr()), None, C.c_void_p(rport.data_ptr()), C.byref(o), S()))
+        # written: status 1 + acl 4 + nq 1 + one question's qtype 2 + kind 1 + value 4
+        per_unit = nbytes / n + 4 + 4 + 2 + 13
+        unit = ("B/datagram (payload + 4 offset + 4 sender + 2 port in; status, rule, count "
+                "and one question's qtype/kind/value out)")
+        kern = "dnsd_kernel"
+        hb, ho = blob.cpu().numpy(), off.cpu().numpy().view(np.uint32)
+        h4, hp = r4.cpu().numpy().view(np.uint32), rport.cpu().numpy().view(np.uint16)
+        hres = {"status": np.empty(n, np.uint8), "kind": np.empty((n, V.DNSD_MAXQ), np.uint8),
+                "value": np.empty((n, V.DNSD_MAXQ), np.int32)}
+        ho_ = V._lib.VcDnsdOut(**{k_: v_.ctypes.data for k_, v_ in hres.items()})
+        P = lambda x: C.c_void_p(x.ctypes.data)
+        extra["end_to_end_host_buffers_M_per_s"] = end_to_end(
+            lambda: V.check(V.lib().vc_dns_datagrams(clf.h, P(hb), P(ho), n, None, P(h4), None,
+                                                     P(hp), C.byref(ho_))), n)
+        extra["end_to_end_note"] = ("vc_dns_datagrams on pageable host arrays (payloads, "
+                                    "offsets, senders in; status/kind/value out): staged H2D + "
+                                    "kernel + D2H, synchronous")
+        fn()
+        torch.cuda.synchronize()
+        st = res["status"].cpu().numpy()
+        extra["status_mix"] = {nm: round(float((st == c_).mean()), 4) for c_, nm in enumerate(
+            ("answer", "recursive", "response", "rejected", "empty", "malformed", "host"))}
+        if O is not None:
+            og = O.Groups(groups)
+            oh = O.Hosts(O.hosts_parse(hosts)[0])
+
+            def run(k, threads):
+                sb, so = sample_blob(dblob, doff, pidx[:k])
+                t0 = time.perf_counter()
+                O.dnsd_batch_np(tcp, udp, True, oh, og, sb, so, None, h4[:k], None, hp[:k],
+                                nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 4.0, "datagrams of the workload, oracle UDP "
+                            "SecurityGroup scan (10k rules) + parsePackets + hosts lookup and "
+                            "searchForGroup scan over 100k groups", cap=n)
     elif args.workload == "sni":
         _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
         holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]

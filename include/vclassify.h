@@ -35,9 +35,9 @@
  *    (base/src/main/java/vproxybase/processor/Hint.java:146-150) -- is taken
  *    in UTF-16 units of the annotation, so non-ASCII URIs score as in Java.
  *    The exception is DNS: qnames are the wire bytes Formatter.parseDomainName
- *    produces (base/.../dns/Formatter.java:225-257 makes one char per byte,
- *    ISO-8859-1): a qname byte 0xE9 is the char U+00E9 and matches the
- *    annotation bytes C3 A9, as in Java.  vc_compile_hosts_text reads the
+ *    reads (base/.../dns/Formatter.java:225-257 appends (char) b per byte b,
+ *    and the Java byte -> char cast sign-extends): a qname byte 0xE9 is the
+ *    char U+FFE9 and matches the annotation bytes EF BF A9, as in Java.  vc_compile_hosts_text reads the
  *    hosts file as UTF-8, as Resolver.getHosts' InputStreamReader does with a
  *    UTF-8 default charset.
  *  - Rule tables are compiled into immutable snapshots and published
@@ -193,6 +193,46 @@ int vc_dns_classify_dev(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff,
                         uint8_t *out_kind, int32_t *out_value, void *stream);
 int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int64_t n,
                     uint8_t *out_kind, int32_t *out_value);
+
+/* DNSServer's drain loop per datagram (DNSServer.java:457-500): for UDP
+ * payload i = blob[off[i], off[i+1]) from the remote address (family 4/6,
+ * remote4 in IP.ipv4Bytes2Int order or 16 remote6 bytes, 16-byte aligned)
+ * and port: securityGroup.allow(Protocol.UDP, remote, remote port) on the
+ * compiled SecurityGroup's UDP list; `read == 0`; Formatter.parsePackets
+ * (Formatter.java:162-372: header, questions, resources, the A / AAAA /
+ * CNAME / PTR / TXT / SRV rdata checks); then p.isResponse, the opcode and
+ * handleRequest's classification of each question in order (the kinds of
+ * vc_dns_classify) until one sends the packet to runRecursive.  The
+ * answers themselves (server choice, records) stay with the caller. */
+#define VC_DNSD_ANSWER     0  /* handleRequest answers every question locally */
+#define VC_DNSD_RECURSIVE  1  /* runRecursive(p, remote): opcode != QUERY (nq = 0), a
+                                 qtype other than A / AAAA / SRV, or a name no table
+                                 knows (the last evaluated question) */
+#define VC_DNSD_RESPONSE   2  /* p.isResponse: logged and skipped */
+#define VC_DNSD_REJECTED   3  /* securityGroup.allow false: skipped */
+#define VC_DNSD_EMPTY      4  /* read == 0: the loop returns */
+#define VC_DNSD_MALFORMED  5  /* parsePackets threw InvalidDNSPacketException: the loop returns */
+#define VC_DNSD_HOST       6  /* outside this entry point's shapes, run the Java path: a
+                                 second packet in the datagram, more than VC_DNSD_MAXQ
+                                 questions, a qname over 256 chars, a chain of more than
+                                 16 compression pointers (nq = 0) */
+#define VC_DNSD_MAXQ       4
+typedef struct {
+    uint8_t *status;          /* VC_DNSD_* (required) */
+    int32_t *acl;             /* matched UDP rule index, -1 = default (optional) */
+    uint8_t *nq;              /* questions evaluated (optional) */
+    uint16_t *qtype;          /* [n][VC_DNSD_MAXQ] (optional) */
+    uint8_t *kind;            /* [n][VC_DNSD_MAXQ] VC_DNS_* of question q < nq (required) */
+    int32_t *value;           /* [n][VC_DNSD_MAXQ] its value (required) */
+} vc_dnsd_out;
+int vc_dns_datagrams_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
+                         const uint8_t *remote_family, const uint32_t *remote4,
+                         const uint8_t *remote6, const uint16_t *remote_port,
+                         const vc_dnsd_out *out, void *stream);
+int vc_dns_datagrams(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
+                     const uint8_t *remote_family, const uint32_t *remote4,
+                     const uint8_t *remote6, const uint16_t *remote_port,
+                     const vc_dnsd_out *out);
 
 /* ------------------------------------------------------------------------ */
 /* TLS certificate choice by SNI (SSLContextHolder.java:47-186)             */

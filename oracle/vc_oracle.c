@@ -837,9 +837,11 @@ int vo_dns_classify(const vo_hosts *hosts, const vo_group *g, int ng,
                     const char *qwire, int qwlen, int32_t *value)
 {
     /* Formatter.parseDomainName (Formatter.java:225-257) builds the qname
-     * with (char) b per wire byte -- ISO-8859-1.  Strings here are the UTF-8
-     * bytes of the Java strings, so bytes >= 0x80 become two bytes. */
-    char qbuf[1024];
+     * with sb.append((char) b) per wire byte b, a Java byte: the cast
+     * sign-extends (JLS 5.1.4), so a byte c >= 0x80 is the char U+FF00 | c.
+     * Strings here are the UTF-8 bytes of the Java strings: such a char is
+     * three bytes, EF (BE | BF) (80 | c & 3F). */
+    char qbuf[1536];
     const char *qname = qwire;
     int qlen = qwlen, ascii = 1;
     for (int i = 0; i < qwlen; ++i)
@@ -855,7 +857,8 @@ int vo_dns_classify(const vo_hosts *hosts, const vo_group *g, int ng,
             if (c < 0x80) {
                 qbuf[qlen++] = (char)c;
             } else {
-                qbuf[qlen++] = (char)(0xC0 | (c >> 6));
+                qbuf[qlen++] = (char)0xEF;
+                qbuf[qlen++] = (char)(0xBC | (c >> 6));
                 qbuf[qlen++] = (char)(0x80 | (c & 0x3F));
             }
         }
@@ -1516,4 +1519,281 @@ void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups
     parallel_for(n, nthreads, source_range, &c);
     free(order);
     free(size);
+}
+
+/* ------------------------------------------------------------------------ */
+/* DNSServer's drain loop per datagram -- core/src/main/java/vproxy/dns/     */
+/* DNSServer.java:457-500: securityGroup.allow(UDP, remote, remote port),    */
+/* `read == 0`, Formatter.parsePackets (base/.../dns/Formatter.java:162-372) */
+/* with the rdata parsers (dns/rdata/A.java:51-56, AAAA.java:45-50,          */
+/* CNAME.java:51-58, PTR.java:22-29, TXT.java:54-73, SRV.java:27-36), then   */
+/* isResponse / opcode / handleRequest (DNSServer.java:116-166).  Restated   */
+/* the Java way: a recursive parseDomainName over ByteArray views whose      */
+/* get(i) throws past the view's end.  The library's contract (VO_DNSD_HOST) */
+/* is applied on top: more than one packet, more than VO_DNSD_MAXQ          */
+/* questions, a qname of more than VO_DNSD_NAMECAP chars, a pointer chain   */
+/* deeper than VO_DNSD_MAXPTR (Java would recurse on; a loop overflows).    */
+/* ------------------------------------------------------------------------ */
+#define DN_BAD (-1)    /* IndexOutOfBoundsException / InvalidDNSPacketException */
+#define DN_DEEP (-2)   /* deeper than VO_DNSD_MAXPTR pointers */
+
+typedef struct {
+    const uint8_t *raw; int rawlen;      /* rawPacket: the whole datagram */
+    char *sb; int sbn, sbcap;            /* the StringBuilder (chars = wire bytes) */
+} dn_ctx;
+
+/* ByteArray view [vs, vs + vlen) of the datagram: get(i) */
+static int dn_get(const dn_ctx *c, int vs, int vlen, int i, int *b)
+{
+    if (i >= vlen) return DN_BAD;         /* AbstractByteArray.checkBoundForOffset */
+    *b = c->raw[vs + i];
+    return 0;
+}
+
+static void dn_append(dn_ctx *c, int ch)
+{
+    if (c->sb && c->sbn < c->sbcap) c->sb[c->sbn] = (char)ch;
+    c->sbn++;
+}
+
+/* Formatter.parseDomainName(data, rawPacket, offsetHolder), data = view */
+static int dn_name(dn_ctx *c, int vs, int vlen, int *holder, int depth)
+{
+    int len = 0, i = 0, b;
+    for (;; ++i) {
+        if (dn_get(c, vs, vlen, i, &b)) return DN_BAD;
+        if (len == 0) {
+            if (b == 0) {
+                break;
+            } else if ((b & 0xC0) == 0xC0) {             /* is pointer */
+                int off = (b & 0x3F) << 8, b2;
+                if (dn_get(c, vs, vlen, ++i, &b2)) return DN_BAD;
+                off |= b2;
+                if (depth + 1 > VO_DNSD_MAXPTR) return DN_DEEP;
+                /* rawPacket.sub(offset, rawPacket.length() - offset) */
+                int rc = dn_name(c, off, c->rawlen - off, holder, depth + 1);
+                if (rc) return rc;
+                break;                                   /* pointer ends the name */
+            } else {
+                len = b;
+            }
+        } else {
+            dn_append(c, b);
+            --len;
+            if (len == 0) dn_append(c, '.');
+        }
+    }
+    *holder = i + 1;
+    return 0;
+}
+
+static int dn_u16(const dn_ctx *c, int vs, int vlen, int i, int *v)
+{
+    int a, b;
+    if (dn_get(c, vs, vlen, i, &a) || dn_get(c, vs, vlen, i + 1, &b)) return DN_BAD;
+    *v = (a << 8) | b;
+    return 0;
+}
+
+/* DNSClass lookup (Formatter.parseClass) */
+static int dn_class(int clazz, int question)
+{
+    if (clazz == 1 || clazz == 3 || clazz == 4) return 0;
+    if (clazz == 254 || clazz == 255) return question ? 0 : DN_BAD;
+    return DN_BAD;                                       /* unknown class */
+}
+
+/* Formatter.parseQuestion over the view [vs, vs + vlen) */
+static int dn_question(dn_ctx *c, int vs, int vlen, int *used, int *qtype)
+{
+    int holder = 0, qclass, rc = dn_name(c, vs, vlen, &holder, 0);
+    if (rc) return rc;
+    if (dn_u16(c, vs, vlen, holder, qtype) || dn_u16(c, vs, vlen, holder + 2, &qclass))
+        return DN_BAD;
+    /* parseType(qtype, true) never throws (unknown -> OTHER) */
+    if (dn_class(qclass, 1)) return DN_BAD;
+    *used = holder + 4;
+    return 0;
+}
+
+/* Formatter.parseResource over the view [vs, vs + vlen) */
+static int dn_resource(dn_ctx *c, int vs, int vlen, int *used)
+{
+    int holder = 0, type, clazz, rdlen, x, rc = dn_name(c, vs, vlen, &holder, 0);
+    if (rc) return rc;
+    int off = holder;
+    if (dn_u16(c, vs, vlen, off, &type) || dn_u16(c, vs, vlen, off + 2, &clazz) ||
+        dn_u16(c, vs, vlen, off + 4, &x) || dn_u16(c, vs, vlen, off + 6, &x) ||
+        dn_u16(c, vs, vlen, off + 8, &rdlen))
+        return DN_BAD;
+    if (type >= 252 && type <= 255) return DN_BAD;       /* question-only DNSType */
+    if (type != 41 && dn_class(clazz, 0)) return DN_BAD; /* OPT: NOT_CLASS */
+    off += 10;
+    if (vlen - off < rdlen) return DN_BAD;               /* data.sub(offset, rdlen) */
+    const int rs = vs + off;                             /* rdataBytes view [rs, rs + rdlen) */
+    if (type == 1) {                                     /* A */
+        if (rdlen != 4) return DN_BAD;
+    } else if (type == 28) {                             /* AAAA */
+        if (rdlen != 16) return DN_BAD;
+    } else if (type == 5 || type == 12) {                /* CNAME, PTR */
+        int h = 0;
+        rc = dn_name(c, rs, rdlen, &h, 0);
+        if (rc) return rc;
+        if (h != rdlen) return DN_BAD;
+    } else if (type == 16) {                             /* TXT */
+        int o = 0;
+        while (o < rdlen) {
+            int l = c->raw[rs + o];
+            ++o;
+            if (rdlen - o < l) return DN_BAD;
+            o += l;
+        }
+    } else if (type == 33) {                             /* SRV */
+        /* priority/weight/port read from rawPacket (offsets 0..5), then the
+         * target from data.sub(6, len - 6); its offsetHolder is compared with
+         * data.length(), which it can never equal */
+        int h = 0;
+        rc = dn_name(c, rs + 6, rdlen - 6, &h, 0);
+        if (rc) return rc;
+        if (h != rdlen) return DN_BAD;
+    }
+    *used = off + rdlen;
+    return 0;
+}
+
+void vo_dns_datagram(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                     int default_allow, const vo_hosts *hosts, const vo_group *g, int ng,
+                     const uint8_t *p, int n, const uint8_t *ip, int iplen, int port,
+                     vo_dnsd_out *out)
+{
+    memset(out, 0, sizeof *out);
+    int verdict = 0;
+    out->acl = vo_sg_allow(tcp, ntcp, udp, nudp, default_allow, 17, ip, iplen, port, &verdict);
+    if (!verdict) {                                      /* DNSServer.java:469-472 */
+        out->status = VO_DNSD_REJECTED;
+        return;
+    }
+    if (n == 0) {                                        /* :473-476 */
+        out->status = VO_DNSD_EMPTY;
+        return;
+    }
+    dn_ctx c = {p, n, NULL, 0, 0};
+    /* Formatter.parsePackets, first packet (totalOffset 0: data == input) */
+    int qtype[VO_DNSD_MAXQ + 1], qat[VO_DNSD_MAXQ + 1];
+    int st = 0, b2 = 0, b3 = 0, opcode = 0, qd = 0, nres = 0, at = 12, x;
+    if (dn_get(&c, 0, n, 0, &x) || dn_get(&c, 0, n, 1, &x) || dn_get(&c, 0, n, 2, &b2)) {
+        st = DN_BAD;
+    } else {
+        opcode = (b2 >> 3) & 0x0F;                       /* parseOpcode */
+        if (!(opcode == 0 || opcode == 1 || opcode == 2 || opcode == 4 || opcode == 5 ||
+              opcode == 6))
+            st = DN_BAD;
+        else if (dn_get(&c, 0, n, 3, &b3) || (b3 & 0x0F) > 11)     /* parseRCode */
+            st = DN_BAD;
+        else {
+            int an, ns, ar;
+            if (dn_u16(&c, 0, n, 4, &qd) || dn_u16(&c, 0, n, 6, &an) ||
+                dn_u16(&c, 0, n, 8, &ns) || dn_u16(&c, 0, n, 10, &ar))
+                st = DN_BAD;
+            nres = an + ns + ar;
+        }
+    }
+    for (int q = 0; q < qd && !st; ++q) {
+        int used = 0, t = 0;
+        st = dn_question(&c, at, n - at, &used, &t);
+        if (!st && q <= VO_DNSD_MAXQ) {
+            qtype[q] = t;
+            qat[q] = at;
+        }
+        at += used;
+    }
+    for (int k = 0; k < nres && !st; ++k) {
+        int used = 0;
+        st = dn_resource(&c, at, n - at, &used);
+        at += used;
+    }
+    if (st) {
+        out->status = st == DN_BAD ? VO_DNSD_MALFORMED : VO_DNSD_HOST;
+        return;
+    }
+    if (at < n) {                                        /* another packet follows */
+        out->status = VO_DNSD_HOST;
+        return;
+    }
+    if (b2 & 0x80) {                                     /* p.isResponse: :490-493 */
+        out->status = VO_DNSD_RESPONSE;
+        return;
+    }
+    if (opcode != 0) {                                   /* runRecursive: :494-497 */
+        out->status = VO_DNSD_RECURSIVE;
+        return;
+    }
+    if (qd > VO_DNSD_MAXQ) {
+        out->status = VO_DNSD_HOST;
+        return;
+    }
+    out->status = VO_DNSD_ANSWER;
+    for (int q = 0; q < qd; ++q) {                       /* handleRequest */
+        char name[VO_DNSD_NAMECAP];
+        dn_ctx d = {p, n, name, 0, VO_DNSD_NAMECAP};
+        int holder = 0;
+        dn_name(&d, qat[q], n - qat[q], &holder, 0);
+        out->nq = q + 1;
+        out->qtype[q] = qtype[q];
+        if (qtype[q] != 1 && qtype[q] != 28 && qtype[q] != 33) {   /* not A / AAAA / SRV */
+            out->kind[q] = VO_DNS_RECURSIVE;
+            out->status = VO_DNSD_RECURSIVE;
+            return;
+        }
+        if (d.sbn > VO_DNSD_NAMECAP) {                   /* the Java path decides */
+            out->status = VO_DNSD_HOST;
+            out->nq = 0;
+            return;
+        }
+        int32_t v = 0;
+        out->kind[q] = vo_dns_classify(hosts, g, ng, name, d.sbn, &v);
+        out->value[q] = v;
+        if (out->kind[q] == VO_DNS_RECURSIVE) {
+            out->status = VO_DNSD_RECURSIVE;
+            return;
+        }
+    }
+}
+
+typedef struct {
+    const vo_sg_rule *tcp; int ntcp; const vo_sg_rule *udp; int nudp; int dflt;
+    const vo_hosts *hosts; const vo_group *g; int ng;
+    const uint8_t *blob; const uint32_t *off; const uint8_t *fam; const uint32_t *r4;
+    const uint8_t *r6; const uint16_t *rport; vo_dnsd_out *out;
+} dnsd_batch_ctx;
+
+static void dnsd_range(void *p, int64_t lo, int64_t hi)
+{
+    dnsd_batch_ctx *c = (dnsd_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        uint8_t ip[16];
+        int iplen = 4;
+        if (c->fam && c->fam[i] == 6) {
+            memcpy(ip, c->r6 + 16 * i, 16);
+            iplen = 16;
+        } else {
+            const uint32_t r = c->r4[i];
+            ip[0] = (uint8_t)(r >> 24); ip[1] = (uint8_t)(r >> 16);
+            ip[2] = (uint8_t)(r >> 8); ip[3] = (uint8_t)r;
+        }
+        vo_dns_datagram(c->tcp, c->ntcp, c->udp, c->nudp, c->dflt, c->hosts, c->g, c->ng,
+                        c->blob + c->off[i], (int)(c->off[i + 1] - c->off[i]), ip, iplen,
+                        c->rport[i], &c->out[i]);
+    }
+}
+
+void vo_dnsd_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                   int default_allow, const vo_hosts *hosts, const vo_group *g, int ng,
+                   const uint8_t *blob, const uint32_t *off, int64_t n, const uint8_t *family,
+                   const uint32_t *remote4, const uint8_t *remote6, const uint16_t *remote_port,
+                   vo_dnsd_out *out, int nthreads)
+{
+    dnsd_batch_ctx c = {tcp, ntcp, udp, nudp, default_allow, hosts, g, ng, blob, off, family,
+                        remote4, remote6, remote_port, out};
+    parallel_for(n, nthreads, dnsd_range, &c);
 }

@@ -262,4 +262,28 @@ void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups
 #ifdef __cplusplus
 }
 #endif
+
+/* DNSServer's drain loop per datagram (DNSServer.java:457-500, Formatter.
+ * parsePackets, handleRequest); the status codes equal vclassify.h's
+ * VC_DNSD_*.  qtype/kind/value are set for the first nq questions. */
+enum { VO_DNSD_ANSWER = 0, VO_DNSD_RECURSIVE = 1, VO_DNSD_RESPONSE = 2, VO_DNSD_REJECTED = 3,
+       VO_DNSD_EMPTY = 4, VO_DNSD_MALFORMED = 5, VO_DNSD_HOST = 6 };
+#define VO_DNSD_MAXQ 4
+#define VO_DNSD_NAMECAP 256
+#define VO_DNSD_MAXPTR 16
+typedef struct {
+    int32_t status, acl, nq;
+    int32_t qtype[VO_DNSD_MAXQ], kind[VO_DNSD_MAXQ], value[VO_DNSD_MAXQ];
+} vo_dnsd_out;
+void vo_dns_datagram(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                     int default_allow, const vo_hosts *hosts, const vo_group *g, int ng,
+                     const uint8_t *p, int n, const uint8_t *ip, int iplen, int port,
+                     vo_dnsd_out *out);
+/* remote4 in IP.ipv4Bytes2Int order; family may be NULL (all IPv4) */
+void vo_dnsd_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int nudp,
+                   int default_allow, const vo_hosts *hosts, const vo_group *g, int ng,
+                   const uint8_t *blob, const uint32_t *off, int64_t n, const uint8_t *family,
+                   const uint32_t *remote4, const uint8_t *remote6, const uint16_t *remote_port,
+                   vo_dnsd_out *out, int nthreads);
+
 #endif

@@ -14,6 +14,7 @@ here executes reference code.  Re-run this script to regenerate the JSON.
 import ipaddress
 import json
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -211,17 +212,20 @@ def kats():
                      ["x.vproxy.local.", 4, 0],
                      ["nothing.org.", 5, 0]]},
     ]
-    # DNS qnames as wire bytes (hex): Formatter.parseDomainName (Formatter.java:225-257)
-    # makes one char per byte ((char) b, ISO-8859-1); annotations and hosts-file keys
-    # are Java strings (UTF-8 across the boundary, Resolver reads the file in UTF-8)
+    # DNS qnames as wire bytes (hex): Formatter.parseDomainName (Formatter.java:230,247)
+    # appends (char) b for each label byte b, a Java byte: the cast sign-extends
+    # (JLS 5.1.4 byte -> int -> char), so a byte c >= 0x80 is the char U+FF00 | c
+    # (0xE9 -> U+FFE9), not ISO-8859-1.  Annotations and hosts-file keys are Java
+    # strings (UTF-8 across the boundary, Resolver reads the file in UTF-8).
     dns_wire = [
-        {"source": "Formatter.java:225-257 (char) b + DNSServer.java:116-166",
-         "groups": [[{}, {"host": "caf\u00e9.com"}], [{}, {"host": "b.com"}]],
-         "hosts": [["h\u00f4te.local.", 7], ["h\u00f4te.local", 7]],
-         "queries": [[b"caf\xe9.com.".hex(), 2, 0],            # U+00E9 == the annotation's char
-                     [b"x.caf\xe9.com.".hex(), 2, 0],
-                     [b"caf\xc3\xa9.com.".hex(), 5, 0],        # UTF-8 on the wire: "caf\u00c3\u00a9"
-                     [b"h\xf4te.local.".hex(), 1, 7],
+        {"source": "Formatter.java:225-257 (char) b (sign-extended) + DNSServer.java:116-166",
+         "groups": [[{}, {"host": "caf\u00e9.com"}], [{}, {"host": "b.com"}],
+                    [{}, {"host": "caf\uffe9.com"}]],
+         "hosts": [["h\u00f4te.local.", 7], ["h\ufff4te.local.", 8]],
+         "queries": [[b"caf\xe9.com.".hex(), 2, 2],            # U+FFE9: the third group, not the first
+                     [b"x.caf\xe9.com.".hex(), 2, 2],
+                     [b"caf\xc3\xa9.com.".hex(), 5, 0],        # "caf\uffc3\uffa9.com": no key
+                     [b"h\xf4te.local.".hex(), 1, 8],          # U+FFF4, the second hosts key
                      [b"b.com.".hex(), 2, 1],
                      [b"\xff.vproxy.local.".hex(), 4, 0],
                      [b"\xe9\xe9.1.2.3.".hex(), 5, 0]]},
@@ -260,7 +264,102 @@ def kats():
     dump("kats.json", {"mask_match": [{"expect": e, "input": i, "net": n}
                                       for e, i, n in mask_match],
                        "hints": hints, "dns": dns, "dns_wire": dns_wire,
-                       "security_group": sg})
+                       "security_group": sg, "dns_datagrams": dns_datagrams()})
+
+
+def dns_datagrams():
+    """DNSServer's drain loop per datagram (DNSServer.java:457-500) over wire
+    packets built as Formatter.format lays them out (vproxy_amd/dnswire.py).  The
+    first two are TestResolver.packet's packet (TestResolver.java:41-66,
+    which asserts it parses back into exactly one packet); the expected
+    outcomes of the others are hand-derived from Formatter.parsePackets /
+    parseHeader / parseQuestion / parseResource / parseDomainName
+    (Formatter.java:162-372), the rdata parsers (dns/rdata/*.java) and
+    DNSServer.handleRequest (DNSServer.java:116-166).  Status codes are
+    vclassify.h's VC_DNSD_*; per question [qtype, VC_DNS_* kind, value]."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from vproxy_amd import dnswire as W
+    ANSWER, RECURSIVE, RESPONSE, REJECTED, EMPTY, MALFORMED, HOST = range(7)
+    K_HOSTS, K_GROUP, K_IP, K_INTERNAL, K_REC = 1, 2, 3, 4, 5
+    q = W.query
+    ex = [("example.com.", W.A)]
+    ok = "1.2.3.4"
+    cases = [
+        ("TestResolver.packet as sent (a response)", W.reference_packet(True), ok, 5353,
+         RESPONSE, 0, []),
+        ("TestResolver.packet as a query: qtype ANY -> runRecursive", W.reference_packet(False),
+         ok, 5353, RECURSIVE, 1, [[255, K_REC, 0]]),
+        ("A for a hint-host", q(ex), ok, 5353, ANSWER, 1, [[1, K_GROUP, 0]]),
+        ("AAAA for a hosts name", q([("db.example.com.", W.AAAA)]), ok, 5353, ANSWER, 1,
+         [[28, K_HOSTS, 5]]),
+        ("SRV for a sub-domain", q([("a.test.com.", W.SRV)]), ok, 5353, ANSWER, 1,
+         [[33, K_GROUP, 1]]),
+        ("A for an IPv4 literal", q([("1.2.3.4.", W.A)]), ok, 5353, ANSWER, 1, [[1, K_IP, 4]]),
+        ("A for .vproxy.local", q([("x.vproxy.local.", W.A)]), ok, 5353, ANSWER, 1,
+         [[1, K_INTERNAL, 0]]),
+        ("second of three questions unknown: recursive, third not evaluated",
+         q([("example.com.", W.A), ("nothing.org.", W.A), ("test.com.", W.A)]), ok, 5353,
+         RECURSIVE, 2, [[1, K_GROUP, 0], [1, K_REC, 0]]),
+        ("MX query: default case -> recursive", q([("example.com.", W.MX)]), ok, 5353,
+         RECURSIVE, 1, [[15, K_REC, 0]]),
+        ("opcode STATUS -> runRecursive", q(ex, opcode=2), ok, 5353, RECURSIVE, 0, []),
+        ("opcode 3: parseOpcode throws", q(ex, opcode=3), ok, 5353, MALFORMED, 0, []),
+        ("rcode 12: parseRCode throws", q(ex, rcode=12), ok, 5353, MALFORMED, 0, []),
+        ("11-byte header", q(ex)[:11], ok, 5353, MALFORMED, 0, []),
+        ("read == 0", b"", ok, 5353, EMPTY, 0, []),
+        ("sender in 10.0.0.0/8 (UDP rule 0 denies)", q(ex), "10.1.2.3", 5353, REJECTED, 0, []),
+        ("sender port 9999 (UDP rule 1 denies)", q(ex), ok, 9999, REJECTED, 0, []),
+        ("IPv6 sender ::1: the v4 rules do not match, default allow", q(ex), "::1", 5353,
+         ANSWER, 1, [[1, K_GROUP, 0]]),
+        ("question class CH", q([("example.com.", W.A, W.CH)]), ok, 5353, ANSWER, 1,
+         [[1, K_GROUP, 0]]),
+        ("question class 2: parseClass throws", q([("example.com.", W.A, 2)]), ok, 5353,
+         MALFORMED, 0, []),
+        ("question class ANY", q([("example.com.", W.A, W.ANY_CLASS)]), ok, 5353, ANSWER, 1,
+         [[1, K_GROUP, 0]]),
+        ("second question compressed: www + pointer to the first name",
+         W.header(qd=2) + W.question("example.com.", W.A) +
+         W.raw_question(b"\x03www\xc0\x0c", W.AAAA), ok, 5353, ANSWER, 2,
+         [[1, K_GROUP, 0], [28, K_GROUP, 0]]),
+        ("pointer to itself: Java recurses until its stack overflows",
+         W.header(qd=1) + W.raw_question(b"\xc0\x0c"), ok, 5353, HOST, 0, []),
+        ("pointer past the end of the datagram", W.header(qd=1) + W.raw_question(b"\xc0\xff"),
+         ok, 5353, MALFORMED, 0, []),
+        ("five questions", q(ex * 5), ok, 5353, HOST, 0, []),
+        ("two packets in one datagram", q(ex) + q(ex), ok, 5353, HOST, 0, []),
+        ("EDNS0 OPT record in the additional section", q(ex, extra=W.opt_record(), ar=1), ok,
+         5353, ANSWER, 1, [[1, K_GROUP, 0]]),
+        ("answer of type ANY: question-only type in a resource",
+         q(ex, extra=W.resource("a.", W.ANY, b""), an=1), ok, 5353, MALFORMED, 0, []),
+        ("A record with a 5-byte rdata", q(ex, extra=W.resource("a.", W.A, bytes(5)), an=1), ok,
+         5353, MALFORMED, 0, []),
+        ("SRV record: its target's offset is compared with the whole rdata length",
+         q(ex, extra=W.resource("a.", W.SRV, bytes(6) + W.name("t.example.")), an=1), ok, 5353,
+         MALFORMED, 0, []),
+        ("TXT string longer than its rdata", q(ex, extra=W.resource("a.", W.TXT, b"\x05ab"),
+                                                an=1), ok, 5353, MALFORMED, 0, []),
+        ("CNAME record", q(ex, extra=W.resource("a.", W.CNAME, W.name("b.c.")), an=1), ok,
+         5353, ANSWER, 1, [[1, K_GROUP, 0]]),
+        ("CNAME rdata with a trailing byte", q(ex, extra=W.resource(
+            "a.", W.CNAME, W.name("b.c.") + b"\0"), an=1), ok, 5353, MALFORMED, 0, []),
+        ("resource of class NONE: question-only class",
+         q(ex, extra=W.resource("a.", W.A, bytes(4), rclass=W.NONE_CLASS), an=1), ok, 5353,
+         MALFORMED, 0, []),
+        ("response whose answer is malformed: parsePackets throws first",
+         q(ex, extra=W.resource("a.", W.A, bytes(3)), an=1, response=True), ok, 5353,
+         MALFORMED, 0, []),
+        ("qname of 305 chars", q([((("x" * 60) + ".") * 5, W.A)]), ok, 5353, HOST, 0, []),
+        ("question cut inside its qtype", q(ex)[:-3], ok, 5353, MALFORMED, 0, []),
+    ]
+    return {"source": "TestResolver.java:41-112; Formatter.java:162-372; DNSServer.java:116-166,"
+                      "457-500 (hand-derived)",
+            "groups": [[{}, {"host": "example.com"}], [{}, {"host": "test.com"}]],
+            "hosts": [["localhost.", 0], ["localhost", 0], ["db.example.com.", 5]],
+            "udp_rules": [["deny-ten", "10.0.0.0/8", 0, 65535, False],
+                          ["deny-9999", "0.0.0.0/0", 9999, 9999, False]],
+            "default_allow": True,
+            "cases": [{"what": w, "datagram": d.hex(), "remote": r, "port": port, "status": st,
+                       "nq": nq, "questions": qs} for w, d, r, port, st, nq, qs in cases]}
 
 
 if __name__ == "__main__":

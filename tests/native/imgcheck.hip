@@ -23,6 +23,8 @@ AclFamilyImage fam_img(const vc::AclFamilyBuilt& b) {
     f.bounds6 = b.bounds6.data();
     f.desc = b.desc.data();
     f.pieces = b.pieces.data();
+    f.dir4 = b.dir4.empty() ? nullptr : b.dir4.data();
+    f.dir_bits = b.dir_bits;
     f.nb = b.nb;
     f.np = int32_t(b.pieces.size() / 2);
     return f;
@@ -79,7 +81,11 @@ int ic_acl(const vc_acl_rule* tcp, int nt, const vc_acl_rule* udp, int nu, int d
         AclFamilyImage f = fam_img(b.fam[l][family == 4 ? 0 : 1]);
         int j;
         if (family == 4) {
-            j = bsearch_u32(f.bounds4, f.nb, static_cast<const uint32_t*>(src)[i]);
+            // through the bucket directory (when built), checked against the
+            // whole binary search
+            const uint32_t key = static_cast<const uint32_t*>(src)[i];
+            j = acl4_interval(f, key);
+            if (j != bsearch_u32(f.bounds4, f.nb, key)) return -100;
         } else {
             uint64_t hi, lo;
             v6_key(static_cast<const uint4*>(src)[i], &hi, &lo);

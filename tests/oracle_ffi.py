@@ -69,6 +69,11 @@ class VoHosts(C.Structure):
                 ("values", C.POINTER(C.c_int32)), ("n", C.c_int)]
 
 
+class VoDnsdOut(C.Structure):
+    _fields_ = [("status", C.c_int32), ("acl", C.c_int32), ("nq", C.c_int32),
+                ("qtype", C.c_int32 * 4), ("kind", C.c_int32 * 4), ("value", C.c_int32 * 4)]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -138,6 +143,12 @@ def lib():
         L.vo_mirror_switch_batch.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int, vp, vp, i64,
                                              C.c_int, vp, C.c_int]
         L.vo_source_batch.argtypes = [P(VoServer), vp, C.c_int, C.c_int, vp, vp, i64, vp, C.c_int]
+        L.vo_dns_datagram.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int,
+                                      P(VoHosts), P(VoGroup), C.c_int, vp, C.c_int, vp, C.c_int,
+                                      C.c_int, P(VoDnsdOut)]
+        L.vo_dnsd_batch.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int,
+                                    P(VoHosts), P(VoGroup), C.c_int, vp, vp, i64, vp, vp, vp, vp,
+                                    P(VoDnsdOut), C.c_int]
         _lib = L
     return _lib
 
@@ -665,3 +676,30 @@ def source_batch_np(groups, view, grp, src4, nthreads=1):
                           _ptr(np.ascontiguousarray(grp, np.int32)), _ptr(_u32a(src4)), n,
                           _ptr(out), nthreads)
     return out
+
+
+def dnsd_batch_np(tcp, udp, dflt, hosts, groups, blob, off, family, remote4, remote6,
+                  remote_port, nthreads=1):
+    """DNSServer drain loop per datagram (vo_dnsd_batch) -> dict of numpy
+    arrays shaped like Classifier.dns_datagrams' (kind/value/qtype only for
+    q < nq; the rest zero)."""
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    h = hosts if isinstance(hosts, Hosts) else Hosts(hosts)
+    n = len(off) - 1
+    out = (VoDnsdOut * max(1, n))()
+    t = tcp if len(tcp) else np.zeros(1, tcp.dtype)
+    u = udp if len(udp) else np.zeros(1, udp.dtype)
+    fam = None if family is None else np.ascontiguousarray(family, np.uint8)
+    r6 = None if remote6 is None else np.ascontiguousarray(remote6, np.uint8)
+    lib().vo_dnsd_batch(_cast(t, VoSgRule), len(tcp), _cast(u, VoSgRule), len(udp),
+                        1 if dflt else 0, C.byref(h.h), g.arr, g.n,
+                        _ptr(np.ascontiguousarray(blob, np.uint8)), _ptr(_u32a(off)), n,
+                        _ptr(fam), _ptr(_u32a(remote4)), _ptr(r6),
+                        _ptr(np.ascontiguousarray(remote_port, np.uint16)), out, nthreads)
+    a = np.frombuffer(out, dtype=np.int32).reshape(max(1, n), 15)[:n]
+    nq = a[:, 2].astype(np.uint8)
+    live = np.arange(4)[None, :] < nq[:, None]
+    return {"status": a[:, 0].astype(np.uint8), "acl": a[:, 1].copy(), "nq": nq,
+            "qtype": np.where(live, a[:, 3:7], 0).astype(np.uint16),
+            "kind": np.where(live, a[:, 7:11], 0).astype(np.uint8),
+            "value": np.where(live, a[:, 11:15], 0).astype(np.int32)}

@@ -1,0 +1,146 @@
+"""GPU tier: vc_dns_datagrams[_dev] -- DNSServer's drain loop per datagram
+(core/src/main/java/vproxy/dns/DNSServer.java:457-500) in one kernel:
+
+    securityGroup.allow(Protocol.UDP, remote.getAddress(), remote.getPort())
+    `read == 0`
+    Formatter.parsePackets (base/.../dns/Formatter.java:162-372, rdata/*.java)
+    isResponse / opcode / handleRequest's question classification
+        (DNSServer.java:116-166)
+
+against the hand-derived KATs (tests/golden/kats.json, TestResolver.packet's
+packet among them) and the oracle's restatement (vo_dnsd_batch) over random
+and mutated datagrams from IPv4 and IPv6 senders.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from vproxy_amd import dnswire as DW
+import oracle_ffi as O
+import vproxy_amd as V
+from vproxy_amd import workloads as W
+
+from cases import rule_row
+from test_dnsd_cpu import check_against_kats, kat_inputs, kats, udp_rules
+
+pytestmark = pytest.mark.gpu
+
+
+def _compile_acl(clf, tcp, udp, dflt):
+    a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+    b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1 if dflt else 0))
+
+
+def _same(got, want, nq_from="want"):
+    """status / acl / nq equal everywhere; qtype / kind / value for q < nq"""
+    for k in ("status", "acl", "nq"):
+        np.testing.assert_array_equal(np.asarray(got[k]), want[k], err_msg=k)
+    live = np.arange(V.DNSD_MAXQ)[None, :] < want["nq"][:, None]
+    for k in ("qtype", "kind", "value"):
+        g = np.asarray(got[k]).astype(want[k].dtype)
+        np.testing.assert_array_equal(np.where(live, g, 0), want[k], err_msg=k)
+
+
+def _cpu(res):
+    return {k: v.cpu().numpy() for k, v in res.items()}
+
+
+def test_dns_datagram_kats():
+    import torch
+    k = kats()
+    clf = V.Classifier(0)
+    try:
+        _compile_acl(clf, np.zeros(0, W.RULE_DT), udp_rules(k["udp_rules"]), k["default_allow"])
+        clf.compile_upstream(k["groups"])
+        clf.compile_hosts([tuple(x) for x in k["hosts"]])
+        cases, blob, off, fam, r4, r6, port = kat_inputs(k)
+        res = clf.dns_datagrams((blob, off), r4, port, remote6=r6, remote_family=fam)
+        check_against_kats(res, cases)
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        dres = _cpu(clf.dns_datagrams((T(blob), T(off.view(np.int32))), T(r4.view(np.int32)),
+                                      T(port.view(np.int16)), remote6=T(r6),
+                                      remote_family=T(fam)))
+        dres["qtype"] = dres["qtype"].view(np.uint16)
+        check_against_kats(dres, cases)
+    finally:
+        clf.close()
+
+
+def _remotes(rng, n):
+    fam = np.where(rng.random(n) < 0.75, 4, 6).astype(np.uint8)
+    base = rng.choice(np.array([0x0A000000, 0x0A010000, 0xC0A80000, 0x08080000], np.uint64), n)
+    r4 = (base | rng.integers(0, 1 << 16, n).astype(np.uint64)).astype(np.uint32)
+    r6 = np.zeros((n, 16), np.uint8)
+    k = rng.integers(0, 2, n)
+    r6[k == 0, 10:12] = 0xFF                         # ::ffff:a.b.c.d
+    r6[k == 0, 12:] = W.v4_to_bytes(r4)[k == 0]
+    r6[k == 1, :4] = [0x20, 0x01, 0x0D, 0xB8]
+    r6[:, 14:] = rng.integers(0, 256, (n, 2))
+    port = np.where(rng.random(n) < 0.9, 53, rng.integers(0, 65536, n)).astype(np.uint16)
+    return fam, r4, r6, port
+
+
+@pytest.mark.parametrize("shift", [0, 1])
+def test_dns_datagrams_vs_oracle(shift):
+    """Random queries over group / hosts / literal / internal / unknown names
+    (1-5 questions, compression pointers, OPT and answer records), a quarter
+    of them mutated (flipped byte, truncated, extended); shift 1 puts the
+    blob at an odd address (the unstaged kernel)."""
+    import torch
+    rng = np.random.default_rng(23)
+    prng = random.Random(29)
+    clf = V.Classifier(0)
+    try:
+        udp = np.concatenate([rule_row(*r) for r in (
+            ("10.0.0.0/8", 0, 65535, False), ("8.8.0.0/16", 53, 53, True),
+            ("0.0.0.0/0", 1000, 2000, False), ("::ffff:192.168.0.0/112", 0, 65535, False),
+            ("2001:db8::/32", 0, 52, False))])
+        tcp = np.concatenate([rule_row("0.0.0.0/0", 0, 65535, False)])
+        _compile_acl(clf, tcp, udp, True)
+        groups, ghosts = W.gen_groups(3000, 41)
+        clf.compile_upstream(groups)
+        hosts = [(h + ".", i) for i, h in enumerate(ghosts[:40])] + [("localhost.", 900)]
+        clf.compile_hosts(hosts)
+        names = W.gen_hostnames(ghosts, 4000, 42, dns=True)
+        names += [b"1.2.3.4.", b"::1.", b"x.vproxy.local.", b"nope.org.", b"caf\xe9.com.",
+                  b"localhost.", b"."]
+        dg = [DW.random_datagram(prng, names) for _ in range(60013)]
+        dg += [DW.reference_packet(True), DW.reference_packet(False), b""]
+        n = len(dg)
+        fam, r4, r6, port = _remotes(rng, n)
+        blob, off = W.pack(dg)
+        want = O.dnsd_batch_np(tcp, udp, True, hosts, groups, blob, off, fam, r4, r6, port,
+                               nthreads=16)
+        st = want["status"]
+        for s in range(7):
+            assert (st == s).sum() > 0, s          # every outcome occurs
+        # device entry point (blob shifted by `shift` bytes)
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        dblob = torch.zeros(len(blob) + 16, dtype=torch.uint8, device="cuda")
+        dblob[shift:shift + len(blob)] = T(blob)
+        res = _cpu(clf.dns_datagrams((dblob[shift:], T(off.view(np.int32))),
+                                     T(r4.view(np.int32)), T(port.view(np.int16)),
+                                     remote6=T(r6), remote_family=T(fam)))
+        res["qtype"] = res["qtype"].view(np.uint16)
+        _same(res, want)
+        # the host entry point gives the same
+        _same(clf.dns_datagrams((blob, off), r4, port, remote6=r6, remote_family=fam), want)
+    finally:
+        clf.close()
+
+
+def test_dns_datagrams_bad_arguments():
+    import ctypes as C
+    clf = V.Classifier(0)
+    try:
+        one = C.c_void_p(1)
+        o = V._lib.VcDnsdOut()                          # no status / kind / value arrays
+        rc = V.lib().vc_dns_datagrams_dev(clf.h, one, one, 1, None, one, None, one,
+                                          C.byref(o), None)
+        assert rc != 0                                  # EINVAL, nothing launched
+        rc = V.lib().vc_dns_datagrams(clf.h, None, None, 1, None, None, None, None, C.byref(o))
+        assert rc != 0
+    finally:
+        clf.close()

@@ -8,6 +8,8 @@ from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,
                    NotFoundException, StateError, VcError, XException, check, lib,
                    COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP, PROTO_TCP, PROTO_UDP,
                    DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE,
+                   DNSD_ANSWER, DNSD_RECURSIVE, DNSD_RESPONSE, DNSD_REJECTED, DNSD_EMPTY,
+                   DNSD_MALFORMED, DNSD_HOST, DNSD_MAXQ,
                    SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6,
                    LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401

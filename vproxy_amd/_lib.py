@@ -16,6 +16,10 @@ VC_OK, VC_EINVAL, VC_EEXIST, VC_ENOTFOUND, VC_EXEXC, VC_EDEVICE, VC_ENOMEM, VC_E
 PROTO_TCP, PROTO_UDP = 6, 17
 DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE = 1, 2, 3, 4, 5
 COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP = 0, 1, 2
+# vc_dns_datagrams status codes (VC_DNSD_*)
+(DNSD_ANSWER, DNSD_RECURSIVE, DNSD_RESPONSE, DNSD_REJECTED, DNSD_EMPTY, DNSD_MALFORMED,
+ DNSD_HOST) = range(7)
+DNSD_MAXQ = 4
 SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6 = 0, 4, 6
 LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6 = 0, 1, 4, 6
 
@@ -44,6 +48,13 @@ class VcPktOut(C.Structure):
                 ("proto", C.c_void_p), ("vni", C.c_void_p), ("ether_type", C.c_void_p),
                 ("src4", C.c_void_p), ("dst4", C.c_void_p), ("src6", C.c_void_p),
                 ("dst6", C.c_void_p), ("sport", C.c_void_p), ("dport", C.c_void_p)]
+
+
+class VcDnsdOut(C.Structure):
+    """vc_dnsd_out: per-datagram status / rule / question count, and per
+    question [n][VC_DNSD_MAXQ] qtype / kind / value."""
+    _fields_ = [("status", C.c_void_p), ("acl", C.c_void_p), ("nq", C.c_void_p),
+                ("qtype", C.c_void_p), ("kind", C.c_void_p), ("value", C.c_void_p)]
 
 
 class VcPackets(C.Structure):
@@ -190,6 +201,8 @@ def lib():
                                              vp, vp, vp, vp]
         L.vc_switch_classify.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, i32, P(VcPktOut), vp,
                                          vp, vp]
+        L.vc_dns_datagrams_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut), vp]
+        L.vc_dns_datagrams.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut)]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

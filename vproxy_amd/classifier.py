@@ -18,8 +18,8 @@ import ipaddress
 import numpy as np
 
 from . import _lib
-from ._lib import (PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcGroupAnnos, VcNet, VcPktOut,
-                   VcServer, check, lib)
+from ._lib import (DNSD_MAXQ, PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcDnsdOut,
+                   VcGroupAnnos, VcNet, VcPktOut, VcServer, check, lib)
 
 HINT_HOST = "vproxy/hint-host"   # AnnotationKeys.ServerGroup_HintHost
 HINT_PORT = "vproxy/hint-port"   # AnnotationKeys.ServerGroup_HintPort
@@ -497,6 +497,48 @@ class Classifier:
         val = np.empty(n, np.int32)
         check(lib().vc_dns_classify(self.h, _ptr(qb), _ptr(qo), n, _ptr(kind), _ptr(val)))
         return kind, val
+
+    def dns_datagrams(self, datagrams, remote4, remote_port, remote6=None, remote_family=None):
+        """DNSServer's drain loop per datagram (vc_dns_datagrams[_dev],
+        DNSServer.java:457-500): securityGroup.allow(UDP, remote, remote
+        port), Formatter.parsePackets, isResponse / opcode / handleRequest's
+        question classification.  datagrams: (blob, off) torch CUDA tensors
+        or numpy arrays, or a list of bytes; remote4 uint32 keys, remote_port
+        uint16, remote6 [n, 16] uint8 and remote_family uint8 (4/6) optional.
+        Returns dict(status, acl, nq, qtype[n, MAXQ], kind[n, MAXQ],
+        value[n, MAXQ]); kind / value / qtype are meaningful for q < nq."""
+        if isinstance(datagrams, (list, tuple)) and not (
+                len(datagrams) == 2 and hasattr(datagrams[1], "dtype")):
+            blob, off, _ = pack_strings(datagrams)
+        else:
+            blob, off = datagrams
+        n = len(off) - 1
+        if _is_dev(blob):
+            import torch
+            dev = blob.device
+            mk = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)
+            res = {"status": mk(n, torch.uint8), "acl": mk(n, torch.int32),
+                   "nq": mk(n, torch.uint8), "qtype": mk((n, DNSD_MAXQ), torch.int16),
+                   "kind": mk((n, DNSD_MAXQ), torch.uint8),
+                   "value": mk((n, DNSD_MAXQ), torch.int32)}
+            o = VcDnsdOut(**{k: v.data_ptr() for k, v in res.items()})
+            check(lib().vc_dns_datagrams_dev(self.h, _ptr(blob), _ptr(off), n,
+                                             _ptr(remote_family), _ptr(remote4), _ptr(remote6),
+                                             _ptr(remote_port), C.byref(o), _stream()))
+            return res
+        res = {"status": np.empty(n, np.uint8), "acl": np.empty(n, np.int32),
+               "nq": np.empty(n, np.uint8), "qtype": np.zeros((n, DNSD_MAXQ), np.uint16),
+               "kind": np.zeros((n, DNSD_MAXQ), np.uint8),
+               "value": np.zeros((n, DNSD_MAXQ), np.int32)}
+        keep = [np.ascontiguousarray(blob, np.uint8), np.ascontiguousarray(off, np.uint32),
+                np.ascontiguousarray(remote4, np.uint32),
+                np.ascontiguousarray(remote_port, np.uint16)]
+        fam = None if remote_family is None else np.ascontiguousarray(remote_family, np.uint8)
+        r6 = None if remote6 is None else np.ascontiguousarray(remote6, np.uint8).reshape(-1, 16)
+        o = VcDnsdOut(**{k: v.ctypes.data for k, v in res.items()})
+        check(lib().vc_dns_datagrams(self.h, _ptr(keep[0]), _ptr(keep[1]), n, _ptr(fam),
+                                     _ptr(keep[2]), _ptr(r6), _ptr(keep[3]), C.byref(o)))
+        return res
 
     def pipeline_v4(self, proto, src4, dst4, dport, host_id, pool_group, outs=None,
                     want_allow=False, kernel_done_event=None, count_stream=None):

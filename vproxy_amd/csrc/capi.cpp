@@ -340,6 +340,8 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
             fi.bounds6 = f == 1 ? s->upload(fb.bounds6, &e) : nullptr;
             fi.desc = s->upload(fb.desc, &e);
             fi.pieces = s->upload(fb.pieces, &e);
+            fi.dir4 = fb.dir4.empty() ? nullptr : s->upload(fb.dir4, &e);
+            fi.dir_bits = fb.dir4.empty() ? 0 : fb.dir_bits;
             fi.nb = fb.nb;
             fi.np = static_cast<int32_t>(fb.pieces.size() / 2);
         }
@@ -1028,6 +1030,69 @@ int vc_parse_packets_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, 
         return fail(VC_EINVAL, "src6/dst6 must be 16-byte aligned");
     hipError_t e = vc::launch_packets(ctx->cfg(stream), blob, off, n, layer, *out);
     return e == hipSuccess ? VC_OK : hip_fail(e, "packet launch");
+}
+
+int vc_dns_datagrams_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
+                         const uint8_t* remote_family, const uint32_t* remote4,
+                         const uint8_t* remote6, const uint16_t* remote_port,
+                         const vc_dnsd_out* out, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!blob || !off || !remote4 || !remote_port || !out || !out->status ||
+                            !out->kind || !out->value || (remote_family && !remote6))))
+        return fail(VC_EINVAL, "bad batch arguments");
+    if (reinterpret_cast<uintptr_t>(remote6) & 15)
+        return fail(VC_EINVAL, "remote6 must be 16-byte aligned");
+    auto a = ctx->get(ctx->acl);
+    auto h = ctx->get(ctx->hint);
+    if (!a || !h) return fail(VC_ESTATE, "SecurityGroup and Upstream (rrsets) must be compiled");
+    auto ho = ctx->get(ctx->hosts);
+    HostsImage hi{};
+    if (ho) hi = ho->img;
+    hipError_t e = vc::launch_dns_datagrams(ctx->cfg(stream), hi, h->img, a->img, blob, off, n,
+                                            remote_family, remote4, remote6, remote_port,
+                                            out->status, out->acl, out->nq, out->qtype, out->kind,
+                                            out->value);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "dns datagram launch");
+}
+
+int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
+                     const uint8_t* remote_family, const uint32_t* remote4,
+                     const uint8_t* remote6, const uint16_t* remote_port,
+                     const vc_dnsd_out* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!blob || !off || !remote4 || !remote_port || !out || !out->status || !out->kind ||
+        !out->value || (remote_family && !remote6))
+        return fail(VC_EINVAL, "bad batch arguments");
+    Staging st(ctx->pool, ctx->stream);
+    hipStream_t s = ctx->stream;
+    const size_t un = size_t(n), uq = un * VC_DNSD_MAXQ;
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
+    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4, s));
+    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un, s));
+    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4, s));
+    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16, s));
+    auto* dp = static_cast<uint16_t*>(st.in(remote_port, un * 2, s));
+    vc_dnsd_out d{};
+    d.status = static_cast<uint8_t*>(st.out(out->status, un));
+    d.acl = static_cast<int32_t*>(st.out(out->acl, un * 4));
+    d.nq = static_cast<uint8_t*>(st.out(out->nq, un));
+    d.qtype = static_cast<uint16_t*>(st.out(out->qtype, uq * 2));
+    d.kind = static_cast<uint8_t*>(st.out(out->kind, uq));
+    d.value = static_cast<int32_t*>(st.out(out->value, uq * 4));
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_dns_datagrams_dev(ctx, db, doff, n, dfam, d4, d6, dp, &d, s);
+    if (rc) return rc;
+    st.back(out->status, d.status, un, s);
+    st.back(out->acl, d.acl, un * 4, s);
+    st.back(out->nq, d.nq, un, s);
+    st.back(out->qtype, d.qtype, uq * 2, s);
+    st.back(out->kind, d.kind, uq, s);
+    st.back(out->value, d.value, uq * 4, s);
+    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "dns datagrams");
 }
 
 int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,

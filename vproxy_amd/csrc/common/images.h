@@ -29,8 +29,16 @@ struct AclFamilyImage {
     const uint64_t* bounds6;      // v6: nb boundaries as (hi, lo) pairs, 2*nb words
     const uint32_t* desc;         // 2*nb words: (x, y) per interval
     const uint32_t* pieces;       // 2*np words: (port_start, value)
+    // v4, 16 < nb < 65536: a bucket directory over the key's top dir_bits
+    // bits, entry t = s(t) | (s(t + 1) - s(t)) << 16, s(t) = the interval of
+    // key t << (32 - dir_bits): a key of bucket t is in [s(t), s(t + 1)].
+    // Kernels that search the boundaries in global memory start there
+    // (acl4_interval) -- about two dependent loads instead of log2(nb).
+    const uint32_t* dir4;         // null: none
     int32_t nb;
     int32_t np;
+    int32_t dir_bits;
+    int32_t pad_;
 };
 
 struct AclImage {

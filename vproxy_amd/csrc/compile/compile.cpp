@@ -206,6 +206,26 @@ void build_acl_family(const vc_acl_rule* rules, int n, int family, AclFamilyBuil
         out->desc.push_back(y);
     }
     out->nb = static_cast<int32_t>(out->desc.size() / 2);
+    if (family == 0 && out->nb > 16 && out->nb < 65536) {
+        // bucket directory over the key's top D bits: entry t = s(t) |
+        // (s(t + 1) - s(t)) << 16, s(t) = last j with bounds4[j] <= t << (32 - D)
+        int d = 4;
+        while ((1 << d) < out->nb && d < 12) ++d;
+        const auto& b = out->bounds4;
+        auto s = [&](uint64_t key) {
+            return uint32_t(std::upper_bound(b.begin(), b.end(), key,
+                                             [](uint64_t k, uint32_t x) { return k < x; }) -
+                            b.begin()) - 1;
+        };
+        out->dir_bits = d;
+        out->dir4.resize(size_t(1) << d);
+        for (uint32_t t = 0; t < (1u << d); ++t) {
+            const uint32_t s0 = s(uint64_t(t) << (32 - d));
+            const uint32_t s1 = t + 1 < (1u << d) ? s(uint64_t(t + 1) << (32 - d))
+                                                  : uint32_t(out->nb - 1);
+            out->dir4[t] = s0 | ((s1 - s0) << 16);
+        }
+    }
 }
 
 }  // namespace

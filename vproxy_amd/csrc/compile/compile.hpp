@@ -17,7 +17,9 @@ struct AclFamilyBuilt {
     std::vector<uint64_t> bounds6;   // (hi, lo) pairs
     std::vector<uint32_t> desc;      // (x, y) pairs
     std::vector<uint32_t> pieces;    // (port_start, value) pairs
+    std::vector<uint32_t> dir4;      // v4: bucket directory (images.h AclFamilyImage)
     int32_t nb = 0;
+    int32_t dir_bits = 0;
 };
 
 struct AclBuilt {

@@ -9,12 +9,32 @@
 
 namespace vcd {
 
+// Typed reads.  A table pointer taken from a struct or chosen per item (the
+// protocol's list) is generic to the compiler, and a generic read compiles
+// to flat_load, which also waits on vmcnt: LDS-staged boundaries are read
+// through an LDS pointer (ds_read), the image's tables through a global one.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define VC_AS_LDS __attribute__((address_space(3)))
+#define VC_AS_GLB __attribute__((address_space(1)))
+#else
+#define VC_AS_LDS
+#define VC_AS_GLB
+#endif
+template <class T>
+VC_HD T lds_ld(const T* p) { return *(const VC_AS_LDS T*)(p); }
+template <class T>
+VC_HD T glb_ld(const T* p) { return *(const VC_AS_GLB T*)(p); }
+template <bool kL, class T>
+VC_HD T tbl_ld(const T* p) { return kL ? lds_ld(p) : glb_ld(p); }
+
 // Last j with b[j] <= key (b[0] == 0, so j >= 0).  Fixed trip count per nb.
+// kL: b is staged in LDS.
+template <bool kL = false>
 VC_HD int bsearch_u32(const uint32_t* b, int nb, uint32_t key) {
     int lo = 0, len = nb;
     while (len > 1) {
         int half = len >> 1;
-        lo = (b[lo + half] <= key) ? lo + half : lo;
+        lo = (tbl_ld<kL>(b + lo + half) <= key) ? lo + half : lo;
         len -= half;
     }
     return lo;
@@ -25,15 +45,27 @@ VC_HD bool le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
 }
 
 // bounds6 = (hi, lo) pairs; last j with bounds[j] <= key
+template <bool kL = false>
 VC_HD int bsearch_u128(const uint64_t* b, int nb, uint64_t kh, uint64_t kl) {
     int lo = 0, len = nb;
     while (len > 1) {
         int half = len >> 1;
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(b + 2 * (lo + half));
+        const ulonglong2 v = tbl_ld<kL>(reinterpret_cast<const ulonglong2*>(b + 2 * (lo + half)));
         lo = le128(v.x, v.y, kh, kl) ? lo + half : lo;
         len -= half;
     }
     return lo;
+}
+
+// The v4 interval of `key` from the global boundaries: through the bucket
+// directory when the image has one (images.h), else a whole binary search.
+VC_HD int acl4_interval(const AclFamilyImage& f, uint32_t key) {
+    if (f.dir4) {
+        const uint32_t e = glb_ld(f.dir4 + (key >> (32 - f.dir_bits)));
+        const int s = int(e & 0xFFFFu);
+        return s + bsearch_u32(f.bounds4 + s, int(e >> 16) + 1, key);
+    }
+    return bsearch_u32(f.bounds4, f.nb, key);
 }
 
 // desc (x, y) -> rule index (or VC_NONE) for `port`
@@ -42,9 +74,9 @@ VC_HD uint32_t port_lookup(const uint32_t* pieces, uint2 d, uint32_t port) {
     const uint2* p = reinterpret_cast<const uint2*>(pieces) + d.x;
     int n = int(d.y);
     if (n <= 8) {
-        uint32_t v = p[0].y;
+        uint32_t v = glb_ld(p).y;
         for (int k = 1; k < n; ++k) {
-            uint2 q = p[k];
+            uint2 q = glb_ld(p + k);
             if (q.x > port) break;
             v = q.y;
         }
@@ -53,14 +85,14 @@ VC_HD uint32_t port_lookup(const uint32_t* pieces, uint2 d, uint32_t port) {
     int lo = 0, len = n;
     while (len > 1) {
         int half = len >> 1;
-        lo = (p[lo + half].x <= port) ? lo + half : lo;
+        lo = (glb_ld(p + lo + half).x <= port) ? lo + half : lo;
         len -= half;
     }
-    return p[lo].y;
+    return glb_ld(p + lo).y;
 }
 
 VC_HD uint2 load_desc(const uint32_t* desc, int j) {
-    return reinterpret_cast<const uint2*>(desc)[j];
+    return glb_ld(reinterpret_cast<const uint2*>(desc) + j);
 }
 
 }  // namespace vcd

@@ -44,11 +44,13 @@ __device__ __forceinline__ int fence_count(int nb, int shift) {
     return (nb + (1 << shift) - 1) >> shift;
 }
 
+// kL: a.f is staged in LDS (else it is the global boundary list, shift 0)
+template <bool kL>
 __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint32_t key,
                                                uint32_t port) {
     const int l = tcp ? 0 : 1;
-    int j = bsearch_u32(a.f[l], a.nf[l], key);
-    if (a.shift) {
+    int j = bsearch_u32<kL>(a.f[l], a.nf[l], key);
+    if (kL && a.shift) {
         const int base = j << a.shift;
         const int rest = a.nb[l] - base;
         j = base + bsearch_u32(a.b[l] + base, rest < (1 << a.shift) ? rest : (1 << a.shift), key);
@@ -62,7 +64,7 @@ __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t
     *idx_out = out_index(v);
     if (allow_out) {
         *allow_out = v == VC_NONE ? uint8_t(img.default_allow)
-                                  : img.allow[(tcp ? 0 : img.n_tcp) + v];
+                                  : glb_ld(img.allow + (tcp ? 0 : img.n_tcp) + v);
     }
 }
 
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-            v[k] = acl_v4_one(a, tcp[k], key[k], po[k]);
+            v[k] = acl_v4_one<kLds>(a, tcp[k], key[k], po[k]);
         }
         int4 o;
         uint32_t al = 0;
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
         const int64_t i = (n4 << 2) + threadIdx.x;
         const bool t = proto[i] == VC_PROTO_TCP;
-        const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
+        const uint32_t v = acl_v4_one<kLds>(a, t, src[i], port[i]);
         acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
-        const uint32_t v = acl_v4_one(a, t, src[i], port[i]);
+        const uint32_t v = acl_v4_one<kLds>(a, t, src[i], port[i]);
         acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
@@ -204,7 +206,7 @@ __device__ __forceinline__ uint32_t acl_v6_fenced(const AclV6Ctx& a, bool tcp, u
     const int l = tcp ? 0 : 1;
     uint64_t hi, lo;
     v6_key(w, &hi, &lo);
-    const int k = bsearch_u128(a.f[l], a.nf[l], hi, lo);
+    const int k = bsearch_u128<true>(a.f[l], a.nf[l], hi, lo);
     const int base = k << a.shift;
     const int rest = a.nb[l] - base;
     const int len = rest < (1 << a.shift) ? rest : (1 << a.shift);
@@ -511,7 +513,7 @@ __device__ __forceinline__ PipeLds pipe_lds_setup(const AclImage& img, const Pip
 }
 
 // One IPv4 packet through ACL -> route -> pool group (scalar form, also the tail).
-template <bool kCount>
+template <bool kLds, bool kCount>
 __device__ __forceinline__ void pipeline_one(
     const AclImage& img, const AclV4Ctx& a, const uint32_t* nodes, int rb, const uint8_t* proto,
     const uint32_t* src, const uint32_t* dst, const uint16_t* dport, const uint32_t* host_id,
@@ -523,7 +525,7 @@ __device__ __forceinline__ void pipeline_one(
     const uint32_t h = host_id[i];
     const int32_t grp = int64_t(h) < n_pool ? pool_group[h] : -1;
     const bool tcp = proto[i] == VC_PROTO_TCP;
-    const uint32_t v = acl_v4_one(a, tcp, src[i], dport[i]);
+    const uint32_t v = acl_v4_one<kLds>(a, tcp, src[i], dport[i]);
     acl_emit(img, tcp, v, out_allow ? out_allow + i : nullptr, out_acl + i);
     const int32_t r = out_index(route_chase(nodes, rb, e, d));
     out_route[i] = r;
@@ -562,7 +564,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
     PipeTally t;
     if (!kVec) {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-            pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
+            pipeline_one<kLds, kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
                                  n_pool, i, out_acl, out_route, out_group, out_allow, pc, L, &t);
     } else {
         for (int64_t i = lo + 4 * threadIdx.x; i + 3 < hi; i += 4 * blockDim.x) {
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-                v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+                v[k] = acl_v4_one<kLds>(a, tcp[k], sk[k], po[k]);
             }
             int4 oa, orr;
             uint32_t al = 0;
@@ -613,7 +615,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
         // last partial group of 4 (only the final slice, when n % 4 != 0)
         const int64_t tail = hi & ~int64_t(3);
         if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
-            pipeline_one<kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
+            pipeline_one<kLds, kCount>(img, a, nodes, rb, proto, src, dst, dport, host_id, pool_group,
                                  n_pool, tail + threadIdx.x, out_acl, out_route, out_group,
                                  out_allow, pc, L, &t);
     }
@@ -653,7 +655,7 @@ struct PipeTries {
     int32_t rb4, rb6;
 };
 
-template <bool kCount>
+template <bool kLds, bool kCount>
 __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx& a,
                                              const AclV6Ctx& a6, const PipeTries& tr,
                                              const PipeIn& in, int64_t i, const PipeOut& out,
@@ -676,7 +678,7 @@ __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx
     } else {
         const uint32_t d = in.dst4[i];
         e = route_chase(tr.n4, tr.rb4, tr.n4[d >> (32 - tr.rb4)], d);
-        v = acl_v4_one(a, tcp, in.src4[i], port);
+        v = acl_v4_one<kLds>(a, tcp, in.src4[i], port);
     }
     acl_emit(img, tcp, v, out.allow ? out.allow + i : nullptr, out.acl + i);
     const int32_t r = out_index(e);
@@ -720,7 +722,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
     PipeTally t;
     if (!kVec) {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-            pipe_mix_one<kCount>(img, a, a6, tr, in, i, out, pc, L, &t);
+            pipe_mix_one<kLds, kCount>(img, a, a6, tr, in, i, out, pc, L, &t);
     } else {
         const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
         const uint64_t below_me = (uint64_t(1) << lane) - 1;
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
             if (act) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (!v6[k]) v[k] = acl_v4_one(a, tcp[k], sk[k], po[k]);
+                    if (!v6[k]) v[k] = acl_v4_one<kLds>(a, tcp[k], sk[k], po[k]);
                 int4 oa, orr;
                 uint32_t al = 0;
                 int32_t* pa = reinterpret_cast<int32_t*>(&oa);
@@ -824,7 +826,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
         }
         const int64_t tail = hi & ~int64_t(3);
         if (hi == n && tail >= lo && int(threadIdx.x) < int(hi - tail))
-            pipe_mix_one<kCount>(img, a, a6, tr, in, tail + threadIdx.x, out, pc, L, &t);
+            pipe_mix_one<kLds, kCount>(img, a, a6, tr, in, tail + threadIdx.x, out, pc, L, &t);
     }
     if (kCount) pipe_count_flush(pc, L.ah, L.rc, L.gc, tally, t);
 }
@@ -853,6 +855,7 @@ int v4_fence_shift(const AclImage& img, size_t words) {
 int v4_staged_words(const AclImage& img, int shift) {
     return vcd_fences(img.fam[0][0].nb, shift) + vcd_fences(img.fam[1][0].nb, shift);
 }
+
 
 }  // namespace
 

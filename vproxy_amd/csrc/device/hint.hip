@@ -10,6 +10,7 @@
 // hash probes: the query host is scanned right-to-left once, producing the
 // reversed-FNV hash of every dot-suffix ("." + annoHost candidates) and of
 // the whole host; each probe is confirmed by a byte compare.
+#include "acl_dev.h"
 #include "hint_dev.h"
 #include "launch.h"
 #include "stage.h"
@@ -262,6 +263,289 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     VC_PEND();
 }
 
+
+// ---------------------------------------------------------------------------
+// DNSServer's drain loop, one datagram per lane (DNSServer.java:457-500):
+// securityGroup.allow(UDP, remote address, remote port) -> `read == 0`
+// -> Formatter.parsePackets (Formatter.java:162-372: header, questions,
+// answer / authority / additional resources with the A, AAAA, CNAME, PTR,
+// TXT and SRV rdata checks) -> isResponse / opcode / handleRequest's
+// per-question classification (DNSServer.java:116-166, dns_one).  The
+// datagram is validated completely before any question is classified (a
+// malformed packet anywhere makes parsePackets throw).  Shapes outside the
+// kernel's contract come back VC_DNSD_HOST for the Java path: more than one
+// packet in the datagram, more than VC_DNSD_MAXQ questions, a decoded qname
+// over kNameCap bytes, a compression-pointer chain over kMaxPtr (Java
+// recurses once per pointer; a pointer loop overflows its stack).
+// ---------------------------------------------------------------------------
+constexpr int kDnsdBlock = 128;
+constexpr int kDnsdWaves = kDnsdBlock / 64;
+constexpr uint32_t kDnsdStage = 8192;         // per wave: 64 datagrams of up to 128 B on average
+constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
+constexpr int kNameCap = 256;                 // decoded qname bytes a lane classifies
+constexpr int kNameWords = (kNameCap + 2 * kApron) / 4;
+constexpr int kMaxPtr = 16;
+
+enum : int { kNameOk = 0, kNameBad = 1, kNameHost = 2 };
+
+// Formatter.parseDomainName over the datagram p[0, n): the name at index 0
+// of the view [vs, vs + vlen) (vlen may be <= 0: SubByteArray takes a
+// negative length and its first get throws).  Reads past the view are the
+// ByteArray bounds exceptions parsePackets turns into a malformed packet; a
+// pointer restarts in the view [o, n) of the whole datagram (rawPacket).
+// *used = bytes of the view the name takes (offsetHolder[0]); out(b) gets
+// the qname's chars ((char) b per label byte, '.' after each label).
+template <class Out>
+__device__ __forceinline__ int parse_name(const uint8_t* p, int n, int vs, int vlen, int* used,
+                                          Out out) {
+    int i = 0, len = 0, depth = 0;
+    bool top = true;
+    for (;;) {
+        if (i >= vlen) return kNameBad;
+        const int b = p[vs + i];
+        if (len == 0) {
+            if (b == 0) break;
+            if ((b & 0xC0) == 0xC0) {                 // pointer: the rest of the name is there
+                if (i + 1 >= vlen) return kNameBad;
+                const int o = ((b & 0x3F) << 8) | p[vs + i + 1];
+                if (top) *used = i + 2;
+                top = false;
+                if (++depth > kMaxPtr) return kNameHost;
+                vs = o;
+                vlen = n - o;
+                i = 0;
+                continue;
+            }
+            len = b;                                  // any other byte is a label length
+        } else {
+            out(b);
+            if (--len == 0) out('.');
+        }
+        ++i;
+    }
+    if (top) *used = i + 1;
+    return kNameOk;
+}
+
+struct NoOut {
+    __device__ void operator()(int) const {}
+};
+
+__device__ __forceinline__ int be16(const uint8_t* p, int i) { return (p[i] << 8) | p[i + 1]; }
+
+// DNSClass lookup (Formatter.parseClass): IN 1, CH 3, HS 4 anywhere; NONE
+// 254 and ANY 255 in questions only; anything else throws.
+__device__ __forceinline__ bool dns_class_ok(int c, bool question) {
+    return c == 1 || c == 3 || c == 4 || (question && (c == 254 || c == 255));
+}
+
+// One resource record at `at` (Formatter.parseResource); the packet ends at
+// n.  Returns the record's length, or -1 (malformed) / -2 (host).
+__device__ __forceinline__ int dns_resource(const uint8_t* p, int n, int at) {
+    int used = 0;
+    const int r = parse_name(p, n, at, n - at, &used, NoOut{});
+    if (r != kNameOk) return r == kNameBad ? -1 : -2;
+    const int o = at + used;
+    if (o + 10 > n) return -1;                        // type, class, ttl, rdlen
+    const int type = be16(p, o), clazz = be16(p, o + 2), rdlen = be16(p, o + 8);
+    if (type >= 252 && type <= 255) return -1;        // question-only types (DNSType)
+    if (type != 41 && !dns_class_ok(clazz, false)) return -1;   // OPT: no class
+    const int rd = o + 10;
+    if (n - rd < rdlen) return -1;                    // data.sub(offset, rdlen)
+    switch (type) {
+    case 1:                                           // A
+        if (rdlen != 4) return -1;
+        break;
+    case 28:                                          // AAAA
+        if (rdlen != 16) return -1;
+        break;
+    case 5:                                           // CNAME
+    case 12: {                                        // PTR
+        int u = 0;
+        const int q = parse_name(p, n, rd, rdlen, &u, NoOut{});
+        if (q != kNameOk) return q == kNameBad ? -1 : -2;
+        if (u != rdlen) return -1;
+        break;
+    }
+    case 16: {                                        // TXT: length-prefixed strings, exactly
+        int k = 0;
+        while (k < rdlen) {
+            const int l = p[rd + k];
+            ++k;
+            if (rdlen - k < l) return -1;
+            k += l;
+        }
+        break;
+    }
+    case 33: {                                        // SRV: the target is parsed from
+        int u = 0;                                    // rdata[6:] but its length compared
+        const int q = parse_name(p, n, rd + 6, rdlen - 6, &u, NoOut{});   // with the whole
+        if (q == kNameHost) return -2;                // rdata (SRV.java:27-36): never equal
+        return -1;
+    }
+    default:
+        break;
+    }
+    return rd + rdlen - at;
+}
+
+struct DnsdIn {
+    const uint8_t* rfam;            // remote family per datagram (4/6), null = all IPv4
+    const uint32_t* r4;
+    const uint8_t* r6;              // 16 bytes per datagram, 16-byte aligned
+    const uint16_t* rport;
+};
+
+// Per datagram: status; UDP rule; questions evaluated; per question (up to
+// VC_DNSD_MAXQ) its qtype, VC_DNS_* kind and value.
+struct DnsdOut {
+    uint8_t* status;
+    int32_t* acl;
+    uint8_t* nq;
+    uint16_t* qtype;
+    uint8_t* kind;
+    int32_t* value;
+};
+
+template <class Bytes>
+__device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImage& img,
+                                         const HintImage* slow_img, const AclImage& acl,
+                                         const DnsdIn& in, const DnsdOut& out, int64_t i,
+                                         const uint8_t* p, int n, uint32_t* name) {
+    // securityGroup.allow(Protocol.UDP, remote.getAddress(), remote.getPort())
+    const bool six = in.rfam && in.rfam[i] == 6;
+    const uint32_t port = in.rport[i];
+    uint32_t v;
+    if (six) {
+        const AclFamilyImage& f = acl.fam[1][1];
+        uint64_t hi, lo;
+        v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
+        v = port_lookup(f.pieces, load_desc(f.desc, bsearch_u128(f.bounds6, f.nb, hi, lo)), port);
+    } else {
+        const AclFamilyImage& f = acl.fam[1][0];
+        v = port_lookup(f.pieces, load_desc(f.desc, acl4_interval(f, in.r4[i])), port);
+    }
+    const bool allow = v == VC_NONE ? acl.default_allow != 0
+                                    : glb_ld(acl.allow + acl.n_tcp + v) != 0;
+    if (out.acl) out.acl[i] = out_index(v);
+    int nq = 0;
+    uint8_t st;
+    auto put = [&](int q, int qtype, uint8_t kd, int32_t val) {
+        const int64_t k = i * VC_DNSD_MAXQ + q;
+        if (out.qtype) out.qtype[k] = uint16_t(qtype);
+        out.kind[k] = kd;
+        out.value[k] = val;
+    };
+    if (!allow) {
+        st = VC_DNSD_REJECTED;
+    } else if (n == 0) {
+        st = VC_DNSD_EMPTY;
+    } else if (n < 12) {
+        st = VC_DNSD_MALFORMED;
+    } else {
+        // Formatter.parseHeader
+        const int b2 = p[2], b3 = p[3];
+        const int opcode = (b2 >> 3) & 15, rcode = b3 & 15;
+        const int qd = be16(p, 4);
+        const int nres = be16(p, 6) + be16(p, 8) + be16(p, 10);
+        st = VC_DNSD_ANSWER;
+        if (!(opcode <= 2 || (opcode >= 4 && opcode <= 6)) || rcode > 11) st = VC_DNSD_MALFORMED;
+        // questions (Formatter.parseQuestion), then every resource
+        int at = 12;
+        for (int q = 0; q < qd && st == VC_DNSD_ANSWER; ++q) {
+            int used = 0;
+            const int r = parse_name(p, n, at, n - at, &used, NoOut{});
+            if (r != kNameOk) {
+                st = r == kNameBad ? VC_DNSD_MALFORMED : VC_DNSD_HOST;
+                break;
+            }
+            at += used;
+            if (at + 4 > n || !dns_class_ok(be16(p, at + 2), true)) st = VC_DNSD_MALFORMED;
+            at += 4;
+        }
+        for (int k = 0; k < nres && st == VC_DNSD_ANSWER; ++k) {
+            const int r = dns_resource(p, n, at);
+            if (r < 0) st = r == -1 ? VC_DNSD_MALFORMED : VC_DNSD_HOST;
+            else at += r;
+        }
+        if (st == VC_DNSD_ANSWER) {
+            if (at != n) {
+                st = VC_DNSD_HOST;                    // another packet follows (parsePackets loops)
+            } else if (b2 & 0x80) {
+                st = VC_DNSD_RESPONSE;                // p.isResponse: skipped
+            } else if (opcode != 0) {
+                st = VC_DNSD_RECURSIVE;               // runRecursive(p, remote)
+            } else if (qd > VC_DNSD_MAXQ) {
+                st = VC_DNSD_HOST;
+            } else {
+                // handleRequest: questions in order until one goes recursive
+                at = 12;
+                uint8_t* nb = reinterpret_cast<uint8_t*>(name) + kApron;
+                for (int q = 0; q < qd; ++q) {
+                    int used = 0, len = 0;
+                    parse_name(p, n, at, n - at, &used, [&](int b) {
+                        if (len < kNameCap) nb[len] = uint8_t(b);
+                        ++len;
+                    });
+                    at += used;
+                    const int qtype = be16(p, at);
+                    at += 4;
+                    nq = q + 1;
+                    if (qtype != 1 && qtype != 28 && qtype != 33) {   // not A / AAAA / SRV
+                        put(q, qtype, VC_DNS_RECURSIVE, 0);
+                        st = VC_DNSD_RECURSIVE;
+                        break;
+                    }
+                    if (len > kNameCap) {               // the Java path decides
+                        st = VC_DNSD_HOST;
+                        nq = 0;
+                        break;
+                    }
+                    uint8_t kd;
+                    int32_t val;
+                    dns_one(hosts, img, slow_img, LdsSrc{name, int(kApron)}, len, &kd, &val);
+                    put(q, qtype, kd, val);
+                    if (kd == VC_DNS_RECURSIVE) {
+                        st = VC_DNSD_RECURSIVE;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    out.status[i] = st;
+    if (out.nq) out.nq[i] = uint8_t(nq);
+}
+
+template <bool kStage>
+__global__ __launch_bounds__(kDnsdBlock, 2) void dnsd_kernel(
+    HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
+    const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out) {
+    __shared__ uint32_t stage[kStage ? kDnsdWaves : 1][kStage ? kDnsdStageWords : 1];
+    __shared__ uint32_t names[kDnsdBlock][kNameWords];
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    HintImage slow_img = img;
+    const int64_t wstride = int64_t(gridDim.x) * kDnsdWaves * 64;
+    for (int64_t base = (int64_t(blockIdx.x) * kDnsdWaves + w) * 64; base < n; base += wstride) {
+        const int64_t i = base + lane;
+        const int64_t last = base + 64 < n ? base + 64 : n;
+        uint32_t a0 = 0;
+        const bool staged =
+            kStage && stage_wave<kDnsdStage>(blob, off[base], off[last], stage[w], &a0);
+        if (i < n) {
+            const uint32_t a = off[i], e = off[i + 1];
+            if (staged)
+                dnsd_one<int>(hosts, img, &slow_img, acl, in, out, i,
+                              reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
+                              int(e - a), names[threadIdx.x]);
+            else
+                dnsd_one<int>(hosts, img, &slow_img, acl, in, out, i, blob + a, int(e - a),
+                              names[threadIdx.x]);
+        }
+        if (kStage) wave_done();
+    }
+}
+
 }  // namespace vcd
 
 namespace vc {
@@ -328,6 +612,29 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
     if (e != hipSuccess || !group_counters) return e;
     return launch_hist(c, VC_HIST_DNS, value, kind, n, hints.n_groups, 0, hints.n_groups, 0,
                        group_counters);
+}
+
+hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
+                                const HintImage& hints, const AclImage& acl, const uint8_t* blob,
+                                const uint32_t* off, int64_t n, const uint8_t* rfam,
+                                const uint32_t* r4, const uint8_t* r6, const uint16_t* rport,
+                                uint8_t* status, int32_t* out_acl, uint8_t* nq, uint16_t* qtype,
+                                uint8_t* kind, int32_t* value) {
+    if (n <= 0) return hipSuccess;
+    const int64_t want = (n + vcd::kDnsdBlock - 1) / vcd::kDnsdBlock;
+    const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
+    const void* k = stage ? reinterpret_cast<const void*>(vcd::dnsd_kernel<true>)
+                          : reinterpret_cast<const void*>(vcd::dnsd_kernel<false>);
+    const int grid = resident_grid(c, k, vcd::kDnsdBlock, 0, want);
+    const vcd::DnsdIn in{rfam, r4, r6, rport};
+    const vcd::DnsdOut o{status, out_acl, nq, qtype, kind, value};
+    if (stage)
+        hipLaunchKernelGGL(vcd::dnsd_kernel<true>, dim3(grid), dim3(vcd::kDnsdBlock), 0, c.stream,
+                           hosts, hints, acl, blob, off, n, in, o);
+    else
+        hipLaunchKernelGGL(vcd::dnsd_kernel<false>, dim3(grid), dim3(vcd::kDnsdBlock), 0,
+                           c.stream, hosts, hints, acl, blob, off, n, in, o);
+    return hipGetLastError();
 }
 
 }  // namespace vc

@@ -800,15 +800,15 @@ VC_HD void dns_flow(const HostsImage& hosts, const HintImage& img, const HintIma
     }
 }
 
-// Formatter.parseDomainName (Formatter.java:225-257) turns each wire byte
-// into a char with (char) b: the qname string is ISO-8859-1.  Annotations
-// and hosts keys arrive as UTF-8, so a qname byte >= 0x80 is the two UTF-8
-// bytes of U+0080..U+00FF; the rare non-ASCII qname is transcoded into a
-// private buffer and classified from there.  Wire names are at most 255
-// bytes; a non-ASCII name over 512 bytes is reported as recursive.
-VC_HDN __noinline__ void dns_latin1(const HostsImage& hosts, const HintImage* slow_img,
-                                    const uint8_t* qp, int qn, uint8_t* kind, int32_t* value) {
-    uint8_t buf[1024];
+// Formatter.parseDomainName appends (char) b per wire byte b, a Java byte:
+// the cast sign-extends (JLS 5.1.4), so a byte c >= 0x80 is the char
+// U+FF00 | c, whose UTF-8 form is EF (BE | BF) (80 | c & 3F).  The rare
+// qname with such bytes is transcoded into a private buffer and classified
+// from there.  Wire names are at most 255 bytes; a non-ASCII name over 512
+// bytes is reported as recursive.
+VC_HDN __noinline__ void dns_highbytes(const HostsImage& hosts, const HintImage* slow_img,
+                                       const uint8_t* qp, int qn, uint8_t* kind, int32_t* value) {
+    uint8_t buf[1536];
     if (qn > 512) {
         *kind = VC_DNS_RECURSIVE;
         *value = 0;
@@ -820,7 +820,8 @@ VC_HDN __noinline__ void dns_latin1(const HostsImage& hosts, const HintImage* sl
         if (c < 0x80) {
             buf[n++] = c;
         } else {
-            buf[n++] = uint8_t(0xC0 | (c >> 6));
+            buf[n++] = 0xEF;
+            buf[n++] = uint8_t(0xBC | (c >> 6));
             buf[n++] = uint8_t(0x80 | (c & 0x3F));
         }
     }
@@ -834,7 +835,7 @@ VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImag
                    const Src& q, int qn, uint8_t* kind, int32_t* value) {
     uint32_t hi = 0;
     for (int pos = 0; pos < qn; pos += 4) hi |= q.word(pos, 0, qn);
-    if (hi & 0x80808080u) dns_latin1(hosts, slow_img, q.ptr(), qn, kind, value);
+    if (hi & 0x80808080u) dns_highbytes(hosts, slow_img, q.ptr(), qn, kind, value);
     else dns_flow(hosts, img, slow_img, q, qn, kind, value);
 }
 

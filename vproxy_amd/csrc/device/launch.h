@@ -186,6 +186,12 @@ hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32
 hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_t* off, int64_t n,
                           int layer, const vc_pkt_out& out);
 // Parse + bare-VXLAN ACL on the sender + inner route in one pass (packet.hip)
+hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
+                                const HintImage& hints, const AclImage& acl, const uint8_t* blob,
+                                const uint32_t* off, int64_t n, const uint8_t* rfam,
+                                const uint32_t* r4, const uint8_t* r6, const uint16_t* rport,
+                                uint8_t* status, int32_t* out_acl, uint8_t* nq, uint16_t* qtype,
+                                uint8_t* kind, int32_t* value);
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
                          const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,

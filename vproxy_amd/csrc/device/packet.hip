@@ -106,8 +106,7 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
                         in.bind_port);
     } else {
         const AclFamilyImage& f = acl.fam[1][0];
-        v = port_lookup(f.pieces, load_desc(f.desc, bsearch_u32(f.bounds4, f.nb, in.r4[i])),
-                        in.bind_port);
+        v = port_lookup(f.pieces, load_desc(f.desc, acl4_interval(f, in.r4[i])), in.bind_port);
     }
     const bool allow = v == VC_NONE ? acl.default_allow != 0 : acl.allow[acl.n_tcp + v] != 0;
     if (so.acl) so.acl[i] = out_index(v);
