@@ -214,7 +214,7 @@ int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int
 #define VC_DNSD_MALFORMED  5  /* parsePackets threw InvalidDNSPacketException: the loop returns */
 #define VC_DNSD_HOST       6  /* outside this entry point's shapes, run the Java path: a
                                  second packet in the datagram, more than VC_DNSD_MAXQ
-                                 questions, a qname over 256 chars, a chain of more than
+                                 questions, a qname over 128 chars, a chain of more than
                                  16 compression pointers (nq = 0) */
 #define VC_DNSD_MAXQ       4
 typedef struct {

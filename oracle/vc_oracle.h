@@ -269,7 +269,7 @@ void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups
 enum { VO_DNSD_ANSWER = 0, VO_DNSD_RECURSIVE = 1, VO_DNSD_RESPONSE = 2, VO_DNSD_REJECTED = 3,
        VO_DNSD_EMPTY = 4, VO_DNSD_MALFORMED = 5, VO_DNSD_HOST = 6 };
 #define VO_DNSD_MAXQ 4
-#define VO_DNSD_NAMECAP 256
+#define VO_DNSD_NAMECAP 128
 #define VO_DNSD_MAXPTR 16
 typedef struct {
     int32_t status, acl, nq;

@@ -349,6 +349,10 @@ def dns_datagrams():
          q(ex, extra=W.resource("a.", W.A, bytes(3)), an=1, response=True), ok, 5353,
          MALFORMED, 0, []),
         ("qname of 305 chars", q([((("x" * 60) + ".") * 5, W.A)]), ok, 5353, HOST, 0, []),
+        ("qname of 128 chars", q([((("x" * 63) + ".") * 2, W.A)]), ok, 5353, RECURSIVE, 1,
+         [[1, K_REC, 0]]),
+        ("qname of 129 chars", q([((("x" * 63) + ".") * 2 + "y.", W.A)]), ok, 5353, HOST, 0,
+         []),
         ("question cut inside its qtype", q(ex)[:-3], ok, 5353, MALFORMED, 0, []),
     ]
     return {"source": "TestResolver.java:41-112; Formatter.java:162-372; DNSServer.java:116-166,"

@@ -280,10 +280,16 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kDnsdBlock = 128;
 constexpr int kDnsdWaves = kDnsdBlock / 64;
-constexpr uint32_t kDnsdStage = 8192;         // per wave: 64 datagrams of up to 128 B on average
+// LDS per 128-thread workgroup: two 4 KiB stages (64 queries of up to 64 B
+// on average per wave; longer spans are read from global memory) and a
+// per-lane qname buffer -- 28.7 KiB, five workgroups per CU.
+constexpr uint32_t kDnsdStage = 4096;
 constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
-constexpr int kNameCap = 256;                 // decoded qname bytes a lane classifies
-constexpr int kNameWords = (kNameCap + 2 * kApron) / 4;
+constexpr int kNameCap = 128;                 // decoded qname chars a lane classifies
+// an odd stride in words: lane l's word k sits in bank (41 l + k) mod 64, so
+// the lanes' buffers do not collide when they read the same word index
+// (an even stride of 40 words put them on 8 banks)
+constexpr int kNameWords = (kNameCap + 2 * kApron) / 4 + 1;
 constexpr int kMaxPtr = 16;
 
 enum : int { kNameOk = 0, kNameBad = 1, kNameHost = 2 };
@@ -518,7 +524,7 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
 }
 
 template <bool kStage>
-__global__ __launch_bounds__(kDnsdBlock, 2) void dnsd_kernel(
+__global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out) {
     __shared__ uint32_t stage[kStage ? kDnsdWaves : 1][kStage ? kDnsdStageWords : 1];
