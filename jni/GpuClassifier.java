@@ -75,6 +75,16 @@ public final class GpuClassifier {
                                              int bindPort, ByteBuffer[] out, ByteBuffer outAcl,
                                              ByteBuffer outAllow, ByteBuffer outRoute) throws IOException;
 
+    /**
+     * DNSServer's drain loop per datagram (DNSServer.java:457-500): securityGroup.allow(UDP,
+     * remote, remote port), Formatter.parsePackets, isResponse / opcode / handleRequest's
+     * question classification.  out: status, acl, nq, qtype, kind, value (vc_dnsd_out order;
+     * the per-question arrays hold VC_DNSD_MAXQ entries per datagram).
+     */
+    public static native void dnsDatagrams(long ctx, ByteBuffer blob, ByteBuffer off, int n,
+                                           ByteBuffer remoteFamily, ByteBuffer remote4, ByteBuffer remote6,
+                                           ByteBuffer remotePort, ByteBuffer[] out) throws IOException;
+
     /** servers: packed vc_server[] (32 B each) per group; groupOff: n + 1 ints. */
     public static native void compileServers(long ctx, ByteBuffer servers, ByteBuffer groupOff, int nGroups)
         throws IOException;

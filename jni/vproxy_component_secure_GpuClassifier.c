@@ -241,6 +241,24 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_switchClassify
                                       addr(env, outAllow), addr(env, outRoute)));
 }
 
+/* DNSServer's drain loop per datagram (DNSServer.java:457-500): out = status,
+ * acl, nq, qtype, kind, value (vc_dnsd_out order; acl / nq / qtype may be null) */
+JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_dnsDatagrams
+  (JNIEnv *env, jclass self, jlong ctx, jobject blob, jobject off, jint n,
+   jobject remoteFamily, jobject remote4, jobject remote6, jobject remotePort,
+   jobjectArray out) {
+    vc_dnsd_out o;
+    void *f[6];
+    int i;
+    (void) self;
+    for (i = 0; i < 6; ++i)
+        f[i] = out ? addr(env, (*env)->GetObjectArrayElement(env, out, i)) : NULL;
+    o.status = f[0]; o.acl = f[1]; o.nq = f[2]; o.qtype = f[3]; o.kind = f[4]; o.value = f[5];
+    jni_throw(env, vc_dns_datagrams(CTX(ctx), addr(env, blob), addr(env, off), n,
+                                    addr(env, remoteFamily), addr(env, remote4),
+                                    addr(env, remote6), addr(env, remotePort), &o));
+}
+
 /* SSLContextHolder: certificate names (UTF-8 blob + offsets) and holder per name */
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileCerts
   (JNIEnv *env, jclass self, jlong ctx, jobject names, jobject off, jobject holder,
