@@ -374,7 +374,7 @@ def test_dns_kats_and_random(clf):
         kind, val = clf.dns_classify([q for q, _, _ in case["queries"]])
         assert [(int(k), int(v)) for k, v in zip(kind, val)] == \
             [(k, v) for _, k, v in case["queries"]], case["source"]
-    # qnames as wire bytes: ISO-8859-1 chars vs UTF-8 annotations (Formatter.java:225-257)
+    # qnames as wire bytes: (char) b sign-extends (U+FF80..) vs UTF-8 annotations (Formatter.java:225-257)
     for case in kats["dns_wire"]:
         clf.compile_upstream(case["groups"])
         clf.compile_hosts([tuple(x) for x in case["hosts"]])

@@ -100,8 +100,9 @@ def test_dns_kats():
 
 
 def test_dns_wire_kats():
-    """qnames as wire bytes: ISO-8859-1 chars (Formatter.java:225-257) against
-    UTF-8 annotations / hosts keys."""
+    """qnames as wire bytes: (char) b per byte (Formatter.java:225-257), which
+    sign-extends a byte >= 0x80 to U+FF80..U+FFFF, against UTF-8 annotations
+    / hosts keys."""
     for case in load("kats.json")["dns_wire"]:
         g = O.Groups(case["groups"])
         h = O.Hosts(case["hosts"])
