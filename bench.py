@@ -710,6 +710,45 @@ def _time(fn, steps, warmup):
     return el, float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
+def dnsd_tables(clf, n_templates=1 << 20):
+    """The `dnsd` workload's tables, compiled into clf: 100k hint-host
+    groups, a 50k-line hosts file, a 10k-rule SecurityGroup (default allow);
+    and n_templates query datagrams over the DNS-flavoured C4 hostnames (one
+    A (70 %) or AAAA question, 30 % with an EDNS0 OPT record)."""
+    from vproxy_amd import dnswire as DW
+    t = types.SimpleNamespace()
+    t.groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+    clf.compile_upstream(t.groups)
+    t.hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
+                        for i in range(50_000))
+    clf.compile_hosts_text(t.hosts)
+    t.tcp, t.udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+    a, na, ka = W.as_ctypes(t.tcp, V._lib.VcAclRule)
+    b, nb, kb = W.as_ctypes(t.udp, V._lib.VcAclRule)
+    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1))
+    qn = W.gen_hostnames(ghosts, n_templates, W.SEED + 6, dns=True, port_frac=0)
+    trng = np.random.default_rng(W.SEED + 20)
+    qt = np.where(trng.random(len(qn)) < 0.7, DW.A, DW.AAAA)
+    edns = trng.random(len(qn)) < 0.3
+    dgs = [DW.header(qd=1, ar=int(e), ident=i & 0xFFFF) + DW.question(q, int(qt_)) +
+           (DW.opt_record() if e else b"") for i, (q, qt_, e) in enumerate(zip(qn, qt, edns))]
+    t.dblob, t.doff = W.pack(dgs)
+    return t
+
+
+def dnsd_batch(t, n, dev):
+    """n datagrams drawn from the templates (seeded), on the device, with
+    random IPv4 senders and ports: (blob, off, payload bytes, remote4,
+    remote_port, template index per datagram)."""
+    pidx = np.random.default_rng(W.SEED + 21).integers(0, len(t.doff) - 1, n)
+    blob, off, nbytes = gather_strings_dev(t.dblob, t.doff, pidx, dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(23)
+    r4 = dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
+    rport = torch.randint(1024, 65536, (n,), generator=g, device=dev).to(torch.int16)
+    return blob, off, nbytes, r4, rport, pidx
+
+
 def sub_bench(args, clf, dev, rank, world):
     """Single-classifier benchmarks.  Each line carries `roofline` (its
     dominant kernel's algorithmic bytes over its event-timed duration) and,
@@ -928,30 +967,10 @@ def sub_bench(args, clf, dev, rank, world):
         # -> parsePackets -> handleRequest classification over 100k groups
         # + 50k hosts; queries of one A / AAAA question, 30 % with an EDNS0
         # OPT record, from random IPv4 senders
-        from vproxy_amd import dnswire as DW
-        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
-        clf.compile_upstream(groups)
-        hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
-                          for i in range(50_000))
-        clf.compile_hosts_text(hosts)
-        tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
-        a_, na_, ka_ = W.as_ctypes(tcp, V._lib.VcAclRule)
-        b_, nb_, kb_ = W.as_ctypes(udp, V._lib.VcAclRule)
-        V.check(V.lib().vc_compile_acl(clf.h, a_, na_, b_, nb_, 1))
-        qn = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
-        trng = np.random.default_rng(W.SEED + 20)
-        qt = np.where(trng.random(len(qn)) < 0.7, DW.A, DW.AAAA)
-        edns = trng.random(len(qn)) < 0.3
-        dgs = [DW.header(qd=1, ar=int(e), ident=i & 0xFFFF) + DW.question(q, int(t)) +
-               (DW.opt_record() if e else b"") for i, (q, t, e) in enumerate(zip(qn, qt, edns))]
-        dblob, doff = W.pack(dgs)
+        t = dnsd_tables(clf)
+        groups, hosts, tcp, udp, dblob, doff = t.groups, t.hosts, t.tcp, t.udp, t.dblob, t.doff
         n = 16 << 20
-        pidx = np.random.default_rng(W.SEED + 21).integers(0, len(dgs), n)
-        blob, off, nbytes = gather_strings_dev(dblob, doff, pidx, dev)
-        g = torch.Generator(device=dev)
-        g.manual_seed(23)
-        r4 = dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
-        rport = torch.randint(1024, 65536, (n,), generator=g, device=dev).to(torch.int16)
+        blob, off, nbytes, r4, rport, pidx = dnsd_batch(t, n, dev)
         res = {"status": torch.empty(n, dtype=torch.uint8, device=dev),
                "acl": torch.empty(n, dtype=torch.int32, device=dev),
                "nq": torch.empty(n, dtype=torch.uint8, device=dev),

@@ -266,6 +266,53 @@ def test_dns_c4_scale():
         clf.close()
 
 
+def test_dnsd_bench_workload():
+    """The `dnsd` sub-bench exactly as bench.py builds it (bench.dnsd_tables /
+    dnsd_batch: 10k-rule SecurityGroup, 100k groups, 50k hosts, 4M of its
+    datagrams from random IPv4 senders): every status, rule and question
+    result of an oracle sample (DNSServer drain loop, vo_dnsd_batch), and
+    whole-batch properties -- every allowed datagram answered, the rejected
+    ones exactly the senders the UDP list denies."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        t = B.dnsd_tables(clf)
+        n = 4 << 20
+        blob, off, nbytes, r4, rport, pidx = B.dnsd_batch(t, n, "cuda")
+        res = {k: v.cpu().numpy() for k, v in clf.dns_datagrams(
+            (blob, off), r4, rport).items()}
+        res["qtype"] = res["qtype"].view(np.uint16)
+        torch.cuda.synchronize()
+        h4 = r4.cpu().numpy().view(np.uint32)
+        hp = rport.cpu().numpy().view(np.uint16)
+        og = O.Groups(t.groups)
+        oh = O.Hosts(O.hosts_parse(t.hosts)[0])
+        s = np.sort(np.random.default_rng(5).choice(n, 3000, replace=False))
+        sb, so = W.pack([bytes(t.dblob[t.doff[j]:t.doff[j + 1]]) for j in pidx[s]])
+        want = O.dnsd_batch_np(t.tcp, t.udp, True, oh, og, sb, so, None, h4[s], None, hp[s],
+                               nthreads=16)
+        for k in ("status", "acl", "nq"):
+            np.testing.assert_array_equal(res[k][s], want[k], err_msg=k)
+        live = want["nq"] > 0                          # per-question fields for q < nq
+        assert live.mean() > 0.99
+        for k in ("qtype", "kind", "value"):
+            np.testing.assert_array_equal(res[k][s, 0][live].astype(want[k].dtype),
+                                          want[k][live, 0], err_msg=k)
+        # whole batch: answered or rejected, one question, and the rule equal
+        # to the ACL kernel's (LDS-staged boundaries, not the bucket
+        # directory) over all 4M senders, rejected iff that rule denies
+        st = res["status"]
+        assert set(np.unique(st)) <= {V.DNSD_ANSWER, V.DNSD_REJECTED}
+        assert np.all(res["nq"][st == V.DNSD_ANSWER] == 1)
+        proto = torch.full((n,), 17, dtype=torch.uint8, device="cuda")
+        idx, allow = clf.acl_v4(proto, r4, rport)
+        np.testing.assert_array_equal(res["acl"], idx.cpu().numpy())
+        np.testing.assert_array_equal(st == V.DNSD_REJECTED, allow.cpu().numpy() == 0)
+        assert 0 < (st == V.DNSD_REJECTED).sum() < n
+    finally:
+        clf.close()
+
+
 def test_counters_values_outside_the_space():
     """A counter space above 65,536 bins (the bucketed path) fed values at or
     past its size -- e.g. a hostname pool classified against an older, larger
