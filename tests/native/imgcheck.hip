@@ -21,7 +21,7 @@ AclFamilyImage fam_img(const vc::AclFamilyBuilt& b) {
     AclFamilyImage f{};
     f.bounds4 = b.bounds4.data();
     f.bounds6 = b.bounds6.data();
-    f.desc = b.desc.data();
+    f.rec = b.rec.data();
     f.pieces = b.pieces.data();
     f.dir4 = b.dir4.empty() ? nullptr : b.dir4.data();
     f.dir_bits = b.dir_bits;
@@ -91,7 +91,11 @@ int ic_acl(const vc_acl_rule* tcp, int nt, const vc_acl_rule* udp, int nu, int d
             v6_key(static_cast<const uint4*>(src)[i], &hi, &lo);
             j = bsearch_u128(f.bounds6, f.nb, hi, lo);
         }
-        uint32_t v = port_lookup(f.pieces, load_desc(f.desc, j), port[i]);
+        // the interval's packed record, checked against (x, y) + pieces
+        uint32_t v = acl_value(f.rec, f.pieces, j, port[i]);
+        const uint2 d = make_uint2(b.fam[l][family == 4 ? 0 : 1].desc[2 * j],
+                                   b.fam[l][family == 4 ? 0 : 1].desc[2 * j + 1]);
+        if (v != port_lookup(f.pieces, d, port[i])) return -101;
         out[i] = out_index(v);
         allow[i] = v == VC_NONE ? uint8_t(b.default_allow) : b.allow[(l ? b.n_tcp : 0) + v];
     }

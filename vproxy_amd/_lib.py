@@ -201,8 +201,9 @@ def lib():
                                              vp, vp, vp, vp]
         L.vc_switch_classify.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, i32, P(VcPktOut), vp,
                                          vp, vp]
-        L.vc_dns_datagrams_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut), vp]
-        L.vc_dns_datagrams.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut)]
+        if hasattr(L, "vc_dns_datagrams"):     # (A/B runs load older builds without it)
+            L.vc_dns_datagrams_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut), vp]
+            L.vc_dns_datagrams.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, P(VcDnsdOut)]
         L.vc_counters_enable.argtypes = [vp, i32]
         L.vc_counters_device.argtypes = [vp, i32, P(vp), P(C.c_int64)]
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]

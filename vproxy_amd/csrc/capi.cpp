@@ -338,7 +338,7 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
             AclFamilyImage& fi = s->img.fam[l][f];
             fi.bounds4 = f == 0 ? s->upload(fb.bounds4, &e) : nullptr;
             fi.bounds6 = f == 1 ? s->upload(fb.bounds6, &e) : nullptr;
-            fi.desc = s->upload(fb.desc, &e);
+            fi.rec = s->upload(fb.rec, &e);
             fi.pieces = s->upload(fb.pieces, &e);
             fi.dir4 = fb.dir4.empty() ? nullptr : s->upload(fb.dir4, &e);
             fi.dir_bits = fb.dir4.empty() ? 0 : fb.dir_bits;

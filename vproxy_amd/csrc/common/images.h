@@ -27,7 +27,12 @@
 struct AclFamilyImage {
     const uint32_t* bounds4;      // v4: nb boundaries (bounds4[0] == 0)
     const uint64_t* bounds6;      // v6: nb boundaries as (hi, lo) pairs, 2*nb words
-    const uint32_t* desc;         // 2*nb words: (x, y) per interval
+    // 4*nb words: one 16-byte record per interval, read with one load:
+    // word 0 = value of piece 0 (port 0 up; 16 bits, 0xFFFF = VC_NONE) |
+    // piece count k << 16, words 1..k-1 = port_start << 16 | value of the
+    // next pieces; k == 0xFF: words 1, 2 = (x, y) into `pieces` (more than
+    // four pieces or a rule index >= 0xFFFF; y == 0: the value is x)
+    const uint32_t* rec;
     const uint32_t* pieces;       // 2*np words: (port_start, value)
     // v4, 16 < nb < 65536: a bucket directory over the key's top dir_bits
     // bits, entry t = s(t) | (s(t + 1) - s(t)) << 16, s(t) = the interval of

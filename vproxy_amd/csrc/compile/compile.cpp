@@ -206,6 +206,33 @@ void build_acl_family(const vc_acl_rule* rules, int n, int family, AclFamilyBuil
         out->desc.push_back(y);
     }
     out->nb = static_cast<int32_t>(out->desc.size() / 2);
+    // one 16-byte record per interval: up to four port pieces inline, else
+    // (x, y) of desc for the pieces array (images.h AclFamilyImage.rec)
+    out->rec.assign(size_t(out->nb) * 4, 0u);
+    auto v16 = [](uint32_t v) { return v == VC_NONE ? 0xFFFFu : v; };
+    for (int32_t j = 0; j < out->nb; ++j) {
+        const uint32_t x = out->desc[2 * j], y = out->desc[2 * j + 1];
+        uint32_t* r = &out->rec[size_t(j) * 4];
+        bool inl = y <= 4;
+        const uint32_t k = y == 0 ? 1 : y;
+        for (uint32_t i = 0; inl && i < k; ++i) {
+            const uint32_t v = y == 0 ? x : out->pieces[2 * (x + i) + 1];
+            inl = v == VC_NONE || v < 0xFFFFu;
+        }
+        if (!inl) {
+            r[0] = 0xFFu << 16;
+            r[1] = x;
+            r[2] = y;
+            continue;
+        }
+        if (y == 0) {
+            r[0] = v16(x) | (1u << 16);
+            continue;
+        }
+        r[0] = v16(out->pieces[2 * x + 1]) | (k << 16);     // piece 0 starts at port 0
+        for (uint32_t i = 1; i < k; ++i)
+            r[i] = (out->pieces[2 * (x + i)] << 16) | v16(out->pieces[2 * (x + i) + 1]);
+    }
     if (family == 0 && out->nb > 16 && out->nb < 65536) {
         // bucket directory over the key's top D bits: entry t = s(t) |
         // (s(t + 1) - s(t)) << 16, s(t) = last j with bounds4[j] <= t << (32 - D)

@@ -16,6 +16,7 @@ struct AclFamilyBuilt {
     std::vector<uint32_t> bounds4;
     std::vector<uint64_t> bounds6;   // (hi, lo) pairs
     std::vector<uint32_t> desc;      // (x, y) pairs
+    std::vector<uint32_t> rec;       // 4 words per interval (images.h AclFamilyImage.rec)
     std::vector<uint32_t> pieces;    // (port_start, value) pairs
     std::vector<uint32_t> dir4;      // v4: bucket directory (images.h AclFamilyImage)
     int32_t nb = 0;

@@ -21,7 +21,13 @@ namespace vcd {
 #define VC_AS_GLB
 #endif
 template <class T>
-VC_HD T lds_ld(const T* p) { return *(const VC_AS_LDS T*)(p); }
+VC_HD T lds_ld(const T* p) {
+#if defined(VC_GENERIC_LDS)       // A/B builds only: the generic (flat) read
+    return *p;
+#else
+    return *(const VC_AS_LDS T*)(p);
+#endif
+}
 template <class T>
 VC_HD T glb_ld(const T* p) { return *(const VC_AS_GLB T*)(p); }
 template <bool kL, class T>
@@ -91,8 +97,18 @@ VC_HD uint32_t port_lookup(const uint32_t* pieces, uint2 d, uint32_t port) {
     return glb_ld(p + lo).y;
 }
 
-VC_HD uint2 load_desc(const uint32_t* desc, int j) {
-    return glb_ld(reinterpret_cast<const uint2*>(desc) + j);
+// Rule index (or VC_NONE) of interval j for `port`: one 16-byte record
+// load (images.h AclFamilyImage.rec); the pieces array only for intervals
+// with more than four port pieces.
+VC_HD uint32_t acl_value(const uint32_t* rec, const uint32_t* pieces, int j, uint32_t port) {
+    const uint4 r = glb_ld(reinterpret_cast<const uint4*>(rec) + j);
+    const uint32_t k = (r.x >> 16) & 0xFFu;
+    if (k == 0xFFu) return port_lookup(pieces, make_uint2(r.y, r.z), port);
+    uint32_t v = r.x & 0xFFFFu;
+    if (k > 1 && port >= (r.y >> 16)) v = r.y & 0xFFFFu;
+    if (k > 2 && port >= (r.z >> 16)) v = r.z & 0xFFFFu;
+    if (k > 3 && port >= (r.w >> 16)) v = r.w & 0xFFFFu;
+    return v == 0xFFFFu ? VC_NONE : v;
 }
 
 }  // namespace vcd

@@ -34,7 +34,7 @@ constexpr int kPipeBlock = 1024;
 struct AclV4Ctx {
     const uint32_t* f[2];          // LDS: every boundary (shift 0) or the fences
     const uint32_t* b[2];          // global boundaries
-    const uint32_t* desc[2];
+    const uint32_t* rec[2];
     const uint32_t* pieces[2];
     int nf[2], nb[2];
     int shift;                     // uniform per launch
@@ -55,8 +55,7 @@ __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint
         const int rest = a.nb[l] - base;
         j = base + bsearch_u32(a.b[l] + base, rest < (1 << a.shift) ? rest : (1 << a.shift), key);
     }
-    const uint2 d = load_desc(a.desc[l], j);
-    return port_lookup(a.pieces[l], d, port);
+    return acl_value(a.rec[l], a.pieces[l], j, port);
 }
 
 __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t v,
@@ -81,7 +80,7 @@ __device__ __forceinline__ AclV4Ctx acl_v4_ctx(const AclImage& img, const uint32
         a.nf[l] = fence_count(f.nb, a.shift);
         a.b[l] = f.bounds4;
         a.f[l] = lds ? lds + off : f.bounds4;
-        a.desc[l] = f.desc;
+        a.rec[l] = f.rec;
         a.pieces[l] = f.pieces;
         off += a.nf[l];
     }
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel_scalar(
 struct AclV6Ctx {
     const uint64_t* f[2];          // LDS fences, (hi, lo) pairs
     const uint64_t* b[2];          // global boundaries
-    const uint32_t* desc[2];
+    const uint32_t* rec[2];
     const uint32_t* pieces[2];
     int nf[2], nb[2];
     int shift;
@@ -190,7 +189,7 @@ __device__ __forceinline__ AclV6Ctx stage_fences(const AclImage& img, uint64_t* 
         a.nb[l] = f.nb;
         a.nf[l] = fence_count(f.nb, shift);
         a.b[l] = f.bounds6;
-        a.desc[l] = f.desc;
+        a.rec[l] = f.rec;
         a.pieces[l] = f.pieces;
         a.f[l] = lds + 2 * off;
         for (int k = threadIdx.x; k < a.nf[l]; k += blockDim.x)
@@ -211,7 +210,7 @@ __device__ __forceinline__ uint32_t acl_v6_fenced(const AclV6Ctx& a, bool tcp, u
     const int rest = a.nb[l] - base;
     const int len = rest < (1 << a.shift) ? rest : (1 << a.shift);
     const int j = base + bsearch_u128(a.b[l] + 2 * int64_t(base), len, hi, lo);
-    return port_lookup(a.pieces[l], load_desc(a.desc[l], j), port);
+    return acl_value(a.rec[l], a.pieces[l], j, port);
 }
 
 __global__ __launch_bounds__(kBlock) void acl_v6_kernel(

@@ -102,11 +102,10 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
         const AclFamilyImage& f = acl.fam[1][1];
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
-        v = port_lookup(f.pieces, load_desc(f.desc, bsearch_u128(f.bounds6, f.nb, hi, lo)),
-                        in.bind_port);
+        v = acl_value(f.rec, f.pieces, bsearch_u128(f.bounds6, f.nb, hi, lo), in.bind_port);
     } else {
         const AclFamilyImage& f = acl.fam[1][0];
-        v = port_lookup(f.pieces, load_desc(f.desc, acl4_interval(f, in.r4[i])), in.bind_port);
+        v = acl_value(f.rec, f.pieces, acl4_interval(f, in.r4[i]), in.bind_port);
     }
     const bool allow = v == VC_NONE ? acl.default_allow != 0 : acl.allow[acl.n_tcp + v] != 0;
     if (so.acl) so.acl[i] = out_index(v);
