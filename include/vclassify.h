@@ -222,9 +222,13 @@ typedef struct {
     int32_t *acl;             /* matched UDP rule index, -1 = default (optional) */
     uint8_t *nq;              /* questions evaluated (optional) */
     uint16_t *qtype;          /* [n][VC_DNSD_MAXQ] (optional) */
-    uint8_t *kind;            /* [n][VC_DNSD_MAXQ] VC_DNS_* of question q < nq (required) */
+    uint8_t *kind;            /* [n][VC_DNSD_MAXQ] VC_DNS_* of question q < nq, 0 for the
+                                 other slots (required) */
     int32_t *value;           /* [n][VC_DNSD_MAXQ] its value (required) */
 } vc_dnsd_out;
+/* With counters on (vc_counters_enable), a call counts the matched UDP rule
+ * of every datagram (when out->acl is given) and the group of every question
+ * classified VC_DNS_GROUP. */
 int vc_dns_datagrams_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
                          const uint8_t *remote_family, const uint32_t *remote4,
                          const uint8_t *remote6, const uint16_t *remote_port,

@@ -120,11 +120,27 @@ def test_dns_datagrams_vs_oracle(shift):
         T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
         dblob = torch.zeros(len(blob) + 16, dtype=torch.uint8, device="cuda")
         dblob[shift:shift + len(blob)] = T(blob)
+        clf.counters_enable(True)
+        clf.counters_reset()
         res = _cpu(clf.dns_datagrams((dblob[shift:], T(off.view(np.int32))),
                                      T(r4.view(np.int32)), T(port.view(np.int16)),
                                      remote6=T(r6), remote_family=T(fam)))
+        torch.cuda.synchronize()
+        clf.counters_enable(False)
         res["qtype"] = res["qtype"].view(np.uint16)
         _same(res, want)
+        # the unevaluated question slots read kind 0
+        live = np.arange(V.DNSD_MAXQ)[None, :] < want["nq"][:, None]
+        assert not res["kind"][~live].any()
+        # hit counters: the UDP rule of every datagram ([tcp][udp][tcp dflt][udp dflt])
+        # and the group of every question classified VC_DNS_GROUP
+        nt, nu = len(tcp), len(udp)
+        acl_bins = np.where(want["acl"] >= 0, nt + want["acl"], nt + nu + 1)
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ACL),
+                                      np.bincount(acl_bins, minlength=nt + nu + 2))
+        g = want["value"][live & (want["kind"] == V.DNS_GROUP)]
+        np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP),
+                                      np.bincount(g, minlength=len(groups) + 1))
         # the host entry point gives the same
         _same(clf.dns_datagrams((blob, off), r4, port, remote6=r6, remote_family=fam), want)
     finally:

@@ -1049,10 +1049,22 @@ int vc_dns_datagrams_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, 
     auto ho = ctx->get(ctx->hosts);
     HostsImage hi{};
     if (ho) hi = ho->img;
-    hipError_t e = vc::launch_dns_datagrams(ctx->cfg(stream), hi, h->img, a->img, blob, off, n,
-                                            remote_family, remote4, remote6, remote_port,
-                                            out->status, out->acl, out->nq, out->qtype, out->kind,
-                                            out->value);
+    const vc::LaunchCfg c = ctx->cfg(stream);
+    hipError_t e = vc::launch_dns_datagrams(c, hi, h->img, a->img, blob, off, n, remote_family,
+                                            remote4, remote6, remote_port, out->status, out->acl,
+                                            out->nq, out->qtype, out->kind, out->value);
+    if (e == hipSuccess && ctx->counters_on) {
+        // hit counters: the UDP rule matched for every datagram (when the
+        // caller asks for the rule indices: no aux = the UDP list), and the
+        // group of every question classified VC_DNS_GROUP
+        const int64_t nr = int64_t(a->img.n_tcp) + a->img.n_udp;
+        if (out->acl)
+            e = vc::launch_hist(c, VC_HIST_ACL, out->acl, nullptr, n, nr, 0, nr, a->img.n_tcp,
+                                a->counters);
+        if (e == hipSuccess)
+            e = vc::launch_hist(c, VC_HIST_DNS, out->value, out->kind, n * VC_DNSD_MAXQ,
+                                h->img.n_groups, 0, h->img.n_groups, 0, h->counters);
+    }
     return e == hipSuccess ? VC_OK : hip_fail(e, "dns datagram launch");
 }
 

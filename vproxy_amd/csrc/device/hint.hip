@@ -521,6 +521,7 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
     }
     out.status[i] = st;
     if (out.nq) out.nq[i] = uint8_t(nq);
+    for (int q = nq; q < VC_DNSD_MAXQ; ++q) out.kind[i * VC_DNSD_MAXQ + q] = 0;   // not evaluated
 }
 
 template <bool kStage>
