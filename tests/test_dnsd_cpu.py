@@ -99,3 +99,143 @@ def test_oracle_random_datagrams_are_total():
     assert np.all(res["nq"] <= 4)
     for s in (0, 1, 2, 5, 6):          # answer, recursive, response, malformed, host all occur
         assert (st == s).sum() > 0, s
+
+
+# ---------------------------------------------------------------------------
+# A second, independent restatement of Formatter.parsePackets' first packet
+# (Formatter.java:162-372) in Python, written from the Java again, to check
+# the C oracle's parse outcome (malformed / host / parsed) on random and
+# mutated datagrams.  Only the parse: classification is pinned elsewhere.
+# ---------------------------------------------------------------------------
+class _Bad(Exception):
+    """IndexOutOfBoundsException / InvalidDNSPacketException"""
+
+
+class _Deep(Exception):
+    """the pointer chain the library hands to the Java path"""
+
+
+def _py_name(raw, vs, vlen, depth=0):
+    """parseDomainName(data = raw[vs:vs+vlen], rawPacket = raw) -> (chars, used)"""
+    def get(i):
+        if i >= vlen:
+            raise _Bad()
+        return raw[vs + i]
+    out, ln, i = [], 0, 0
+    while True:
+        b = get(i)
+        if ln == 0:
+            if b == 0:
+                break
+            if b & 0xC0 == 0xC0:
+                i += 1
+                off = ((b & 0x3F) << 8) | get(i)
+                if depth + 1 > 16:
+                    raise _Deep()
+                sub, _ = _py_name(raw, off, len(raw) - off, depth + 1)
+                out += sub
+                break
+            ln = b
+        else:
+            out.append(b)
+            ln -= 1
+            if ln == 0:
+                out.append(ord("."))
+        i += 1
+    return out, i + 1
+
+
+def _py_u16(raw, vs, vlen, i):
+    if i + 1 >= vlen:
+        raise _Bad()
+    return (raw[vs + i] << 8) | raw[vs + i + 1]
+
+
+def _py_parse(raw):
+    """-> ("bad" | "deep" | "more" | "ok", questions [(qtype, name bytes)])"""
+    n = len(raw)
+    try:
+        if n < 3:
+            raise _Bad()
+        opcode = (raw[2] >> 3) & 15
+        if opcode not in (0, 1, 2, 4, 5, 6):
+            raise _Bad()
+        if n < 4 or (raw[3] & 15) > 11:
+            raise _Bad()
+        qd, an, ns, ar = (_py_u16(raw, 0, n, k) for k in (4, 6, 8, 10))
+        at, qs = 12, []
+        for _ in range(qd):
+            name, used = _py_name(raw, at, n - at)
+            qtype = _py_u16(raw, at, n - at, used)
+            qclass = _py_u16(raw, at, n - at, used + 2)
+            if qclass not in (1, 3, 4, 254, 255):
+                raise _Bad()
+            qs.append((qtype, bytes(name)))
+            at += used + 4
+        for _ in range(an + ns + ar):
+            _, used = _py_name(raw, at, n - at)
+            vs, vlen = at, n - at
+            rtype, rclass = _py_u16(raw, vs, vlen, used), _py_u16(raw, vs, vlen, used + 2)
+            _py_u16(raw, vs, vlen, used + 4), _py_u16(raw, vs, vlen, used + 6)
+            rdlen = _py_u16(raw, vs, vlen, used + 8)
+            if 252 <= rtype <= 255:
+                raise _Bad()
+            if rtype != 41 and rclass not in (1, 3, 4):
+                raise _Bad()
+            off = used + 10
+            if vlen - off < rdlen:
+                raise _Bad()
+            rs = vs + off
+            if (rtype == 1 and rdlen != 4) or (rtype == 28 and rdlen != 16):
+                raise _Bad()
+            if rtype in (5, 12):
+                _, u = _py_name(raw, rs, rdlen)
+                if u != rdlen:
+                    raise _Bad()
+            if rtype == 16:
+                o = 0
+                while o < rdlen:
+                    ln = raw[rs + o]
+                    o += 1
+                    if rdlen - o < ln:
+                        raise _Bad()
+                    o += ln
+            if rtype == 33:
+                _py_name(raw, rs + 6, rdlen - 6)
+                raise _Bad()          # the target's offset never equals rdlen
+            at += off + rdlen
+        return ("more" if at < n else "ok"), qs
+    except _Bad:
+        return "bad", []
+    except _Deep:
+        return "deep", []
+
+
+def test_oracle_parse_matches_second_restatement():
+    rng = random.Random(11)
+    names = ["example.com.", "a.b.c.", "1.2.3.4.", b"caf\xe9.com.", ".", "x" * 63 + ".y."]
+    dg = [DW.random_datagram(rng, names, mutate=0.5) for _ in range(4000)]
+    dg += [DW.reference_packet(True), DW.reference_packet(False),
+           DW.header(qd=1) + DW.raw_question(b"\xc0\x0c"), DW.header(qd=1) + b"\x01a\xc0\x0c"]
+    blob, off = W.pack(dg)
+    n = len(dg)
+    res = O.dnsd_batch_np(np.zeros(0, W.RULE_DT), np.zeros(0, W.RULE_DT), True, [], [],
+                          blob, off, None, np.zeros(n, np.uint32), None,
+                          np.full(n, 53, np.uint16), nthreads=4)
+    seen = set()
+    for i, d in enumerate(dg):
+        kind, qs = _py_parse(d)
+        st = int(res["status"][i])
+        seen.add(kind)
+        if len(d) == 0:
+            assert st == 4
+        elif kind == "bad":
+            assert st == 5, i
+        elif kind in ("deep", "more"):
+            assert st == 6, i
+        else:
+            assert st not in (4, 5), i
+            if st in (0, 1) and res["nq"][i]:
+                assert [int(t) for t in res["qtype"][i][:res["nq"][i]]] == \
+                    [t for t, _ in qs[:res["nq"][i]]], i
+    assert seen == {"bad", "deep", "more", "ok"}
