@@ -30,6 +30,21 @@ def test_acl_v4_random(n_rules, p_range, weighted, seed):
         np.testing.assert_array_equal(allow, wv)
 
 
+@pytest.mark.parametrize("n_rules", [25000, 70000])
+def test_acl_v4_directory_and_records_large(n_rules):
+    """Lists of ~25k and ~70k intervals: the bucket directory (images.h
+    dir4, built for 17-65535 intervals: here 12-bit buckets holding ~6 or
+    none) and the 16-byte interval records; the harness checks every lookup
+    against a whole binary search and the (x, y) + pieces form, and the
+    results against the oracle on a sample."""
+    tcp, udp = W.gen_sg_rules(n_rules, 9, p_range=0.3, weighted=True)
+    proto, src, port = W.gen_acl_queries(tcp, udp, 6000, 109)
+    got, allow, stats = IC.acl(tcp, udp, False, 4, proto, src, port)
+    want, wv = O.sg_batch_v4_np(tcp, udp, False, proto, src, port, nthreads=8)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(allow, wv)
+
+
 def test_acl_edges_v4_v6():
     tcp, udp = acl_edge_rules()
     rng = np.random.default_rng(7)
