@@ -838,7 +838,10 @@ namespace {
 
 // LDS budget for the staged v4 ACL boundaries (words); above it every
 // (1 << shift)-th boundary is staged as a fence (acl_v4_one).
-constexpr int kLdsWords = 30 * 1024;
+#ifndef VC_ACL_LDS_WORDS
+#define VC_ACL_LDS_WORDS (30 * 1024)
+#endif
+constexpr int kLdsWords = VC_ACL_LDS_WORDS;
 
 int vcd_fences(int nb, int shift) { return (nb + (1 << shift) - 1) >> shift; }
 
