@@ -533,14 +533,16 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     HintImage slow_img = img;
     const int64_t wstride = int64_t(gridDim.x) * kDnsdWaves * 64;
-    for (int64_t base = (int64_t(blockIdx.x) * kDnsdWaves + w) * 64; base < n; base += wstride) {
+    int64_t base = (int64_t(blockIdx.x) * kDnsdWaves + w) * 64;
+    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
+    for (; base < n; base += wstride) {
         const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged =
-            kStage && stage_wave<kDnsdStage>(blob, off[base], off[last], stage[w], &a0);
+        uint32_t o0, o1, a0 = 0;
+        span_of(cur, base, n, &o0, &o1);
+        const uint32_t a = cur.a, e = cur.e;
+        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const bool staged = kStage && stage_wave<kDnsdStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
-            const uint32_t a = off[i], e = off[i + 1];
             if (staged)
                 dnsd_one<int>(hosts, img, &slow_img, acl, in, out, i,
                               reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),

@@ -23,7 +23,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
 
 // Frames staged per wave in LDS as in packet.hip (kStage), parsed from there.
 constexpr int kMirrorWaves = kMirrorBlock / 64;
-constexpr uint32_t kMirrorStage = 8192;
+constexpr uint32_t kMirrorStage = 7168;      // as packet.hip kPktStage: 5 blocks per CU
 constexpr uint32_t kMirrorStageWords = (kMirrorStage + 2 * kApron) / 4;
 
 template <bool kStage>
@@ -34,18 +34,21 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     const MirrorImage& fi = img;
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kMirrorWaves * 64;
-    for (int64_t base = (int64_t(blockIdx.x) * kMirrorWaves + w) * 64; base < n; base += wstride) {
+    int64_t base = (int64_t(blockIdx.x) * kMirrorWaves + w) * 64;
+    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
+    for (; base < n; base += wstride) {
         const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged =
-            kStage && stage_wave<kMirrorStage>(blob, off[base], off[last], stage[w], &a0);
+        uint32_t o0, o1, a0 = 0;
+        span_of(cur, base, n, &o0, &o1);
+        const uint32_t a = cur.a, e = cur.e;
+        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const bool staged = kStage && stage_wave<kMirrorStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
-            const uint32_t a = off[i], e = off[i + 1];
             uint64_t m;
             if (staged)
-                m = mirror_switch_one(fi, origin, reinterpret_cast<const uint8_t*>(stage[w]) +
-                                                      kApron + (a - a0), int(e - a), layer);
+                m = mirror_switch_one(
+                    fi, origin, reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
+                    int(e - a), layer);
             else
                 m = mirror_switch_one(fi, origin, blob + a, int(e - a), layer);
             out[i] = m;

@@ -9,7 +9,13 @@ namespace vcd {
 
 constexpr int kPktBlock = 256;
 constexpr int kPktWaves = kPktBlock / 64;
-constexpr uint32_t kPktStage = 8192;     // per wave: 64 frames of up to 128 B on average
+#ifndef VC_PKT_STAGE
+#define VC_PKT_STAGE 7168
+#endif
+// per wave: 64 frames of up to 112 B on average.  LDS bounds the residency of
+// these latency-bound kernels: 7 KiB gives 5 blocks per CU where 8 KiB gave
+// 4 (switch 1.70 -> 1.47 ms); 6 KiB overflows on the benchmark's 100-B frames.
+constexpr uint32_t kPktStage = VC_PKT_STAGE;
 constexpr uint32_t kPktStageWords = (kPktStage + 2 * kApron) / 4;
 
 __device__ __forceinline__ void store_pkt(const vc_pkt_out& out, int64_t i, const PktOut& o) {
@@ -22,10 +28,8 @@ __device__ __forceinline__ void store_pkt(const vc_pkt_out& out, int64_t i, cons
     if (out.sport) out.sport[i] = o.sport;
     if (out.dport) out.dport[i] = o.dport;
     const bool v4 = o.l3 == VC_L3_IPV4;
-    if (out.src4) out.src4[i] = v4 ? (uint32_t(o.src[0]) << 24 | uint32_t(o.src[1]) << 16 |
-                                      uint32_t(o.src[2]) << 8 | o.src[3]) : 0u;
-    if (out.dst4) out.dst4[i] = v4 ? (uint32_t(o.dst[0]) << 24 | uint32_t(o.dst[1]) << 16 |
-                                      uint32_t(o.dst[2]) << 8 | o.dst[3]) : 0u;
+    if (out.src4) out.src4[i] = v4 ? bswap32(o.src[0]) : 0u;
+    if (out.dst4) out.dst4[i] = v4 ? bswap32(o.dst[0]) : 0u;
     const bool v6 = o.l3 == VC_L3_IPV6;
     if (out.src6) {
         uint4 w = make_uint4(0, 0, 0, 0);
@@ -50,14 +54,16 @@ __global__ __launch_bounds__(kPktBlock) void packet_kernel(
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
-    for (int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64; base < n; base += wstride) {
+    int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64;
+    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
+    for (; base < n; base += wstride) {
         const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged =
-            kStage && stage_wave<kPktStage>(blob, off[base], off[last], stage[w], &a0);
+        uint32_t o0, o1, a0 = 0;
+        span_of(cur, base, n, &o0, &o1);
+        const uint32_t a = cur.a, e = cur.e;
+        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const bool staged = kStage && stage_wave<kPktStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
-            const uint32_t a = off[i], e = off[i + 1];
             PktOut o;
             if (staged) {
                 const uint8_t* lp = reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0);
@@ -114,9 +120,7 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
     int32_t r = -1;
     if (allow && o.status == VC_PKT_OK) {
         if (o.l3 == VC_L3_IPV4) {
-            const uint32_t d = uint32_t(o.dst[0]) << 24 | uint32_t(o.dst[1]) << 16 |
-                               uint32_t(o.dst[2]) << 8 | o.dst[3];
-            r = out_index(trie_v4(rt.fam[0].nodes, rt.fam[0].root_bits, d));
+            r = out_index(trie_v4(rt.fam[0].nodes, rt.fam[0].root_bits, bswap32(o.dst[0])));
         } else if (o.l3 == VC_L3_IPV6) {
             uint64_t hi, lo;
             v6_key(*reinterpret_cast<const uint4*>(o.dst), &hi, &lo);
@@ -133,14 +137,16 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
-    for (int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64; base < n; base += wstride) {
+    int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64;
+    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
+    for (; base < n; base += wstride) {
         const int64_t i = base + lane;
-        const int64_t last = base + 64 < n ? base + 64 : n;
-        uint32_t a0 = 0;
-        const bool staged =
-            kStage && stage_wave<kPktStage>(blob, off[base], off[last], stage[w], &a0);
+        uint32_t o0, o1, a0 = 0;
+        span_of(cur, base, n, &o0, &o1);
+        const uint32_t a = cur.a, e = cur.e;
+        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const bool staged = kStage && stage_wave<kPktStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
-            const uint32_t a = off[i], e = off[i + 1];
             PktOut o;
             if (staged) {
                 const uint8_t* lp = reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0);

@@ -18,9 +18,11 @@ namespace vcd {
 
 enum : int { kPOk = 0, kPErr = 1, kPThrow = 2, kPHang = 3 };
 
+// Addresses are kept as the frame's raw bytes, four to a word in memory
+// order (IPv4: word 0 only), so a parse moves 8 words instead of 32 bytes.
 struct PktOut {
-    uint8_t src[16] __attribute__((aligned(16)));
-    uint8_t dst[16] __attribute__((aligned(16)));
+    uint32_t src[4] __attribute__((aligned(16)));
+    uint32_t dst[4] __attribute__((aligned(16)));
     uint32_t vni;
     uint16_t ether_type, sport, dport;
     uint8_t status, l3, l4, proto;
@@ -28,6 +30,14 @@ struct PktOut {
 
 VC_HD int pk_u8(const uint8_t* p, int i) { return p[i]; }
 VC_HD int pk_u16(const uint8_t* p, int i) { return (int(p[i]) << 8) | p[i + 1]; }
+// four bytes at p + i in memory order: one unaligned dword read (LDS or
+// global) that stays inside the frame.  Two aligned reads and a byte align
+// cut the parse's VALU by a quarter but ran slower (packet 1.32 -> 1.35 ms).
+VC_HD uint32_t pk_raw32(const uint8_t* p, int i) {
+    uint32_t v;
+    __builtin_memcpy(&v, p + i, 4);
+    return v;
+}
 
 // TcpPacket.from: an option of length 0 or 1 makes TcpOption.from read
 // outside its own sub-array (ByteArray.get bounds check) -> throws.
@@ -78,10 +88,8 @@ VC_HD int pk_ipv4(const uint8_t* p, int len, PktOut* o) {
     if (total < ihl * 4) return kPErr;
     if (total != len) return kPErr;
     o->proto = uint8_t(pk_u8(p, 9));
-    for (int k = 0; k < 4; ++k) {
-        o->src[k] = p[12 + k];
-        o->dst[k] = p[16 + k];
-    }
+    o->src[0] = pk_raw32(p, 12);
+    o->dst[0] = pk_raw32(p, 16);
     return pk_l4(p + ihl * 4, total - ihl * 4, o->proto, false, o);
 }
 
@@ -99,9 +107,9 @@ VC_HD int pk_ipv6(const uint8_t* p, int len, PktOut* o) {
     const int payload = pk_u16(p, 4);
     if (payload == 0) return kPErr;
     if (40 + payload != len) return kPErr;
-    for (int k = 0; k < 16; ++k) {
-        o->src[k] = p[8 + k];
-        o->dst[k] = p[24 + k];
+    for (int k = 0; k < 4; ++k) {
+        o->src[k] = pk_raw32(p, 8 + 4 * k);
+        o->dst[k] = pk_raw32(p, 24 + 4 * k);
     }
     int proto = pk_u8(p, 6), skip = 0;
     if (pk_v6_ext(proto)) {
@@ -128,7 +136,7 @@ VC_HD int pk_arp(const uint8_t* p, int len) {
 VC_HD void pk_clear_ip(PktOut* o) {
     o->l4 = o->proto = 0;
     o->sport = o->dport = 0;
-    for (int k = 0; k < 16; ++k) o->src[k] = o->dst[k] = 0;
+    for (int k = 0; k < 4; ++k) o->src[k] = o->dst[k] = 0;
 }
 
 VC_HD int pk_ether(const uint8_t* p, int len, PktOut* o) {

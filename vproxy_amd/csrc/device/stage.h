@@ -36,6 +36,28 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
     return true;
 }
 
+// A lane's item [a, e) of the chunk starting at `base` (clamped to n past
+// the end).  The streaming kernels load the next chunk's offsets before
+// parsing the current one, and take the chunk's span from lanes 0 and
+// last (span_of), so a chunk costs one blob round trip instead of three
+// dependent ones (offsets of the span, the blob, the lane's offsets).
+struct LaneSpan {
+    uint32_t a, e;
+};
+
+__device__ __forceinline__ LaneSpan lane_span(const uint32_t* off, int64_t base, int64_t n) {
+    const int64_t i = base + int(threadIdx.x & 63);
+    return LaneSpan{off[i < n ? i : n], off[i + 1 < n ? i + 1 : n]};
+}
+
+// [o0, o1) of the chunk's items, from the lanes' spans (wave-uniform)
+__device__ __forceinline__ void span_of(const LaneSpan& s, int64_t base, int64_t n, uint32_t* o0,
+                                        uint32_t* o1) {
+    const int lastl = int((base + 64 < n ? base + 64 : n) - base - 1);
+    *o0 = uint32_t(__builtin_amdgcn_readfirstlane(int(s.a)));
+    *o1 = uint32_t(__builtin_amdgcn_readlane(int(s.e), lastl));
+}
+
 __device__ __forceinline__ void wave_done() {
     // every lane has finished reading the staged items before the next copy
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
