@@ -109,3 +109,18 @@ def test_unstaged_paths(clf, shift, pad):
         res[k] = res[k].view(np.uint16)
     for i, w in enumerate(want):
         assert _rows(res, i) == w, (i, frames[i][:80].hex())
+
+
+def test_ragged_batch_sizes(clf):
+    """Chunk boundaries of the staged kernels: each wave takes the next
+    chunk's offsets one chunk ahead and the span's end from the last live
+    lane (stage.h span_of), so batches of 1, 63, 64, 65, 127, 129 frames and
+    one that leaves a partial chunk after a full grid stride are checked
+    against the oracle (the switch, mirror and DNS-datagram kernels share
+    the loop)."""
+    frames_all = gen_frames(np.random.default_rng(123), 70000)
+    for n in (1, 2, 63, 64, 65, 127, 128, 129, 4097, 65536 + 65):
+        frames = frames_all[:n]
+        res = clf.parse_packets(frames, 0)
+        for i in list(range(min(n, 200))) + list(range(max(0, n - 200), n)):
+            assert _rows(res, i) == O.parse_packet(frames[i], 0), (n, i)
