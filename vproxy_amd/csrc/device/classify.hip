@@ -861,6 +861,10 @@ int v4_staged_words(const AclImage& img, int shift) {
 
 }  // namespace
 
+#ifndef VC_LDS_GRANULE
+#define VC_LDS_GRANULE 512
+#endif
+
 int resident_per_cu(const void* kernel, int block, size_t shmem) {
     static std::mutex mu;
     static std::map<std::pair<const void*, size_t>, int> cache;
@@ -872,6 +876,20 @@ int resident_per_cu(const void* kernel, int block, size_t shmem) {
         per_cu < 1) {
         (void)hipGetLastError();
         per_cu = 1;
+    }
+    // LDS is handed out per workgroup in VC_LDS_GRANULE-byte units; the
+    // occupancy query counts exact bytes, and a grid sized from it can hold a
+    // second, partial round of workgroups that runs after the first
+    hipFuncAttributes fa;
+    int dev = 0, lds_cu = 0;
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) ==
+            hipSuccess) {
+        const size_t g = VC_LDS_GRANULE;
+        const size_t wg = (fa.sharedSizeBytes + shmem + g - 1) / g * g;
+        if (wg > 0 && lds_cu > 0) per_cu = std::max(1, std::min(per_cu, int(size_t(lds_cu) / wg)));
+    } else {
+        (void)hipGetLastError();
     }
     cache[{kernel, shmem}] = per_cu;
     return per_cu;
