@@ -862,7 +862,7 @@ int v4_staged_words(const AclImage& img, int shift) {
 }  // namespace
 
 #ifndef VC_LDS_GRANULE
-#define VC_LDS_GRANULE 512
+#define VC_LDS_GRANULE 1024
 #endif
 
 int resident_per_cu(const void* kernel, int block, size_t shmem) {
