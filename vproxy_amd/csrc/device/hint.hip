@@ -282,10 +282,11 @@ constexpr int kDnsdBlock = 128;
 constexpr int kDnsdWaves = kDnsdBlock / 64;
 // LDS per 128-thread workgroup: two 4 KiB stages (64 queries of up to 64 B
 // on average per wave; longer spans are read from global memory) and a
-// per-lane qname buffer -- 28.7 KiB, five workgroups per CU.  An 8-byte
-// apron on the qname buffers (26.6 KiB, six workgroups, 12 waves per CU)
-// ran 5.30 -> 7.18 ms; with the same 8-byte apron at the old stride 5.27 ms:
-// the extra residency, not the layout, costs (profiles/r02_ab_dnsd_residency.txt).
+// per-lane qname buffer -- 28.7 KiB, five workgroups per CU.  A smaller
+// qname apron (26.6 KiB) does not make room for a sixth once LDS is counted
+// in allocation granules (classify.hip resident_per_cu); before that cap the
+// grid asked for six and ran a second round, 5.30 -> 7.18 ms
+// (profiles/r02_ab_dnsd_residency.txt).
 constexpr uint32_t kDnsdStage = 4096;
 constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
 constexpr int kNameCap = 128;                 // decoded qname chars a lane classifies
