@@ -282,18 +282,21 @@ constexpr int kDnsdBlock = 128;
 constexpr int kDnsdWaves = kDnsdBlock / 64;
 // LDS per 128-thread workgroup: two 4 KiB stages (64 queries of up to 64 B
 // on average per wave; longer spans are read from global memory) and a
-// per-lane qname buffer -- 28.7 KiB, five workgroups per CU.  A smaller
-// qname apron (26.6 KiB) does not make room for a sixth once LDS is counted
-// in allocation granules (classify.hip resident_per_cu); before that cap the
-// grid asked for six and ran a second round, 5.30 -> 7.18 ms
+// per-lane qname buffer -- 25.6 KiB, six workgroups per CU in 1 KiB LDS
+// granules (classify.hip resident_per_cu).  A 16-byte qname apron made it
+// 28.7 KiB and five: 5.28 -> 4.44 ms with the sixth
 // (profiles/r02_ab_dnsd_residency.txt).
 constexpr uint32_t kDnsdStage = 4096;
 constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
 constexpr int kNameCap = 128;                 // decoded qname chars a lane classifies
-// an odd stride in words: lane l's word k sits in bank (41 l + k) mod 64, so
+// Readable bytes around a qname: LdsSrc reads the aligned word pair that
+// holds [pos, pos + 4) for pos in [-3, len + 3].
+constexpr int kNameApron = 4;
+// an odd stride in words: lane l's word k sits in bank (35 l + k) mod 64, so
 // the lanes' buffers do not collide when they read the same word index
 // (an even stride of 40 words put them on 8 banks)
-constexpr int kNameWords = (kNameCap + 2 * kApron) / 4 + 1;
+constexpr int kNameWords = (kNameCap + 2 * kNameApron) / 4 + 1;
+static_assert((kNameApron + kNameCap + 3) / 4 + 1 < kNameWords, "qname buffer too short");
 constexpr int kMaxPtr = 16;
 
 enum : int { kNameOk = 0, kNameBad = 1, kNameHost = 2 };
@@ -490,7 +493,7 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
             } else {
                 // handleRequest: questions in order until one goes recursive
                 at = 12;
-                uint8_t* nb = reinterpret_cast<uint8_t*>(name) + kApron;
+                uint8_t* nb = reinterpret_cast<uint8_t*>(name) + kNameApron;
                 for (int q = 0; q < qd; ++q) {
                     int used = 0, len = 0;
                     parse_name(p, n, at, n - at, &used, [&](int b) {
@@ -513,7 +516,7 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
                     }
                     uint8_t kd;
                     int32_t val;
-                    dns_one(hosts, img, slow_img, LdsSrc{name, int(kApron)}, len, &kd, &val);
+                    dns_one(hosts, img, slow_img, LdsSrc{name, kNameApron}, len, &kd, &val);
                     put(q, qtype, kd, val);
                     if (kd == VC_DNS_RECURSIVE) {
                         st = VC_DNSD_RECURSIVE;
