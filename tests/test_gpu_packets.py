@@ -124,3 +124,48 @@ def test_ragged_batch_sizes(clf):
         res = clf.parse_packets(frames, 0)
         for i in list(range(min(n, 200))) + list(range(max(0, n - 200), n)):
             assert _rows(res, i) == O.parse_packet(frames[i], 0), (n, i)
+
+
+@pytest.mark.parametrize("shift", [0, 1])
+def test_blob_at_allocation_end(clf, shift):
+    """The frames' last byte is the last byte of a device allocation (a
+    32 MiB torch block -- above 10 MiB the caching allocator gives a request
+    its own segment -- filled from its end) and the offsets array ends one
+    element past n likewise: staged (aligned) and unstaged (shift 1) parse
+    kernels must read nothing beyond [0, off[n]) and off[0..n]."""
+    import torch
+    frames = gen_frames(np.random.default_rng(131 + shift), 9000)
+    raw = np.frombuffer(b"".join(frames), np.uint8)
+    cap = 32 << 20
+    assert len(raw) + shift <= cap
+    block = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    start = cap - len(raw)           # the blob's last byte is the block's last byte
+    if (start % 4 == 0) != (shift == 0):
+        # trailing padding frame of 1-3 bytes moves the start to the wanted alignment
+        pad = (start % 4) if shift == 0 else 1
+        frames = frames + [bytes(pad)]
+        raw = np.frombuffer(b"".join(frames), np.uint8)
+        start = cap - len(raw)
+    block[start:start + len(raw)] = torch.from_numpy(raw.copy()).cuda()
+    blob = block[start:]
+    if shift == 0:
+        assert blob.data_ptr() % 4 == 0
+    else:
+        assert blob.data_ptr() % 4 != 0
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.int32)
+    off[1:] = np.cumsum(lens)
+    obuf = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+    doff = obuf[cap // 4 - len(off):]
+    doff.copy_(torch.from_numpy(off).cuda())
+    res = clf.parse_packets((blob, doff), 0)
+    torch.cuda.synchronize()
+    res = {k: v.cpu().numpy() for k, v in res.items()}
+    for k in ("src6", "dst6"):
+        res[k] = res[k].view(np.uint8)
+    for k in ("src4", "dst4", "vni"):
+        res[k] = res[k].view(np.uint32)
+    for k in ("sport", "dport", "ether_type"):
+        res[k] = res[k].view(np.uint16)
+    for i in list(range(300)) + list(range(len(frames) - 300, len(frames))):
+        assert _rows(res, i) == O.parse_packet(frames[i], 0), i

@@ -197,15 +197,13 @@ def test_pipeline_without_family_or_hosts(setup):
     np.testing.assert_array_equal(grp2.cpu().numpy(), want[2])
 
 
-@pytest.mark.parametrize("registered", [False, True])
-def test_host_entry_point_equals_device(setup, registered):
-    """vc_pipeline over host arrays: pageable (chunked staging, 3 chunks) and
+def host_entry_point_equals_device(clf, t, registered):
+    """vc_pipeline over host arrays: pageable (chunked staging, 3 chunks) or
     registered (zero-copy) give the device entry point's outputs."""
     import torch
-    clf, t = setup
     n = (9 << 20) + 5
     p = _packets(t, n, 23)
-    pool = np.ascontiguousarray(t["pool"], np.int32)
+    pool = np.array(t["pool"], np.int32)          # an array of its own (it may be registered)
     d = _dev(p)
     ref = [x.cpu().numpy() for x in _call(clf, d, torch.from_numpy(pool).cuda())]
     outs = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32),
@@ -223,6 +221,10 @@ def test_host_entry_point_equals_device(setup, registered):
                 V.check(V.lib().vc_host_unregister(x.ctypes.data))
     for g, r in zip(got, ref):
         np.testing.assert_array_equal(g, r)
+
+
+def test_host_entry_point_equals_device(setup):
+    host_entry_point_equals_device(*setup, registered=False)
 
 
 def test_bad_arguments(setup):

@@ -2,7 +2,9 @@
 // publication, uploads, and the host-side control-plane mirrors.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -31,16 +33,370 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(VC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Device allocation owned by a snapshot.
+// ---------------------------------------------------------------------------
+// Retired device memory.  A snapshot's last reference can drop on any
+// thread -- often an event-loop thread finishing a classify call that pinned
+// the old tables -- and hipFree waits for the whole device.  Its buffers go
+// here instead, and the control thread frees them (vc_compile_*, vc_destroy):
+// the thread that recompiles pays the wait, the classify threads never do.
+// ---------------------------------------------------------------------------
+struct Graveyard {
+    std::mutex mu;
+    std::vector<void*> ptrs;
+    size_t bytes = 0;
+    void bury(void* p, size_t n) {
+        std::lock_guard<std::mutex> lk(mu);
+        ptrs.push_back(p);
+        bytes += n;
+    }
+    void drain() {
+        std::vector<void*> v;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            v.swap(ptrs);
+            bytes = 0;
+        }
+        for (void* p : v) (void)hipFree(p);
+    }
+};
+
+// Device allocation owned by a snapshot; retired through the graveyard.
 struct DevBuf {
     void* p = nullptr;
+    size_t n = 0;
+    std::shared_ptr<Graveyard> grave;
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() {
-        // hipFree synchronises with in-flight work on the device, so a
-        // snapshot released while a batch still reads it is freed after it.
-        if (p) (void)hipFree(p);
+        if (p) grave->bury(p, n);
+    }
+};
+
+// A growable bump arena of device (hipMalloc) or page-locked host
+// (hipHostMalloc) memory.  alloc never moves earlier allocations: a request
+// that does not fit opens a new block; reset(), called only when nothing
+// uses the arena, merges the blocks into one sized for the high-water mark,
+// so a steady stream of calls allocates nothing.
+class Arena {
+public:
+    explicit Arena(bool host) : host_(host) {}
+    Arena(const Arena&) = delete;
+    Arena& operator=(const Arena&) = delete;
+    ~Arena() { release(); }
+    void* alloc(size_t bytes, hipError_t* err) {
+        const size_t b = (std::max<size_t>(bytes, 1) + 255) & ~size_t(255);
+        if (blocks_.empty() || used_ + b > blocks_.back().second) {
+            const size_t grow = blocks_.empty() ? 0 : 2 * blocks_.back().second;
+            const size_t want = std::max(b, std::max(size_t(1) << 20, grow));
+            void* p = nullptr;
+            const hipError_t e = host_ ? hipHostMalloc(&p, want, hipHostMallocDefault)
+                                       : hipMalloc(&p, want);
+            if (e != hipSuccess) {
+                *err = e;
+                return nullptr;
+            }
+            blocks_.emplace_back(static_cast<uint8_t*>(p), want);
+            used_ = 0;
+        }
+        uint8_t* p = blocks_.back().first + used_;
+        used_ += b;
+        return p;
+    }
+    hipError_t reset() {
+        used_ = 0;
+        if (blocks_.size() <= 1) return hipSuccess;
+        size_t total = 0;
+        for (auto& b : blocks_) total += b.second;
+        release();
+        void* p = nullptr;
+        const hipError_t e = host_ ? hipHostMalloc(&p, total, hipHostMallocDefault)
+                                   : hipMalloc(&p, total);
+        if (e == hipSuccess) blocks_.emplace_back(static_cast<uint8_t*>(p), total);
+        return e;
+    }
+    void release() {
+        for (auto& b : blocks_) (void)(host_ ? hipHostFree(b.first) : hipFree(b.first));
+        blocks_.clear();
+        used_ = 0;
+    }
+
+private:
+    bool host_;
+    std::vector<std::pair<uint8_t*, size_t>> blocks_;
+    size_t used_ = 0;
+};
+
+// One staging lane: a stream, device memory for a call's inputs and
+// outputs, and a page-locked bounce buffer.  Every DMA of the host entry
+// points runs between memory the library allocated itself: caller arrays
+// are copied into the bounce buffer with memcpy on the calling thread, and
+// results are copied out of it after the lane's stream has drained.  No
+// pageable-memory DMA (which makes the runtime look up, pin or stage the
+// caller's pages) and no stream-ordered pool allocation is on this path.
+struct StageLane {
+    hipStream_t s = nullptr;
+    Arena dev{false}, host{true};
+    struct Back {
+        void* user;
+        const void* pinned;
+        size_t bytes;
+    };
+    std::vector<Back> backs;
+    bool busy = false;      // copies or kernels issued since the last finish
+
+    // wait for the lane's work without giving its memory back
+    hipError_t wait() { return busy ? hipStreamSynchronize(s) : hipSuccess; }
+    // wait, deliver the results to the caller's arrays (deliver), and reset
+    // the arenas for the next user
+    hipError_t finish(bool deliver) {
+        hipError_t e = busy ? hipStreamSynchronize(s) : hipSuccess;
+        busy = false;
+        if (e == hipSuccess && deliver)
+            for (const Back& b : backs) std::memcpy(b.user, b.pinned, b.bytes);
+        backs.clear();
+        const hipError_t r1 = dev.reset(), r2 = host.reset();
+        return e != hipSuccess ? e : r1 != hipSuccess ? r1 : r2;
+    }
+};
+
+// Lanes 0 and 1 carry a chunked call's alternating chunks (host_chunks);
+// lane 2 holds whole-call data (the pipeline's hostname-pool results) and
+// the uploads of a compile.
+struct Stager {
+    StageLane lane[3];
+};
+
+struct Snapshot;
+struct AclSnap;
+struct RouteSnap;
+struct HintSnap;
+struct HostsSnap;
+struct ServerSnap;
+struct CertSnap;
+struct MirrorSnap;
+
+}  // namespace
+
+struct vc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
+    std::mutex handoff_mu;
+    vc::ScratchRing scratch;       // counter-pass scratch, reused across calls
+    vc::TicketRing tickets;        // work counters of the string kernels
+    int num_cus = 256;
+    bool sync_check = false;       // VC_SYNC_CHECK: synchronise + check after every launch / copy
+    std::atomic<bool> counters_on{false};
+    std::mutex compile_mu;   // serialises compiles; classify never takes it
+    std::shared_ptr<Graveyard> grave = std::make_shared<Graveyard>();
+    std::mutex stage_mu;     // idle stagers (one per concurrent host-buffer call)
+    std::vector<std::unique_ptr<Stager>> stagers;
+    std::shared_ptr<const AclSnap> acl;
+    std::shared_ptr<const RouteSnap> route;
+    std::shared_ptr<const HintSnap> hint;
+    std::shared_ptr<const HostsSnap> hosts;
+    std::shared_ptr<const ServerSnap> servers;
+    std::shared_ptr<const CertSnap> certs;
+    std::shared_ptr<const MirrorSnap> mirror;
+
+    template <class S>
+    std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
+        return std::atomic_load(&p);
+    }
+    template <class S>
+    void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
+        std::atomic_store(&slot, std::move(v));
+        // the previous tables' buffers, if no call pins them any more
+        grave->drain();
+    }
+    // `s` is the caller's hipStream_t; NULL is HIP's null stream, as in
+    // every HIP API (torch's default stream reports itself as 0).
+    // CUs a stream may run on: its CU mask (hipExtStreamCreateWithCUMask),
+    // so grids sized to one resident round fill a partitioned stream's share
+    int stream_cus(hipStream_t s) const {
+        uint32_t m[32] = {};
+        if (hipExtStreamGetCUMask(s, 32, m) != hipSuccess) return num_cus;
+        int k = 0;
+        for (uint32_t w : m) k += __builtin_popcount(w);
+        return k > 0 && k < num_cus ? k : num_cus;
+    }
+    vc::LaunchCfg cfg(void* s) const {
+        vc::LaunchCfg c;
+        c.stream = static_cast<hipStream_t>(s);
+        c.num_cus = stream_cus(c.stream);
+        c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
+        c.scratch = const_cast<vc::ScratchRing*>(&scratch);
+        c.tickets = const_cast<vc::TicketRing*>(&tickets);
+        return c;
+    }
+};
+
+namespace {
+
+int set_dev(vc_ctx* ctx) {
+    if (!ctx) return fail(VC_EINVAL, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? VC_OK : hip_fail(e, "hipSetDevice");
+}
+
+// Device-side check flags of a VC_DEVCHECK build (dev_common.h): the first
+// failing site per kernel file, read and cleared.  Always empty otherwise.
+int devcheck_report(const char* what) {
+    uint32_t f[4] = {};
+    if (vc::devcheck_take(f) != hipSuccess || f[0] == 0) return VC_OK;
+    return fail(VC_EDEVICE, std::string(what) + ": device check failed at site " +
+                                std::to_string(f[0]) + " (" + std::to_string(f[1]) +
+                                " hits, detail " + std::to_string(f[2]) + ", " +
+                                std::to_string(f[3]) + ")");
+}
+
+// The status of a launch: its launch error, and under VC_SYNC_CHECK the
+// stream's completion and the device check flags, named by the entry point.
+int launched(vc_ctx* ctx, hipError_t e, void* stream, const char* what) {
+    if (e != hipSuccess) return hip_fail(e, what);
+    if (!ctx->sync_check) return VC_OK;
+    e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, (std::string(what) + " (sync check)").c_str());
+    return devcheck_report(what);
+}
+
+// An idle stager for one host-buffer call, returned when the call ends.
+class StagerLease {
+public:
+    explicit StagerLease(vc_ctx* ctx) : ctx_(ctx) {
+        {
+            std::lock_guard<std::mutex> lk(ctx->stage_mu);
+            if (!ctx->stagers.empty()) {
+                st_ = std::move(ctx->stagers.back());
+                ctx->stagers.pop_back();
+                return;
+            }
+        }
+        auto st = std::make_unique<Stager>();
+        for (StageLane& l : st->lane)
+            if ((err_ = hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking)) != hipSuccess) {
+                destroy(st.get());
+                return;
+            }
+        st_ = std::move(st);
+    }
+    StagerLease(const StagerLease&) = delete;
+    StagerLease& operator=(const StagerLease&) = delete;
+    ~StagerLease() {
+        if (!st_) return;
+        // a call that failed part-way may leave copies in flight into the
+        // lane's memory: wait for them before the stager is reused
+        for (StageLane& l : st_->lane) (void)l.finish(false);
+        std::lock_guard<std::mutex> lk(ctx_->stage_mu);
+        ctx_->stagers.push_back(std::move(st_));
+    }
+    explicit operator bool() const { return st_ != nullptr; }
+    hipError_t err() const { return err_; }
+    StageLane& lane(int k) { return st_->lane[k]; }
+    static void destroy(Stager* st) {
+        for (StageLane& l : st->lane) {
+            if (!l.s) continue;
+            (void)hipStreamSynchronize(l.s);
+            (void)hipStreamDestroy(l.s);
+            l.s = nullptr;
+            l.dev.release();
+            l.host.release();
+        }
+    }
+
+private:
+    vc_ctx* ctx_;
+    std::unique_ptr<Stager> st_;
+    hipError_t err_ = hipSuccess;
+};
+
+// One call's (or one chunk's) staging on a lane: inputs copied host ->
+// bounce -> device, outputs allocated on the device and copied back into
+// the bounce buffer; finish() hands them to the caller's arrays.
+struct Staging {
+    vc_ctx* ctx;
+    StageLane& L;
+    const char* what;
+    hipError_t err = hipSuccess;
+    Staging(vc_ctx* c, StageLane& l, const char* w) : ctx(c), L(l), what(w) {}
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    hipStream_t stream() const { return L.s; }
+    void copied() {
+        L.busy = true;
+        if (err == hipSuccess && ctx->sync_check) {
+            err = hipStreamSynchronize(L.s);
+            if (err == hipSuccess) err = hipGetLastError();
+        }
+    }
+    void* in(const void* h, size_t bytes) {
+        if (!h || err != hipSuccess) return nullptr;
+        void* d = L.dev.alloc(bytes, &err);
+        void* p = err == hipSuccess && bytes ? L.host.alloc(bytes, &err) : nullptr;
+        if (err != hipSuccess || !bytes) return d;
+        std::memcpy(p, h, bytes);
+        err = hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, L.s);
+        copied();
+        return d;
+    }
+    void* out(const void* h, size_t bytes) {
+        if (!h || err != hipSuccess) return nullptr;
+        return L.dev.alloc(bytes, &err);
+    }
+    void back(void* h, const void* d, size_t bytes) {
+        if (!h || !d || !bytes || err != hipSuccess) return;
+        void* p = L.host.alloc(bytes, &err);
+        if (err != hipSuccess) return;
+        err = hipMemcpyAsync(p, d, bytes, hipMemcpyDeviceToHost, L.s);
+        if (err == hipSuccess) L.backs.push_back(StageLane::Back{h, p, bytes});
+        copied();
+    }
+    // status of the call: wait for the lane and deliver the results
+    int finish() {
+        const hipError_t e = err != hipSuccess ? err : L.finish(true);
+        if (e != hipSuccess) return hip_fail(e, what);
+        return ctx->sync_check ? devcheck_report(what) : VC_OK;
+    }
+};
+
+// A compile's uploads: host vectors through a stager's bounce buffer into
+// device buffers the snapshot owns, on lane 2's stream, waited for once.
+struct Upload {
+    vc_ctx* ctx;
+    StagerLease lease;
+    hipError_t err;
+    explicit Upload(vc_ctx* c) : ctx(c), lease(c), err(lease.err()) {}
+    StageLane& L() { return lease.lane(2); }
+    void* dev(Snapshot& s, size_t bytes);
+    template <class T>
+    const T* operator()(Snapshot& s, const std::vector<T>& v) {
+        void* d = dev(s, v.size() * sizeof(T));
+        if (d && !v.empty() && err == hipSuccess) {
+            const size_t bytes = v.size() * sizeof(T);
+            void* p = L().host.alloc(bytes, &err);
+            if (err != hipSuccess) return nullptr;
+            std::memcpy(p, v.data(), bytes);
+            L().busy = true;
+            err = hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, L().s);
+        }
+        return static_cast<const T*>(d);
+    }
+    // zero-filled device counters
+    unsigned long long* zeros(Snapshot& s, int64_t n) {
+        const size_t bytes = size_t(std::max<int64_t>(n, 1)) * 8;
+        void* d = dev(s, bytes);
+        if (d && err == hipSuccess) {
+            L().busy = true;
+            err = hipMemsetAsync(d, 0, bytes, L().s);
+        }
+        return static_cast<unsigned long long*>(d);
+    }
+    hipError_t done() {
+        if (!lease) return err;
+        const hipError_t e = L().finish(false);
+        return err != hipSuccess ? err : e;
     }
 };
 
@@ -49,28 +405,26 @@ struct Snapshot {
     unsigned long long* counters = nullptr;
     int64_t n_counters = 0;
 
-    template <class T>
-    const T* upload(const std::vector<T>& v, hipError_t* err) {
-        auto b = std::make_unique<DevBuf>();
-        size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
-        hipError_t e = hipMalloc(&b->p, bytes);
-        if (e == hipSuccess && !v.empty()) e = hipMemcpy(b->p, v.data(), v.size() * sizeof(T),
-                                                         hipMemcpyHostToDevice);
-        if (e != hipSuccess) *err = e;
-        const T* p = static_cast<const T*>(b->p);
-        bufs.push_back(std::move(b));
-        return p;
-    }
-    hipError_t alloc_counters(int64_t n) {
-        auto b = std::make_unique<DevBuf>();
-        hipError_t e = hipMalloc(&b->p, size_t(std::max<int64_t>(n, 1)) * 8);
-        if (e == hipSuccess) e = hipMemset(b->p, 0, size_t(std::max<int64_t>(n, 1)) * 8);
-        counters = static_cast<unsigned long long*>(b->p);
+    void alloc_counters(Upload& up, int64_t n) {
+        counters = up.zeros(*this, n);
         n_counters = n;
-        bufs.push_back(std::move(b));
-        return e;
     }
 };
+
+void* Upload::dev(Snapshot& s, size_t bytes) {
+    if (err != hipSuccess) return nullptr;
+    auto b = std::make_unique<DevBuf>();
+    b->n = std::max<size_t>(bytes, 16);
+    b->grave = ctx->grave;
+    err = hipMalloc(&b->p, b->n);
+    if (err != hipSuccess) {
+        b->p = nullptr;
+        return nullptr;
+    }
+    void* p = b->p;
+    s.bufs.push_back(std::move(b));
+    return p;
+}
 
 struct AclSnap : Snapshot {
     AclImage img{};
@@ -102,106 +456,6 @@ struct ServerSnap : Snapshot {
 
 }  // namespace
 
-struct vc_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t lane[2] = {nullptr, nullptr};   // chunked host-buffer calls (host_chunks)
-    hipMemPool_t pool = nullptr;   // scratch of the counter passes
-    hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
-    std::mutex handoff_mu;
-    vc::ScratchRing scratch;       // counter-pass scratch, reused across calls
-    vc::TicketRing tickets;        // work counters of the string kernels
-    int num_cus = 256;
-    std::atomic<bool> counters_on{false};
-    std::mutex compile_mu;   // serialises compiles; classify never takes it
-    std::shared_ptr<const AclSnap> acl;
-    std::shared_ptr<const RouteSnap> route;
-    std::shared_ptr<const HintSnap> hint;
-    std::shared_ptr<const HostsSnap> hosts;
-    std::shared_ptr<const ServerSnap> servers;
-    std::shared_ptr<const CertSnap> certs;
-    std::shared_ptr<const MirrorSnap> mirror;
-
-    template <class S>
-    std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
-        return std::atomic_load(&p);
-    }
-    template <class S>
-    void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
-        std::atomic_store(&slot, std::move(v));
-    }
-    // `s` is the caller's hipStream_t; NULL is HIP's null stream, as in
-    // every HIP API (torch's default stream reports itself as 0).
-    // CUs a stream may run on: its CU mask (hipExtStreamCreateWithCUMask),
-    // so grids sized to one resident round fill a partitioned stream's share
-    int stream_cus(hipStream_t s) const {
-        uint32_t m[32] = {};
-        if (hipExtStreamGetCUMask(s, 32, m) != hipSuccess) return num_cus;
-        int k = 0;
-        for (uint32_t w : m) k += __builtin_popcount(w);
-        return k > 0 && k < num_cus ? k : num_cus;
-    }
-    vc::LaunchCfg cfg(void* s) const {
-        vc::LaunchCfg c;
-        c.stream = static_cast<hipStream_t>(s);
-        c.num_cus = stream_cus(c.stream);
-        c.pool = pool;
-        c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
-        c.scratch = const_cast<vc::ScratchRing*>(&scratch);
-        c.tickets = const_cast<vc::TicketRing*>(&tickets);
-        return c;
-    }
-};
-
-namespace {
-
-int set_dev(vc_ctx* ctx) {
-    if (!ctx) return fail(VC_EINVAL, "null context");
-    hipError_t e = hipSetDevice(ctx->device);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "hipSetDevice");
-}
-
-// Synchronous host-pointer staging for the plain (non _dev) entry points:
-// stream-ordered allocations from the context's pool (no hipMalloc /
-// hipFree device synchronisation per call), copies on the context stream,
-// freed in stream order when the call returns.
-struct Staging {
-    hipMemPool_t pool;
-    hipStream_t s;
-    std::vector<void*> bufs;
-    hipError_t err = hipSuccess;
-    Staging(hipMemPool_t p, hipStream_t st) : pool(p), s(st) {}
-    Staging(const Staging&) = delete;
-    Staging& operator=(const Staging&) = delete;
-    ~Staging() {
-        for (void* p : bufs) (void)hipFreeAsync(p, s);
-    }
-    void* alloc(size_t bytes) {
-        void* p = nullptr;
-        if (err == hipSuccess)
-            err = pool ? hipMallocFromPoolAsync(&p, std::max<size_t>(bytes, 16), pool, s)
-                       : hipMallocAsync(&p, std::max<size_t>(bytes, 16), s);
-        if (err == hipSuccess) bufs.push_back(p);
-        return p;
-    }
-    void* in(const void* h, size_t bytes, hipStream_t) {
-        if (!h) return nullptr;
-        void* p = alloc(bytes);
-        if (err == hipSuccess && bytes) err = hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s);
-        return p;
-    }
-    void* out(const void* h, size_t bytes) {
-        if (!h) return nullptr;
-        return alloc(bytes);
-    }
-    void back(void* h, const void* d, size_t bytes, hipStream_t) {
-        if (h && d && bytes && err == hipSuccess)
-            err = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
-    }
-};
-
-}  // namespace
-
 extern "C" {
 
 const char* vc_version(void) { return "vclassify 0.1 (gfx950)"; }
@@ -224,39 +478,19 @@ int vc_create(int device, vc_ctx** out) {
     auto* c = new vc_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount;
+    const char* sc = std::getenv("VC_SYNC_CHECK");
+    c->sync_check = sc && *sc && std::strcmp(sc, "0") != 0;
     if ((e = hipSetDevice(device)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->lane[0], hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->lane[1], hipStreamNonBlocking)) != hipSuccess) {
-        for (hipStream_t s : {c->stream, c->lane[0], c->lane[1]})
-            if (s) (void)hipStreamDestroy(s);
-        delete c;
-        return hip_fail(e, "stream create");
-    }
-    // Staging pool of the host-buffer entry points: calls may come on several
-    // streams at once, so a block freed on one stream is never handed to
-    // another without a stream-order dependency; memory stays cached.
-    hipMemPoolProps props{};
-    props.allocType = hipMemAllocationTypePinned;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = device;
-    if ((e = hipMemPoolCreate(&c->pool, &props)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming)) != hipSuccess ||
         (e = c->scratch.init()) != hipSuccess || (e = c->tickets.init()) != hipSuccess) {
         c->scratch.destroy();
         c->tickets.destroy();
         if (c->handoff) (void)hipEventDestroy(c->handoff);
-        if (c->pool) (void)hipMemPoolDestroy(c->pool);
-        (void)hipStreamDestroy(c->stream);
-        (void)hipStreamDestroy(c->lane[0]);
-        (void)hipStreamDestroy(c->lane[1]);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
         delete c;
-        return hip_fail(e, "mem pool create");
+        return hip_fail(e, "context create");
     }
-    int off = 0;
-    uint64_t keep = ~uint64_t(0);
-    (void)hipMemPoolSetAttribute(c->pool, hipMemPoolReuseAllowOpportunistic, &off);
-    (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep);
     *out = c;
     return VC_OK;
 }
@@ -264,7 +498,8 @@ int vc_create(int device, vc_ctx** out) {
 void vc_destroy(vc_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    // batches may still run on callers' streams and read the tables
+    (void)hipDeviceSynchronize();
     ctx->acl.reset();
     ctx->route.reset();
     ctx->hint.reset();
@@ -272,18 +507,10 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->servers.reset();
     ctx->certs.reset();
     ctx->mirror.reset();
+    ctx->grave->drain();
+    for (auto& st : ctx->stagers) StagerLease::destroy(st.get());
+    ctx->stagers.clear();
     (void)hipStreamDestroy(ctx->stream);
-    for (hipStream_t s : ctx->lane) {
-        (void)hipStreamSynchronize(s);
-        (void)hipStreamDestroy(s);
-    }
-    if (ctx->pool) {
-        // batches may still run on callers' streams: their scratch is freed
-        // in stream order, so wait for the device before the pool goes
-        (void)hipDeviceSynchronize();
-        (void)hipMemPoolDestroy(ctx->pool);
-    }
-    (void)hipDeviceSynchronize();
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     ctx->scratch.destroy();
     ctx->tickets.destroy();
@@ -331,26 +558,26 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
     if (rc) return fail(rc, "invalid SecurityGroup rule (network must be a valid Network)");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<AclSnap>();
-    hipError_t e = hipSuccess;
+    Upload up(ctx);
     for (int l = 0; l < 2; ++l)
         for (int f = 0; f < 2; ++f) {
             const vc::AclFamilyBuilt& fb = b.fam[l][f];
             AclFamilyImage& fi = s->img.fam[l][f];
-            fi.bounds4 = f == 0 ? s->upload(fb.bounds4, &e) : nullptr;
-            fi.bounds6 = f == 1 ? s->upload(fb.bounds6, &e) : nullptr;
-            fi.rec = s->upload(fb.rec, &e);
-            fi.pieces = s->upload(fb.pieces, &e);
-            fi.dir4 = fb.dir4.empty() ? nullptr : s->upload(fb.dir4, &e);
+            fi.bounds4 = f == 0 ? up(*s, fb.bounds4) : nullptr;
+            fi.bounds6 = f == 1 ? up(*s, fb.bounds6) : nullptr;
+            fi.rec = up(*s, fb.rec);
+            fi.pieces = up(*s, fb.pieces);
+            fi.dir4 = fb.dir4.empty() ? nullptr : up(*s, fb.dir4);
             fi.dir_bits = fb.dir4.empty() ? 0 : fb.dir_bits;
             fi.nb = fb.nb;
             fi.np = static_cast<int32_t>(fb.pieces.size() / 2);
         }
-    s->img.allow = s->upload(b.allow, &e);
+    s->img.allow = up(*s, b.allow);
     s->img.n_tcp = b.n_tcp;
     s->img.n_udp = b.n_udp;
     s->img.default_allow = b.default_allow;
-    if (e == hipSuccess) e = s->alloc_counters(int64_t(n_tcp) + n_udp + 2);
-    if (e != hipSuccess) return hip_fail(e, "ACL upload");
+    s->alloc_counters(up, int64_t(n_tcp) + n_udp + 2);
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "ACL upload");
     ctx->publish(ctx->acl, std::shared_ptr<const AclSnap>(std::move(s)));
     return VC_OK;
 }
@@ -372,7 +599,7 @@ static int acl_dev(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
                             port, n, out_idx, out_allow, cnt)
         : vc::launch_acl_v6(ctx->cfg(stream), s->img, proto, static_cast<const uint8_t*>(src),
                             port, n, out_idx, out_allow, cnt);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "ACL launch");
+    return launched(ctx, e, stream, "ACL launch");
 }
 
 int vc_acl_classify_v4_dev(vc_ctx* ctx, const uint8_t* proto, const uint32_t* src4,
@@ -390,8 +617,7 @@ int vc_acl_classify_v6_dev(vc_ctx* ctx, const uint8_t* proto, const uint8_t* src
 // Host-buffer batches of fixed-size items in chunks: chunk k's upload,
 // kernel and download are ordered on lane k % 2, so one chunk's H2D copy,
 // the next chunk's kernel and the previous chunk's D2H copy overlap (PCIe is
-// full duplex).  Each chunk's staging is freed in stream order right after
-// its download is enqueued, so the pool reuses it for chunk k + 2.
+// full duplex).
 constexpr int64_t kHostChunk = int64_t(4) << 20;
 
 // Buffers registered through vc_host_register: base -> length.  A zero-copy
@@ -428,20 +654,38 @@ static void* mapped(const void* h, size_t bytes, uintptr_t align = 1) {
 }
 
 extern "C++" {
+// Chunk k runs on lane k % 2 of one stager: its inputs are copied into the
+// lane's bounce buffer and uploaded, the kernel runs, and its outputs come
+// back into the bounce buffer, all in the lane's stream order.  Before a
+// lane takes chunk k + 2 the host waits for chunk k and copies its results
+// out, so one lane's transfers and kernel overlap the other lane's and the
+// host copies.
 template <class Body>   // int body(Staging&, int64_t lo, int64_t cnt, hipStream_t)
-static int host_chunks(vc_ctx* ctx, int64_t n, const char* what, Body body) {
+static int host_chunks(vc_ctx* ctx, StagerLease& lease, int64_t n, const char* what, Body body) {
+    if (!lease) return hip_fail(lease.err(), what);
     int rc = VC_OK;
     for (int64_t lo = 0, k = 0; lo < n && rc == VC_OK; lo += kHostChunk, ++k) {
-        hipStream_t s = ctx->lane[k & 1];
-        Staging st(ctx->pool, s);
-        rc = body(st, lo, std::min(kHostChunk, n - lo), s);
+        StageLane& L = lease.lane(int(k & 1));
+        const hipError_t e = L.finish(true);            // chunk k - 2's results
+        if (e != hipSuccess) {
+            rc = hip_fail(e, what);
+            break;
+        }
+        Staging st(ctx, L, what);
+        rc = body(st, lo, std::min(kHostChunk, n - lo), st.stream());
         if (rc == VC_OK && st.err != hipSuccess) rc = hip_fail(st.err, what);
     }
-    const hipError_t e0 = hipStreamSynchronize(ctx->lane[0]);
-    const hipError_t e1 = hipStreamSynchronize(ctx->lane[1]);
-    if (rc != VC_OK) return rc;
-    const hipError_t e = e0 != hipSuccess ? e0 : e1;
-    return e == hipSuccess ? VC_OK : hip_fail(e, what);
+    for (int k = 0; k < 2; ++k) {
+        const hipError_t e = lease.lane(k).finish(rc == VC_OK);
+        if (rc == VC_OK && e != hipSuccess) rc = hip_fail(e, what);
+    }
+    if (rc == VC_OK && ctx->sync_check) rc = devcheck_report(what);
+    return rc;
+}
+template <class Body>
+static int host_chunks(vc_ctx* ctx, int64_t n, const char* what, Body body) {
+    StagerLease lease(ctx);
+    return host_chunks(ctx, lease, n, what, body);
 }
 }  // extern "C++"
 
@@ -459,22 +703,23 @@ static int acl_host(vc_ctx* ctx, int fam, const uint8_t* proto, const void* src,
                      static_cast<int32_t*>(mi), static_cast<uint8_t*>(ma), ctx->stream);
         if (rc) return rc;
         hipError_t e = hipStreamSynchronize(ctx->stream);
-        return e == hipSuccess ? VC_OK : hip_fail(e, "ACL classify");
+        if (e != hipSuccess) return hip_fail(e, "ACL classify");
+        return ctx->sync_check ? devcheck_report("ACL classify") : VC_OK;
     }
     const auto pin = ctx->get(ctx->acl);
     return host_chunks(ctx, n, "ACL classify", [&](Staging& st, int64_t lo, int64_t c,
                                                    hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
-        auto* dp = static_cast<uint8_t*>(st.in(proto + u, m, s));
-        auto* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw, s);
-        auto* dq = static_cast<uint16_t*>(st.in(port + u, m * 2, s));
+        auto* dp = static_cast<uint8_t*>(st.in(proto + u, m));
+        auto* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw);
+        auto* dq = static_cast<uint16_t*>(st.in(port + u, m * 2));
         auto* di = static_cast<int32_t*>(st.out(out_idx, m * 4));
         auto* da = static_cast<uint8_t*>(st.out(out_allow, m));
         if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
         int r = acl_dev(ctx, fam, dp, ds, dq, c, di, da, s, pin);
         if (r) return r;
-        st.back(out_idx + u, di, m * 4, s);
-        if (out_allow) st.back(out_allow + u, da, m, s);
+        st.back(out_idx + u, di, m * 4);
+        if (out_allow) st.back(out_allow + u, da, m);
         return VC_OK;
     });
 }
@@ -501,18 +746,18 @@ int vc_compile_routes(vc_ctx* ctx, const vc_net* v4, int n4, const vc_net* v6, i
     if ((rc = vc::build_trie(v6, n6, 1, &t6)) != VC_OK) return fail(rc, "invalid IPv6 route rule");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<RouteSnap>();
-    hipError_t e = hipSuccess;
+    Upload up(ctx);
     vc::TrieBuilt* tb[2] = {&t4, &t6};
     for (int f = 0; f < 2; ++f) {
-        s->img.fam[f].nodes = s->upload(tb[f]->nodes, &e);
+        s->img.fam[f].nodes = up(*s, tb[f]->nodes);
         s->img.fam[f].root_bits = tb[f]->root_bits;
         s->img.fam[f].key_bits = tb[f]->key_bits;
         s->img.fam[f].n_rules = tb[f]->n_rules;
     }
     s->n4 = n4;
     s->n6 = n6;
-    if (e == hipSuccess) e = s->alloc_counters(int64_t(n4) + n6 + 2);
-    if (e != hipSuccess) return hip_fail(e, "route upload");
+    s->alloc_counters(up, int64_t(n4) + n6 + 2);
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "route upload");
     ctx->publish(ctx->route, std::shared_ptr<const RouteSnap>(std::move(s)));
     return VC_OK;
 }
@@ -531,7 +776,7 @@ static int route_dev(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t* 
                               n, out, cnt, 0, nn)
         : vc::launch_route_v6(ctx->cfg(stream), s->img.fam[1], static_cast<const uint8_t*>(dst),
                               n, out, cnt, s->n4, nn + 1);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "route launch");
+    return launched(ctx, e, stream, "route launch");
 }
 
 int vc_route_lookup_v4_dev(vc_ctx* ctx, const uint32_t* dst4, int64_t n, int32_t* out,
@@ -555,18 +800,19 @@ static int route_host(vc_ctx* ctx, int fam, const void* dst, int64_t n, int32_t*
         rc = route_dev(ctx, fam, md, n, static_cast<int32_t*>(mo), ctx->stream);
         if (rc) return rc;
         hipError_t e = hipStreamSynchronize(ctx->stream);
-        return e == hipSuccess ? VC_OK : hip_fail(e, "route lookup");
+        if (e != hipSuccess) return hip_fail(e, "route lookup");
+        return ctx->sync_check ? devcheck_report("route lookup") : VC_OK;
     }
     const auto pin = ctx->get(ctx->route);
     return host_chunks(ctx, n, "route lookup", [&](Staging& st, int64_t lo, int64_t c,
                                                    hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
-        void* dd = st.in(static_cast<const uint8_t*>(dst) + u * sw, m * sw, s);
+        void* dd = st.in(static_cast<const uint8_t*>(dst) + u * sw, m * sw);
         auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
         if (st.err != hipSuccess) return VC_OK;
         int r = route_dev(ctx, fam, dd, c, dout, s, pin);
         if (r) return r;
-        st.back(out + u, dout, m * 4, s);
+        st.back(out + u, dout, m * 4);
         return VC_OK;
     });
 }
@@ -590,26 +836,26 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     if ((rc = vc::build_hints(groups, n, &b)) != VC_OK) return fail(rc, "invalid annotations");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<HintSnap>();
-    hipError_t e = hipSuccess;
+    Upload up(ctx);
     static_assert(sizeof(KeySlot) == sizeof(vc::KeySlotH), "slot layout");
     static_assert(sizeof(HostRec) == 64 && sizeof(HostExt) == 16, "record layout");
-    s->img.blob = s->upload(b.blob, &e);
-    s->img.host_recs = s->upload(b.host.recs, &e);
-    s->img.host_ext = s->upload(b.host.ext, &e);
-    s->img.host_tags = s->upload(b.host.tags, &e);
-    s->img.uri_slots = reinterpret_cast<const KeySlot*>(s->upload(b.uri_slots, &e));
-    s->img.uri_tags = s->upload(b.uri_tags, &e);
-    s->img.lists = s->upload(b.lists, &e);
-    s->img.port_mins = reinterpret_cast<const PortMin*>(s->upload(b.port_mins, &e));
-    s->img.groups = reinterpret_cast<const GroupRec*>(s->upload(b.groups, &e));
+    s->img.blob = up(*s, b.blob);
+    s->img.host_recs = up(*s, b.host.recs);
+    s->img.host_ext = up(*s, b.host.ext);
+    s->img.host_tags = up(*s, b.host.tags);
+    s->img.uri_slots = reinterpret_cast<const KeySlot*>(up(*s, b.uri_slots));
+    s->img.uri_tags = up(*s, b.uri_tags);
+    s->img.lists = up(*s, b.lists);
+    s->img.port_mins = reinterpret_cast<const PortMin*>(up(*s, b.port_mins));
+    s->img.groups = reinterpret_cast<const GroupRec*>(up(*s, b.groups));
     s->img.host_mask = static_cast<uint32_t>(b.host.tags.size() - 1);
     s->img.uri_mask = static_cast<uint32_t>(b.uri_slots.size() - 1);
     s->img.n_groups = n;
     s->img.wildcard_slot = b.wildcard_slot;
     s->img.uri_star_slot = b.uri_star_slot;
     s->img.has_uri_keys = b.has_uri_keys;
-    if (e == hipSuccess) e = s->alloc_counters(int64_t(n) + 1);
-    if (e != hipSuccess) return hip_fail(e, "hint upload");
+    s->alloc_counters(up, int64_t(n) + 1);
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "hint upload");
     ctx->publish(ctx->hint, std::shared_ptr<const HintSnap>(std::move(s)));
     return VC_OK;
 }
@@ -627,7 +873,7 @@ int vc_hint_search_dev(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* ho
     hipError_t e = vc::launch_hint(ctx->cfg(stream), s->img, host_blob, host_off, host_null, port,
                                    uri_blob, uri_off, uri_null, n, out_group,
                                    ctx->counters_on ? s->counters : nullptr);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "hint launch");
+    return launched(ctx, e, stream, "hint launch");
 }
 
 int vc_hint_search(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_off,
@@ -639,23 +885,24 @@ int vc_hint_search(vc_ctx* ctx, const uint8_t* host_blob, const uint32_t* host_o
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!out_group || (host_blob && !host_off) || (uri_blob && !uri_off))
         return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "hint search");
+    Staging st(ctx, lease.lane(0), "hint search");
+    hipStream_t s = st.stream();
     size_t hb = host_blob ? host_off[n] : 0, ub = uri_blob ? uri_off[n] : 0;
-    auto* dhb = static_cast<uint8_t*>(host_blob ? st.in(host_blob, hb, s) : nullptr);
-    auto* dho = static_cast<uint32_t*>(host_blob ? st.in(host_off, size_t(n + 1) * 4, s) : nullptr);
-    auto* dhn = static_cast<uint8_t*>(st.in(host_null, size_t(n), s));
-    auto* dp = static_cast<uint16_t*>(st.in(port, size_t(n) * 2, s));
-    auto* dub = static_cast<uint8_t*>(uri_blob ? st.in(uri_blob, ub, s) : nullptr);
-    auto* duo = static_cast<uint32_t*>(uri_blob ? st.in(uri_off, size_t(n + 1) * 4, s) : nullptr);
-    auto* dun = static_cast<uint8_t*>(st.in(uri_null, size_t(n), s));
+    auto* dhb = static_cast<uint8_t*>(host_blob ? st.in(host_blob, hb) : nullptr);
+    auto* dho = static_cast<uint32_t*>(host_blob ? st.in(host_off, size_t(n + 1) * 4) : nullptr);
+    auto* dhn = static_cast<uint8_t*>(st.in(host_null, size_t(n)));
+    auto* dp = static_cast<uint16_t*>(st.in(port, size_t(n) * 2));
+    auto* dub = static_cast<uint8_t*>(uri_blob ? st.in(uri_blob, ub) : nullptr);
+    auto* duo = static_cast<uint32_t*>(uri_blob ? st.in(uri_off, size_t(n + 1) * 4) : nullptr);
+    auto* dun = static_cast<uint8_t*>(st.in(uri_null, size_t(n)));
     auto* dout = static_cast<int32_t*>(st.out(out_group, size_t(n) * 4));
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_hint_search_dev(ctx, dhb, dho, dhn, dp, dub, duo, dun, n, dout, s);
     if (rc) return rc;
-    st.back(out_group, dout, size_t(n) * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "hint search");
+    st.back(out_group, dout, size_t(n) * 4);
+    return st.finish();
 }
 
 int vc_compile_hosts(vc_ctx* ctx, const char* const* keys, const int32_t* key_lens,
@@ -668,13 +915,13 @@ int vc_compile_hosts(vc_ctx* ctx, const char* const* keys, const int32_t* key_le
         return fail(rc, "invalid hosts entry");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<HostsSnap>();
-    hipError_t e = hipSuccess;
-    s->img.blob = s->upload(b.blob, &e);
-    s->img.recs = s->upload(b.table.recs, &e);
-    s->img.tags = s->upload(b.table.tags, &e);
+    Upload up(ctx);
+    s->img.blob = up(*s, b.blob);
+    s->img.recs = up(*s, b.table.recs);
+    s->img.tags = up(*s, b.table.tags);
     s->img.mask = static_cast<uint32_t>(b.table.tags.size() - 1);
     s->img.n = b.n;
-    if (e != hipSuccess) return hip_fail(e, "hosts upload");
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "hosts upload");
     ctx->publish(ctx->hosts, std::shared_ptr<const HostsSnap>(std::move(s)));
     return VC_OK;
 }
@@ -705,7 +952,7 @@ int vc_dns_classify_dev(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff,
     if (ho) hi = ho->img;
     hipError_t e = vc::launch_dns(ctx->cfg(stream), hi, h->img, qblob, qoff, n, out_kind, out_value,
                                   ctx->counters_on ? h->counters : nullptr);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "dns launch");
+    return launched(ctx, e, stream, "dns launch");
 }
 
 int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int64_t n,
@@ -714,19 +961,20 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!qblob || !qoff || !out_kind || !out_value) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    auto* db = static_cast<uint8_t*>(st.in(qblob, qoff[n], s));
-    auto* dof = static_cast<uint32_t*>(st.in(qoff, size_t(n + 1) * 4, s));
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "dns classify");
+    Staging st(ctx, lease.lane(0), "dns classify");
+    hipStream_t s = st.stream();
+    auto* db = static_cast<uint8_t*>(st.in(qblob, qoff[n]));
+    auto* dof = static_cast<uint32_t*>(st.in(qoff, size_t(n + 1) * 4));
     auto* dk = static_cast<uint8_t*>(st.out(out_kind, size_t(n)));
     auto* dv = static_cast<int32_t*>(st.out(out_value, size_t(n) * 4));
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_dns_classify_dev(ctx, db, dof, n, dk, dv, s);
     if (rc) return rc;
-    st.back(out_kind, dk, size_t(n), s);
-    st.back(out_value, dv, size_t(n) * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "dns classify");
+    st.back(out_kind, dk, size_t(n));
+    st.back(out_value, dv, size_t(n) * 4);
+    return st.finish();
 }
 
 // ---------------------------------------------------------------------------
@@ -743,14 +991,14 @@ int vc_compile_certs(vc_ctx* ctx, const char* const* names, const int32_t* name_
         return fail(rc, "invalid certificate name or holder index");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<CertSnap>();
-    hipError_t e = hipSuccess;
-    s->img.names.blob = s->upload(b.blob, &e);
-    s->img.names.recs = s->upload(b.table.recs, &e);
-    s->img.names.tags = s->upload(b.table.tags, &e);
+    Upload up(ctx);
+    s->img.names.blob = up(*s, b.blob);
+    s->img.names.recs = up(*s, b.table.recs);
+    s->img.names.tags = up(*s, b.table.tags);
     s->img.names.mask = static_cast<uint32_t>(b.table.tags.size() - 1);
     s->img.names.n = b.n;
     s->img.n_holders = n_holders;
-    if (e != hipSuccess) return hip_fail(e, "certificate table upload");
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "certificate table upload");
     ctx->publish(ctx->certs, std::shared_ptr<const CertSnap>(std::move(s)));
     return VC_OK;
 }
@@ -765,7 +1013,7 @@ int vc_cert_choose_dev(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni
     if (!s) return fail(VC_ESTATE, "no certificate holders compiled");
     hipError_t e = vc::launch_certs(ctx->cfg(stream), s->img, sni_blob, sni_off, sni_null, n,
                                     out_holder);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "cert launch");
+    return launched(ctx, e, stream, "cert launch");
 }
 
 int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off,
@@ -774,18 +1022,19 @@ int vc_cert_choose(vc_ctx* ctx, const uint8_t* sni_blob, const uint32_t* sni_off
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!sni_blob || !sni_off || !out_holder) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    auto* db = static_cast<uint8_t*>(st.in(sni_blob, sni_off[n], s));
-    auto* dof = static_cast<uint32_t*>(st.in(sni_off, size_t(n + 1) * 4, s));
-    auto* dn = static_cast<uint8_t*>(st.in(sni_null, size_t(n), s));
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "cert choose");
+    Staging st(ctx, lease.lane(0), "cert choose");
+    hipStream_t s = st.stream();
+    auto* db = static_cast<uint8_t*>(st.in(sni_blob, sni_off[n]));
+    auto* dof = static_cast<uint32_t*>(st.in(sni_off, size_t(n + 1) * 4));
+    auto* dn = static_cast<uint8_t*>(st.in(sni_null, size_t(n)));
     auto* dout = static_cast<int32_t*>(st.out(out_holder, size_t(n) * 4));
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_cert_choose_dev(ctx, db, dof, dn, n, dout, s);
     if (rc) return rc;
-    st.back(out_holder, dout, size_t(n) * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "cert choose");
+    st.back(out_holder, dout, size_t(n) * 4);
+    return st.finish();
 }
 
 int vc_host_register(void* p, int64_t bytes) {
@@ -819,10 +1068,10 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
         return fail(rc, "invalid mirror filter (mirror index, port range or network)");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<MirrorSnap>();
-    hipError_t e = hipSuccess;
-    s->img.f = s->upload(recs, &e);
+    Upload up(ctx);
+    s->img.f = up(*s, recs);
     s->img.n = n;
-    if (e != hipSuccess) return hip_fail(e, "mirror filter upload");
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "mirror filter upload");
     ctx->publish(ctx->mirror, std::shared_ptr<const MirrorSnap>(std::move(s)));
     return VC_OK;
 }
@@ -840,7 +1089,7 @@ int vc_mirror_match_dev(vc_ctx* ctx, int32_t origin, const vc_mirror_items* item
     auto s = ctx->get(ctx->mirror);
     if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
     hipError_t e = vc::launch_mirror_match(ctx->cfg(stream), s->img, origin, *items, n, out_mirrors);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror launch");
+    return launched(ctx, e, stream, "mirror launch");
 }
 
 int vc_mirror_match(vc_ctx* ctx, int32_t origin, const vc_mirror_items* items, int64_t n,
@@ -849,27 +1098,28 @@ int vc_mirror_match(vc_ctx* ctx, int32_t origin, const vc_mirror_items* items, i
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!items || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "mirror match");
+    Staging st(ctx, lease.lane(0), "mirror match");
+    hipStream_t s = st.stream();
     const size_t un = size_t(n);
     vc_mirror_items d{};
-    d.mac_src = static_cast<const uint8_t*>(st.in(items->mac_src, un * 6, s));
-    d.mac_dst = static_cast<const uint8_t*>(st.in(items->mac_dst, un * 6, s));
-    d.ip_src_len = static_cast<const uint8_t*>(st.in(items->ip_src_len, un, s));
-    d.ip_dst_len = static_cast<const uint8_t*>(st.in(items->ip_dst_len, un, s));
-    d.ip_src = static_cast<const uint8_t*>(st.in(items->ip_src, un * 16, s));
-    d.ip_dst = static_cast<const uint8_t*>(st.in(items->ip_dst, un * 16, s));
-    d.transport = static_cast<const int32_t*>(st.in(items->transport, un * 4, s));
-    d.port_src = static_cast<const int32_t*>(st.in(items->port_src, un * 4, s));
-    d.port_dst = static_cast<const int32_t*>(st.in(items->port_dst, un * 4, s));
-    d.app = static_cast<const int32_t*>(st.in(items->app, un * 4, s));
+    d.mac_src = static_cast<const uint8_t*>(st.in(items->mac_src, un * 6));
+    d.mac_dst = static_cast<const uint8_t*>(st.in(items->mac_dst, un * 6));
+    d.ip_src_len = static_cast<const uint8_t*>(st.in(items->ip_src_len, un));
+    d.ip_dst_len = static_cast<const uint8_t*>(st.in(items->ip_dst_len, un));
+    d.ip_src = static_cast<const uint8_t*>(st.in(items->ip_src, un * 16));
+    d.ip_dst = static_cast<const uint8_t*>(st.in(items->ip_dst, un * 16));
+    d.transport = static_cast<const int32_t*>(st.in(items->transport, un * 4));
+    d.port_src = static_cast<const int32_t*>(st.in(items->port_src, un * 4));
+    d.port_dst = static_cast<const int32_t*>(st.in(items->port_dst, un * 4));
+    d.app = static_cast<const int32_t*>(st.in(items->app, un * 4));
     auto* dout = static_cast<uint64_t*>(st.out(out_mirrors, un * 8));
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_mirror_match_dev(ctx, origin, &d, n, dout, s);
     if (rc) return rc;
-    st.back(out_mirrors, dout, un * 8, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror match");
+    st.back(out_mirrors, dout, un * 8);
+    return st.finish();
 }
 
 int vc_mirror_switch_dev(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uint32_t* off,
@@ -884,7 +1134,7 @@ int vc_mirror_switch_dev(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const
     if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
     hipError_t e = vc::launch_mirror_switch(ctx->cfg(stream), s->img, origin, blob, off, n, layer,
                                             out_mirrors);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror switch launch");
+    return launched(ctx, e, stream, "mirror switch launch");
 }
 
 int vc_mirror_switch(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uint32_t* off,
@@ -893,17 +1143,18 @@ int vc_mirror_switch(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const uin
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!blob || !off || !out_mirrors) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
-    auto* dof = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "mirror switch");
+    Staging st(ctx, lease.lane(0), "mirror switch");
+    hipStream_t s = st.stream();
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n]));
+    auto* dof = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4));
     auto* dout = static_cast<uint64_t*>(st.out(out_mirrors, size_t(n) * 8));
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_mirror_switch_dev(ctx, origin, db, dof, n, layer, dout, s);
     if (rc) return rc;
-    st.back(out_mirrors, dout, size_t(n) * 8, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "mirror switch");
+    st.back(out_mirrors, dout, size_t(n) * 8);
+    return st.finish();
 }
 
 // ---------------------------------------------------------------------------
@@ -918,14 +1169,14 @@ int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* gro
         return fail(rc, "invalid server lists");
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
     auto s = std::make_shared<ServerSnap>();
-    hipError_t e = hipSuccess;
-    s->img.view_off = s->upload(b.view_off, &e);
-    s->img.order = s->upload(b.order, &e);
-    s->img.healthy = s->upload(b.healthy, &e);
-    s->img.group_base = s->upload(b.group_base, &e);
+    Upload up(ctx);
+    s->img.view_off = up(*s, b.view_off);
+    s->img.order = up(*s, b.order);
+    s->img.healthy = up(*s, b.healthy);
+    s->img.group_base = up(*s, b.group_base);
     s->img.n_groups = b.n_groups;
     s->img.n_servers = b.n_servers;
-    if (e != hipSuccess) return hip_fail(e, "server upload");
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "server upload");
     ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(s)));
     return VC_OK;
 }
@@ -944,9 +1195,9 @@ int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers
     auto ns = std::make_shared<ServerSnap>();
     ns->img = s->img;
     ns->lists = s->lists ? s->lists : s;
-    hipError_t e = hipSuccess;
-    ns->img.healthy = ns->upload(h, &e);
-    if (e != hipSuccess) return hip_fail(e, "health upload");
+    Upload up(ctx);
+    ns->img.healthy = up(*ns, h);
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "health upload");
     ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(ns)));
     return VC_OK;
 }
@@ -964,7 +1215,7 @@ static int source_dev(vc_ctx* ctx, int fam, const int32_t* group, const void* sr
     auto s = pin ? pin : ctx->get(ctx->servers);
     if (!s) return fail(VC_ESTATE, "no servers compiled");
     hipError_t e = vc::launch_source(ctx->cfg(stream), s->img, group, src, fam, n, view, out);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "source launch");
+    return launched(ctx, e, stream, "source launch");
 }
 
 static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* src, int64_t n,
@@ -980,19 +1231,20 @@ static int source_host(vc_ctx* ctx, int fam, const int32_t* group, const void* s
                         static_cast<int32_t*>(mo), ctx->stream);
         if (rc) return rc;
         hipError_t e = hipStreamSynchronize(ctx->stream);
-        return e == hipSuccess ? VC_OK : hip_fail(e, "source select");
+        if (e != hipSuccess) return hip_fail(e, "source select");
+        return ctx->sync_check ? devcheck_report("source select") : VC_OK;
     }
     const auto pin = ctx->get(ctx->servers);
     return host_chunks(ctx, n, "source select", [&](Staging& st, int64_t lo, int64_t c,
                                                     hipStream_t s) {
         const size_t u = size_t(lo), m = size_t(c);
-        auto* dg = static_cast<int32_t*>(st.in(group + u, m * 4, s));
-        void* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw, s);
+        auto* dg = static_cast<int32_t*>(st.in(group + u, m * 4));
+        void* ds = st.in(static_cast<const uint8_t*>(src) + u * sw, m * sw);
         auto* dout = static_cast<int32_t*>(st.out(out, m * 4));
         if (st.err != hipSuccess) return VC_OK;
         int r = source_dev(ctx, fam, dg, ds, c, view, dout, s, pin);
         if (r) return r;
-        st.back(out + u, dout, m * 4, s);
+        st.back(out + u, dout, m * 4);
         return VC_OK;
     });
 }
@@ -1029,7 +1281,7 @@ int vc_parse_packets_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, 
                   (reinterpret_cast<uintptr_t>(out->dst6) & 15)))
         return fail(VC_EINVAL, "src6/dst6 must be 16-byte aligned");
     hipError_t e = vc::launch_packets(ctx->cfg(stream), blob, off, n, layer, *out);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "packet launch");
+    return launched(ctx, e, stream, "packet launch");
 }
 
 int vc_dns_datagrams_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
@@ -1065,7 +1317,7 @@ int vc_dns_datagrams_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, 
             e = vc::launch_hist(c, VC_HIST_DNS, out->value, out->kind, n * VC_DNSD_MAXQ,
                                 h->img.n_groups, 0, h->img.n_groups, 0, h->counters);
     }
-    return e == hipSuccess ? VC_OK : hip_fail(e, "dns datagram launch");
+    return launched(ctx, e, stream, "dns datagram launch");
 }
 
 int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
@@ -1078,15 +1330,17 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     if (!blob || !off || !remote4 || !remote_port || !out || !out->status || !out->kind ||
         !out->value || (remote_family && !remote6))
         return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "dns datagrams");
+    Staging st(ctx, lease.lane(0), "dns datagrams");
+    hipStream_t s = st.stream();
     const size_t un = size_t(n), uq = un * VC_DNSD_MAXQ;
-    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
-    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4, s));
-    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un, s));
-    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4, s));
-    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16, s));
-    auto* dp = static_cast<uint16_t*>(st.in(remote_port, un * 2, s));
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n]));
+    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4));
+    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un));
+    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4));
+    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16));
+    auto* dp = static_cast<uint16_t*>(st.in(remote_port, un * 2));
     vc_dnsd_out d{};
     d.status = static_cast<uint8_t*>(st.out(out->status, un));
     d.acl = static_cast<int32_t*>(st.out(out->acl, un * 4));
@@ -1097,14 +1351,13 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_dns_datagrams_dev(ctx, db, doff, n, dfam, d4, d6, dp, &d, s);
     if (rc) return rc;
-    st.back(out->status, d.status, un, s);
-    st.back(out->acl, d.acl, un * 4, s);
-    st.back(out->nq, d.nq, un, s);
-    st.back(out->qtype, d.qtype, uq * 2, s);
-    st.back(out->kind, d.kind, uq, s);
-    st.back(out->value, d.value, uq * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "dns datagrams");
+    st.back(out->status, d.status, un);
+    st.back(out->acl, d.acl, un * 4);
+    st.back(out->nq, d.nq, un);
+    st.back(out->qtype, d.qtype, uq * 2);
+    st.back(out->kind, d.kind, uq);
+    st.back(out->value, d.value, uq * 4);
+    return st.finish();
 }
 
 int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
@@ -1131,7 +1384,7 @@ int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off
     hipError_t e = vc::launch_switch(ctx->cfg(stream), a->img, r->img, blob, off, n, layer, o,
                                      remote_family, remote4, remote6, bind_port, out_acl,
                                      out_allow, out_route);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "switch launch");
+    return launched(ctx, e, stream, "switch launch");
 }
 
 // Device copies of the host arrays of a vc_pkt_out (NULL stays NULL).
@@ -1152,20 +1405,19 @@ static vc_pkt_out stage_pkt_out(Staging& st, const vc_pkt_out& out, size_t un) {
     return d;
 }
 
-static void back_pkt_out(Staging& st, const vc_pkt_out& out, const vc_pkt_out& d, size_t un,
-                         hipStream_t s) {
-    st.back(out.status, d.status, un, s);
-    st.back(out.l3, d.l3, un, s);
-    st.back(out.l4, d.l4, un, s);
-    st.back(out.proto, d.proto, un, s);
-    st.back(out.vni, d.vni, un * 4, s);
-    st.back(out.ether_type, d.ether_type, un * 2, s);
-    st.back(out.src4, d.src4, un * 4, s);
-    st.back(out.dst4, d.dst4, un * 4, s);
-    st.back(out.src6, d.src6, un * 16, s);
-    st.back(out.dst6, d.dst6, un * 16, s);
-    st.back(out.sport, d.sport, un * 2, s);
-    st.back(out.dport, d.dport, un * 2, s);
+static void back_pkt_out(Staging& st, const vc_pkt_out& out, const vc_pkt_out& d, size_t un) {
+    st.back(out.status, d.status, un);
+    st.back(out.l3, d.l3, un);
+    st.back(out.l4, d.l4, un);
+    st.back(out.proto, d.proto, un);
+    st.back(out.vni, d.vni, un * 4);
+    st.back(out.ether_type, d.ether_type, un * 2);
+    st.back(out.src4, d.src4, un * 4);
+    st.back(out.dst4, d.dst4, un * 4);
+    st.back(out.src6, d.src6, un * 16);
+    st.back(out.dst6, d.dst6, un * 16);
+    st.back(out.sport, d.sport, un * 2);
+    st.back(out.dport, d.dport, un * 2);
 }
 
 int vc_switch_classify(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
@@ -1177,16 +1429,18 @@ int vc_switch_classify(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, in
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!blob || !off || !out_route || !remote4 || (remote_family && !remote6))
         return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "switch classify");
+    Staging st(ctx, lease.lane(0), "switch classify");
+    hipStream_t s = st.stream();
     const size_t un = size_t(n);
     const vc_pkt_out none{};
     const vc_pkt_out& o = out ? *out : none;
-    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
-    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4, s));
-    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un, s));
-    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4, s));
-    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16, s));
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n]));
+    auto* doff = static_cast<uint32_t*>(st.in(off, (un + 1) * 4));
+    auto* dfam = static_cast<uint8_t*>(st.in(remote_family, un));
+    auto* d4 = static_cast<uint32_t*>(st.in(remote4, un * 4));
+    auto* d6 = static_cast<uint8_t*>(st.in(remote6, un * 16));
     const vc_pkt_out d = stage_pkt_out(st, o, un);
     auto* dacl = static_cast<int32_t*>(st.out(out_acl, un * 4));
     auto* dal = static_cast<uint8_t*>(st.out(out_allow, un));
@@ -1195,12 +1449,11 @@ int vc_switch_classify(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, in
     rc = vc_switch_classify_dev(ctx, db, doff, n, layer, dfam, d4, d6, bind_port, &d, dacl, dal, dr,
                                 s);
     if (rc) return rc;
-    back_pkt_out(st, o, d, un, s);
-    st.back(out_acl, dacl, un * 4, s);
-    st.back(out_allow, dal, un, s);
-    st.back(out_route, dr, un * 4, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "switch classify");
+    back_pkt_out(st, o, d, un);
+    st.back(out_acl, dacl, un * 4);
+    st.back(out_allow, dal, un);
+    st.back(out_route, dr, un * 4);
+    return st.finish();
 }
 
 int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
@@ -1209,10 +1462,12 @@ int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     if (rc) return rc;
     if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
     if (!blob || !off || !out) return fail(VC_EINVAL, "bad batch arguments");
-    Staging st(ctx->pool, ctx->stream);
-    hipStream_t s = ctx->stream;
-    auto* db = static_cast<uint8_t*>(st.in(blob, off[n], s));
-    auto* doff = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4, s));
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "parse packets");
+    Staging st(ctx, lease.lane(0), "parse packets");
+    hipStream_t s = st.stream();
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n]));
+    auto* doff = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4));
     vc_pkt_out d{};
     const size_t un = size_t(n);
     d.status = static_cast<uint8_t*>(st.out(out->status, un));
@@ -1230,20 +1485,19 @@ int vc_parse_packets(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     if (st.err != hipSuccess) return hip_fail(st.err, "staging");
     rc = vc_parse_packets_dev(ctx, db, doff, n, layer, &d, s);
     if (rc) return rc;
-    st.back(out->status, d.status, un, s);
-    st.back(out->l3, d.l3, un, s);
-    st.back(out->l4, d.l4, un, s);
-    st.back(out->proto, d.proto, un, s);
-    st.back(out->vni, d.vni, un * 4, s);
-    st.back(out->ether_type, d.ether_type, un * 2, s);
-    st.back(out->src4, d.src4, un * 4, s);
-    st.back(out->dst4, d.dst4, un * 4, s);
-    st.back(out->src6, d.src6, un * 16, s);
-    st.back(out->dst6, d.dst6, un * 16, s);
-    st.back(out->sport, d.sport, un * 2, s);
-    st.back(out->dport, d.dport, un * 2, s);
-    hipError_t e = st.err != hipSuccess ? st.err : hipStreamSynchronize(s);
-    return e == hipSuccess ? VC_OK : hip_fail(e, "parse packets");
+    st.back(out->status, d.status, un);
+    st.back(out->l3, d.l3, un);
+    st.back(out->l4, d.l4, un);
+    st.back(out->proto, d.proto, un);
+    st.back(out->vni, d.vni, un * 4);
+    st.back(out->ether_type, d.ether_type, un * 2);
+    st.back(out->src4, d.src4, un * 4);
+    st.back(out->dst4, d.dst4, un * 4);
+    st.back(out->src6, d.src6, un * 16);
+    st.back(out->dst6, d.dst6, un * 16);
+    st.back(out->sport, d.sport, un * 2);
+    st.back(out->dport, d.dport, un * 2);
+    return st.finish();
 }
 
 // ---------------------------------------------------------------------------
@@ -1307,7 +1561,7 @@ static int pipeline_dev(vc_ctx* ctx, const vc_packets& in, int64_t n, const int3
     hipError_t e = vc::launch_pipeline(ctx->cfg(stream), pin.a->img, pin.r->img, pin.r->n4,
                                        pin.r->n6, p, cnt, static_cast<hipEvent_t>(kernel_done),
                                        static_cast<hipStream_t>(count_stream));
-    return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline launch");
+    return launched(ctx, e, stream, "pipeline launch");
 }
 
 int vc_pipeline_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,
@@ -1364,26 +1618,31 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
         rc = pipeline_dev(ctx, m, n, mpool, n_pool, mo, ctx->stream, nullptr, nullptr, pin);
         if (rc) return rc;
         hipError_t e = hipStreamSynchronize(ctx->stream);
-        return e == hipSuccess ? VC_OK : hip_fail(e, "pipeline");
+        if (e != hipSuccess) return hip_fail(e, "pipeline");
+        return ctx->sync_check ? devcheck_report("pipeline") : VC_OK;
     }
-    // chunked staging; the hostname pool results are uploaded once
-    Staging pst(ctx->pool, ctx->stream);
+    // chunked staging; the hostname pool results are uploaded once, on the
+    // stager's whole-call lane, and stay there for every chunk
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "pipeline");
+    Staging pst(ctx, lease.lane(2), "pool upload");
     const int32_t* dpool = pool_bytes
-        ? static_cast<const int32_t*>(pst.in(pool_group, pool_bytes, ctx->stream)) : nullptr;
-    if (pst.err == hipSuccess) pst.err = hipStreamSynchronize(ctx->stream);
+        ? static_cast<const int32_t*>(pst.in(pool_group, pool_bytes)) : nullptr;
+    if (pst.err == hipSuccess) pst.err = lease.lane(2).wait();
     if (pst.err != hipSuccess) return hip_fail(pst.err, "pool upload");
-    return host_chunks(ctx, n, "pipeline", [&](Staging& st, int64_t lo, int64_t c, hipStream_t s) {
+    return host_chunks(ctx, lease, n, "pipeline", [&](Staging& st, int64_t lo, int64_t c,
+                                                      hipStream_t s) {
         const size_t u = size_t(lo), k = size_t(c);
         vc_packets d{};
         vc_pipeline_out o{};
-        d.family = six ? static_cast<const uint8_t*>(st.in(in->family + u, k, s)) : nullptr;
-        d.proto = static_cast<const uint8_t*>(st.in(in->proto + u, k, s));
-        d.src4 = static_cast<const uint32_t*>(st.in(in->src4 + u, k * 4, s));
-        d.dst4 = static_cast<const uint32_t*>(st.in(in->dst4 + u, k * 4, s));
-        d.src6 = six ? static_cast<const uint8_t*>(st.in(in->src6 + u * 16, k * 16, s)) : nullptr;
-        d.dst6 = six ? static_cast<const uint8_t*>(st.in(in->dst6 + u * 16, k * 16, s)) : nullptr;
-        d.dport = static_cast<const uint16_t*>(st.in(in->dport + u, k * 2, s));
-        d.host_id = in->host_id ? static_cast<const uint32_t*>(st.in(in->host_id + u, k * 4, s))
+        d.family = six ? static_cast<const uint8_t*>(st.in(in->family + u, k)) : nullptr;
+        d.proto = static_cast<const uint8_t*>(st.in(in->proto + u, k));
+        d.src4 = static_cast<const uint32_t*>(st.in(in->src4 + u, k * 4));
+        d.dst4 = static_cast<const uint32_t*>(st.in(in->dst4 + u, k * 4));
+        d.src6 = six ? static_cast<const uint8_t*>(st.in(in->src6 + u * 16, k * 16)) : nullptr;
+        d.dst6 = six ? static_cast<const uint8_t*>(st.in(in->dst6 + u * 16, k * 16)) : nullptr;
+        d.dport = static_cast<const uint16_t*>(st.in(in->dport + u, k * 2));
+        d.host_id = in->host_id ? static_cast<const uint32_t*>(st.in(in->host_id + u, k * 4))
                                 : nullptr;
         o.acl = static_cast<int32_t*>(st.out(out->acl, k * 4));
         o.route = static_cast<int32_t*>(st.out(out->route, k * 4));
@@ -1392,10 +1651,10 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
         if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
         int r = pipeline_dev(ctx, d, c, dpool, n_pool, o, s, nullptr, nullptr, pin);
         if (r) return r;
-        st.back(out->acl + u, o.acl, k * 4, s);
-        st.back(out->route + u, o.route, k * 4, s);
-        st.back(out->group + u, o.group, k * 4, s);
-        if (out->allow) st.back(out->allow + u, o.allow, k, s);
+        st.back(out->acl + u, o.acl, k * 4);
+        st.back(out->route + u, o.route, k * 4);
+        st.back(out->group + u, o.group, k * 4);
+        if (out->allow) st.back(out->allow + u, o.allow, k);
         return VC_OK;
     });
 }
@@ -1490,7 +1749,7 @@ int vc_counters_add_dev(vc_ctx* ctx, int kind, const int32_t* out, const uint8_t
     } else {
         return fail(VC_EINVAL, "unknown counter kind");
     }
-    return e == hipSuccess ? VC_OK : hip_fail(e, "counter pass");
+    return launched(ctx, e, stream, "counter pass");
 }
 
 // ---------------------------------------------------------------------------

@@ -69,6 +69,7 @@ VC_HD int acl4_interval(const AclFamilyImage& f, uint32_t key) {
     if (f.dir4) {
         const uint32_t e = glb_ld(f.dir4 + (key >> (32 - f.dir_bits)));
         const int s = int(e & 0xFFFFu);
+        VC_CHECK(s + int(e >> 16) < f.nb, 201, key, e);
         return s + bsearch_u32(f.bounds4 + s, int(e >> 16) + 1, key);
     }
     return bsearch_u32(f.bounds4, f.nb, key);

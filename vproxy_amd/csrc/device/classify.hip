@@ -865,6 +865,36 @@ int v4_staged_words(const AclImage& img, int shift) {
 #define VC_LDS_GRANULE 1024
 #endif
 
+#if defined(VC_DEVCHECK)
+hipError_t devcheck_take_classify(uint32_t out[4]);
+hipError_t devcheck_take_hint(uint32_t out[4]);
+hipError_t devcheck_take_packet(uint32_t out[4]);
+hipError_t devcheck_take_mirror(uint32_t out[4]);
+hipError_t devcheck_take_select(uint32_t out[4]);
+hipError_t devcheck_take_counters(uint32_t out[4]);
+#endif
+
+hipError_t devcheck_take(uint32_t out[4]) {
+    out[0] = out[1] = out[2] = out[3] = 0;
+#if defined(VC_DEVCHECK)
+    hipError_t (*const take[])(uint32_t*) = {devcheck_take_classify, devcheck_take_hint,
+                                              devcheck_take_packet,   devcheck_take_mirror,
+                                              devcheck_take_select,   devcheck_take_counters};
+    for (auto f : take) {
+        uint32_t w[4];
+        const hipError_t e = f(w);
+        if (e != hipSuccess) return e;
+        if (w[0] && !out[0]) {
+            out[0] = w[0];
+            out[2] = w[2];
+            out[3] = w[3];
+        }
+        out[1] += w[1];
+    }
+#endif
+    return hipSuccess;
+}
+
 int resident_per_cu(const void* kernel, int block, size_t shmem) {
     static std::mutex mu;
     static std::map<std::pair<const void*, size_t>, int> cache;
@@ -1173,3 +1203,5 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
 }
 
 }  // namespace vc
+
+VC_DEVCHECK_READER(classify)

@@ -684,3 +684,5 @@ hipError_t big_hist_finish(const LaunchCfg& c, BigHist* h, int mode, const int32
 }
 
 }  // namespace vc
+
+VC_DEVCHECK_READER(counters)

@@ -32,4 +32,43 @@ VC_HD int32_t out_index(uint32_t v) {
     return v == VC_NONE ? -1 : int32_t(v);
 }
 
+// Device-side checks (debug builds, -DVC_DEVCHECK: vproxy_amd/libvclassify_chk.so).
+// VC_CHECK(cond, site, a, b) records the first failing site of the kernel
+// file in a device word with two detail values, counts every failure, and
+// lets the access go ahead; the library's VC_SYNC_CHECK mode reads the
+// words after every launch (launch.h devcheck_take) and names the entry
+// point.  Sites: 1xx stage.h, 2xx acl_dev.h, 3xx hint.hip, 4xx classify.hip,
+// 5xx packet.hip.  Normal builds compile the checks away.
+#if defined(VC_DEVCHECK)
+static __device__ uint32_t vc_devcheck_flags[4];
+#endif
+#if defined(VC_DEVCHECK) && defined(__HIP_DEVICE_COMPILE__)
+__device__ __noinline__ inline void devcheck_fail(uint32_t site, uint32_t a, uint32_t b) {
+    if (atomicCAS(&vc_devcheck_flags[0], 0u, site) == 0u) {
+        vc_devcheck_flags[2] = a;
+        vc_devcheck_flags[3] = b;
+    }
+    atomicAdd(&vc_devcheck_flags[1], 1u);
+}
+#define VC_CHECK(cond, site, a, b) \
+    do { if (!(cond)) ::vcd::devcheck_fail((site), uint32_t(a), uint32_t(b)); } while (0)
+#else
+#define VC_CHECK(cond, site, a, b) ((void)0)
+#endif
+
 }  // namespace vcd
+
+// One reader per kernel file (each code object has its own flag words).
+#if defined(VC_DEVCHECK)
+#define VC_DEVCHECK_READER(name)                                                            \
+    namespace vc {                                                                          \
+    hipError_t devcheck_take_##name(uint32_t out[4]) {                                      \
+        const uint32_t z[4] = {};                                                           \
+        hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(vcd::vc_devcheck_flags), 16);    \
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(vcd::vc_devcheck_flags), z, 16); \
+        return e;                                                                           \
+    }                                                                                       \
+    }
+#else
+#define VC_DEVCHECK_READER(name)
+#endif

@@ -133,6 +133,7 @@ __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_
             o0 = off[base];
             o1 = off[base + 64 < n ? base + 64 : n];
             o2 = off[base + 128 < n ? base + 128 : n];
+            VC_CHECK(o0 <= o1 && o1 <= o2 && o2 <= off[n], 301, base, o2);
         }
         uint32_t a0 = 0;
         int nsub = 1;
@@ -151,6 +152,7 @@ __device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_
                 A0 = off[i < n ? i : n];
                 E0 = off[i + 1 < n ? i + 1 : n];
             }
+            VC_CHECK(!off || (A0 <= E0 && E0 <= off[n]), 303, base, E0);
             body(c + sub, staged, a0, kPre == 2 && sub ? A1 : A0, kPre == 2 && sub ? E1 : E0);
         }
         wave_done();
@@ -226,6 +228,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
         VC_PMARK(0);
         if (i < n) {
             const uint32_t a = qoff[i], e = qoff[i + 1];
+            VC_CHECK(a <= e && e <= qoff[n], 302, i, e);
             uint8_t kd;
             int32_t val;
             if (staged)
@@ -663,3 +666,5 @@ extern "C" int vc_debug_hint_prof(unsigned long long* out) {
     return hipMemcpyToSymbol(HIP_SYMBOL(vcd::vc_hint_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+VC_DEVCHECK_READER(hint)

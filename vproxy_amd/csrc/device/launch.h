@@ -91,11 +91,15 @@ private:
 struct LaunchCfg {
     int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
     hipStream_t stream = nullptr;
-    hipMemPool_t pool = nullptr;   // staging pool of the host entry points
     Handoff handoff;
     ScratchRing* scratch = nullptr;   // counter-pass scratch (required by the launchers)
     TicketRing* tickets = nullptr;    // work counters; null: static grid-stride split
 };
+
+// Device-side check flags of a VC_DEVCHECK build (dev_common.h VC_CHECK):
+// the first failing site of any kernel file, its hit count and two detail
+// words, read and cleared.  A normal build reports nothing.
+hipError_t devcheck_take(uint32_t out[4]);
 
 // Workgroups per CU that can be resident at once for `kernel` (occupancy
 // query, cached per kernel).

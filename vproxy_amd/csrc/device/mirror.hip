@@ -95,3 +95,5 @@ hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int3
 }
 
 }  // namespace vc
+
+VC_DEVCHECK_READER(mirror)

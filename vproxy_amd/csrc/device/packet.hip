@@ -205,3 +205,5 @@ hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_
 }
 
 }  // namespace vc
+
+VC_DEVCHECK_READER(packet)

@@ -93,3 +93,5 @@ hipError_t launch_source(const LaunchCfg& c, const ServerImage& img, const int32
 }
 
 }  // namespace vc
+
+VC_DEVCHECK_READER(select)

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dev_common.h"
+
 namespace vcd {
 
 constexpr uint32_t kApron = 16;          // readable bytes before and after the items
@@ -16,6 +18,7 @@ constexpr uint32_t kApron = 16;          // readable bytes before and after the 
 template <uint32_t kBytes>
 __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uint32_t o1,
                                            uint32_t* stage, uint32_t* a0_out) {
+    VC_CHECK(o0 <= o1, 102, o0, o1);
     const uint32_t a0 = o0 & ~3u;                  // blob is dword aligned (launcher checks)
     *a0_out = a0;
     if (o1 - a0 > kBytes) return false;
@@ -47,7 +50,12 @@ struct LaneSpan {
 
 __device__ __forceinline__ LaneSpan lane_span(const uint32_t* off, int64_t base, int64_t n) {
     const int64_t i = base + int(threadIdx.x & 63);
-    return LaneSpan{off[i < n ? i : n], off[i + 1 < n ? i + 1 : n]};
+    const LaneSpan s{off[i < n ? i : n], off[i + 1 < n ? i + 1 : n]};
+#if defined(VC_DEVCHECK)
+    // offsets ascend and stay inside the blob [0, off[n])
+    VC_CHECK(s.a <= s.e && s.e <= off[n], 101, i, s.e);
+#endif
+    return s;
 }
 
 // [o0, o1) of the chunk's items, from the lanes' spans (wave-uniform)
