@@ -715,7 +715,8 @@ def dnsd_tables(clf, n_templates=1 << 20):
     groups, a 50k-line hosts file, a 10k-rule SecurityGroup (default allow);
     and n_templates query datagrams over the DNS-flavoured C4 hostnames (one
     A (70 %) or AAAA question, 30 % with an EDNS0 OPT record)."""
-    from vproxy_amd import dnswire as DW
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dnswire as DW          # wire-format encoder (test infrastructure)
     t = types.SimpleNamespace()
     t.groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
     clf.compile_upstream(t.groups)

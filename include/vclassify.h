@@ -142,6 +142,16 @@ int vc_route_lookup_v6_dev(vc_ctx *ctx, const uint8_t *dst6, int64_t n, int32_t 
 int vc_route_lookup_v4(vc_ctx *ctx, const uint32_t *dst4, int64_t n, int32_t *out);
 int vc_route_lookup_v6(vc_ctx *ctx, const uint8_t *dst6, int64_t n, int32_t *out);
 
+/* Switch.tables (Switch.java:560-566): one RouteTable per VNI, for the
+ * switch entry points (vc_switch_classify[_dev]).  Table t has VNI vni[t]
+ * (24-bit, distinct) and rules v4[v4_off[t] .. v4_off[t + 1]) and
+ * v6[v6_off[t] .. v6_off[t + 1]) in list order (CSR offsets, n_tables + 1
+ * entries each).  n_tables == 0 removes the per-VNI tables. */
+#define VC_SWITCH_NO_TABLE (-2)
+int vc_compile_vni_routes(vc_ctx *ctx, const int32_t *vni, const vc_net *v4,
+                          const int32_t *v4_off, const vc_net *v6, const int32_t *v6_off,
+                          int n_tables);
+
 /* ------------------------------------------------------------------------ */
 /* Upstream hint matching: core/.../svrgroup/Upstream.java + Hint.java       */
 /* ------------------------------------------------------------------------ */
@@ -430,10 +440,20 @@ int vc_parse_packets(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int6
  *       bind_port) -- the compiled SecurityGroup's UDP list (index, -1 =
  *       defaultAllow decided);
  *   `out` = VXLanPacket.from(payload) etc., as vc_parse_packets;
- *   out_route[i] = RouteTable.lookup(inner dst) (L3.java:423-444): an index
- *       in rulesV4 (inner IPv4) or rulesV6 (inner IPv6), -1 when none
- *       matches, the datagram is denied, or it does not parse into an IP
- *       packet.
+ *   out_route[i] = ctx.table.routeTable.lookup(inner dst) (L3.java:423-444),
+ *       where ctx.table is the switch's Table of the packet's VNI
+ *       (Switch.java:560-566 tables.get(vni)): an index in that table's
+ *       rulesV4 (inner IPv4) or rulesV6 (inner IPv6); -1 when none matches,
+ *       the datagram is denied, or it does not parse into an IP packet;
+ *       VC_SWITCH_NO_TABLE when the datagram parsed and was allowed but its
+ *       VNI has no table (inputVXLan drops it).  The per-VNI tables come
+ *       from vc_compile_vni_routes; a context without them routes every
+ *       packet through the single table of vc_compile_routes (a one-network
+ *       switch).
+ * Precondition: the batch holds only datagrams for which
+ * VProxyEncryptedPacket.from failed (Switch.java:648-679): user-iface
+ * traffic is decrypted and routed by the Java path first, since its
+ * bareVXLanAccess check and bare-VXLAN parse never run in the reference.
  * The switch's further per-packet decisions (remote-switch ifaces, MAC
  * checks, synthetic IPs, hop limit) stay with the caller.  remote_family:
  * 4/6 per datagram (NULL = all IPv4); remote4 / remote6 (16-byte aligned)
@@ -609,6 +629,9 @@ int vc_routetable_del_rule(vc_routetable *rt, const char *alias);
 /* family 4 -> rulesV4, 6 -> rulesV6; returns count (writes up to cap). */
 int vc_routetable_rules(const vc_routetable *rt, int family, vc_net *out, int cap);
 int vc_routetable_compile(vc_ctx *ctx, const vc_routetable *rt);
+/* The switch's tables: each RouteTable under the VNI it was created with
+ * (vc_routetable_new), as vc_compile_vni_routes. */
+int vc_routetables_compile_vni(vc_ctx *ctx, const vc_routetable *const *tables, int n);
 
 #ifdef __cplusplus
 }

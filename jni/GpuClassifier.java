@@ -45,10 +45,20 @@ public final class GpuClassifier {
     /** v4 / v6: packed vc_net[] (40 B each) of rulesV4 / rulesV6 in list order. */
     public static native void compileRoutes(long ctx, ByteBuffer v4, int n4, ByteBuffer v6, int n6)
         throws IOException;
+    /**
+     * Switch.tables (Switch.java:560-566): vni[n] ints; v4 / v6 packed vc_net[] of every table in turn,
+     * split by the n + 1 int offsets v4Off / v6Off.  switchClassify then routes each packet in the
+     * table of its VNI (VC_SWITCH_NO_TABLE = -2: tables.get(vni) is null).
+     */
+    public static native void compileVniRoutes(long ctx, ByteBuffer vni, ByteBuffer v4, ByteBuffer v4Off,
+                                               ByteBuffer v6, ByteBuffer v6Off, int n) throws IOException;
     public static native void lookupRouteV4(long ctx, ByteBuffer dst4, int n, ByteBuffer out) throws IOException;
     public static native void lookupRouteV6(long ctx, ByteBuffer dst6, int n, ByteBuffer out) throws IOException;
 
-    /** groups: packed vc_group_annos[] whose string slots hold offsets into `strings` (-1 = null). */
+    /**
+     * groups: packed vc_group_annos[] whose string slots hold offsets into `strings` (-1 = null);
+     * the buffer is not modified (the shim rebases a copy).
+     */
     public static native void compileUpstream(long ctx, ByteBuffer groups, int n, ByteBuffer strings)
         throws IOException;
     public static native void searchHints(long ctx, ByteBuffer hostBlob, ByteBuffer hostOff, ByteBuffer hostNull,
@@ -68,7 +78,9 @@ public final class GpuClassifier {
 
     /**
      * Switch.PacketHandler.readable per datagram: bareVXLanAccess.allow on the sender, the VXLAN
-     * parse (out: 12 buffers in vc_pkt_out order, null = skip) and the inner packet's route.
+     * parse (out: 12 buffers in vc_pkt_out order, null = skip) and the inner packet's route in the
+     * table of its VNI.  Only datagrams VProxyEncryptedPacket.from rejected belong in the batch
+     * (Switch.java:648-679): user-iface traffic takes the Java path first.
      */
     public static native void switchClassify(long ctx, ByteBuffer blob, ByteBuffer off, int n, int layer,
                                              ByteBuffer remoteFamily, ByteBuffer remote4, ByteBuffer remote6,

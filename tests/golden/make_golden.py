@@ -269,7 +269,7 @@ def kats():
 
 def dns_datagrams():
     """DNSServer's drain loop per datagram (DNSServer.java:457-500) over wire
-    packets built as Formatter.format lays them out (vproxy_amd/dnswire.py).  The
+    packets built as Formatter.format lays them out (tests/dnswire.py).  The
     first two are TestResolver.packet's packet (TestResolver.java:41-66,
     which asserts it parses back into exactly one packet); the expected
     outcomes of the others are hand-derived from Formatter.parsePackets /
@@ -277,8 +277,8 @@ def dns_datagrams():
     (Formatter.java:162-372), the rdata parsers (dns/rdata/*.java) and
     DNSServer.handleRequest (DNSServer.java:116-166).  Status codes are
     vclassify.h's VC_DNSD_*; per question [qtype, VC_DNS_* kind, value]."""
-    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
-    from vproxy_amd import dnswire as W
+    sys.path.insert(0, os.path.dirname(HERE))          # tests/ (dnswire)
+    import dnswire as W
     ANSWER, RECURSIVE, RESPONSE, REJECTED, EMPTY, MALFORMED, HOST = range(7)
     K_HOSTS, K_GROUP, K_IP, K_INTERNAL, K_REC = 1, 2, 3, 4, 5
     q = W.query

@@ -1,0 +1,299 @@
+/*
+ * jni_harness.c -- runs the JNI shim (jni/vproxy_component_secure_GpuClassifier.c)
+ * under a fake JNIEnv (test infrastructure only; built against
+ * tests/native/jni_spec/jni.h).  Direct ByteBuffers are {address, capacity}
+ * objects; ThrowNew records the exception class and message.
+ *
+ *   jni_harness cpu  -- no GPU: create throws IOException; a buffer shorter
+ *                       than the batch throws IllegalArgumentException
+ *                       before the library is called; an annotation string
+ *                       outside the strings buffer is refused.
+ *   jni_harness gpu  -- through the shim vs the C ABI directly: ACL, routes,
+ *                       per-VNI routes + switch, and compileUpstream twice
+ *                       on one groups buffer (rebased in a copy, so the
+ *                       second compile reads the same offsets).
+ * Prints "JNI OK" and exits 0 when every check holds.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "vclassify.h"
+
+struct _jobject {
+    void *p;
+    jlong cap;
+};
+
+static char thrown_cls[128], thrown_msg[512];
+static int n_thrown;
+
+static jclass fake_find_class(JNIEnv *env, const char *name) {
+    static struct _jobject c[8];
+    static int k;
+    (void) env;
+    c[k & 7].p = (void *) name;
+    return &c[k++ & 7];
+}
+static jint fake_throw_new(JNIEnv *env, jclass clazz, const char *msg) {
+    (void) env;
+    snprintf(thrown_cls, sizeof thrown_cls, "%s", (const char *) clazz->p);
+    snprintf(thrown_msg, sizeof thrown_msg, "%s", msg ? msg : "");
+    ++n_thrown;
+    return 0;
+}
+static void *fake_addr(JNIEnv *env, jobject b) {
+    (void) env;
+    return b ? b->p : NULL;
+}
+static jlong fake_cap(JNIEnv *env, jobject b) {
+    (void) env;
+    return b ? b->cap : -1;
+}
+static jobject fake_elem(JNIEnv *env, jobjectArray a, jsize i) {
+    (void) env;
+    return ((jobject *) a->p)[i];
+}
+static const char *fake_utf(JNIEnv *env, jstring s, jboolean *c) {
+    (void) env; (void) c;
+    return (const char *) s->p;
+}
+static void fake_release(JNIEnv *env, jstring s, const char *x) {
+    (void) env; (void) s; (void) x;
+}
+static jstring fake_new_utf(JNIEnv *env, const char *u) {
+    static struct _jobject o;
+    (void) env;
+    o.p = (void *) u;
+    return &o;
+}
+
+static struct JNINativeInterface_ table;
+static JNIEnv env_obj = &table;
+static JNIEnv *env = &env_obj;
+
+/* the shim's exports */
+#define J(name) Java_vproxy_component_secure_GpuClassifier_##name
+jlong J(create)(JNIEnv *, jclass, jint);
+void J(destroy)(JNIEnv *, jclass, jlong);
+void J(compileAcl)(JNIEnv *, jclass, jlong, jobject, jint, jobject, jint, jboolean);
+void J(classifyAclV4)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jint, jobject, jobject);
+void J(compileRoutes)(JNIEnv *, jclass, jlong, jobject, jint, jobject, jint);
+void J(lookupRouteV4)(JNIEnv *, jclass, jlong, jobject, jint, jobject);
+void J(compileVniRoutes)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject, jint);
+void J(compileUpstream)(JNIEnv *, jclass, jlong, jobject, jint, jobject);
+void J(searchHints)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject, jobject,
+                    jobject, jint, jobject);
+void J(switchClassify)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jobject, jobject,
+                       jobject, jint, jobjectArray, jobject, jobject, jobject);
+
+static struct _jobject B(void *p, jlong cap) {
+    struct _jobject o;
+    o.p = p;
+    o.cap = cap;
+    return o;
+}
+
+static int fails;
+#define CHECK(c, what) do { if (!(c)) { fprintf(stderr, "FAIL %s (%s: %s)\n", what, thrown_cls, thrown_msg); ++fails; } } while (0)
+
+static void expect_throw(const char *cls, const char *msg_part, const char *what) {
+    CHECK(n_thrown == 1 && strcmp(thrown_cls, cls) == 0 && strstr(thrown_msg, msg_part), what);
+    n_thrown = 0;
+    thrown_cls[0] = thrown_msg[0] = 0;
+}
+
+static void net4(vc_net *n, uint32_t ip, int len) {
+    int k;
+    memset(n, 0, sizeof *n);
+    n->ip_len = n->mask_len = 4;
+    for (k = 0; k < 4; ++k) {
+        const int bits = len - 8 * k;
+        n->ip[k] = (uint8_t) (ip >> (24 - 8 * k));
+        n->mask[k] = (uint8_t) (bits >= 8 ? 0xFF : bits <= 0 ? 0 : (0xFF << (8 - bits)) & 0xFF);
+        n->ip[k] &= n->mask[k];
+    }
+}
+
+static void cpu_mode(void) {
+    uint8_t proto[8] = {6, 6, 17, 17, 6, 6, 6, 6};
+    uint32_t src[8] = {0};
+    uint16_t port[8] = {0};
+    int32_t out[8];
+    struct _jobject bp = B(proto, 8), bs = B(src, 31), bq = B(port, 16), bo = B(out, 32);
+    vc_group_annos g;
+    char strings[8] = "a.com";
+    struct _jobject bg = B(&g, sizeof g), bstr = B(strings, 5);
+    (void) J(create)(env, NULL, 0);
+    expect_throw("java/io/IOException", "", "create without a GPU throws IOException");
+    /* 8 items need 32 bytes of src4: a 31-byte buffer is refused before any vc_ call */
+    J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, 8, &bo, NULL);
+    expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",
+                 "short src4 buffer");
+    bs.cap = 32;
+    bo.cap = 31;
+    J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, 8, &bo, NULL);
+    expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",
+                 "short output buffer");
+    J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, -1, &bo, NULL);
+    expect_throw("java/lang/IllegalArgumentException", "smaller than the batch", "negative n");
+    /* an annotation whose string runs past the strings buffer */
+    memset(&g, 0, sizeof g);
+    g.handle.host = (const char *) (intptr_t) 2;
+    g.handle.host_len = 4;
+    g.handle.uri = (const char *) (intptr_t) -1;
+    g.group.host = (const char *) (intptr_t) -1;
+    g.group.uri = (const char *) (intptr_t) -1;
+    J(compileUpstream)(env, NULL, 0, &bg, 1, &bstr);
+    expect_throw("java/lang/IllegalArgumentException", "outside the strings buffer",
+                 "annotation string past the buffer");
+    CHECK((intptr_t) g.handle.host == 2, "the caller's groups buffer is left as it was");
+}
+
+static uint32_t rnd_state = 12345;
+static uint32_t rnd(void) {
+    rnd_state = rnd_state * 1103515245u + 12345u;
+    return (rnd_state >> 8) ^ (rnd_state << 13);
+}
+
+static void gpu_mode(void) {
+    enum { NR = 300, N = 50000, NV = 4 };
+    static vc_acl_rule tcp[NR], udp[NR];
+    static uint8_t proto[N];
+    static uint32_t src[N], dst[N];
+    static uint16_t port[N];
+    static int32_t o1[N], o2[N];
+    static uint8_t a1[N], a2[N];
+    static vc_net routes[NR];
+    jlong h;
+    vc_ctx *ctx = NULL;
+    int i;
+    struct _jobject bt = B(tcp, sizeof tcp), bu = B(udp, sizeof udp), bp = B(proto, N),
+                    bs = B(src, 4 * N), bq = B(port, 2 * N), bo = B(o1, 4 * N), ba = B(a1, N),
+                    br = B(routes, sizeof routes), bd = B(dst, 4 * N);
+    h = J(create)(env, NULL, 0);
+    CHECK(h && !n_thrown, "create");
+    CHECK(vc_create(0, &ctx) == VC_OK, "vc_create");
+    for (i = 0; i < NR; ++i) {
+        net4(&tcp[i].net, rnd(), 8 + (int) (rnd() % 17));
+        tcp[i].min_port = (int32_t) (rnd() % 1000);
+        tcp[i].max_port = tcp[i].min_port + (int32_t) (rnd() % 30000);
+        tcp[i].allow = (int32_t) (rnd() & 1);
+        udp[i] = tcp[(i * 7) % NR];
+        udp[i].allow ^= 1;
+        net4(&routes[i], rnd(), 4 + (int) (rnd() % 21));
+    }
+    for (i = 0; i < N; ++i) {
+        proto[i] = (rnd() & 1) ? 6 : 17;
+        src[i] = (i & 3) ? (uint32_t) ((tcp[rnd() % NR].net.ip[0] << 24) | (rnd() & 0xFFFFFF)) : rnd();
+        port[i] = (uint16_t) (rnd() % 40000);
+        dst[i] = (uint32_t) ((routes[rnd() % NR].ip[0] << 24) | (rnd() & 0xFFFFFF));
+    }
+    J(compileAcl)(env, NULL, h, &bt, NR, &bu, NR, 0);
+    CHECK(!n_thrown, "compileAcl");
+    J(classifyAclV4)(env, NULL, h, &bp, &bs, &bq, N, &bo, &ba);
+    CHECK(!n_thrown, "classifyAclV4");
+    CHECK(vc_compile_acl(ctx, tcp, NR, udp, NR, 0) == VC_OK, "vc_compile_acl");
+    CHECK(vc_acl_classify_v4(ctx, proto, src, port, N, o2, a2) == VC_OK, "vc_acl_classify_v4");
+    CHECK(memcmp(o1, o2, sizeof o1) == 0 && memcmp(a1, a2, sizeof a1) == 0,
+          "ACL through the shim == the C ABI");
+    J(compileRoutes)(env, NULL, h, &br, NR, NULL, 0);
+    CHECK(!n_thrown, "compileRoutes");
+    J(lookupRouteV4)(env, NULL, h, &bd, N, &bo);
+    CHECK(vc_compile_routes(ctx, routes, NR, NULL, 0) == VC_OK, "vc_compile_routes");
+    CHECK(vc_route_lookup_v4(ctx, dst, N, o2) == VC_OK, "vc_route_lookup_v4");
+    CHECK(memcmp(o1, o2, sizeof o1) == 0, "routes through the shim == the C ABI");
+    {   /* per-VNI tables through the shim: the VNI-10 table is routes[0..150) */
+        int32_t vni[2] = {10, 20}, off4[3] = {0, 150, NR}, off6[3] = {0, 0, 0};
+        struct _jobject bv = B(vni, 8), b4o = B(off4, 12), b6o = B(off6, 12);
+        J(compileVniRoutes)(env, NULL, h, &bv, &br, &b4o, NULL, &b6o, 2);
+        CHECK(!n_thrown, "compileVniRoutes");
+        b4o.cap = 11;
+        J(compileVniRoutes)(env, NULL, h, &bv, &br, &b4o, NULL, &b6o, 2);
+        expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",
+                     "short vni offsets");
+    }
+    {   /* compileUpstream twice from one groups buffer of offsets */
+        static vc_group_annos g[3], gd[3];
+        static const char strings[] = "a.example.com" "b.example.com" "/api";
+        static const char *names[6] = {"a.example.com", "x.b.example.com", "b.example.com",
+                                       "nope.org", "a.example.com", "www.b.example.com"};
+        static uint8_t blob[128];
+        static uint32_t off[7];
+        static uint16_t hp[6];
+        static int32_t r1[6], r2[6], r3[6];
+        struct _jobject bg = B(g, sizeof g), bst = B((void *) strings, sizeof strings - 1),
+                        bb = B(blob, sizeof blob), bof = B(off, sizeof off), bhp = B(hp, sizeof hp),
+                        bres = B(r1, sizeof r1);
+        int k, pos = 0;
+        for (k = 0; k < 3; ++k) {
+            vc_annos *a[2] = {&g[k].handle, &g[k].group};
+            int j;
+            for (j = 0; j < 2; ++j) {
+                a[j]->host = (const char *) (intptr_t) -1;
+                a[j]->uri = (const char *) (intptr_t) -1;
+                a[j]->host_len = a[j]->uri_len = 0;
+                a[j]->port = 0;
+            }
+        }
+        g[0].handle.host = (const char *) (intptr_t) 0;
+        g[0].handle.host_len = 13;
+        g[1].group.host = (const char *) (intptr_t) 13;
+        g[1].group.host_len = 13;
+        g[2].handle.host = (const char *) (intptr_t) 13;
+        g[2].handle.host_len = 13;
+        g[2].handle.uri = (const char *) (intptr_t) 26;
+        g[2].handle.uri_len = 4;
+        for (k = 0; k < 6; ++k) {
+            off[k] = (uint32_t) pos;
+            memcpy(blob + pos, names[k], strlen(names[k]));
+            pos += (int) strlen(names[k]);
+        }
+        off[6] = (uint32_t) pos;
+        J(compileUpstream)(env, NULL, h, &bg, 3, &bst);
+        CHECK(!n_thrown, "compileUpstream");
+        J(searchHints)(env, NULL, h, &bb, &bof, NULL, &bhp, NULL, NULL, NULL, 6, &bres);
+        CHECK(!n_thrown, "searchHints");
+        bres.p = r3;
+        J(compileUpstream)(env, NULL, h, &bg, 3, &bst);         /* same buffer again */
+        CHECK(!n_thrown, "second compileUpstream from the same buffer");
+        J(searchHints)(env, NULL, h, &bb, &bof, NULL, &bhp, NULL, NULL, NULL, 6, &bres);
+        for (k = 0; k < 3; ++k) {
+            vc_annos *s[2] = {&g[k].handle, &g[k].group}, *d[2] = {&gd[k].handle, &gd[k].group};
+            int j;
+            for (j = 0; j < 2; ++j) {
+                *d[j] = *s[j];
+                d[j]->host = (intptr_t) s[j]->host < 0 ? NULL : strings + (intptr_t) s[j]->host;
+                d[j]->uri = (intptr_t) s[j]->uri < 0 ? NULL : strings + (intptr_t) s[j]->uri;
+            }
+        }
+        CHECK(vc_compile_upstream(ctx, gd, 3) == VC_OK, "vc_compile_upstream");
+        CHECK(vc_hint_search(ctx, blob, off, NULL, hp, NULL, NULL, NULL, 6, r2) == VC_OK,
+              "vc_hint_search");
+        CHECK(memcmp(r1, r2, sizeof r1) == 0 && memcmp(r3, r2, sizeof r2) == 0,
+              "hints through the shim (twice) == the C ABI");
+        CHECK(r2[0] == 0 && r2[3] == -1, "a.example.com -> group 0, nope.org -> null");
+    }
+    J(destroy)(env, NULL, h);
+    vc_destroy(ctx);
+}
+
+int main(int argc, char **argv) {
+    table.FindClass = fake_find_class;
+    table.ThrowNew = fake_throw_new;
+    table.GetDirectBufferAddress = fake_addr;
+    table.GetDirectBufferCapacity = fake_cap;
+    table.GetObjectArrayElement = fake_elem;
+    table.GetStringUTFChars = fake_utf;
+    table.ReleaseStringUTFChars = fake_release;
+    table.NewStringUTF = fake_new_utf;
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0)
+        gpu_mode();
+    else
+        cpu_mode();
+    if (fails) return 1;
+    printf("JNI OK\n");
+    return 0;
+}

@@ -8,7 +8,7 @@ import random
 
 import numpy as np
 
-from vproxy_amd import dnswire as DW
+import dnswire as DW
 import oracle_ffi as O
 from vproxy_amd import workloads as W
 

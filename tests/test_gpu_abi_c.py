@@ -99,3 +99,16 @@ def test_abi_c_sequence_matches_ctypes_and_oracle(tmp_path):
         assert clf.counters_prometheus("host=gpu0") == d["prom"]
     finally:
         clf.close()
+
+
+def test_jni_shim_on_gpu():
+    """The JNI shim under a fake JNIEnv (tests/native/jni_harness.c) against
+    the C ABI called directly: ACL, routes, per-VNI routes and two
+    compileUpstream calls from one groups buffer give identical results."""
+    import os
+    native = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+    exe = os.path.join(native, "build", "jni_harness")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", native, "build/jni_harness"])
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "JNI OK" in r.stdout, r.stdout + r.stderr

@@ -16,7 +16,7 @@ import random
 import numpy as np
 import pytest
 
-from vproxy_amd import dnswire as DW
+import dnswire as DW
 import oracle_ffi as O
 import vproxy_amd as V
 from vproxy_amd import workloads as W

@@ -10,6 +10,8 @@ one kernel, against the oracle's restatements of each step:
 
 Frames are the parse-chain cases of tests/cases.py (every layer, malformed
 and truncated shapes); senders are IPv4 and IPv6 (incl. IPv4-mapped).
+With per-VNI tables (Switch.tables, Switch.java:560-566) the route comes
+from the table of the packet's VNI, and an undefined VNI is dropped.
 """
 import numpy as np
 import pytest
@@ -50,6 +52,57 @@ def _remotes(rng, n):
     return fam, r4, r6
 
 
+def _nets(rng, k4, k6):
+    """k4 IPv4 and k6 IPv6 distinct random prefixes in a random list order"""
+    plen = rng.integers(1, 20, k4)
+    net = rng.integers(0, 2**32, k4, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
+    _, first = np.unique(key, return_index=True)
+    nets4 = W.v4_nets(net[np.sort(first)], plen[np.sort(first)])
+    rng.shuffle(nets4)
+    hi = rng.integers(0, 2**64, k6, dtype=np.uint64)
+    p6 = rng.integers(1, 24, k6)
+    hi &= np.where(p6 >= 64, np.uint64(2**64 - 1),
+                   np.uint64(2**64 - 1) << (64 - p6).astype(np.uint64))
+    keyh = np.stack([hi.view(np.int64), p6], 1)
+    _, f6 = np.unique(keyh, axis=0, return_index=True)
+    nets6 = W.v6_nets(hi[np.sort(f6)], np.zeros(len(f6), np.uint64), p6[np.sort(f6)])
+    return nets4, nets6
+
+
+def _want_route(frames, allow, tables, single=None):
+    """the oracle's route per datagram: parse, then RouteTable.lookup in the
+    table of the packet's VNI (tables: vni -> (nets4, nets6)), or in
+    `single` for every VNI; -2 for an allowed, parsed packet whose VNI has
+    no table"""
+    want = np.full(len(frames), -1, np.int32)
+    for i, f in enumerate(frames):
+        p = O.parse_packet(f, V.LAYER_VXLAN)
+        _want_route.vni[i] = p["vni"]
+        if not allow[i] or p["status"] != 0:
+            continue
+        t = single if single is not None else tables.get(p["vni"])
+        if t is None:
+            want[i] = V.SWITCH_NO_TABLE
+            continue
+        if p["l3"] not in (4, 6):
+            continue
+        dst = bytes.fromhex(p["dst"])
+        if p["l3"] == 4:
+            want[i] = O.rt_batch_v4_np(t[0], np.frombuffer(dst, ">u4").astype(np.uint32))[0]
+        else:
+            want[i] = O.rt_batch_v6_np(t[1], np.frombuffer(dst, np.uint8).reshape(1, 16))[0]
+    return want
+
+
+_want_route.vni = {}
+
+
+def _rt_nets(rt, family):
+    arr, n = rt.rules_raw(family)
+    return np.frombuffer(bytes(arr)[:n * W.NET_DT.itemsize], W.NET_DT).copy()
+
+
 @pytest.mark.parametrize("dflt", [False, True])
 def test_switch_classify_vs_oracle(dflt):
     import torch
@@ -60,19 +113,7 @@ def test_switch_classify_vs_oracle(dflt):
         a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
         b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
         V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1 if dflt else 0))
-        plen = rng.integers(1, 20, 3000)
-        net = rng.integers(0, 2**32, 3000, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
-        key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
-        _, first = np.unique(key, return_index=True)
-        nets4 = W.v4_nets(net[np.sort(first)], plen[np.sort(first)])
-        rng.shuffle(nets4)
-        hi = rng.integers(0, 2**64, 2000, dtype=np.uint64)
-        p6 = rng.integers(1, 24, 2000)
-        hi &= np.where(p6 >= 64, np.uint64(2**64 - 1),
-                       np.uint64(2**64 - 1) << (64 - p6).astype(np.uint64))
-        keyh = np.stack([hi.view(np.int64), p6], 1)
-        _, f6 = np.unique(keyh, axis=0, return_index=True)
-        nets6 = W.v6_nets(hi[np.sort(f6)], np.zeros(len(f6), np.uint64), p6[np.sort(f6)])
+        nets4, nets6 = _nets(rng, 3000, 2000)
         ra, rn, rk = W.as_ctypes(nets4, V._lib.VcNet)
         rb, rbn, rbk = W.as_ctypes(nets6, V._lib.VcNet)
         clf.compile_routes_raw(ra, rn, rb, rbn)
@@ -123,5 +164,79 @@ def test_switch_classify_vs_oracle(dflt):
                                            P(h_route)))
         for g, w in ((h_route, route), (h_acl, acl), (h_allow, allow), (h_l3, l3)):
             np.testing.assert_array_equal(g, w)
+    finally:
+        clf.close()
+
+
+def test_switch_per_vni_tables():
+    """Three networks with different RouteTables: each packet is routed in
+    the table of its VNI (Switch.java:560-566 tables.get(vni), L3.java:444
+    ctx.table.routeTable.lookup); a packet of an undefined VNI comes back
+    VC_SWITCH_NO_TABLE.  Both the raw CSR entry point and the RouteTable
+    mirrors (vc_routetables_compile_vni); removing the per-VNI tables goes
+    back to the single table."""
+    import torch
+    rng = np.random.default_rng(29)
+    clf = V.Classifier(0)
+    try:
+        tcp, udp = _rules(rng)
+        a, na, ka = W.as_ctypes(tcp, V._lib.VcAclRule)
+        b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+        V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 1))
+        single = _nets(rng, 500, 300)
+        ra, rn, rk = W.as_ctypes(single[0], V._lib.VcNet)
+        rb, rbn, rbk = W.as_ctypes(single[1], V._lib.VcNet)
+        clf.compile_routes_raw(ra, rn, rb, rbn)
+        vnis = [7, 100, 0xABCDE]
+        tables = {v: _nets(rng, 1500 + 700 * k, 900 + 300 * k) for k, v in enumerate(vnis)}
+        clf.compile_vni_routes([(v, tables[v][0], tables[v][1]) for v in (100, 0xABCDE, 7)])
+        frames = gen_frames(rng, 20011)
+        pick = np.array(vnis + [55])
+        for i, f in enumerate(frames):                     # rewrite the VXLAN vni
+            if len(f) >= 8:
+                v = int(rng.choice(pick))
+                frames[i] = f[:4] + bytes([(v >> 16) & 255, (v >> 8) & 255, v & 255]) + f[7:]
+        n = len(frames)
+        fam, r4, r6 = _remotes(rng, n)
+        blob, off = W.pack(frames)
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+        def run():
+            res, acl, allow, route = clf.switch_classify(
+                (T(blob), T(off.astype(np.int32))), T(r4.view(np.int32)), BIND_PORT,
+                remote6=T(r6), remote_family=T(fam))
+            torch.cuda.synchronize()
+            return allow.cpu().numpy(), route.cpu().numpy()
+
+        allow, route = run()
+        assert 0.1 < allow.mean()
+        want = _want_route(frames, allow, tables)
+        np.testing.assert_array_equal(route, want)
+        vni_of = np.array([_want_route.vni[i] for i in range(n)])
+        for v in vnis:                                     # every table was used
+            assert ((route >= 0) & (vni_of == v)).sum() > 100, v
+        assert (route == V.SWITCH_NO_TABLE).sum() > 500
+        # the same tables from RouteTable mirrors, each created with its vni
+        rts = []
+        for v in vnis:
+            rt = V.RouteTable("10.0.0.0/8", None, v)
+            for k in range(len(tables[v][0])):
+                try:
+                    rt.add_rule("r%d" % k, O.net_str(V._lib.VcNet.from_buffer_copy(
+                        tables[v][0][k].tobytes())))
+                except V.VcError:
+                    pass
+            rts.append(rt)
+        clf.compile_route_tables_vni(rts)
+        allow2, route2 = run()
+        mirror = {v: (_rt_nets(rt, 4), _rt_nets(rt, 6)) for v, rt in zip(vnis, rts)}
+        np.testing.assert_array_equal(allow2, allow)
+        np.testing.assert_array_equal(route2, _want_route(frames, allow, mirror))
+        # no per-VNI tables: every packet uses the single table
+        clf.compile_vni_routes([])
+        allow3, route3 = run()
+        np.testing.assert_array_equal(route3, _want_route(frames, allow, None, single=single))
+        with pytest.raises(V.AlreadyExistException):
+            clf.compile_vni_routes([(7, tables[7][0], tables[7][1])] * 2)
     finally:
         clf.close()

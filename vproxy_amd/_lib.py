@@ -22,6 +22,7 @@ COUNTERS_ACL, COUNTERS_ROUTE, COUNTERS_GROUP = 0, 1, 2
 DNSD_MAXQ = 4
 SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6 = 0, 4, 6
 LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6 = 0, 1, 4, 6
+SWITCH_NO_TABLE = -2           # vc_switch_classify: the packet's VNI has no table
 
 
 class VcNet(C.Structure):
@@ -166,6 +167,9 @@ def lib():
             getattr(L, f).argtypes = [vp, vp, i64, vp, vp]
         for f in ("vc_route_lookup_v4", "vc_route_lookup_v6"):
             getattr(L, f).argtypes = [vp, vp, i64, vp]
+        if hasattr(L, "vc_compile_vni_routes"):    # (A/B runs load older builds without it)
+            L.vc_compile_vni_routes.argtypes = [vp, vp, vp, vp, vp, vp, i32]
+            L.vc_routetables_compile_vni.argtypes = [vp, vp, i32]
         L.vc_compile_upstream.argtypes = [vp, P(VcGroupAnnos), i32]
         L.vc_hint_search_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp]
         L.vc_hint_search.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]

@@ -377,6 +377,26 @@ class Classifier:
     def compile_route_table(self, rt):
         check(lib().vc_routetable_compile(self.h, rt.h))
 
+    def compile_vni_routes(self, tables):
+        """Switch.tables (Switch.java:560-566): the route table of each VNI
+        for switch_classify.  tables: list of (vni, nets4, nets6), nets as
+        workloads.NET_DT arrays in list order; [] removes them."""
+        from .workloads import NET_DT
+        vni = np.array([t[0] for t in tables] or [0], np.int32)
+        o4 = np.zeros(len(tables) + 1, np.int32)
+        o6 = np.zeros(len(tables) + 1, np.int32)
+        o4[1:] = np.cumsum([len(t[1]) for t in tables]) if tables else []
+        o6[1:] = np.cumsum([len(t[2]) for t in tables]) if tables else []
+        a4 = np.concatenate([t[1] for t in tables] + [np.zeros(1, NET_DT)])
+        a6 = np.concatenate([t[2] for t in tables] + [np.zeros(1, NET_DT)])
+        check(lib().vc_compile_vni_routes(self.h, _ptr(vni), _ptr(a4), _ptr(o4), _ptr(a6),
+                                          _ptr(o6), len(tables)))
+
+    def compile_route_tables_vni(self, rts):
+        """Switch.tables from RouteTable mirrors, each under its own VNI."""
+        arr = (C.c_void_p * max(1, len(rts)))(*[rt.h.value for rt in rts])
+        check(lib().vc_routetables_compile_vni(self.h, arr, len(rts)))
+
     def compile_upstream(self, groups):
         arr, n, keep = group_array(groups)
         check(lib().vc_compile_upstream(self.h, arr, n))

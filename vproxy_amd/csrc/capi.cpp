@@ -175,6 +175,7 @@ struct HostsSnap;
 struct ServerSnap;
 struct CertSnap;
 struct MirrorSnap;
+struct VniSnap;
 
 }  // namespace
 
@@ -199,6 +200,7 @@ struct vc_ctx {
     std::shared_ptr<const ServerSnap> servers;
     std::shared_ptr<const CertSnap> certs;
     std::shared_ptr<const MirrorSnap> mirror;
+    std::shared_ptr<const VniSnap> vni;      // Switch.tables (vc_compile_vni_routes)
 
     template <class S>
     std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
@@ -254,11 +256,17 @@ int devcheck_report(const char* what) {
 // The status of a launch: its launch error, and under VC_SYNC_CHECK the
 // stream's completion and the device check flags, named by the entry point.
 int launched(vc_ctx* ctx, hipError_t e, void* stream, const char* what) {
-    if (e != hipSuccess) return hip_fail(e, what);
+    if (e != hipSuccess) {
+        ctx->tickets.mark_dirty();
+        return hip_fail(e, what);
+    }
     if (!ctx->sync_check) return VC_OK;
     e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
     if (e == hipSuccess) e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, (std::string(what) + " (sync check)").c_str());
+    if (e != hipSuccess) {
+        ctx->tickets.mark_dirty();
+        return hip_fail(e, (std::string(what) + " (sync check)").c_str());
+    }
     return devcheck_report(what);
 }
 
@@ -356,7 +364,10 @@ struct Staging {
     // status of the call: wait for the lane and deliver the results
     int finish() {
         const hipError_t e = err != hipSuccess ? err : L.finish(true);
-        if (e != hipSuccess) return hip_fail(e, what);
+        if (e != hipSuccess) {
+            ctx->tickets.mark_dirty();
+            return hip_fail(e, what);
+        }
         return ctx->sync_check ? devcheck_report(what) : VC_OK;
     }
 };
@@ -433,6 +444,9 @@ struct RouteSnap : Snapshot {
     RouteImage img{};
     int32_t n4 = 0, n6 = 0;
 };
+struct VniSnap : Snapshot {
+    VniImage img{};
+};
 struct HintSnap : Snapshot {
     HintImage img{};
 };
@@ -507,6 +521,7 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->servers.reset();
     ctx->certs.reset();
     ctx->mirror.reset();
+    ctx->vni.reset();
     ctx->grave->drain();
     for (auto& st : ctx->stagers) StagerLease::destroy(st.get());
     ctx->stagers.clear();
@@ -823,6 +838,63 @@ int vc_route_lookup_v4(vc_ctx* ctx, const uint32_t* dst4, int64_t n, int32_t* ou
 
 int vc_route_lookup_v6(vc_ctx* ctx, const uint8_t* dst6, int64_t n, int32_t* out) {
     return route_host(ctx, 6, dst6, n, out);
+}
+
+int vc_compile_vni_routes(vc_ctx* ctx, const int32_t* vni, const vc_net* v4, const int32_t* v4_off,
+                          const vc_net* v6, const int32_t* v6_off, int n_tables) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n_tables < 0 || (n_tables > 0 && (!vni || !v4_off || !v6_off)))
+        return fail(VC_EINVAL, "bad table arrays");
+    std::vector<int> order(static_cast<size_t>(n_tables));
+    for (int t = 0; t < n_tables; ++t) {
+        order[size_t(t)] = t;
+        if (vni[t] < 0 || vni[t] > 0xFFFFFF) return fail(VC_EINVAL, "vni out of range");
+        if (v4_off[t] < 0 || v4_off[t + 1] < v4_off[t] || v6_off[t] < 0 || v6_off[t + 1] < v6_off[t])
+            return fail(VC_EINVAL, "bad rule offsets");
+    }
+    if (n_tables > 0 && ((v4_off[n_tables] > 0 && !v4) || (v6_off[n_tables] > 0 && !v6)))
+        return fail(VC_EINVAL, "null rule array");
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return vni[a] < vni[b]; });
+    for (int k = 1; k < n_tables; ++k)
+        if (vni[order[size_t(k)]] == vni[order[size_t(k - 1)]])
+            return fail(VC_EEXIST, "vni defined twice: " + std::to_string(vni[order[size_t(k)]]));
+    std::vector<vc::TrieBuilt> tries(static_cast<size_t>(2 * n_tables));
+    for (int k = 0; k < n_tables; ++k) {
+        const int t = order[size_t(k)];
+        if ((rc = vc::build_trie(v4 + v4_off[t], v4_off[t + 1] - v4_off[t], 0,
+                                 &tries[size_t(2 * k)])) != VC_OK)
+            return fail(rc, "invalid IPv4 route rule in vni " + std::to_string(vni[t]));
+        if ((rc = vc::build_trie(v6 + v6_off[t], v6_off[t + 1] - v6_off[t], 1,
+                                 &tries[size_t(2 * k + 1)])) != VC_OK)
+            return fail(rc, "invalid IPv6 route rule in vni " + std::to_string(vni[t]));
+    }
+    std::lock_guard<std::mutex> lk(ctx->compile_mu);
+    if (n_tables == 0) {
+        ctx->publish(ctx->vni, std::shared_ptr<const VniSnap>());
+        return VC_OK;
+    }
+    auto s = std::make_shared<VniSnap>();
+    Upload up(ctx);
+    std::vector<RouteImage> imgs(static_cast<size_t>(n_tables));
+    std::vector<uint32_t> keys(static_cast<size_t>(n_tables));
+    for (int k = 0; k < n_tables; ++k) {
+        keys[size_t(k)] = uint32_t(vni[order[size_t(k)]]);
+        for (int f = 0; f < 2; ++f) {
+            const vc::TrieBuilt& tb = tries[size_t(2 * k + f)];
+            TrieImage& ti = imgs[size_t(k)].fam[f];
+            ti.nodes = up(*s, tb.nodes);
+            ti.root_bits = tb.root_bits;
+            ti.key_bits = tb.key_bits;
+            ti.n_rules = tb.n_rules;
+        }
+    }
+    s->img.vni = up(*s, keys);
+    s->img.tables = up(*s, imgs);
+    s->img.n = n_tables;
+    if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "vni route upload");
+    ctx->publish(ctx->vni, std::shared_ptr<const VniSnap>(std::move(s)));
+    return VC_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1380,8 +1452,11 @@ int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off
         return fail(VC_EINVAL, "src6 / dst6 / remote6 must be 16-byte aligned");
     auto a = ctx->get(ctx->acl);
     auto r = ctx->get(ctx->route);
-    if (!a || !r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
-    hipError_t e = vc::launch_switch(ctx->cfg(stream), a->img, r->img, blob, off, n, layer, o,
+    auto vt = ctx->get(ctx->vni);
+    if (!a || (!r && !vt))
+        return fail(VC_ESTATE, "SecurityGroup and RouteTable (or per-VNI tables) must be compiled");
+    hipError_t e = vc::launch_switch(ctx->cfg(stream), a->img, r ? r->img : RouteImage{},
+                                     vt ? vt->img : VniImage{}, blob, off, n, layer, o,
                                      remote_family, remote4, remote6, bind_port, out_acl,
                                      out_allow, out_route);
     return launched(ctx, e, stream, "switch launch");
@@ -1947,6 +2022,21 @@ int vc_routetable_compile(vc_ctx* ctx, const vc_routetable* rt) {
     vc_routetable_rules(rt, 6, b.data(), static_cast<int>(b.size()));
     return vc_compile_routes(ctx, a.data(), static_cast<int>(a.size()), b.data(),
                              static_cast<int>(b.size()));
+}
+
+int vc_routetables_compile_vni(vc_ctx* ctx, const vc_routetable* const* tables, int n) {
+    if (n < 0 || (n && !tables)) return fail(VC_EINVAL, "bad table array");
+    std::vector<int32_t> vni, o4{0}, o6{0};
+    std::vector<vc_net> a, b;
+    for (int t = 0; t < n; ++t) {
+        if (!tables[t]) return fail(VC_EINVAL, "null table");
+        vni.push_back(tables[t]->rt.vni());
+        for (const auto& r : tables[t]->rt.v4()) a.push_back(r.rule);
+        for (const auto& r : tables[t]->rt.v6()) b.push_back(r.rule);
+        o4.push_back(static_cast<int32_t>(a.size()));
+        o6.push_back(static_cast<int32_t>(b.size()));
+    }
+    return vc_compile_vni_routes(ctx, vni.data(), a.data(), o4.data(), b.data(), o6.data(), n);
 }
 
 }  // extern "C"

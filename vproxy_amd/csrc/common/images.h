@@ -78,6 +78,15 @@ struct RouteImage {
     TrieImage fam[2];             // 0 = rulesV4, 1 = rulesV6
 };
 
+// Switch.tables: the RouteTable of each VNI (Switch.java:560-566), for the
+// switch kernel.  vni[] ascending; tables[t] is the route image of vni[t].
+struct VniImage {
+    const uint32_t* vni;
+    const RouteImage* tables;
+    int32_t n;                    // 0: one network, the context's RouteImage
+    int32_t pad_;
+};
+
 // ---------------------------------------------------------------------------
 // Upstream hint matching + DNS hosts.
 //

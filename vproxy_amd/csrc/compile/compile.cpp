@@ -370,7 +370,7 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
                 child = v & ~VC_PTR;
             } else {
                 child = n_children++;
-                if (child >= VC_PTR) return VC_ENOMEM;
+                if (child >= VC_ONE) return VC_ENOMEM;   // ids at VC_ONE and up would read as records
                 out->nodes.resize(out->nodes.size() + 256, v);
                 out->nodes[entry] = VC_PTR | child;
             }

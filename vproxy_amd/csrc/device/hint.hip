@@ -81,6 +81,8 @@ struct Chunks {
             t = atomicAdd(ticket, 1u);
             const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
             const uint32_t ntickets = uint32_t((nchunks + kPerTicket - 1) / kPerTicket);
+            // a slot left nonzero by an aborted launch (launch.h TicketRing)
+            VC_CHECK(t <= ntickets + nwaves - 1, 304, t, ntickets + nwaves);
             if (t == ntickets + nwaves - 1) atomicExch(ticket, 0u);
         }
         return int64_t(__shfl(t, 0, 64)) * kPerTicket;
@@ -577,12 +579,12 @@ hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_
         hipLaunchKernelGGL(vcd::cert_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
-                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
+                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
     else
         hipLaunchKernelGGL(vcd::cert_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::cert_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
-                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next() : nullptr);
+                           certs, blob, off, null, n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
     return hipGetLastError();
 }
 
@@ -597,13 +599,13 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out, c.tickets ? c.tickets->next() : nullptr);
+                           n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
     else
         hipLaunchKernelGGL(vcd::hint_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out, c.tickets ? c.tickets->next() : nullptr);
+                           n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, img.n_groups, 0, img.n_groups, 0,
@@ -620,13 +622,13 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<true>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value,
-                           c.tickets ? c.tickets->next() : nullptr);
+                           c.tickets ? c.tickets->next(c.stream) : nullptr);
     else
         hipLaunchKernelGGL(vcd::dns_kernel<false>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<false>), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value,
-                           c.tickets ? c.tickets->next() : nullptr);
+                           c.tickets ? c.tickets->next(c.stream) : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !group_counters) return e;
     return launch_hist(c, VC_HIST_DNS, value, kind, n, hints.n_groups, 0, hints.n_groups, 0,

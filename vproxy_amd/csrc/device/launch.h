@@ -68,7 +68,12 @@ private:
 // so workgroups that become resident late -- beside another stream's kernel
 // -- do not hold back a fixed share of the work.  The wave that takes the
 // launch's last ticket resets the counter to zero, so a slot needs no
-// memset before reuse; slots go round-robin (kSlots launches in flight).
+// memset before reuse; slots go round-robin (kSlots launches in flight, far
+// more than the context's streams ever queue).  A launch that fails or
+// faults part-way can leave its slot nonzero, and every later launch on
+// that slot would skip work: the context marks the ring dirty on any device
+// error (capi.cpp `launched`), and the next launch re-zeroes the whole ring
+// on its stream first.
 class TicketRing {
 public:
     static constexpr uint32_t kSlots = 4096;
@@ -81,11 +86,19 @@ public:
         if (d_) (void)hipFree(d_);
         d_ = nullptr;
     }
-    uint32_t* next() { return d_ ? d_ + next_.fetch_add(1) % kSlots : nullptr; }
+    void mark_dirty() { dirty_.store(true); }
+    uint32_t* next(hipStream_t s) {
+        if (!d_) return nullptr;
+        if (dirty_.exchange(false) &&
+            hipMemsetAsync(d_, 0, kSlots * sizeof(uint32_t), s) != hipSuccess)
+            dirty_.store(true);
+        return d_ + next_.fetch_add(1) % kSlots;
+    }
 
 private:
     uint32_t* d_ = nullptr;
     std::atomic<uint32_t> next_{0};
+    std::atomic<bool> dirty_{false};
 };
 
 struct LaunchCfg {
@@ -197,7 +210,7 @@ hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
                                 uint8_t* status, int32_t* out_acl, uint8_t* nq, uint16_t* qtype,
                                 uint8_t* kind, int32_t* value);
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
-                         const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                         const VniImage& vt, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
                          const uint8_t* r6, int bind_port, int32_t* out_acl, uint8_t* out_allow,
                          int32_t* out_route);

@@ -98,9 +98,21 @@ struct SwitchOut {
     int32_t* route;
 };
 
+// The route image of `vni` (Switch.java:562 tables.get(vni)): a binary
+// search over the compiled VNIs (a few dozen words, L2-resident), or null.
+__device__ __forceinline__ const RouteImage* vni_table(const VniImage& vt, uint32_t vni) {
+    int lo = 0, len = vt.n;
+    while (len > 1) {
+        const int half = len >> 1;
+        lo = glb_ld(vt.vni + lo + half) <= vni ? lo + half : lo;
+        len -= half;
+    }
+    return glb_ld(vt.vni + lo) == vni ? vt.tables + lo : nullptr;
+}
+
 __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage& rt,
-                                           const SwitchIn& in, int64_t i, const PktOut& o,
-                                           const SwitchOut& so) {
+                                           const VniImage& vt, const SwitchIn& in, int64_t i,
+                                           const PktOut& o, const SwitchOut& so) {
     // SecurityGroup.allow(Protocol.UDP, remote, port): the UDP list
     const bool six = in.rfam && in.rfam[i] == 6;
     uint32_t v;
@@ -116,15 +128,30 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
     const bool allow = v == VC_NONE ? acl.default_allow != 0 : acl.allow[acl.n_tcp + v] != 0;
     if (so.acl) so.acl[i] = out_index(v);
     if (so.allow) so.allow[i] = allow ? 1 : 0;
-    // the inner packet's route, for allowed datagrams that parsed into IP
+    // the inner packet's route in the table of its VNI, for allowed
+    // datagrams that parsed
     int32_t r = -1;
     if (allow && o.status == VC_PKT_OK) {
-        if (o.l3 == VC_L3_IPV4) {
-            r = out_index(trie_v4(rt.fam[0].nodes, rt.fam[0].root_bits, bswap32(o.dst[0])));
+        TrieImage t4 = rt.fam[0], t6 = rt.fam[1];
+        bool have = true;
+        if (vt.n > 0) {
+            const RouteImage* tb = vni_table(vt, o.vni);
+            have = tb != nullptr;
+            if (have) {
+                t4.nodes = glb_ld(&tb->fam[0].nodes);
+                t4.root_bits = glb_ld(&tb->fam[0].root_bits);
+                t6.nodes = glb_ld(&tb->fam[1].nodes);
+                t6.root_bits = glb_ld(&tb->fam[1].root_bits);
+            }
+        }
+        if (!have) {
+            r = VC_SWITCH_NO_TABLE;                   // inputVXLan: vni not defined, drop
+        } else if (o.l3 == VC_L3_IPV4) {
+            r = out_index(trie_v4(t4.nodes, t4.root_bits, bswap32(o.dst[0])));
         } else if (o.l3 == VC_L3_IPV6) {
             uint64_t hi, lo;
             v6_key(*reinterpret_cast<const uint4*>(o.dst), &hi, &lo);
-            r = out_index(trie_v6(rt.fam[1].nodes, rt.fam[1].root_bits, hi, lo));
+            r = out_index(trie_v6(t6.nodes, t6.root_bits, hi, lo));
         }
     }
     so.route[i] = r;
@@ -133,7 +160,7 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
 template <bool kStage>
 __global__ __launch_bounds__(kPktBlock) void switch_kernel(
     const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n, int layer,
-    vc_pkt_out out, AclImage acl, RouteImage rt, SwitchIn in, SwitchOut so) {
+    vc_pkt_out out, AclImage acl, RouteImage rt, VniImage vt, SwitchIn in, SwitchOut so) {
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
@@ -155,7 +182,7 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
                 parse_packet(blob + a, int(e - a), layer, &o);
             }
             store_pkt(out, i, o);
-            switch_one(acl, rt, in, i, o, so);
+            switch_one(acl, rt, vt, in, i, o, so);
         }
         if (kStage) wave_done();
     }
@@ -166,7 +193,7 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
 namespace vc {
 
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
-                         const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
+                         const VniImage& vt, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
                          const uint8_t* r6, int bind_port, int32_t* out_acl, uint8_t* out_allow,
                          int32_t* out_route) {
@@ -180,10 +207,10 @@ hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteIma
     const vcd::SwitchOut so{out_acl, out_allow, out_route};
     if (stage)
         hipLaunchKernelGGL(vcd::switch_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
-                           blob, off, n, layer, out, acl, rt, in, so);
+                           blob, off, n, layer, out, acl, rt, vt, in, so);
     else
         hipLaunchKernelGGL(vcd::switch_kernel<false>, dim3(grid), dim3(vcd::kPktBlock), 0,
-                           c.stream, blob, off, n, layer, out, acl, rt, in, so);
+                           c.stream, blob, off, n, layer, out, acl, rt, vt, in, so);
     return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@ int SecurityGroup::remove_rule(std::string_view alias) {
 // ---------------------------------------------------------------------------
 // RouteTable
 // ---------------------------------------------------------------------------
-RouteTable::RouteTable(const vc_net& v4net, const vc_net* v6net, int vni) {
+RouteTable::RouteTable(const vc_net& v4net, const vc_net* v6net, int vni) : vni_(vni) {
     has_default_v4_ = true;
     default_v4_.alias = "default";
     default_v4_.rule = v4net;

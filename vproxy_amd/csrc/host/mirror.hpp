@@ -60,6 +60,7 @@ public:
     int del_rule(std::string_view alias);                               // :156-172
     const std::vector<RouteRule>& v4() const { return v4_; }
     const std::vector<RouteRule>& v6() const { return v6_; }
+    int vni() const { return vni_; }                                     // Table.vni
 
 private:
     int validate(const RouteRule& r) const;
@@ -67,6 +68,7 @@ private:
     bool has_default_v4_ = false, has_default_v6_ = false;
     RouteRule default_v4_, default_v6_;
     std::vector<RouteRule> v4_, v6_;
+    int vni_ = 0;
 };
 
 // Resolver.getHosts over file text: map entries in insertion order.
