@@ -16,6 +16,7 @@ import json
 import os
 import sys
 
+REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -172,7 +173,14 @@ def kats():
                     [{}, {"host": "s2.test.com", "uri": "/b"}]],
          "queries": [[{"host": "s1.test.com", "uri": "/"}, 0], [{"host": "s2.test.com", "uri": "/"}, 1],
                      [{"uri": "/a"}, 0], [{"uri": "/b"}, 1], [{"host": "s1.test.com"}, 0],
-                     [{"host": "127.0.0.1", "uri": "/a"}, 0], [{"host": "127.0.0.1", "uri": "/b"}, 1]]},
+                     [{"host": "127.0.0.1", "uri": "/a"}, 0], [{"host": "127.0.0.1", "uri": "/b"}, 1],
+                     # the h2 / h1 clients address the lb as 127.0.0.1:7890 (lbPort,
+                     # TestProtocols.java:54): :authority / Host carry the port, which
+                     # Hint.formatHost cuts (Hint.java:57-73)
+                     [{"host": "127.0.0.1:7890", "uri": "/a"}, 0],
+                     [{"host": "127.0.0.1:7890", "uri": "/b"}, 1],
+                     [{"host": "s1.test.com:7890", "uri": "/"}, 0],
+                     [{"host": "s2.test.com:7890", "uri": "/"}, 1]]},
         {"source": "CI.java:563-630 simpleSocks5 (hint-host + hint-port 8080)",
          "groups": [[{}, {"host": "myexample.com", "port": "8080"}],
                     [{}, {"host": "myexample2.com", "port": "8080"}]],
@@ -264,7 +272,90 @@ def kats():
     dump("kats.json", {"mask_match": [{"expect": e, "input": i, "net": n}
                                       for e, i, n in mask_match],
                        "hints": hints, "dns": dns, "dns_wire": dns_wire,
-                       "security_group": sg, "dns_datagrams": dns_datagrams()})
+                       "security_group": sg, "dns_datagrams": dns_datagrams(),
+                       "certs": certs(), "hosts_text": hosts_text()})
+
+
+def test_cert_names():
+    """CN / SAN dNSNames of TestSSL.TEST_CERT (TestSSL.java:48-...), decoded
+    from the PEM text in the reference test with the stdlib's certificate
+    decoder: the names SSLContextHolder.checkSNI would compare."""
+    import re
+    import ssl
+    import tempfile
+    path = os.path.join(REF, "test/src/test/java/vproxy/test/cases/TestSSL.java")
+    src = open(path).read()
+    m = re.search(r"TEST_CERT = (.*?);\n", src, re.S)
+    pem = "".join(re.findall(r'"((?:[^"\\]|\\.)*)"', m.group(1))).replace("\\n", "\n")
+    with tempfile.NamedTemporaryFile("w", suffix=".pem", delete=False) as f:
+        f.write(pem)
+    d = ssl._ssl._test_decode_cert(f.name)
+    os.unlink(f.name)
+    cn = [v for rdn in d["subject"] for k, v in rdn if k == "commonName"]
+    san = [v for k, v in d.get("subjectAltName", ()) if k == "DNS"]
+    return cn[:1] + san
+
+
+def certs():
+    """SSLContextHolder.choose (SSLContextHolder.java:50-186) scenarios.
+    Holder names come from the reference: TestSSL.TEST_CERT's CN (decoded
+    from the PEM in TestSSL.java), and the three certificates whose DN and
+    SAN lists SSLContextHolder.checkSNI documents (:96-99, :120-123).  The
+    expected holders are derived by hand from choose / chooseNoDefault /
+    compare: one holder -> always it; no match or no SNI -> the first
+    holder; wildcard "*.S" matches a longer SNI ending in ".S" whose prefix
+    holds no dot; plain names compare with String.equals (case-sensitive)."""
+    test_cert = test_cert_names()
+    assert test_cert == ["vproxy.cassite.net"], test_cert
+    pixiv = ["pixiv.net", "*.pixiv.net", "pixiv.net", "*.pixiv.org", "pixiv.org", "*.pximg.net",
+             "pximg.net", "*.ads-pixiv.net", "ads-pixiv.net"]
+    youtube = ["youtube.com", "*.youtube.com", "youtube.com", "*.ytimg.com", "ytimg.com",
+               "*.ggpht.com", "ggpht.com", "*.googlevideo.com", "googlevideo.com",
+               "*.googleapis.com", "googleapis.com", "*.googlesyndication.com",
+               "googlesyndication.com"]
+    google = ["google.com", "*.google.com", "google.com", "*.google.com.hk", "google.com.hk"]
+    return [
+        {"source": "TestSSL.java sslProxy: one CertKey(TEST_CERT), the client connects to "
+                   "127.0.0.1 (no SNI); choose with one holder returns it for any SNI",
+         "holders": [test_cert],
+         "queries": [[None, 0], ["vproxy.cassite.net", 0], ["www.google.com", 0]]},
+        {"source": "SSLContextHolder.java:96-123 documented certificates, after TEST_CERT",
+         "holders": [test_cert, pixiv, youtube, google],
+         "queries": [[None, 0], ["vproxy.cassite.net", 0], ["pixiv.net", 1],
+                     ["www.pixiv.net", 1], ["a.b.pixiv.net", 0], ["i.pximg.net", 1],
+                     ["ads-pixiv.net", 1], ["x.ads-pixiv.net", 1], ["www.youtube.com", 2],
+                     ["youtube.com", 2], ["r1---sn-abc.googlevideo.com", 2],
+                     ["i.ytimg.com", 2], ["www.google.com.hk", 3], ["google.com", 3],
+                     ["maps.google.com", 3], [".pixiv.net", 0], ["pixiv.net.evil", 0],
+                     ["GOOGLE.COM", 0], ["", 0], ["google.com.hk", 3], ["a.google.com.hk.x", 0]]},
+        {"source": "SSLContextHolder.java:50-64: first matching holder in add() order; "
+                   "a later holder listing the same name never wins",
+         "holders": [google, ["*.google.com", "maps.google.com"], pixiv],
+         "queries": [["maps.google.com", 0], ["www.pixiv.net", 2], ["nothing.org", 0]]},
+        {"source": "SSLContextHolder.java:55-57: no holders -> null",
+         "holders": [], "queries": [["a.com", -1], [None, -1]]},
+    ]
+
+
+def hosts_text():
+    """Resolver.getHosts over a Debian-style /etc/hosts (Resolver.java:62-153):
+    TestResolver.resolve expects localhost -> 127.0.0.1 (TestResolver.java:125-136),
+    the first line naming it.  Values are the index of the accepted host line
+    (comments, blank and invalid lines skipped), as vc_compile_hosts_text
+    numbers them; the DNS classification (DNSServer.java:116-166) of each qname."""
+    text = ("127.0.0.1\tlocalhost\n127.0.1.1\tdebian.local debian\n\n"
+            "# The following lines are desirable for IPv6 capable hosts\n"
+            "::1     localhost ip6-localhost ip6-loopback\nff02::1 ip6-allnodes\n"
+            "not-an-ip host.example\n10.0.0.7 svc.internal. # trailing dot form\n")
+    return [{"source": "TestResolver.java:125-144 resolve/resolveIpv6 of localhost via the hosts "
+                       "file; Resolver.java:96-146 (first line wins, x and x. both keyed, "
+                       "comments and non-IP lines skipped)",
+             "text": text,
+             "groups": [],
+             "queries": [["localhost.", 1, 0], ["debian.", 1, 1], ["debian.local.", 1, 1],
+                         ["ip6-localhost.", 1, 2], ["ip6-loopback.", 1, 2],
+                         ["ip6-allnodes.", 1, 3], ["svc.internal.", 1, 4],
+                         ["host.example.", 5, 0], ["nope.", 5, 0]]}]
 
 
 def dns_datagrams():

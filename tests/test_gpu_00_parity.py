@@ -454,3 +454,18 @@ def test_pipeline_and_counters(clf):
     cg = clf.counters_read(V.COUNTERS_GROUP)
     assert int(cg.sum()) == n
     clf.counters_enable(False)
+
+
+def test_hosts_text_kats_on_gpu(clf):
+    """kats.json hosts_text: an /etc/hosts text through vc_compile_hosts_text
+    (Resolver.getHosts: first line wins, x and x. keys, comments and non-IP
+    lines skipped) and vc_dns_classify -- TestResolver.resolve's localhost
+    is the 127.0.0.1 line."""
+    with open(os.path.join(G, "kats.json")) as f:
+        kats = json.load(f)
+    for case in kats["hosts_text"]:
+        clf.compile_upstream(case["groups"])
+        clf.compile_hosts_text(case["text"])
+        kind, value = clf.dns_classify([q for q, _, _ in case["queries"]])
+        assert list(zip(kind.tolist(), value.tolist())) == \
+            [(k, v) for _, k, v in case["queries"]], case["source"]

@@ -69,3 +69,19 @@ def test_errors(clf):
         V.check(V.lib().vc_compile_certs(clf.h, None, None, None, 1, 1))
     clf.compile_certs([["a.com"], ["b.com"]])
     assert clf.cert_choose([]).shape == (0,)
+
+
+def test_reference_cert_kats(clf):
+    """kats.json certs: TestSSL.TEST_CERT's CN (decoded from the reference's
+    PEM) and the certificates SSLContextHolder.checkSNI documents, through
+    vc_compile_certs / vc_cert_choose (no SNI, one holder, no holders,
+    wildcard depth, case, first holder in add() order)."""
+    import json
+    import os
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(G, "kats.json")) as f:
+        cases = json.load(f)["certs"]
+    for case in cases:
+        clf.compile_certs(case["holders"])
+        got = clf.cert_choose([s for s, _ in case["queries"]])
+        assert got.tolist() == [w for _, w in case["queries"]], case["source"]

@@ -160,3 +160,24 @@ def test_hosts_parse():
     assert ips[0] == bytes([127, 0, 0, 1]) and len(ips[2]) == 16
     # "10.0.0.2 db" parses but adds no key: "db" was already present
     assert all(v != 3 for _, v in pairs)
+
+
+def test_cert_kats():
+    """SSLContextHolder.choose with TestSSL.TEST_CERT's name and the
+    certificates SSLContextHolder.checkSNI documents (kats.json certs)."""
+    for case in load("kats.json")["certs"]:
+        c = O.Certs(case["holders"])
+        for sni, want in case["queries"]:
+            assert c.choose(sni) == want, (case["source"], sni)
+
+
+def test_hosts_text_kats():
+    """Resolver.getHosts over an /etc/hosts text, then DNSServer's
+    classification: TestResolver.resolve's localhost -> 127.0.0.1 line."""
+    for case in load("kats.json")["hosts_text"]:
+        pairs, ips = O.hosts_parse(case["text"])
+        h = O.Hosts(pairs)
+        g = O.Groups(case["groups"])
+        for q, kind, value in case["queries"]:
+            assert O.dns_classify(h, g, q) == (kind, value), (case["source"], q)
+        assert ips[0] == bytes([127, 0, 0, 1])

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CK(x)                                                                    \
     do {                                                                         \
@@ -96,8 +97,9 @@ float run(int grid, const uint32_t* keys, int64_t n, const uint32_t* t0, const u
     return best;
 }
 
-int main() {
+int main(int argc, char** argv) {
     const int64_t n = 125000000 / 8 * 8;               // one C5 batch
+    const bool cal = argc > 1 && std::string(argv[1]) == "cal";
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     const int cus = p.multiProcessorCount;
@@ -114,6 +116,32 @@ int main() {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    if (cal) {
+        // PMC calibration (run under rocprofv3 --pmc): one launch per line, in
+        // this order, 4 items per lane, 4 workgroups per CU.  The 4 KiB table
+        // stays in L2, so its launch counts only the key stream (n x 4 B,
+        // 16-B loads) and the result stream (n x 4 B, 16-B stores); the others
+        // add n x G uniformly random 4-byte gathers into the table.
+        printf("launch,table_KB,gathers_per_item,items,ms\n");
+        const int64_t kb[] = {4, 64 << 10, 64 << 10, 1 << 20, 1 << 20};
+        const int gs[] = {1, 1, 2, 1, 2};
+        for (int l = 0; l < 5; ++l) {
+            const uint32_t mask = uint32_t(kb[l] * 1024 / 4 - 1);
+            CK(hipEventRecord(a, 0));
+            if (gs[l] == 1)
+                hipLaunchKernelGGL((gather<1, 4>), dim3(cus * 4), dim3(512), 0, 0, keys, n, t0, t1,
+                                   mask, out);
+            else
+                hipLaunchKernelGGL((gather<2, 4>), dim3(cus * 4), dim3(512), 0, 0, keys, n, t0, t1,
+                                   mask, out);
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("%d,%lld,%d,%lld,%.3f\n", l, (long long)kb[l], gs[l], (long long)n, ms);
+        }
+        return 0;
+    }
     printf("table_MB,gathers_per_item,items_per_lane,blocks_per_cu,ms,G_items_per_s,G_gathers_per_s\n");
     const int sizes_mb[] = {4, 16, 64, 256, 1024};
     for (int mb : sizes_mb) {
