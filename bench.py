@@ -646,8 +646,10 @@ def main():
     traffic, t_commit = load_traffic("c5", dom)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + "
-                              "WRITE_SIZE per launch, taken at commit %s)" % t_commit,
+            "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE + the "
+                              "wide streamed reads' uncounted half (15 B/packet) + WRITE_SIZE "
+                              "per launch, taken at commit %s; random-gather misses are "
+                              "counted whole (profiles/r03_fetch_calibration.json)" % t_commit,
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
             "gather_bound": gather_bound,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
@@ -669,6 +671,11 @@ def main():
                 "data": "synthetic (seeded, generated on device)",
                 "config": {"workload": "C5 combined ACL->route->host pipeline, per-GPU shard of "
                                        "a seeded global batch",
+                           "shard": ("weak scaling: every GPU classifies %d packets per step, "
+                                     "so N = 1 runs one GPU's 125M shard of C5's 1B-packet batch "
+                                     "(N = 8 classifies the whole 1B)" % args.packets
+                                     if args.packets == 125_000_000 else
+                                     "weak scaling: %d packets per GPU per step" % args.packets),
                            "acl_rules": int(len(t.tcp) + len(t.udp)), "routes_v4": int(t.n4),
                            "routes_v6": int(t.n6), "groups": len(t.groups),
                            "hostname_pool": args.pool, "packets_per_gpu_per_step": args.packets,

@@ -9,12 +9,15 @@ FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
 (separate passes, as MI355X_MICROARCH.md §rocprofv3 PMC slots requires).
 
 Per kernel it writes the average per-launch HBM-side bytes.  FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
-coalesced stream (MI355X_MICROARCH.md §HBM), so the read side is reported
-both raw and doubled, and `traffic` = 2 x FETCH + WRITE (the guide's
-correction; other access widths are uncalibrated there -- the gathers in
-these kernels are 4-16 B per lane, so `traffic` is an upper estimate of the
-read side and the raw value a lower one).
+WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts half the bytes of a
+wide coalesced stream (MI355X_MICROARCH.md §HBM) and, by this repo's own
+calibration (scripts/fetch_calibration.py -> profiles/r03_fetch_calibration.json:
+tools/gather_probe cal, known gathers into known tables), one L2 miss of a
+random 4-byte gather as 64 bytes -- the full line request.  So the
+correction applies only to the wide streamed reads: with
+--stream KERNEL=BYTES (the kernel's algorithmic 16-B-per-lane streamed read
+bytes per launch), `traffic` = FETCH + BYTES / 2 + WRITE.  Kernels without
+--stream keep the guide's upper estimate 2 x FETCH + WRITE.
 """
 import argparse
 import csv
@@ -65,6 +68,8 @@ def main():
     ap.add_argument("--kernels", default="pipeline_v4_kernel,hint_kernel")
     ap.add_argument("--l2", default=None, help="rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum output")
     ap.add_argument("--commit", default=None, help="git commit the passes were taken at")
+    ap.add_argument("--stream", action="append", default=[],
+                    help="KERNEL=BYTES: wide streamed read bytes per launch (see module doc)")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     stats = _find(a.stats, "*kernel_stats.csv")
@@ -79,16 +84,24 @@ def main():
     if a.l2:
         hits, miss = counter_avg(a.l2, "TCC_HIT_sum"), counter_avg(a.l2, "TCC_MISS_sum")
         l2 = {k: (hits[k][1], miss[k][1]) for k in hits if k in miss}
+    stream = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in a.stream}
     out = {}
     for k in a.kernels.split(","):
         if k not in fetch or k not in write:
             continue
         fr, wr = fetch[k][1] * 1024, write[k][1] * 1024
-        traffic = 2 * fr + wr
+        if k in stream:
+            traffic = fr + stream[k] / 2 + wr
+            method = ("FETCH_SIZE + streamed reads / 2 (%.4g B, counted at half) + WRITE_SIZE; "
+                      "gather misses counted whole (profiles/r03_fetch_calibration.json)"
+                      % stream[k])
+        else:
+            traffic = 2 * fr + wr
+            method = "2 x FETCH_SIZE + WRITE_SIZE (the guide's stream correction on every read)"
         ns = avg_ns.get(k)
         out[k] = {"launches_fetch_pass": fetch[k][0], "fetch_bytes_raw": fr,
                   "fetch_bytes_x2": 2 * fr, "write_bytes": wr, "traffic_bytes": traffic,
-                  "avg_ns_kernel_trace": ns,
+                  "traffic_method": method, "avg_ns_kernel_trace": ns,
                   "traffic_GBps": traffic / ns if ns else None}
         if k in l2:
             out[k]["tcc_hit"], out[k]["tcc_miss"] = l2[k]
@@ -99,8 +112,8 @@ def main():
     except (OSError, ValueError):
         allw = {}
     allw[a.workload] = {"tag": a.tag, "commit": a.commit, "kernels": out,
-                        "note": "per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024, read side x2 "
-                                "per MI355X_MICROARCH.md §HBM (gfx950 half-count)"}
+                        "note": "per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024; traffic_method "
+                                "per kernel"}
     with open(path, "w") as f:
         json.dump(allw, f, indent=1)
     for src, name in ((a.fetch, "fetch"), (a.write, "write")):

@@ -19,3 +19,4 @@ bash scripts/gpu_steps.sh \
   "cal_fetch:120:timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/cal_fetch -o run -- $G" \
   "cal_write:120:timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/cal_write -o run -- $G" \
   "cal_l2:120:timeout -s KILL 100 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/cal_l2 -o run -- $G"
+bash scripts/gpu_steps.sh "gather_mix:300:tools/gather_probe mix"

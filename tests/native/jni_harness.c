@@ -97,7 +97,7 @@ static struct _jobject B(void *p, jlong cap) {
 }
 
 static int fails;
-#define CHECK(c, what) do { if (!(c)) { fprintf(stderr, "FAIL %s (%s: %s)\n", what, thrown_cls, thrown_msg); ++fails; } } while (0)
+#define CHECK(c, what) do { if (!(c)) { fprintf(stderr, "FAIL %s (%s: %s)\n", what, thrown_cls, thrown_msg); ++fails; } n_thrown = 0; thrown_cls[0] = thrown_msg[0] = 0; } while (0)
 
 static void expect_throw(const char *cls, const char *msg_part, const char *what) {
     CHECK(n_thrown == 1 && strcmp(thrown_cls, cls) == 0 && strstr(thrown_msg, msg_part), what);
@@ -181,9 +181,11 @@ static void gpu_mode(void) {
         tcp[i].min_port = (int32_t) (rnd() % 1000);
         tcp[i].max_port = tcp[i].min_port + (int32_t) (rnd() % 30000);
         tcp[i].allow = (int32_t) (rnd() & 1);
+        net4(&routes[i], rnd(), 4 + (int) (rnd() % 21));
+    }
+    for (i = 0; i < NR; ++i) {
         udp[i] = tcp[(i * 7) % NR];
         udp[i].allow ^= 1;
-        net4(&routes[i], rnd(), 4 + (int) (rnd() % 21));
     }
     for (i = 0; i < N; ++i) {
         proto[i] = (rnd() & 1) ? 6 : 17;

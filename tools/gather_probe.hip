@@ -80,6 +80,33 @@ __global__ __launch_bounds__(512) void gather(const uint32_t* __restrict__ keys,
     }
 }
 
+// Two tables of different sizes: per item one gather into t0 (mask0, the
+// candidate route root) and one into t1 (mask1, the 64 MB pool results);
+// kNt: the t1 gather is a nontemporal load, so its lines should not push
+// t0's out of L2.
+template <bool kNt>
+__global__ __launch_bounds__(512) void gather_mix(const uint32_t* __restrict__ keys, int64_t n,
+                                                  const uint32_t* __restrict__ t0, uint32_t mask0,
+                                                  const uint32_t* __restrict__ t1, uint32_t mask1,
+                                                  uint32_t* __restrict__ out) {
+    const int64_t steps = n / 4;
+    for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < steps;
+         g += int64_t(gridDim.x) * blockDim.x) {
+        const uint4 k = reinterpret_cast<const uint4*>(keys)[g];
+        const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+        uint32_t r[4], q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = t0[kk[j] & mask0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t* a = t1 + (mixh(kk[j]) & mask1);
+            q[j] = kNt ? __builtin_nontemporal_load(a) : *a;
+        }
+        reinterpret_cast<uint4*>(out)[g] =
+            make_uint4(r[0] + q[0], r[1] + q[1], r[2] + q[2], r[3] + q[3]);
+    }
+}
+
 template <int G, int U>
 float run(int grid, const uint32_t* keys, int64_t n, const uint32_t* t0, const uint32_t* t1,
           uint32_t mask, uint32_t* out, hipEvent_t a, hipEvent_t b) {
@@ -116,6 +143,35 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    if (argc > 1 && std::string(argv[1]) == "mix") {
+        // route-root candidates (t0: 1-64 MB) beside the 64 MB pool table (t1)
+        printf("root_MB,pool_MB,pool_nt,blocks_per_cu,ms,G_items_per_s,G_gathers_per_s\n");
+        const uint32_t mask1 = uint32_t((int64_t(64) << 20) / 4 - 1);
+        for (int mb : {1, 2, 4, 8, 16, 64})
+            for (int nt = 0; nt < 2; ++nt)
+                for (int bpc : {2, 4}) {
+                    const uint32_t mask0 = uint32_t((int64_t(mb) << 20) / 4 - 1);
+                    float best = 1e30f;
+                    for (int rep = 0; rep < 4; ++rep) {
+                        CK(hipEventRecord(a, 0));
+                        if (nt)
+                            hipLaunchKernelGGL(gather_mix<true>, dim3(cus * bpc), dim3(512), 0, 0,
+                                               keys, n, t0, mask0, t1, mask1, out);
+                        else
+                            hipLaunchKernelGGL(gather_mix<false>, dim3(cus * bpc), dim3(512), 0, 0,
+                                               keys, n, t0, mask0, t1, mask1, out);
+                        CK(hipEventRecord(b, 0));
+                        CK(hipEventSynchronize(b));
+                        float ms;
+                        CK(hipEventElapsedTime(&ms, a, b));
+                        if (rep > 0 && ms < best) best = ms;
+                    }
+                    printf("%d,64,%d,%d,%.3f,%.2f,%.2f\n", mb, nt, bpc, best, n / (best * 1e-3) / 1e9,
+                           2 * n / (best * 1e-3) / 1e9);
+                    fflush(stdout);
+                }
+        return 0;
+    }
     if (cal) {
         // PMC calibration (run under rocprofv3 --pmc): one launch per line, in
         // this order, 4 items per lane, 4 workgroups per CU.  The 4 KiB table
