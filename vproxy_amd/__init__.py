@@ -11,7 +11,7 @@ from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,
                    DNSD_ANSWER, DNSD_RECURSIVE, DNSD_RESPONSE, DNSD_REJECTED, DNSD_EMPTY,
                    DNSD_MALFORMED, DNSD_HOST, DNSD_MAXQ,
                    SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6,
-                   LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6)
+                   LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6, SWITCH_NO_TABLE)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
                          acl_rule_array, group_array, net_array, pack_strings, parse_ip,
                          server_array, cn_of_dn)
