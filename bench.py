@@ -574,6 +574,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    # VC_BENCH_SHARED_GPU=1: rehearsal of the multi-rank path on a one-GPU
+    # box -- every rank on cuda:0 and gloo for the collectives (RCCL refuses
+    # two ranks on one device).  The timing is then not a scaling result.
+    shared = os.environ.get("VC_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or args.dist
@@ -583,7 +589,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29517")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     clf = V.Classifier(local)
 
     if args.workload != "c5":
