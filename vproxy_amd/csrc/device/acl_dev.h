@@ -101,8 +101,7 @@ VC_HD uint32_t port_lookup(const uint32_t* pieces, uint2 d, uint32_t port) {
 // Rule index (or VC_NONE) of interval j for `port`: one 16-byte record
 // load (images.h AclFamilyImage.rec); the pieces array only for intervals
 // with more than four port pieces.
-VC_HD uint32_t acl_value(const uint32_t* rec, const uint32_t* pieces, int j, uint32_t port) {
-    const uint4 r = glb_ld(reinterpret_cast<const uint4*>(rec) + j);
+VC_HD uint32_t acl_rec_value(uint4 r, const uint32_t* pieces, uint32_t port) {
     const uint32_t k = (r.x >> 16) & 0xFFu;
     if (k == 0xFFu) return port_lookup(pieces, make_uint2(r.y, r.z), port);
     uint32_t v = r.x & 0xFFFFu;
@@ -110,6 +109,10 @@ VC_HD uint32_t acl_value(const uint32_t* rec, const uint32_t* pieces, int j, uin
     if (k > 2 && port >= (r.z >> 16)) v = r.z & 0xFFFFu;
     if (k > 3 && port >= (r.w >> 16)) v = r.w & 0xFFFFu;
     return v == 0xFFFFu ? VC_NONE : v;
+}
+
+VC_HD uint32_t acl_value(const uint32_t* rec, const uint32_t* pieces, int j, uint32_t port) {
+    return acl_rec_value(glb_ld(reinterpret_cast<const uint4*>(rec) + j), pieces, port);
 }
 
 }  // namespace vcd
