@@ -1,6 +1,7 @@
 // capi.cpp -- the C ABI (include/vclassify.h): contexts, snapshot
 // publication, uploads, and the host-side control-plane mirrors.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -148,7 +149,8 @@ public:
     }
     void copy(void* dst, const void* src, size_t n) {
         const int parts = workers_ + 1;
-        if (n < kMin || workers_ == 0) {
+        // a forked child has none of the parent's workers: copy alone there
+        if (n < kMin || workers_ == 0 || ::getpid() != pid_) {
             std::memcpy(dst, src, n);
             return;
         }
@@ -186,7 +188,7 @@ private:
         size_t n;
         std::atomic<int>* left;
     };
-    CopyPool() {
+    CopyPool() : pid_(::getpid()) {
         const unsigned hc = std::thread::hardware_concurrency();
         workers_ = int(std::min(7u, hc > 1 ? hc - 1 : 0u));
     }
@@ -213,6 +215,7 @@ private:
         }
     }
     int workers_ = 0;
+    const pid_t pid_;
     std::once_flag once_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
