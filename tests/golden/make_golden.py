@@ -273,7 +273,27 @@ def kats():
                                       for e, i, n in mask_match],
                        "hints": hints, "dns": dns, "dns_wire": dns_wire,
                        "security_group": sg, "dns_datagrams": dns_datagrams(),
-                       "certs": certs(), "hosts_text": hosts_text()})
+                       "certs": certs(), "hosts_text": hosts_text(),
+                       "source": source_kats()})
+
+
+def source_kats():
+    """ServerGroup source hashing (ServerGroup.java:387-397, 464-490, 620-664)
+    as TestTcpLB exercises it: sg0 = svr0 127.0.0.1:19080 and svr1
+    127.0.0.1:19081, weight 10, healthy (TestTcpLB.java:90-96); the test
+    clients connect from 127.0.0.1.  proxySource (:383-405) asserts every
+    connection reaches the backend that answers "0" -- svr0, index 0 of
+    getServerHandles(); with svr1 removed (:197-205) the answer is svr0 too.
+    Servers: [ip, port, weight, healthy]; views: 0 = next(source)."""
+    lo = "127.0.0.1"
+    return [
+        {"source": "TestTcpLB.java:383-405 proxySource (Method.source, one sg)",
+         "servers": [[lo, 19080, 10, True], [lo, 19081, 10, True]],
+         "queries": [[lo, 0, 0]]},
+        {"source": "TestTcpLB.java:197-205 (svr1 removed)",
+         "servers": [[lo, 19080, 10, True]],
+         "queries": [[lo, 0, 0]]},
+    ]
 
 
 def test_cert_names():

@@ -77,12 +77,20 @@ def test_source_select_vs_oracle(clf):
 
 
 def test_source_sticky_like_tcplb(clf):
-    """TestTcpLB.proxySource: every connection of one client reaches the
-    same backend (TestTcpLB.java:383-405)."""
-    clf.compile_servers([[("127.0.0.1", 19080, 10, True), ("127.0.0.1", 19081, 10, True)]])
-    src = np.full(100, (127 << 24) | 1, np.uint32)
-    got = clf.source_select(np.zeros(100, np.int32), src)
-    assert len(set(got.tolist())) == 1 and got[0] in (0, 1)
+    """TestTcpLB.proxySource: every connection from 127.0.0.1 reaches svr0,
+    the backend that answers "0" (TestTcpLB.java:383-405; kats.json source)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                           "kats.json")) as f:
+        cases = json.load(f)["source"]
+    for case in cases:
+        clf.compile_servers([[tuple(s) for s in case["servers"]]])
+        for client, view, want in case["queries"]:
+            a, b, c, d = (int(x) for x in client.split("."))
+            src = np.full(100, (a << 24) | (b << 16) | (c << 8) | d, np.uint32)
+            got = clf.source_select(np.zeros(100, np.int32), src, view)
+            assert got.tolist() == [want] * 100, case["source"]
 
 
 def test_source_errors(clf):

@@ -181,3 +181,17 @@ def test_hosts_text_kats():
         for q, kind, value in case["queries"]:
             assert O.dns_classify(h, g, q) == (kind, value), (case["source"], q)
         assert ips[0] == bytes([127, 0, 0, 1])
+
+
+def _ip_bytes(s):
+    import ipaddress
+    return ipaddress.ip_address(s).packed
+
+
+def test_source_kats():
+    """ServerGroup source hashing vs TestTcpLB.proxySource: the 127.0.0.1
+    clients all reach svr0 (kats.json source)."""
+    for case in load("kats.json")["source"]:
+        servers = [(_ip_bytes(ip), port, w, h) for ip, port, w, h in case["servers"]]
+        for client, view, want in case["queries"]:
+            assert O.source_select(servers, view, _ip_bytes(client)) == want, case["source"]
