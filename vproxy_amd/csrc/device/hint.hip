@@ -10,9 +10,6 @@
 // hash probes: the query host is scanned right-to-left once, producing the
 // reversed-FNV hash of every dot-suffix ("." + annoHost candidates) and of
 // the whole host; each probe is confirmed by a byte compare.
-#include <algorithm>
-#include <cstdlib>
-
 #include "acl_dev.h"
 #include "hint_dev.h"
 #include "launch.h"
@@ -596,14 +593,7 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                        const uint8_t* uri_blob, const uint32_t* uri_off, const uint8_t* uri_null,
                        int64_t n, int32_t* out, unsigned long long* counters) {
     if (n <= 0) return hipSuccess;
-    int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    // A/B knob (experiment): cap the pool pass at this many workgroups per
-    // CU, so it can share the CUs with a gather-bound kernel on another stream
-    static const int cap_per_cu = [] {
-        const char* v = std::getenv("VC_HINT_WG_PER_CU");
-        return v ? std::atoi(v) : 0;
-    }();
-    if (cap_per_cu > 0 && c.tickets) want = std::min<int64_t>(want, int64_t(c.num_cus) * cap_per_cu);
+    const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
     if (host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0)
         hipLaunchKernelGGL(vcd::hint_kernel<true>,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
