@@ -2,7 +2,7 @@
 # A/B on the GPU box: the C5 schedule with the next pool pass beside the
 # counter finish (default) against the pool pass beside the pipeline kernel
 # with the pool pass capped at K workgroups per CU (VC_HINT_WG_PER_CU, a knob of the
-# A/B build at 3a3e1f5-era commits, since removed), so
+# library at b2524f6, since removed), so
 # the VALU-bound pool pass shares the CUs of the gather-bound pipeline
 # kernel.  Two interleaved rounds; one JSON line per run in gpurun_out/ab_overlap.jsonl.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
