@@ -22,7 +22,7 @@ def lib():
         vp = C.c_void_p
         L.ic_acl.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp,
                              vp, vp]
-        L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp]
+        L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp, C.c_int]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
         L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
@@ -55,11 +55,12 @@ def acl(tcp, udp, dflt, family, proto, src, port):
     return out, allow, stats
 
 
-def route(rules, family, keys):
+def route(rules, family, keys, root_bits=0):
+    """root_bits 0: the library's default for the table size"""
     n = len(keys)
     out = np.empty(n, np.int32)
-    stats = np.zeros(3, np.int32)     # root bits, nodes, one-prefix records
-    rc = lib().ic_route(P(rules), len(rules), family, P(keys), n, P(out), P(stats))
+    stats = np.zeros(3, np.int32)     # root bits, node units, one-prefix records
+    rc = lib().ic_route(P(rules), len(rules), family, P(keys), n, P(out), P(stats), root_bits)
     assert rc == 0, rc
     return out, stats
 

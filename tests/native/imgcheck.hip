@@ -103,9 +103,9 @@ int ic_acl(const vc_acl_rule* tcp, int nt, const vc_acl_rule* udp, int nu, int d
 }
 
 int ic_route(const vc_net* rules, int nr, int family, const void* keys, int64_t n, int32_t* out,
-             int32_t* stats) {
+             int32_t* stats, int root_bits) {
     vc::TrieBuilt t;
-    int rc = vc::build_trie(rules, nr, family == 4 ? 0 : 1, &t);
+    int rc = vc::build_trie(rules, nr, family == 4 ? 0 : 1, &t, root_bits);
     if (rc) return rc;
     stats[0] = t.root_bits;
     stats[1] = t.n_nodes;

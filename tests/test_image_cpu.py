@@ -115,10 +115,42 @@ def test_route_v4_deep_and_long():
     nets = W.v4_nets(net[first], plen[first])
     rng.shuffle(nets)     # arbitrary list order: priority = index, not length
     q = W.v4_lookups(net[first], plen[first], 40000, 22)
-    for nr in (len(nets), 1000):   # 24-bit and 16-bit roots
-        got, stats = IC.route(nets[:nr], 4, q)
+    for nr in (len(nets), 1000):   # 24-bit and 16-bit roots by default
         want = O.rt_batch_v4_np(nets[:nr], q, nthreads=4)
-        np.testing.assert_array_equal(got, want)
+        for rb in (0, 16, 20, 24):
+            got, stats = IC.route(nets[:nr], 4, q, rb)
+            np.testing.assert_array_equal(got, want)
+            assert rb == 0 or stats[0] == rb
+
+
+def test_route_root_20_edges():
+    """A 20-bit root strides 4 bits to the byte boundary, then 8: prefixes
+    of every length 16-32 nested in a few root slots, list order shuffled,
+    queries with each bit 18-25 flipped (the first node's edges)."""
+    rng = np.random.default_rng(23)
+    base = rng.integers(0, 2**32, 12, dtype=np.uint64).astype(np.uint32)
+    plen = rng.integers(16, 33, 3000)
+    net = (base[rng.integers(0, 12, 3000)] ^ rng.integers(0, 2**16, 3000).astype(np.uint32))
+    net = net & W._mask32(plen)
+    key = (net.astype(np.uint64) << 8) | plen.astype(np.uint64)
+    _, first = np.unique(key, return_index=True)
+    nets = W.v4_nets(net[first], plen[first])
+    rng.shuffle(nets)
+    q = W.v4_lookups(net[first], plen[first], 20000, 24, inside=1.0)
+    q = np.concatenate([q] + [q[:2000] ^ np.uint32(1 << (31 - b)) for b in range(18, 26)])
+    want = O.rt_batch_v4_np(nets, q, nthreads=4)
+    got, stats = IC.route(nets, 4, q, 20)
+    np.testing.assert_array_equal(got, want)
+    assert stats[0] == 20 and stats[1] > 0, stats
+    hi, lo, p6 = W.gen_v6_prefixes(3000, 25)
+    n6 = W.v6_nets(hi, lo, p6)
+    q6 = W.v6_lookups(hi, lo, p6, 20000, 26)
+    q6 = np.concatenate([q6] + [_flip(q6[:2000], b) for b in (19, 20, 23, 24, 31)])
+    want6 = O.rt_batch_v6_np(n6, q6, nthreads=4)
+    for rb in (16, 20, 24):
+        got, stats = IC.route(n6, 6, q6, rb)
+        np.testing.assert_array_equal(got, want6)
+        assert stats[0] == rb
 
 
 def test_route_v6():
@@ -189,6 +221,13 @@ def test_route_one_prefix_records():
     got, stats = IC.route(v4n, 4, q4)
     np.testing.assert_array_equal(got, O.rt_batch_v4_np(v4n, q4, nthreads=4))
     assert stats[0] == 16 and stats[2] > 1000, stats
+    # the same under a 20-bit root (records for /21-/32 alone in their slot)
+    got, stats = IC.route(v4n, 4, q4, 20)
+    np.testing.assert_array_equal(got, O.rt_batch_v4_np(v4n, q4, nthreads=4))
+    assert stats[0] == 20 and stats[2] > 1000, stats
+    got, stats = IC.route(nets, 6, qb, 20)
+    np.testing.assert_array_equal(got, O.rt_batch_v6_np(nets, qb, nthreads=4))
+    assert stats[0] == 20 and stats[2] > 500, stats
 
 
 def test_hint_random():

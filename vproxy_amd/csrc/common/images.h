@@ -55,8 +55,12 @@ struct AclImage {
 
 // ---------------------------------------------------------------------------
 // RouteTable: one multibit stride trie per family (DIR-24-8 for IPv4).
-// Root = 2^root_bits entries, every deeper node 256 entries (8-bit stride).
-// Entry: VC_PTR | node_id  -> child at nodes[(1<<root_bits) + node_id*256]
+// Root = 2^root_bits entries (16, 20 or 24).  Below it the walk strides to
+// the next byte boundary, then 8 bits at a time: a node at depth `bits`
+// has 2^(8 - bits % 8) entries (16 under a 20-bit root, else 256).
+// Entry: VC_PTR | node_id  -> child at nodes[(1<<root_bits) + node_id*16]
+//                             (nodes are allocated in 16-entry units, so
+//                             every node starts on a 64-byte line)
 //        VC_PTR | VC_ONE | id -> one-prefix record at ((uint4*)nodes)[id]:
 //                             {key bits 0-31, key bits 32-63, match value,
 //                              miss value (24 bits, 0xFFFFFF = none) | len << 24}

@@ -2,6 +2,7 @@
 #include "compile.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -284,11 +285,21 @@ int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_u
 // ---------------------------------------------------------------------------
 // Route trie
 // ---------------------------------------------------------------------------
-int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
+int default_root_bits(int n, int family) {
+    if (n <= 4096) return 16;
+    // A/B knob while the 20-bit root is measured
+    const char* v = std::getenv(family == 0 ? "VC_ROUTE_ROOT_BITS_V4" : "VC_ROUTE_ROOT_BITS_V6");
+    if (v && (std::atoi(v) == 16 || std::atoi(v) == 20 || std::atoi(v) == 24)) return std::atoi(v);
+    return 24;
+}
+
+int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out, int root_bits) {
     *out = TrieBuilt{};
     out->key_bits = family == 0 ? 32 : 128;
     out->n_rules = n;
-    out->root_bits = n > 4096 ? 24 : 16;
+    if (root_bits == 0) root_bits = default_root_bits(n, family);
+    if (root_bits != 16 && root_bits != 20 && root_bits != 24) return VC_EINVAL;
+    out->root_bits = root_bits;
     const int rb = out->root_bits;
     struct P {
         u128 key;   // left-aligned in 128 bits
@@ -346,8 +357,9 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
         ++per_slot[static_cast<uint32_t>(ps[i].key >> (128 - rb))];
     const bool records_ok = n < 0xFFFFFF;
     std::vector<uint32_t> rec_words, rec_slots;
-    // 3) the other longer prefixes in ascending length: walk/create 8-bit
-    //    nodes; a new node inherits its parent entry's value (leaf pushing).
+    // 3) the other longer prefixes in ascending length: walk/create nodes
+    //    (2^trie_stride entries, allocated in 16-entry units); a new node
+    //    inherits its parent entry's value (leaf pushing).
     uint32_t n_children = 0;
     for (size_t i = split; i < ps.size(); ++i) {
         const P& p = ps[i];
@@ -366,17 +378,20 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
         for (;;) {
             uint32_t v = out->nodes[entry];
             uint32_t child;
+            const int st = 8 - (bits & 7);                   // route_dev.h trie_stride
+            const uint32_t width = 1u << st;
             if (v & VC_PTR) {
                 child = v & ~VC_PTR;
             } else {
-                child = n_children++;
-                if (child >= VC_ONE) return VC_ENOMEM;   // ids at VC_ONE and up would read as records
-                out->nodes.resize(out->nodes.size() + 256, v);
+                child = n_children;
+                n_children += width / 16;
+                if (n_children >= VC_ONE) return VC_ENOMEM;  // ids at VC_ONE and up would read as records
+                out->nodes.resize(out->nodes.size() + width, v);
                 out->nodes[entry] = VC_PTR | child;
             }
-            size_t base = root + size_t(child) * 256;
-            int nb = bits + 8;
-            uint32_t sub = static_cast<uint32_t>(p.key >> (128 - nb)) & 255u;
+            size_t base = root + size_t(child) * 16;
+            int nb = bits + st;
+            uint32_t sub = static_cast<uint32_t>(p.key >> (128 - nb)) & (width - 1);
             if (p.len <= nb) {
                 uint32_t cnt = 1u << (nb - p.len);
                 for (uint32_t e = sub; e < sub + cnt; ++e)
@@ -387,7 +402,7 @@ int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out) {
             bits = nb;
         }
     }
-    out->n_nodes = static_cast<int32_t>(n_children);
+    out->n_nodes = static_cast<int32_t>(n_children);   // 16-entry units
     // records after the nodes (the node array is a multiple of 4 words, so
     // they are 16-byte aligned); an entry addresses them in 16-byte units
     const size_t base = out->nodes.size() / 4;

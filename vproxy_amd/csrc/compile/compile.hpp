@@ -38,12 +38,14 @@ struct TrieBuilt {
     int32_t root_bits = 16;
     int32_t key_bits = 32;
     int32_t n_rules = 0;
-    int32_t n_nodes = 0;             // 256-entry nodes below the root
+    int32_t n_nodes = 0;             // 16-entry units of nodes below the root
     int32_t n_records = 0;           // one-prefix records (images.h VC_ONE)
 };
 
 // One RouteTable family list (list order = priority) -> stride trie.
-int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out);
+// root_bits: 16, 20 or 24; 0 picks default_root_bits(n, family).
+int default_root_bits(int n, int family);
+int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out, int root_bits = 0);
 
 struct KeySlotH {                    // host mirror of KeySlot (URI table)
     uint64_t hash;

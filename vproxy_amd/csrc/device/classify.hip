@@ -246,11 +246,12 @@ __global__ __launch_bounds__(kBlock) void route_v4_kernel(
         for (int k = 0; k < 4; ++k) e[k] = nodes[key[k] >> (32 - rb)];   // 4 probes in flight
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            int shift = 32 - rb;
+            int bits = rb;
             while (e[k] & VC_PTR) {
-                shift -= 8;
-                e[k] = trie_next(nodes, 1u << rb, e[k], (key[k] >> shift) & 255u,
+                const int s = trie_stride(bits);
+                e[k] = trie_next(nodes, 1u << rb, e[k], v4_sub(key[k], bits, s),
                                  uint64_t(key[k]) << 32);
+                bits += s;
             }
         }
         int4 o;
@@ -299,8 +300,9 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (e[k] & VC_PTR) {
-                    e[k] = trie_next(nodes, root, e[k], v6_sub(hi[k], lo[k], bits[k]), hi[k]);
-                    bits[k] += 8;
+                    const int s = trie_stride(bits[k]);
+                    e[k] = trie_next(nodes, root, e[k], v6_sub(hi[k], lo[k], bits[k], s), hi[k]);
+                    bits[k] += s;
                     any = true;
                 }
             }
@@ -380,10 +382,11 @@ __device__ __forceinline__ void stream_st(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, uint32_t e,
                                                 uint32_t d) {
-    int shift = 32 - rb;
+    int bits = rb;
     while (e & VC_PTR) {
-        shift -= 8;
-        e = trie_next(nodes, 1u << rb, e, (d >> shift) & 255u, uint64_t(d) << 32);
+        const int s = trie_stride(bits);
+        e = trie_next(nodes, 1u << rb, e, v4_sub(d, bits, s), uint64_t(d) << 32);
+        bits += s;
     }
     return e;
 }
@@ -393,8 +396,9 @@ __device__ __forceinline__ uint32_t route6_chase(const uint32_t* nodes, int rb, 
     int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
-        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits), hi);
-        bits += 8;
+        const int s = trie_stride(bits);
+        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits, s), hi);
+        bits += s;
     }
     return e;
 }

@@ -1,7 +1,7 @@
 // route_dev.h -- device side of RouteTable.lookup (RouteTable.java:44-59).
 //
-// Walks the leaf-pushed stride trie: root entry, then at most one 8-bit node
-// per remaining byte of the prefix, or one 16-byte one-prefix record where
+// Walks the leaf-pushed stride trie: root entry, then at most one node per
+// remaining byte of the prefix (the first one up to the byte boundary), or one 16-byte one-prefix record where
 // the subtree holds a single prefix (images.h VC_ONE).  Every entry holds the
 // min list index of the prefixes covering it, so the last entry reached is
 // the answer.
@@ -21,27 +21,38 @@ VC_HD uint32_t one_match(uint4 r, uint64_t hi) {
     return miss == 0xFFFFFFu ? VC_NONE : miss;
 }
 
+// Bits a node at depth `bits` consumes: up to the next byte boundary.
+VC_HD int trie_stride(int bits) { return 8 - (bits & 7); }
+
 // Next entry below pointer entry e: the child node's entry `sub`, or the
 // record's answer (never a pointer, so the walk ends).
 VC_HD uint32_t trie_next(const uint32_t* nodes, uint32_t root, uint32_t e, uint32_t sub,
                          uint64_t hi) {
     if (e & VC_ONE) return one_match(reinterpret_cast<const uint4*>(nodes)[e & ~(VC_PTR | VC_ONE)], hi);
-    return nodes[root + (e & ~VC_PTR) * 256u + sub];
+    return nodes[root + (e & ~VC_PTR) * 16u + sub];
+}
+
+// The `s` key bits after the first `bits` (s = trie_stride(bits), so they
+// never straddle a byte boundary).
+VC_HD uint32_t v4_sub(uint32_t key, int bits, int s) {
+    return (key >> (32 - bits - s)) & ((1u << s) - 1u);
 }
 
 VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
     uint32_t e = nodes[key >> (32 - rb)];
-    int shift = 32 - rb;
+    int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
-        shift -= 8;
-        e = trie_next(nodes, root, e, (key >> shift) & 255u, uint64_t(key) << 32);
+        const int s = trie_stride(bits);
+        e = trie_next(nodes, root, e, v4_sub(key, bits, s), uint64_t(key) << 32);
+        bits += s;
     }
     return e;
 }
 
-VC_HD uint32_t v6_sub(uint64_t hi, uint64_t lo, int bits) {
-    return bits < 64 ? uint32_t(hi >> (56 - bits)) & 255u : uint32_t(lo >> (120 - bits)) & 255u;
+VC_HD uint32_t v6_sub(uint64_t hi, uint64_t lo, int bits, int s) {
+    const uint64_t m = (uint64_t(1) << s) - 1u;
+    return bits < 64 ? uint32_t((hi >> (64 - bits - s)) & m) : uint32_t((lo >> (128 - bits - s)) & m);
 }
 
 VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo) {
@@ -49,8 +60,9 @@ VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo) 
     int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
-        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits), hi);
-        bits += 8;
+        const int s = trie_stride(bits);
+        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits, s), hi);
+        bits += s;
     }
     return e;
 }
