@@ -18,9 +18,12 @@ import json, sys
 line = [l for l in open("gpurun_out/ab_one.log") if l.startswith("{")][-1]
 d = json.loads(line)
 o = d["roofline"].get("other_kernel_ms", {})
-print(json.dumps({"cfg": sys.argv[1], "round": int(sys.argv[2]), "workload": d["config"]["workload"],
-                  "ms_per_step": d["ms_per_step"], "value": d["value"],
-                  "kernel_ms": d["roofline"].get("kernel_ms"), "pipe_ms": o.get("pipeline_v4_kernel"),
+sub = "config" not in d          # a sub-bench line (bench.py run_sub)
+print(json.dumps({"cfg": sys.argv[1], "round": int(sys.argv[2]),
+                  "workload": d["workload"] if sub else d["config"]["workload"],
+                  "ms_per_step": d["ms_per_step"], "value": d["M_items_per_s"] if sub else d["value"],
+                  "kernel_ms": d["kernel_ms"] if sub else d["roofline"].get("kernel_ms"),
+                  "pipe_ms": o.get("pipeline_v4_kernel"),
                   "hint_ms": o.get("hint_kernel"), "count_ms": o.get("kernel_end_to_counters_done")}))
 PY
     tail -1 $OUT

@@ -2,7 +2,9 @@
 # Route-root A/B (DESIGN.md §2 "Could a smaller route root move the ceiling?"):
 # parity at a 20-bit root first, then the C5 step and the C3 route kernels
 # with 24- vs 20-bit roots (two interleaved rounds), then TCC hits/misses per
-# pipeline launch for each.  Results: gpurun_out/ab_env.jsonl, gpurun_out/rootpmc/.
+# pipeline launch for each.  Results: gpurun_out/ab_env.jsonl, gpurun_out/rootpmc/
+# (committed as profiles/r03_ab_root.jsonl).  The VC_ROUTE_ROOT_BITS_V4/V6
+# knob it sets existed at commit 660aa3a only (compile.cpp default_root_bits).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R20="VC_ROUTE_ROOT_BITS_V4=20 VC_ROUTE_ROOT_BITS_V6=20"
 T="python -u -m pytest -x -v --timeout 240 --timeout-method thread"

@@ -2,7 +2,6 @@
 #include "compile.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -285,13 +284,10 @@ int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_u
 // ---------------------------------------------------------------------------
 // Route trie
 // ---------------------------------------------------------------------------
-int default_root_bits(int n, int family) {
-    if (n <= 4096) return 16;
-    // A/B knob while the 20-bit root is measured
-    const char* v = std::getenv(family == 0 ? "VC_ROUTE_ROOT_BITS_V4" : "VC_ROUTE_ROOT_BITS_V6");
-    if (v && (std::atoi(v) == 16 || std::atoi(v) == 20 || std::atoi(v) == 24)) return std::atoi(v);
-    return 24;
-}
+// 24 bits above 4096 rules for both families: a 20-bit root measured 2.74
+// L2 misses per C5 packet against 2.19 and a 15 % slower pipeline kernel
+// (profiles/r03_ab_root.jsonl).
+int default_root_bits(int n, int /*family*/) { return n > 4096 ? 24 : 16; }
 
 int build_trie(const vc_net* rules, int n, int family, TrieBuilt* out, int root_bits) {
     *out = TrieBuilt{};
