@@ -274,7 +274,7 @@ def kats():
                        "hints": hints, "dns": dns, "dns_wire": dns_wire,
                        "security_group": sg, "dns_datagrams": dns_datagrams(),
                        "certs": certs(), "hosts_text": hosts_text(),
-                       "source": source_kats()})
+                       "source": source_kats(), "mirror_configs": mirror_configs()})
 
 
 def source_kats():
@@ -293,6 +293,66 @@ def source_kats():
         {"source": "TestTcpLB.java:197-205 (svr1 removed)",
          "servers": [[lo, 19080, 10, True]],
          "queries": [[lo, 0, 0]]},
+    ]
+
+
+def mirror_configs():
+    """The reference's two mirror config files, verbatim (data), with
+    MirrorData items and the filter masks FilterConfig (vmirror/
+    FilterConfig.java:27-94) gives them under Mirror.mirror's level dispatch
+    (Mirror.java:85-113: no IPs -> ether check, no transport -> ip check,
+    no application protocol -> transport check, else the application
+    check), hand-derived.  doc/mirror-example.json documents the semantics
+    in its own filter list ("all entries in a filter can be omitted, which
+    means do not check the field"; port pairs are inclusive [min, max]) and
+    tells the user to remove those explanation strings, which Mirror.java
+    :536 would reject as non-objects.  misc/mirror-switch.json has one empty
+    filter for origin "switch".  Both files say "enabled": false."""
+    ex = json.load(open(os.path.join(REF, "doc/mirror-example.json")))
+    sw = json.load(open(os.path.join(REF, "misc/mirror-switch.json")))
+    Z, F = "00:00:00:00:00:00", "ff:ff:ff:ff:ff:ff"
+    O = "11:22:33:44:55:66"
+    A, B = "172.16.0.9", "172.16.3.55"
+    s = "any string"
+
+    def it(ms, md, ips, ipd, tr, ps, pd, app, want, why):
+        return {"mac_src": ms, "mac_dst": md, "ip_src": ips, "ip_dst": ipd, "transport": tr,
+                "port_src": ps, "port_dst": pd, "app": app, "want": want, "why": why}
+
+    ex_items = [
+        it(Z, F, A, B, s, 40000, 80, s, 1, "every field matches (app level)"),
+        it(F, Z, B, A, s, 80, 40000, s, 1, "the reverse direction: X/Y pairs match either way"),
+        it(Z, O, A, B, s, 40000, 80, s, 0, "mac2 is neither side"),
+        it(Z, F, A, "172.16.3.56", s, 40000, 80, s, 0, "network2 is a /32"),
+        it(Z, F, A, B, s, 40000, 81, s, 0, "port2 [80, 80] holds neither port"),
+        it(Z, F, A, B, s, 80, 80, s, 1, "both ports 80: port [1, 65535] and port2 [80, 80]"),
+        it(Z, F, A, B, s, 0, 80, s, 0, "port 0 is outside [1, 65535] on both sides"),
+        it(Z, F, A, B, "tcp", 40000, 80, s, 0, "transportLayerProtocol differs"),
+        it(Z, F, A, B, s, 40000, 80, "http", 0, "applicationLayerProtocol differs"),
+        it(Z, F, None, None, None, 0, 0, None, 1, "no IPs: the ether check only"),
+        it(Z, Z, None, None, None, 0, 0, None, 0, "ether check: ff:.. on neither side"),
+        it(Z, F, "172.16.0.200", B, None, 0, 0, None, 1, "no transport: the ip check only"),
+        it(Z, F, "172.16.1.1", B, None, 0, 0, None, 0, "172.16.1.1 is outside 172.16.0.0/24"),
+        it(Z, F, A, B, s, 5, 80, None, 1, "no application protocol: the transport check"),
+        it(Z, F, "2001:db8::1", B, None, 0, 0, None, 0, "IPv6 outside an IPv4 network"),
+        it(Z, F, "::ffff:172.16.0.9", B, None, 0, 0, None, 1,
+           "IPv4-mapped IPv6 inside 172.16.0.0/24 (Network.maskMatch, Utils.lowBitsV6V4)"),
+    ]
+    sw_items = [
+        it(Z, F, None, None, None, 0, 0, None, 1, "empty filter: every item of its origin"),
+        it(O, O, "10.0.0.1", "10.0.0.2", "udp", 1, 2, "dns", 1,
+           "empty filter: every item of its origin"),
+    ]
+    return [
+        {"source": "doc/mirror-example.json (explanation strings removed as the file says)",
+         "file": "doc/mirror-example.json", "config": ex, "strip_strings": True,
+         "enabled": False, "mirrors": [["tap0", 1500]], "n_filters": 1,
+         "cases": [{"origin": s, "items": ex_items},
+                   {"origin": "switch", "items": [dict(i, want=0) for i in ex_items[:2]]}]},
+        {"source": "misc/mirror-switch.json", "file": "misc/mirror-switch.json", "config": sw,
+         "strip_strings": False, "enabled": False, "mirrors": [["tap7", 1500]], "n_filters": 1,
+         "cases": [{"origin": "switch", "items": sw_items},
+                   {"origin": "tcp-lb", "items": [dict(i, want=0) for i in sw_items]}]},
     ]
 
 

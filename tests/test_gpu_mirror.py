@@ -106,3 +106,26 @@ def test_switch_unstaged(clf, shift, pad):
     dev = clf.mirror_switch("switch", (blob, torch.from_numpy(off.astype(np.int32)).cuda()), 0)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dev.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.parametrize("k", [0, 1])
+def test_reference_configs(clf, k):
+    """The reference's mirror config files (kats.json mirror_configs,
+    loaded by vproxy_amd.mirror.load_config) compiled for the kernel: the
+    hand-derived masks of every item, host and device entry points."""
+    import torch
+    from test_mirror_config import configs, stripped
+    from vproxy_amd.mirror import load_config
+    case = configs()[k]
+    s = load_config(stripped(case))
+    mf = clf.compile_mirror(s.filters)
+    for c in case["cases"]:
+        items = c["items"]
+        want = np.array([i["want"] for i in items], np.uint64)
+        cols = mirror_columns(items, lambda x: mf.id_of(x, create=False), V.parse_ip)
+        np.testing.assert_array_equal(clf.mirror_match(c["origin"], cols, len(items)), want,
+                                      err_msg=case["source"])
+        dcols = {key: torch.from_numpy(v).cuda() for key, v in cols.items()}
+        dev = clf.mirror_match(c["origin"], dcols, len(items))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy().view(np.uint64), want)

@@ -81,6 +81,123 @@ class MirrorFilters:
         return arr, len(filters)
 
 
+class MirrorSettings:
+    """A parsed mirror config file: `enabled`, the mirrors as (tap, mtu) in
+    list order, the origins some filter names, and the flattened filter list
+    (each filter dict carries its origin and its mirror's index) that
+    Classifier.compile_mirror takes."""
+
+    def __init__(self, enabled, mirrors, origins, filters):
+        self.enabled = enabled
+        self.mirrors = mirrors
+        self.origins = origins
+        self.filters = filters
+
+    def is_enabled(self, origin):
+        """Mirror.isEnabled (Mirror.java:66-71): nothing is mirrored while the
+        config is disabled, and only origins named in it are checked."""
+        return self.enabled and origin in self.origins
+
+
+def load_config(cfg):
+    """Mirror.parseAndLoad (base/src/main/java/vmirror/Mirror.java:345-374,
+    503-601) over a parsed JSON document: `enabled` a boolean, `mirrors` an
+    array of {"tap": string, "mtu": int in [0, 1500], "origins": [{"origin":
+    string, "filters": [object, ...]}]}.  A value of the wrong JSON type is a
+    type error, an absent field a missing field, a bad value (mtu range, a
+    port range with min > max, a mac or network that does not parse) an
+    invalid value -- all IllegalArgumentException here, naming the field
+    being handled as the Java messages do.  Filters keep their list order
+    across mirrors and origins.  The tap devices themselves are not opened
+    (no tap I/O on this path)."""
+    where = ["input"]
+
+    def bad(kind):
+        raise _lib.IllegalArgumentException("%s when handling %s" % (kind, ".".join(where)))
+
+    def get(obj, key, types, kind_missing="missing field"):
+        if not isinstance(obj, dict):
+            bad("type error")
+        if key not in obj:
+            bad(kind_missing)
+        v = obj[key]
+        # JSON true/false are not numbers (vjson getInt on a bool: a cast error)
+        if isinstance(v, bool) and bool not in types:
+            bad("type error")
+        if not isinstance(v, types):
+            bad("type error")
+        return v
+
+    where[:] = ["enabled"]
+    enabled = get(cfg, "enabled", (bool,))
+    where[:] = ["mirrors"]
+    mirrors_j = get(cfg, "mirrors", (list,))
+    mirrors, origins, filters = [], set(), []
+    for mi, m in enumerate(mirrors_j):
+        where[:] = ["mirrors[%d]" % mi]
+        if not isinstance(m, dict):
+            bad("type error")
+        where.append("tap")
+        tap = get(m, "tap", (str,))
+        where[-1] = "packetSize"                  # Mirror.java:509 names mtu so
+        mtu = get(m, "mtu", (int,))
+        if mtu < 0 or mtu > 1500:
+            bad("invalid value")
+        where[-1] = "origins"
+        for oi, o in enumerate(get(m, "origins", (list,))):
+            where[1:] = ["origins[%d]" % oi]
+            if not isinstance(o, dict):
+                bad("type error")
+            where.append("origin")
+            origin = get(o, "origin", (str,))
+            origins.add(origin)
+            where[-1] = "filters"
+            for fi, f in enumerate(get(o, "filters", (list,))):
+                where[2:] = ["filters[%d]" % fi]
+                if not isinstance(f, dict):
+                    bad("type error")
+                flt = {"origin": origin, "mirror": mi}
+                for key, kinds in (("mac", (str,)), ("network", (str,)),
+                                   ("transportLayerProtocol", (str,)), ("port", (list,)),
+                                   ("applicationLayerProtocol", (str,))):
+                    if key not in f:
+                        continue
+                    where[3:] = [key]
+                    flt[key] = get(f, key, kinds)
+                    pair = {"mac": "mac2", "network": "network2", "port": "port2"}.get(key)
+                    if pair and pair in f:    # the second value only with the first
+                        where[3:] = [pair]
+                        flt[pair] = get(f, pair, kinds)
+                for key in ("port", "port2"):
+                    if key in flt:
+                        where[3:] = [key]
+                        arr = flt[key]
+                        if len(arr) < 2:
+                            bad("invalid value")
+                        if any(isinstance(x, bool) or not isinstance(x, int) for x in arr[:2]):
+                            bad("type error")
+                        if arr[0] > arr[1]:
+                            bad("invalid value")
+                        flt[key] = [arr[0], arr[1]]
+                try:
+                    for key in ("mac", "mac2"):
+                        if key in flt:
+                            where[3:] = [key]
+                            parse_mac(flt[key])
+                    for key in ("network", "network2"):
+                        if key in flt:
+                            where[3:] = [key]
+                            from .classifier import Network
+                            Network(flt[key])
+                except _lib.IllegalArgumentException:
+                    bad("invalid value")
+                del where[3:]
+                filters.append(flt)
+            del where[2:]
+        mirrors.append((tap, mtu))
+    return MirrorSettings(enabled, mirrors, origins, filters)
+
+
 def _ptr(a):
     if a is None:
         return None
