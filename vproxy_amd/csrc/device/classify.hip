@@ -5,6 +5,7 @@
 // port loads, 16-byte index stores); the ACL interval boundaries are staged
 // in LDS once per workgroup of a grid-stride (persistent-style) launch.
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -1069,7 +1070,20 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
                (!p.out_allow || aligned(p.out_allow, 4));
     if (mix) vec = vec && aligned(p.family, 4);
     int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
-    const int grid = int(want < c.num_cus ? (want < 1 ? 1 : want) : c.num_cus);
+    // Workgroups (one per CU): the IPv4 kernel takes 7/8 of the CUs (28 of each
+    // XCD's 32).  Its rate is set by the chip's random-gather cap, which 224
+    // CUs reach as well as 256 (4.78 vs 4.83 ms alone), and the CUs left over
+    // run the counter finish of the previous batch beside it instead of
+    // squeezing in between its workgroups: C5 6.12-6.14 ms/step against
+    // 6.19-6.24 with all 256 (profiles/r03_ab_pipe_grid.jsonl).  VC_PIPE_GRID
+    // overrides the count (A/B runs).
+    static const int grid_cap = [] {
+        const char* g = std::getenv("VC_PIPE_GRID");
+        return g ? std::atoi(g) : 0;
+    }();
+    const int cus = grid_cap > 0 ? std::min(grid_cap, c.num_cus)
+                  : (!mix && c.num_cus >= 64 ? (c.num_cus * 7 / 8) & ~7 : c.num_cus);
+    const int grid = int(want < cus ? (want < 1 ? 1 : want) : cus);
     // In-kernel counting where it fits the workgroup's LDS; the rest is
     // counted by separate passes over the outputs afterwards.
     size_t shmem = size_t(words) * 4;
