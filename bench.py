@@ -517,6 +517,41 @@ def gather_ceiling(table_mb=64):
         return None
 
 
+def fabric_ceiling():
+    """Measured L2-to-fabric request rate of the two-gather probe over 64 MB
+    tables (the pipeline's access pattern): the requests of that launch
+    counted by the PMC method of scripts/pmc_traffic.py (FETCH_SIZE / 64 B +
+    WRITE_SIZE / 64 B, profiles/r03_fetch_calibration.json launch 2) over its
+    time (profiles/r01_gather_probe.csv: 64 MB, 2 gathers, 4 items per lane,
+    4 workgroups per CU), in G requests/s."""
+    import csv
+    try:
+        with open(os.path.join(PROFILES, "r03_fetch_calibration.json")) as f:
+            cal = json.load(f)
+        l = [x for x in cal["launches"] if x["table_bytes"] == 64 << 20 and
+             x["gathers_per_item"] == 2][0]
+        req = (l["fetch_bytes"] + l["write_bytes"]) / 64
+        with open(os.path.join(PROFILES, "r01_gather_probe.csv")) as f:
+            ms = [float(r["ms"]) for r in csv.DictReader(f) if int(r["table_MB"]) == 64 and
+                  int(r["gathers_per_item"]) == 2 and int(r["items_per_lane"]) == 4 and
+                  int(r["blocks_per_cu"]) == 4][0]
+        return req / (ms * 1e-3) / 1e9
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
+def load_step_requests(workload):
+    """L2-to-fabric requests of one whole step (profiles/pmc_traffic.json
+    `step`, scripts/pmc_traffic.py --per-step) and the commit they were
+    taken at."""
+    try:
+        with open(os.path.join(PROFILES, "pmc_traffic.json")) as f:
+            d = json.load(f)[workload]
+        return d["step"]["requests"], d.get("commit")
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def load_traffic(workload, kernel):
     """Per-launch HBM-side bytes of `kernel` from the committed PMC passes
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
@@ -653,6 +688,22 @@ def main():
                     "frac": round(g_rate / ceil, 4) if ceil else None,
                     "ceiling_source": "tools/gather_probe.hip -> profiles/r01_gather_probe.csv"}
     traffic, t_commit = load_traffic("c5", dom)
+    step_req, r_commit = load_step_requests("c5")
+    fab_ceil = fabric_ceiling()
+    step_ms = elapsed / args.steps * 1e3
+    fabric = None
+    if step_req:
+        fabric = {"requests_per_step": round(step_req),
+                  "achieved_G_requests_per_s": round(step_req / (step_ms / 1e3) / 1e9, 2),
+                  "ceiling_G_requests_per_s": round(fab_ceil, 2) if fab_ceil else None,
+                  "frac": round(step_req / (step_ms / 1e3) / 1e9 / fab_ceil, 4)
+                  if fab_ceil else None,
+                  "what": "every kernel of one step (pipeline, pool pass, counter finish): L2 "
+                          "read + write requests to the fabric (FETCH_SIZE / 64 B + "
+                          "WRITE_SIZE / 64 B per launch, rocprofv3 --pmc at commit %s) over "
+                          "this run's ms_per_step, against the rate the two-gather probe over "
+                          "64 MB tables reaches (tools/gather_probe.hip; the cap sits past the "
+                          "CUs, tools/gather_paths.hip)" % r_commit}
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE + the "
@@ -661,6 +712,7 @@ def main():
                               "counted whole (profiles/r03_fetch_calibration.json)" % t_commit,
             "kernel": dom, "kernel_ms": round(ms, 4), "algorithmic_bytes": unit_desc,
             "gather_bound": gather_bound,
+            "fabric_bound": fabric,
             "other_kernel_ms": {"hint_kernel": round(hint_ms, 4),
                                 "pipeline_v4_kernel": round(pipe_ms, 4),
                                 "kernel_end_to_counters_done": round(count_ms, 4),

@@ -70,6 +70,11 @@ def main():
     ap.add_argument("--commit", default=None, help="git commit the passes were taken at")
     ap.add_argument("--stream", action="append", default=[],
                     help="KERNEL=BYTES: wide streamed read bytes per launch (see module doc)")
+    ap.add_argument("--per-step", action="append", default=[],
+                    help="KERNEL=COUNT: launches of KERNEL in one bench step; with it the "
+                         "entry gets `step`: the L2-to-fabric requests of one whole step "
+                         "(FETCH_SIZE / 64 B = TCC_EA0_RDREQ, WRITE_SIZE / 64 B = write "
+                         "requests), the quantity tools/gather_paths.hip finds capped")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     stats = _find(a.stats, "*kernel_stats.csv")
@@ -105,6 +110,18 @@ def main():
                   "traffic_GBps": traffic / ns if ns else None}
         if k in l2:
             out[k]["tcc_hit"], out[k]["tcc_miss"] = l2[k]
+    step = None
+    if a.per_step:
+        kinds = {}
+        for kv in a.per_step:
+            k, cnt = kv.split("=")
+            if k in fetch and k in write:
+                req = (fetch[k][1] * 1024 + write[k][1] * 1024) / 64
+                kinds[k] = {"launches": int(cnt), "requests_per_launch": req}
+        step = {"requests": sum(v["launches"] * v["requests_per_launch"] for v in kinds.values()),
+                "kernels": kinds,
+                "method": "per launch FETCH_SIZE / 64 B (read requests, a wide stream's 128-B "
+                          "request counted once) + WRITE_SIZE / 64 B, times launches per step"}
     path = os.path.join(prof, "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -114,6 +131,8 @@ def main():
     allw[a.workload] = {"tag": a.tag, "commit": a.commit, "kernels": out,
                         "note": "per launch; FETCH_SIZE/WRITE_SIZE KiB x 1024; traffic_method "
                                 "per kernel"}
+    if step:
+        allw[a.workload]["step"] = step
     with open(path, "w") as f:
         json.dump(allw, f, indent=1)
     for src, name in ((a.fetch, "fetch"), (a.write, "write")):
