@@ -236,9 +236,15 @@ def hip_stream(dev, cus=None):
 
 
 def cu_split(total, k):
-    """k CU ids spread evenly over [0, total), and the rest."""
-    pick = sorted({int(i * total / k) for i in range(k)}) if k > 0 else []
-    rest = [c for c in range(total) if c not in set(pick)]
+    """k CU-mask bits for one stream and the rest for the other, both with
+    the same number of CUs on every XCD.  Mask bit i selects a CU of XCD
+    i mod 8 (interleaved), and workgroups are dealt to the XCDs round-robin,
+    so a mask must give every XCD the same count -- a multiple of 4 -- or a
+    share of the workgroups runs a second round (profiles/r03_cu_scaling.jsonl:
+    an even spread of ids, every 256/k-th bit, leaves XCDs empty).  The top k
+    bits give k/8 CUs per XCD."""
+    pick = list(range(total - k, total)) if k > 0 else []
+    rest = list(range(total - k))
     return pick, rest
 
 

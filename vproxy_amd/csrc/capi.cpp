@@ -346,6 +346,7 @@ struct vc_ctx {
         vc::LaunchCfg c;
         c.stream = static_cast<hipStream_t>(s);
         c.num_cus = stream_cus(c.stream);
+        c.cu_masked = c.num_cus < num_cus;
         c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
         c.scratch = const_cast<vc::ScratchRing*>(&scratch);
         c.tickets = const_cast<vc::TicketRing*>(&tickets);

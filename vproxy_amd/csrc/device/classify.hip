@@ -1070,8 +1070,8 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
                (!p.out_allow || aligned(p.out_allow, 4));
     if (mix) vec = vec && aligned(p.family, 4);
     int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
-    // Workgroups (one per CU): the IPv4 kernel takes 7/8 of the CUs (28 of each
-    // XCD's 32).  Its rate is set by the chip's random-gather cap, which 224
+    // Workgroups (one per CU): on an unmasked stream the IPv4 kernel takes 7/8
+    // of the CUs (28 of each XCD's 32); a CU-masked stream's share is all its own.  Its rate is set by the chip's random-gather cap, which 224
     // CUs reach as well as 256 (4.78 vs 4.83 ms alone), and the CUs left over
     // run the counter finish of the previous batch beside it instead of
     // squeezing in between its workgroups: C5 6.12-6.14 ms/step against
@@ -1082,7 +1082,8 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
         return g ? std::atoi(g) : 0;
     }();
     const int cus = grid_cap > 0 ? std::min(grid_cap, c.num_cus)
-                  : (!mix && c.num_cus >= 64 ? (c.num_cus * 7 / 8) & ~7 : c.num_cus);
+                  : (!mix && !c.cu_masked && c.num_cus >= 64 ? (c.num_cus * 7 / 8) & ~7
+                                                                : c.num_cus);
     const int grid = int(want < cus ? (want < 1 ? 1 : want) : cus);
     // In-kernel counting where it fits the workgroup's LDS; the rest is
     // counted by separate passes over the outputs afterwards.

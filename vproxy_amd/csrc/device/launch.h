@@ -102,7 +102,8 @@ private:
 };
 
 struct LaunchCfg {
-    int num_cus = 256;        // hipDeviceProp_t.multiProcessorCount
+    int num_cus = 256;        // CUs the stream may use (its CU mask, else all)
+    bool cu_masked = false;   // the stream has a CU mask narrower than the device
     hipStream_t stream = nullptr;
     Handoff handoff;
     ScratchRing* scratch = nullptr;   // counter-pass scratch (required by the launchers)
