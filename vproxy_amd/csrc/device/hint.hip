@@ -36,16 +36,35 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #endif
 
 
-// The 64-item chunks of a launch, in wave-uniform order: taken kPerTicket
-// at a time from the launch's ticket counter (launch.h TicketRing) or,
-// without one, the static grid-stride sequence.  One ticket per 1024 items
-// keeps the counter's same-address atomics (served one at a time at the
-// memory side) far below the kernel's rate: one ticket per 64-name chunk
-// made the hint pass 3.6x slower.  Every wave takes exactly one
-// out-of-range ticket (its last), so the wave holding ticket
-// ntickets + nwaves - 1 is the last taker of the launch and resets the
-// counter for the slot's next launch.
-constexpr int64_t kPerTicket = 16;
+// The 64-item chunks of a launch, in wave-uniform order: taken a ticket at
+// a time from the launch's ticket counter (launch.h TicketRing) or, without
+// one, the static grid-stride sequence.  A ticket is a run of chunks: the
+// first tickets cover kPerTicket chunks (1024 items), which keeps the
+// counter's same-address atomics (served one at a time at the memory side)
+// far below the kernel's rate -- one ticket per 64-name chunk made the hint
+// pass 3.6x slower, four per ticket 17 % slower, 64 per ticket 39 % slower
+// (too few tickets per wave); the last chunks, kTailRounds small tickets per
+// wave, go kTailChunks at a time, so the launch does not end one whole big
+// ticket after most waves ran out of work (a C4 pool pass is only ~2.3 big
+// tickets per wave).  Tails of 4-chunk tickets, two per wave: C4 0.813 ->
+// 0.803 ms, DNS 1.10 -> 1.06, the C5 step 6.13 -> 6.03-6.06 ms; 1- and
+// 2-chunk tails lose to their extra atomics, 8-chunk ones end too coarsely
+// (profiles/r03_ab_ticket.txt).
+// Every wave takes exactly one out-of-range ticket (its last), so the wave
+// holding ticket ntickets + nwaves - 1 is the last taker of the launch and
+// resets the counter for the slot's next launch.
+#ifndef VC_TICKET_CHUNKS
+#define VC_TICKET_CHUNKS 16
+#endif
+#ifndef VC_TICKET_TAIL
+#define VC_TICKET_TAIL 4
+#endif
+constexpr int64_t kPerTicket = VC_TICKET_CHUNKS;
+constexpr int64_t kTailChunks = VC_TICKET_TAIL;     // 0: big tickets to the end
+#ifndef VC_TICKET_TAIL_ROUNDS
+#define VC_TICKET_TAIL_ROUNDS 2
+#endif
+constexpr int64_t kTailRounds = VC_TICKET_TAIL_ROUNDS;
 
 #if defined(VC_HINT_PROF)
 // Profiling build: phase cycles summed over the waves of every launch
@@ -72,32 +91,54 @@ constexpr size_t kProfLds = 0;
 #define VC_PEND() ((void)0)
 #endif
 
+// Ticket t -> its chunk run: big tickets [B t, B t + B) up to chunk head,
+// then tail tickets of kTailChunks.  `end` is the end of the wave's current
+// run (wave-uniform).
 struct Chunks {
     uint32_t* ticket;
     int64_t nchunks;
-    __device__ int64_t take() const {
+    int64_t head = 0;              // chunks covered by big tickets
+    int64_t nbig = 0;              // big tickets
+    int64_t ntickets = 0;
+    int64_t end = 0;
+    __device__ Chunks(uint32_t* t, int64_t nc) : ticket(t), nchunks(nc) {
+        const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
+        const int64_t tail = kTailChunks ? nwaves * kTailChunks * kTailRounds : 0;
+        head = nc > tail ? (nc - tail) / kPerTicket * kPerTicket : 0;
+        if (!kTailChunks) head = nc;
+        nbig = (head + kPerTicket - 1) / kPerTicket;
+        ntickets = nbig + (kTailChunks ? (nc - head + kTailChunks - 1) / kTailChunks : 0);
+    }
+    __device__ int64_t take() {
         uint32_t t = 0;
         if ((threadIdx.x & 63) == 0) {
             t = atomicAdd(ticket, 1u);
             const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-            const uint32_t ntickets = uint32_t((nchunks + kPerTicket - 1) / kPerTicket);
             // a slot left nonzero by an aborted launch (launch.h TicketRing)
-            VC_CHECK(t <= ntickets + nwaves - 1, 304, t, ntickets + nwaves);
-            if (t == ntickets + nwaves - 1) atomicExch(ticket, 0u);
+            VC_CHECK(t <= uint32_t(ntickets) + nwaves - 1, 304, t, uint32_t(ntickets) + nwaves);
+            if (t == uint32_t(ntickets) + nwaves - 1) atomicExch(ticket, 0u);
         }
-        return int64_t(__shfl(t, 0, 64)) * kPerTicket;
+        const int64_t tk = int64_t(__shfl(t, 0, 64));
+        int64_t start;
+        if (tk < nbig) {
+            start = tk * kPerTicket;
+            end = start + kPerTicket < head ? start + kPerTicket : head;
+        } else {
+            start = head + (tk - nbig) * (kTailChunks ? kTailChunks : 1);
+            end = start + kTailChunks;
+        }
+        if (end > nchunks) end = nchunks;
+        return start < nchunks ? start : nchunks;
     }
-    __device__ int64_t first(int w) const {
+    __device__ int64_t first(int w) {
         return ticket ? take() : int64_t(blockIdx.x) * kWaves + w;
     }
-    __device__ int64_t next(int64_t c) const {
+    __device__ int64_t next(int64_t c) {
         if (!ticket) return c + int64_t(gridDim.x) * kWaves;
-        return (c + 1) % kPerTicket != 0 && c + 1 < nchunks ? c + 1 : take();
+        return c + 1 < end ? c + 1 : take();
     }
     // c + 1 is this wave's next chunk (same ticket)
-    __device__ bool paired(int64_t c) const {
-        return ticket && (c + 1) % kPerTicket != 0 && c + 1 < nchunks;
-    }
+    __device__ bool paired(int64_t c) const { return ticket && c + 1 < end; }
 };
 
 // The chunk loop of the string kernels.  A wave stages its chunk's items
@@ -111,7 +152,7 @@ struct Chunks {
 // body -- the hint kernel, where live offsets spill (all four up front:
 // 0.81 -> 0.92 ms; the first chunk's only, kPre 1: 0.83 ms).
 template <uint32_t kBytes, bool kPair, int kPre, class Body>
-__device__ __forceinline__ void chunk_loop(const Chunks& ch, int w, const uint8_t* blob,
+__device__ __forceinline__ void chunk_loop(Chunks& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
     const int lane = int(threadIdx.x & 63);
@@ -172,7 +213,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const Chunks ch{ticket, (n + 63) / 64};
+    Chunks ch(ticket, (n + 63) / 64);
     const bool general = uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
@@ -216,7 +257,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     int32_t* __restrict__ value, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const Chunks ch{ticket, (n + 63) / 64};
+    Chunks ch(ticket, (n + 63) / 64);
     HintImage slow_img = img;
     VC_PBEGIN();
     // one chunk per stage: staging two (chunk_loop) adds live registers
@@ -253,7 +294,7 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const Chunks ch{ticket, (n + 63) / 64};
+    Chunks ch(ticket, (n + 63) / 64);
     VC_PBEGIN();
     chunk_loop<kStageBytes, true, 2>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
                                   [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
