@@ -53,6 +53,10 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 // Every wave takes exactly one out-of-range ticket (its last), so the wave
 // holding ticket ntickets + nwaves - 1 is the last taker of the launch and
 // resets the counter for the slot's next launch.
+// VC_DNSD_TICKETS: dnsd_kernel takes its chunks from the work tickets
+#ifndef VC_DNSD_TICKETS
+#define VC_DNSD_TICKETS 1
+#endif
 #ifndef VC_TICKET_CHUNKS
 #define VC_TICKET_CHUNKS 16
 #endif
@@ -131,10 +135,10 @@ struct Chunks {
         return start < nchunks ? start : nchunks;
     }
     __device__ int64_t first(int w) {
-        return ticket ? take() : int64_t(blockIdx.x) * kWaves + w;
+        return ticket ? take() : int64_t(blockIdx.x) * (blockDim.x / 64) + w;
     }
     __device__ int64_t next(int64_t c) {
-        if (!ticket) return c + int64_t(gridDim.x) * kWaves;
+        if (!ticket) return c + int64_t(gridDim.x) * (blockDim.x / 64);
         return c + 1 < end ? c + 1 : take();
     }
     // c + 1 is this wave's next chunk (same ticket)
@@ -580,20 +584,25 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
 template <bool kStage>
 __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
-    const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out) {
+    const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out,
+    uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kDnsdWaves : 1][kStage ? kDnsdStageWords : 1];
     __shared__ uint32_t names[kDnsdBlock][kNameWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     HintImage slow_img = img;
-    const int64_t wstride = int64_t(gridDim.x) * kDnsdWaves * 64;
-    int64_t base = (int64_t(blockIdx.x) * kDnsdWaves + w) * 64;
-    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
-    for (; base < n; base += wstride) {
+    // 64-datagram chunks from the work tickets (Chunks), or the static
+    // grid-stride sequence without them
+    Chunks ch(ticket, (n + 63) / 64);
+    int64_t c = ch.first(w);
+    LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
+    while (c < ch.nchunks) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         uint32_t o0, o1, a0 = 0;
         span_of(cur, base, n, &o0, &o1);
         const uint32_t a = cur.a, e = cur.e;
-        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const int64_t nx = ch.next(c);
+        if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kDnsdStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
             if (staged)
@@ -605,6 +614,7 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
                               names[threadIdx.x]);
         }
         if (kStage) wave_done();
+        c = nx;
     }
 }
 
@@ -690,12 +700,13 @@ hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
     const int grid = resident_grid(c, k, vcd::kDnsdBlock, 0, want);
     const vcd::DnsdIn in{rfam, r4, r6, rport};
     const vcd::DnsdOut o{status, out_acl, nq, qtype, kind, value};
+    uint32_t* tk = VC_DNSD_TICKETS && c.tickets ? c.tickets->next(c.stream) : nullptr;
     if (stage)
         hipLaunchKernelGGL(vcd::dnsd_kernel<true>, dim3(grid), dim3(vcd::kDnsdBlock), 0, c.stream,
-                           hosts, hints, acl, blob, off, n, in, o);
+                           hosts, hints, acl, blob, off, n, in, o, tk);
     else
         hipLaunchKernelGGL(vcd::dnsd_kernel<false>, dim3(grid), dim3(vcd::kDnsdBlock), 0,
-                           c.stream, hosts, hints, acl, blob, off, n, in, o);
+                           c.stream, hosts, hints, acl, blob, off, n, in, o, tk);
     return hipGetLastError();
 }
 
