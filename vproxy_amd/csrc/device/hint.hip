@@ -13,6 +13,7 @@
 #include "acl_dev.h"
 #include "hint_dev.h"
 #include "launch.h"
+#include "chunks.h"
 #include "stage.h"
 
 namespace vcd {
@@ -35,40 +36,6 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_DNS_MINW 6
 #endif
 
-
-// The 64-item chunks of a launch, in wave-uniform order: taken a ticket at
-// a time from the launch's ticket counter (launch.h TicketRing) or, without
-// one, the static grid-stride sequence.  A ticket is a run of chunks: the
-// first tickets cover kPerTicket chunks (1024 items), which keeps the
-// counter's same-address atomics (served one at a time at the memory side)
-// far below the kernel's rate -- one ticket per 64-name chunk made the hint
-// pass 3.6x slower, four per ticket 17 % slower, 64 per ticket 39 % slower
-// (too few tickets per wave); the last chunks, kTailRounds small tickets per
-// wave, go kTailChunks at a time, so the launch does not end one whole big
-// ticket after most waves ran out of work (a C4 pool pass is only ~2.3 big
-// tickets per wave).  Tails of 4-chunk tickets, two per wave: C4 0.813 ->
-// 0.803 ms, DNS 1.10 -> 1.06, the C5 step 6.13 -> 6.03-6.06 ms; 1- and
-// 2-chunk tails lose to their extra atomics, 8-chunk ones end too coarsely
-// (profiles/r03_ab_ticket.txt).
-// Every wave takes exactly one out-of-range ticket (its last), so the wave
-// holding ticket ntickets + nwaves - 1 is the last taker of the launch and
-// resets the counter for the slot's next launch.
-// VC_DNSD_TICKETS: dnsd_kernel takes its chunks from the work tickets
-#ifndef VC_DNSD_TICKETS
-#define VC_DNSD_TICKETS 1
-#endif
-#ifndef VC_TICKET_CHUNKS
-#define VC_TICKET_CHUNKS 16
-#endif
-#ifndef VC_TICKET_TAIL
-#define VC_TICKET_TAIL 4
-#endif
-constexpr int64_t kPerTicket = VC_TICKET_CHUNKS;
-constexpr int64_t kTailChunks = VC_TICKET_TAIL;     // 0: big tickets to the end
-#ifndef VC_TICKET_TAIL_ROUNDS
-#define VC_TICKET_TAIL_ROUNDS 2
-#endif
-constexpr int64_t kTailRounds = VC_TICKET_TAIL_ROUNDS;
 
 #if defined(VC_HINT_PROF)
 // Profiling build: phase cycles summed over the waves of every launch
@@ -94,56 +61,6 @@ constexpr size_t kProfLds = 0;
 #define VC_PBEGIN() ((void)0)
 #define VC_PEND() ((void)0)
 #endif
-
-// Ticket t -> its chunk run: big tickets [B t, B t + B) up to chunk head,
-// then tail tickets of kTailChunks.  `end` is the end of the wave's current
-// run (wave-uniform).
-struct Chunks {
-    uint32_t* ticket;
-    int64_t nchunks;
-    int64_t head = 0;              // chunks covered by big tickets
-    int64_t nbig = 0;              // big tickets
-    int64_t ntickets = 0;
-    int64_t end = 0;
-    __device__ Chunks(uint32_t* t, int64_t nc) : ticket(t), nchunks(nc) {
-        const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-        const int64_t tail = kTailChunks ? nwaves * kTailChunks * kTailRounds : 0;
-        head = nc > tail ? (nc - tail) / kPerTicket * kPerTicket : 0;
-        if (!kTailChunks) head = nc;
-        nbig = (head + kPerTicket - 1) / kPerTicket;
-        ntickets = nbig + (kTailChunks ? (nc - head + kTailChunks - 1) / kTailChunks : 0);
-    }
-    __device__ int64_t take() {
-        uint32_t t = 0;
-        if ((threadIdx.x & 63) == 0) {
-            t = atomicAdd(ticket, 1u);
-            const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-            // a slot left nonzero by an aborted launch (launch.h TicketRing)
-            VC_CHECK(t <= uint32_t(ntickets) + nwaves - 1, 304, t, uint32_t(ntickets) + nwaves);
-            if (t == uint32_t(ntickets) + nwaves - 1) atomicExch(ticket, 0u);
-        }
-        const int64_t tk = int64_t(__shfl(t, 0, 64));
-        int64_t start;
-        if (tk < nbig) {
-            start = tk * kPerTicket;
-            end = start + kPerTicket < head ? start + kPerTicket : head;
-        } else {
-            start = head + (tk - nbig) * (kTailChunks ? kTailChunks : 1);
-            end = start + kTailChunks;
-        }
-        if (end > nchunks) end = nchunks;
-        return start < nchunks ? start : nchunks;
-    }
-    __device__ int64_t first(int w) {
-        return ticket ? take() : int64_t(blockIdx.x) * (blockDim.x / 64) + w;
-    }
-    __device__ int64_t next(int64_t c) {
-        if (!ticket) return c + int64_t(gridDim.x) * (blockDim.x / 64);
-        return c + 1 < end ? c + 1 : take();
-    }
-    // c + 1 is this wave's next chunk (same ticket)
-    __device__ bool paired(int64_t c) const { return ticket && c + 1 < end; }
-};
 
 // The chunk loop of the string kernels.  A wave stages its chunk's items
 // (contiguous in the blob) into LDS with one coalesced copy; when the next

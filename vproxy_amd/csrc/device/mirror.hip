@@ -6,6 +6,7 @@
 // are scalar and the compares take SGPR operands.
 #include "launch.h"
 #include "mirror_dev.h"
+#include "chunks.h"
 #include "stage.h"
 
 namespace vcd {
@@ -29,19 +30,22 @@ constexpr uint32_t kMirrorStageWords = (kMirrorStage + 2 * kApron) / 4;
 template <bool kStage>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     MirrorImage img, int32_t origin, const uint8_t* __restrict__ blob,
-    const uint32_t* __restrict__ off, int64_t n, int layer, uint64_t* __restrict__ out) {
+    const uint32_t* __restrict__ off, int64_t n, int layer, uint64_t* __restrict__ out,
+    uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kMirrorWaves : 1][kStage ? kMirrorStageWords : 1];
     const MirrorImage& fi = img;
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kMirrorWaves * 64;
-    int64_t base = (int64_t(blockIdx.x) * kMirrorWaves + w) * 64;
-    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
-    for (; base < n; base += wstride) {
+    Chunks ch(ticket, (n + 63) / 64);              // chunks.h: work tickets or static
+    int64_t c = ch.first(w);
+    LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
+    while (c < ch.nchunks) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         uint32_t o0, o1, a0 = 0;
         span_of(cur, base, n, &o0, &o1);
         const uint32_t a = cur.a, e = cur.e;
-        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const int64_t nx = ch.next(c);
+        if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kMirrorStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
             uint64_t m;
@@ -54,6 +58,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
             out[i] = m;
         }
         if (kStage) wave_done();
+        c = nx;
     }
 }
 
@@ -85,12 +90,12 @@ hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int3
         hipLaunchKernelGGL(vcd::mirror_switch_kernel<true>,
                            dim3(mirror_grid(c, vcd::mirror_switch_kernel<true>, n)),
                            dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
-                           out);
+                           out, launch_ticket(c));
     else
         hipLaunchKernelGGL(vcd::mirror_switch_kernel<false>,
                            dim3(mirror_grid(c, vcd::mirror_switch_kernel<false>, n)),
                            dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
-                           out);
+                           out, launch_ticket(c));
     return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@
 #include "launch.h"
 #include "packet_dev.h"
 #include "route_dev.h"
+#include "chunks.h"
 #include "stage.h"
 
 namespace vcd {
@@ -50,18 +51,20 @@ __device__ __forceinline__ void store_pkt(const vc_pkt_out& out, int64_t i, cons
 template <bool kStage>
 __global__ __launch_bounds__(kPktBlock) void packet_kernel(
     const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n, int layer,
-    vc_pkt_out out) {
+    vc_pkt_out out, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
-    int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64;
-    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
-    for (; base < n; base += wstride) {
+    Chunks ch(ticket, (n + 63) / 64);              // chunks.h: work tickets or static
+    int64_t c = ch.first(w);
+    LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
+    while (c < ch.nchunks) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         uint32_t o0, o1, a0 = 0;
         span_of(cur, base, n, &o0, &o1);
         const uint32_t a = cur.a, e = cur.e;
-        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const int64_t nx = ch.next(c);
+        if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kPktStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
             PktOut o;
@@ -74,6 +77,7 @@ __global__ __launch_bounds__(kPktBlock) void packet_kernel(
             store_pkt(out, i, o);
         }
         if (kStage) wave_done();
+        c = nx;
     }
 }
 
@@ -160,18 +164,21 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
 template <bool kStage>
 __global__ __launch_bounds__(kPktBlock) void switch_kernel(
     const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n, int layer,
-    vc_pkt_out out, AclImage acl, RouteImage rt, VniImage vt, SwitchIn in, SwitchOut so) {
+    vc_pkt_out out, AclImage acl, RouteImage rt, VniImage vt, SwitchIn in, SwitchOut so,
+    uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    const int64_t wstride = int64_t(gridDim.x) * kPktWaves * 64;
-    int64_t base = (int64_t(blockIdx.x) * kPktWaves + w) * 64;
-    LaneSpan cur = base < n ? lane_span(off, base, n) : LaneSpan{0, 0};
-    for (; base < n; base += wstride) {
+    Chunks ch(ticket, (n + 63) / 64);              // chunks.h: work tickets or static
+    int64_t c = ch.first(w);
+    LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
+    while (c < ch.nchunks) {
+        const int64_t base = c * 64;
         const int64_t i = base + lane;
         uint32_t o0, o1, a0 = 0;
         span_of(cur, base, n, &o0, &o1);
         const uint32_t a = cur.a, e = cur.e;
-        if (base + wstride < n) cur = lane_span(off, base + wstride, n);   // next chunk's
+        const int64_t nx = ch.next(c);
+        if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kPktStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
             PktOut o;
@@ -185,6 +192,7 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
             switch_one(acl, rt, vt, in, i, o, so);
         }
         if (kStage) wave_done();
+        c = nx;
     }
 }
 
@@ -192,6 +200,10 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
 
 namespace vc {
 
+// The parse and switch kernels keep the static grid-stride split (a null
+// ticket): their per-frame cost is even, and work tickets made them 3-5 %
+// slower, while the mirror kernel, whose cost varies with the filters a frame
+// reaches, gained 16 % from them (profiles/r03_ab_frame_tickets.txt).
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
                          const VniImage& vt, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
@@ -207,10 +219,11 @@ hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteIma
     const vcd::SwitchOut so{out_acl, out_allow, out_route};
     if (stage)
         hipLaunchKernelGGL(vcd::switch_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
-                           blob, off, n, layer, out, acl, rt, vt, in, so);
+                           blob, off, n, layer, out, acl, rt, vt, in, so, nullptr);
     else
         hipLaunchKernelGGL(vcd::switch_kernel<false>, dim3(grid), dim3(vcd::kPktBlock), 0,
-                           c.stream, blob, off, n, layer, out, acl, rt, vt, in, so);
+                           c.stream, blob, off, n, layer, out, acl, rt, vt, in, so,
+                           nullptr);
     return hipGetLastError();
 }
 
@@ -224,10 +237,10 @@ hipError_t launch_packets(const LaunchCfg& c, const uint8_t* blob, const uint32_
     const int grid = resident_grid(c, k, vcd::kPktBlock, 0, want);
     if (stage)
         hipLaunchKernelGGL(vcd::packet_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
-                           blob, off, n, layer, out);
+                           blob, off, n, layer, out, nullptr);
     else
         hipLaunchKernelGGL(vcd::packet_kernel<false>, dim3(grid), dim3(vcd::kPktBlock), 0,
-                           c.stream, blob, off, n, layer, out);
+                           c.stream, blob, off, n, layer, out, nullptr);
     return hipGetLastError();
 }
 
