@@ -59,6 +59,77 @@ __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint
     return acl_value(a.rec[l], a.pieces[l], j, port);
 }
 
+// Four lookups in lockstep (VC_ACL_LOCKSTEP, boundaries fully staged in
+// LDS): acl_v4_one runs each interval search as its own loop, so the four
+// searches of a lane wait on their ds_reads one after another (~14 waits
+// each).  Here one loop steps all four: its trip count is that of the longer
+// list, and a search whose range is down to one interval keeps reading the
+// same boundary (half = 0 leaves lo as it is), so no step needs a bound
+// check; the four record loads then go out together.
+#ifndef VC_ACL_LOCKSTEP
+#define VC_ACL_LOCKSTEP 1
+#endif
+template <bool kL>
+__device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[4],
+                                            const uint32_t key[4], const uint32_t port[4],
+                                            uint32_t v[4]) {
+    if (!VC_ACL_LOCKSTEP || !kL || a.shift) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = acl_v4_one<kL>(a, tcp[k], key[k], port[k]);
+        return;
+    }
+    const int nmax = a.nf[0] > a.nf[1] ? a.nf[0] : a.nf[1];
+    const int steps = nmax > 1 ? 32 - __builtin_clz(uint32_t(nmax - 1)) : 0;
+    // 32-bit LDS pointers, cast once (a generic-to-LDS cast per access
+    // costs a null check and 64-bit address arithmetic)
+    const VC_AS_LDS uint32_t* f0 = (const VC_AS_LDS uint32_t*)a.f[0];
+    const VC_AS_LDS uint32_t* f1 = (const VC_AS_LDS uint32_t*)a.f[1];
+    const VC_AS_LDS uint32_t* f[4];
+    int lo[4], len[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f[k] = tcp[k] ? f0 : f1;
+        len[k] = tcp[k] ? a.nf[0] : a.nf[1];
+        lo[k] = 0;
+    }
+    for (int s = 0; s < steps; ++s) {
+        uint32_t x[4];
+        int half[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            half[k] = len[k] >> 1;
+            x[k] = f[k][lo[k] + half[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            lo[k] = x[k] <= key[k] ? lo[k] + half[k] : lo[k];
+            len[k] -= half[k];
+        }
+    }
+    uint4 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r[k] = glb_ld(reinterpret_cast<const uint4*>(tcp[k] ? a.rec[0] : a.rec[1]) + lo[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        v[k] = acl_rec_value(r[k], tcp[k] ? a.pieces[0] : a.pieces[1], port[k]);
+}
+
+// The IPv4 pipeline's ACL: four separate searches (VC_PIPE_LOCKSTEP 0).  The
+// lockstep form that takes C2 from 0.82 to 0.70 ms made the gather-bound
+// pipeline kernel 0.5-0.7 % slower (profiles/r03_ab_acl_lockstep.txt).
+#ifndef VC_PIPE_LOCKSTEP
+#define VC_PIPE_LOCKSTEP 0
+#endif
+#if VC_PIPE_LOCKSTEP
+#define VC_PIPE_ACL4(a, tcp, key, po, v) acl_v4_four<kLds>(a, tcp, key, po, v)
+#else
+#define VC_PIPE_ACL4(a, tcp, key, po, v)                                              \
+    do {                                                                             \
+        for (int k_ = 0; k_ < 4; ++k_) v[k_] = acl_v4_one<kLds>(a, tcp[k_], key[k_], po[k_]); \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void acl_emit(const AclImage& img, bool tcp, uint32_t v,
                                          uint8_t* allow_out, int32_t* idx_out) {
     *idx_out = out_index(v);
@@ -122,10 +193,8 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
         uint32_t v[4];
         bool tcp[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-            v[k] = acl_v4_one<kLds>(a, tcp[k], key[k], po[k]);
-        }
+        for (int k = 0; k < 4; ++k) tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+        acl_v4_four<kLds>(a, tcp, key, po, v);
         int4 o;
         uint32_t al = 0;
         int32_t* op = reinterpret_cast<int32_t*>(&o);
@@ -591,10 +660,8 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_v4_kernel(
             uint32_t v[4];
             bool tcp[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-                v[k] = acl_v4_one<kLds>(a, tcp[k], sk[k], po[k]);
-            }
+            for (int k = 0; k < 4; ++k) tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+            VC_PIPE_ACL4(a, tcp, sk, po, v);
             int4 oa, orr;
             uint32_t al = 0;
             int32_t* pa = reinterpret_cast<int32_t*>(&oa);
