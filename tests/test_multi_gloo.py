@@ -123,3 +123,16 @@ def test_counter_allreduce_equals_single_rank(world):
     for rank, views, _ in res:
         for got, exp in zip(views, want):
             np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("k", [32, 64, 96, 128])
+def test_cu_split_balanced_over_xcds(k):
+    """bench.cu_split: CU-mask bit i selects a CU of XCD i mod 8 (measured,
+    profiles/r03_cu_scaling.jsonl), so both shares must hold the same number
+    of CUs on every XCD, a multiple of 4 -- an uneven share runs part of a
+    static-slice kernel's workgroups in a second round."""
+    pick, rest = B.cu_split(256, k)
+    assert sorted(pick + rest) == list(range(256))
+    for share in (pick, rest):
+        per_xcd = [sum(1 for c in share if c % 8 == x) for x in range(8)]
+        assert len(set(per_xcd)) == 1 and per_xcd[0] % 4 == 0, per_xcd
