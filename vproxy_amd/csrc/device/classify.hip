@@ -69,13 +69,19 @@ __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint
 #ifndef VC_ACL_LOCKSTEP
 #define VC_ACL_LOCKSTEP 1
 #endif
-template <bool kL>
-__device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[4],
-                                            const uint32_t key[4], const uint32_t port[4],
-                                            uint32_t v[4]) {
+#ifndef VC_ACL_QUADS
+#define VC_ACL_QUADS 2
+#endif
+#ifndef VC_ACL_PREFETCH
+#define VC_ACL_PREFETCH 0
+#endif
+template <bool kL, int kN = 4>
+__device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[kN],
+                                            const uint32_t key[kN], const uint32_t port[kN],
+                                            uint32_t v[kN]) {
     if (!VC_ACL_LOCKSTEP || !kL || a.shift) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = acl_v4_one<kL>(a, tcp[k], key[k], port[k]);
+        for (int k = 0; k < kN; ++k) v[k] = acl_v4_one<kL>(a, tcp[k], key[k], port[k]);
         return;
     }
     const int nmax = a.nf[0] > a.nf[1] ? a.nf[0] : a.nf[1];
@@ -84,34 +90,34 @@ __device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[4]
     // costs a null check and 64-bit address arithmetic)
     const VC_AS_LDS uint32_t* f0 = (const VC_AS_LDS uint32_t*)a.f[0];
     const VC_AS_LDS uint32_t* f1 = (const VC_AS_LDS uint32_t*)a.f[1];
-    const VC_AS_LDS uint32_t* f[4];
-    int lo[4], len[4];
+    const VC_AS_LDS uint32_t* f[kN];
+    int lo[kN], len[kN];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kN; ++k) {
         f[k] = tcp[k] ? f0 : f1;
         len[k] = tcp[k] ? a.nf[0] : a.nf[1];
         lo[k] = 0;
     }
     for (int s = 0; s < steps; ++s) {
-        uint32_t x[4];
-        int half[4];
+        uint32_t x[kN];
+        int half[kN];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kN; ++k) {
             half[k] = len[k] >> 1;
             x[k] = f[k][lo[k] + half[k]];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kN; ++k) {
             lo[k] = x[k] <= key[k] ? lo[k] + half[k] : lo[k];
             len[k] -= half[k];
         }
     }
-    uint4 r[4];
+    uint4 r[kN];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < kN; ++k)
         r[k] = glb_ld(reinterpret_cast<const uint4*>(tcp[k] ? a.rec[0] : a.rec[1]) + lo[k]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < kN; ++k)
         v[k] = acl_rec_value(r[k], tcp[k] ? a.pieces[0] : a.pieces[1], port[k]);
 }
 
@@ -184,28 +190,74 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
     const AclV4Ctx a = acl_v4_ctx(img, kLds ? lds : nullptr, shift);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     const int64_t n4 = n >> 2;
-    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < n4; g += stride) {
-        const uint4 s = reinterpret_cast<const uint4*>(src)[g];
-        const uint32_t pr = reinterpret_cast<const uint32_t*>(proto)[g];
-        const uint2 pt = reinterpret_cast<const uint2*>(port)[g];
-        const uint32_t key[4] = {s.x, s.y, s.z, s.w};
-        const uint32_t po[4] = {pt.x & 0xFFFFu, pt.x >> 16, pt.y & 0xFFFFu, pt.y >> 16};
-        uint32_t v[4];
-        bool tcp[4];
+    // kQ quads of 4 tuples per lane per pass (g, g + stride, ...): the kQ * 4
+    // interval searches step in lockstep, so a pass waits on its LDS reads
+    // (and its loads and record reads) once for all of them
+    constexpr int kQ = VC_ACL_QUADS;
+    // the next pass's tuples are loaded before this pass's searches
+    // (VC_ACL_PREFETCH), so their HBM latency hides behind the LDS steps
+    uint4 s_n[kQ];
+    uint32_t pr_n[kQ];
+    uint2 pt_n[kQ];
+    auto load_pass = [&](int64_t g0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-        acl_v4_four<kLds>(a, tcp, key, po, v);
-        int4 o;
-        uint32_t al = 0;
-        int32_t* op = reinterpret_cast<int32_t*>(&o);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint8_t b = 0;
-            acl_emit(img, tcp[k], v[k], allow ? &b : nullptr, op + k);
-            al |= uint32_t(b) << (8 * k);
+        for (int q = 0; q < kQ; ++q) {
+            // a quad past the end reads the last quad (searched, not stored)
+            const int64_t g = g0 + q * stride < n4 ? g0 + q * stride : n4 - 1;
+            s_n[q] = reinterpret_cast<const uint4*>(src)[g];
+            pr_n[q] = reinterpret_cast<const uint32_t*>(proto)[g];
+            pt_n[q] = reinterpret_cast<const uint2*>(port)[g];
         }
-        reinterpret_cast<int4*>(out)[g] = o;
-        if (allow) reinterpret_cast<uint32_t*>(allow)[g] = al;
+    };
+    const int64_t gfirst = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (VC_ACL_PREFETCH && gfirst < n4) load_pass(gfirst);
+    for (int64_t g0 = gfirst; g0 < n4; g0 += kQ * stride) {
+        uint32_t key[4 * kQ], po[4 * kQ], v[4 * kQ];
+        bool tcp[4 * kQ];
+        if (!VC_ACL_PREFETCH) load_pass(g0);
+        uint4 s_c[kQ];
+        uint32_t pr_c[kQ];
+        uint2 pt_c[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            s_c[q] = s_n[q];
+            pr_c[q] = pr_n[q];
+            pt_c[q] = pt_n[q];
+        }
+        if (VC_ACL_PREFETCH && g0 + kQ * stride < n4) load_pass(g0 + kQ * stride);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint4 s = s_c[q];
+            const uint32_t pr = pr_c[q];
+            const uint2 pt = pt_c[q];
+            key[4 * q + 0] = s.x;
+            key[4 * q + 1] = s.y;
+            key[4 * q + 2] = s.z;
+            key[4 * q + 3] = s.w;
+            po[4 * q + 0] = pt.x & 0xFFFFu;
+            po[4 * q + 1] = pt.x >> 16;
+            po[4 * q + 2] = pt.y & 0xFFFFu;
+            po[4 * q + 3] = pt.y >> 16;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tcp[4 * q + k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+        }
+        acl_v4_four<kLds, 4 * kQ>(a, tcp, key, po, v);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int64_t g = g0 + q * stride;
+            if (q > 0 && g >= n4) break;
+            int4 o;
+            uint32_t al = 0;
+            int32_t* op = reinterpret_cast<int32_t*>(&o);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint8_t b = 0;
+                acl_emit(img, tcp[4 * q + k], v[4 * q + k], allow ? &b : nullptr, op + k);
+                al |= uint32_t(b) << (8 * k);
+            }
+            reinterpret_cast<int4*>(out)[g] = o;
+            if (allow) reinterpret_cast<uint32_t*>(allow)[g] = al;
+        }
     }
     // tail (n % 4 items), handled by the first threads of block 0
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
