@@ -180,7 +180,7 @@ __device__ __forceinline__ void stage_bounds(const AclImage& img, uint32_t* lds,
     __syncthreads();
 }
 
-template <bool kLds>
+template <bool kLds, int kQ>
 __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
     AclImage img, int shift, const uint8_t* __restrict__ proto, const uint32_t* __restrict__ src,
     const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out,
@@ -193,7 +193,6 @@ __global__ __launch_bounds__(kBlock) void acl_v4_kernel(
     // kQ quads of 4 tuples per lane per pass (g, g + stride, ...): the kQ * 4
     // interval searches step in lockstep, so a pass waits on its LDS reads
     // (and its loads and record reads) once for all of them
-    constexpr int kQ = VC_ACL_QUADS;
     // the next pass's tuples are loaded before this pass's searches
     // (VC_ACL_PREFETCH), so their HBM latency hides behind the LDS steps
     uint4 s_n[kQ];
@@ -1098,10 +1097,16 @@ hipError_t launch_acl_v4(const LaunchCfg& c, const AclImage& img, const uint8_t*
                      aligned(out, 16) && (!allow || aligned(allow, 4));
     const int per_cu = words <= 16 * 1024 ? 4 : 2;
     if (vec) {
+        // VC_ACL_QUADS quads per lane per pass once the batch fills every
+        // lane that many times; a smaller batch takes one quad per lane
+        // (a second quad past the end would be searched for nothing)
+        const int64_t quads = n / 4;
         const int grid = grid_for(c, (n + 3) / 4, per_cu);
-        if (hipError_t e = allow_lds(vcd::acl_v4_kernel<true>)) return e;
-        hipLaunchKernelGGL(vcd::acl_v4_kernel<true>, dim3(grid), dim3(vcd::kBlock), shmem,
-                           c.stream, img, shift, proto, src4, port, n, out, allow);
+        const bool multi = quads >= int64_t(grid) * vcd::kBlock * VC_ACL_QUADS;
+        const auto kern = multi ? vcd::acl_v4_kernel<true, VC_ACL_QUADS> : vcd::acl_v4_kernel<true, 1>;
+        if (hipError_t e = allow_lds(kern)) return e;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(vcd::kBlock), shmem, c.stream, img, shift, proto,
+                           src4, port, n, out, allow);
     } else {
         const int grid = grid_for(c, n, per_cu);
         if (hipError_t e = allow_lds(vcd::acl_v4_kernel_scalar<true>)) return e;
