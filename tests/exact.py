@@ -1,0 +1,323 @@
+"""Independent exact checkers for whole-batch parity at the headline sizes.
+
+TEST INFRASTRUCTURE ONLY, like oracle/: nothing under vproxy_amd/ imports
+this module.  The oracle (oracle/vc_oracle.c) restates the Java as the Java
+runs it -- a linear scan of the rule list per item -- which is exact but
+checks only a few thousand of a 16M-64M batch in test time.  The checkers
+here restate the same functions by a different algorithm, one that needs a
+handful of sorted-array probes per item, so a GPU test can compare EVERY
+output of a headline-size batch.  Each is validated against the oracle on
+random sets first (tests/test_exact_cpu.py) and shares no code with the
+kernels or the table compiler.
+
+- route_first_match_v4 / _v6: RouteTable.lookup (RouteTable.java:44-59)
+  returns the first rule in list order whose network contains the address.
+  A prefix of length L contains the address iff the two agree on the top L
+  bits, so at each length at most one distinct network can contain it: the
+  first match is the minimum list index over the lengths of the earliest
+  rule whose network equals the address's top L bits.  One key array per
+  length, sorted stably (so the earliest rule heads each run of equal keys),
+  probed with searchsorted.  This holds for any list order -- it does not
+  lean on the shortest-first / longest-prefix argument (R7).
+- sg_first_match_v4 / _v6: SecurityGroup.allow (SecurityGroup.java:30-45)
+  with SecurityGroupRule.match (SecurityGroupRule.java:27-29): the first rule
+  of the protocol's list (TCP for 6, UDP otherwise) whose network contains
+  the source and whose [minPort, maxPort] holds the port; allow is that
+  rule's bit, defaultAllow when none.  Same per-length probe, then a scan of
+  the (short) run of rules sharing the network for the first one whose port
+  range holds the port.  IPv4 rules only; an IPv6 source reaches them through
+  Network.maskMatch's cases 4/5 (Network.java:246-277): only ::a.b.c.d and
+  ::ffff:a.b.c.d (Utils.lowBitsV6V4) can match, on their low 32 bits.
+- hint_search_dict: Upstream.searchForGroup (Upstream.java:187-198) over
+  host-only hints: Hint.ofHost / formatHost (Hint.java:17-73) and the host
+  part of matchLevel (Hint.java:100-160) with the hint-port filter.  A dict
+  from merged hint-host to its groups: level 3 = the host itself, level 2 =
+  any "."-suffix of it (host.endsWith("." + annoHost)), level 1 = "*"; the
+  strict ">" of searchForGroup makes the answer the earliest group of the
+  best level.
+"""
+import re
+
+import numpy as np
+import torch
+
+CHUNK = 16 << 20
+
+
+def _t(x, dev):
+    if isinstance(x, torch.Tensor):
+        return x.to(dev)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def _u32(x):
+    """any integer tensor holding uint32 bits -> int64 in [0, 2^32)"""
+    return x.to(torch.int64) & 0xFFFFFFFF
+
+
+def _plen_of_masks(mask_words, width):
+    """prefix length of each mask (int64 words, top `width` bits), asserting
+    every mask is a prefix mask (Network.validNetwork masks are)."""
+    m = mask_words.cpu().numpy().astype(np.uint64)
+    if width == 32:
+        m = m & np.uint64(0xFFFFFFFF)
+    plen = np.zeros(len(m), np.int64)
+    x = m.copy()
+    for _ in range(width):
+        plen += (x & np.uint64(1)).astype(np.int64)
+        x >>= np.uint64(1)
+    full = np.uint64((1 << width) - 1)
+    want = np.where(plen == 0, np.uint64(0),
+                    (full << (np.uint64(width) - plen.astype(np.uint64))) & full)
+    assert np.array_equal(m, want), "non-prefix mask"
+    return torch.from_numpy(plen)
+
+
+class _PerLength:
+    """Rules grouped by prefix length: for each length L present, the rules'
+    top-L-bit keys sorted stably (earliest rule first within a key), their
+    list indices, and the longest run of one key."""
+
+    def __init__(self, net, plen, width, dev):
+        self.width = width
+        self.levels = []
+        idx = torch.arange(len(net), dtype=torch.int64)
+        for L in sorted(set(plen.tolist())):
+            sel = plen == L
+            k = self.key(net[sel], L)
+            order = torch.argsort(k, stable=True)
+            k, ridx = k[order], idx[sel][order]
+            run = int(torch.unique_consecutive(k, return_counts=True)[1].max())
+            self.levels.append((L, k.to(dev), ridx.to(dev), run))
+
+    def key(self, x, L):
+        if L == 0:
+            return torch.zeros_like(x)
+        # arithmetic shift of the signed word: equal top-L bits <=> equal keys,
+        # and the order is consistent on both sides of the probe
+        return x >> (self.width - L)
+
+
+def _first_match(levels, q, nrules, port=None, plo=None, phi=None, valid=None):
+    """min list index over the lengths of a rule whose key equals q's key
+    (and, with `port`, whose port range holds it); nrules when none."""
+    best = torch.full(q.shape, nrules, dtype=torch.int64, device=q.device)
+    for L, k, ridx, run in levels.levels:
+        qk = levels.key(q, L)
+        pos = torch.searchsorted(k, qk)
+        for m in range(run if port is not None else 1):
+            c = pos + m
+            inr = c < len(k)
+            c = c.clamp(max=len(k) - 1)
+            ok = inr & (k[c] == qk)
+            r = ridx[c]
+            if port is not None:
+                ok &= (plo[r] <= port) & (port <= phi[r])
+            if valid is not None:
+                ok &= valid
+            best = torch.where(ok, torch.minimum(best, r), best)
+    return best
+
+
+# ---------------------------------------------------------------------------
+# RouteTable.lookup
+# ---------------------------------------------------------------------------
+def _net_words(nets, family):
+    ip = np.ascontiguousarray(nets["ip"])
+    mk = np.ascontiguousarray(nets["mask"])
+    if family == 4:
+        assert np.all(nets["ip_len"] == 4) and np.all(nets["mask_len"] == 4)
+        w = lambda a: torch.from_numpy(a[:, :4].copy().view(">u4").reshape(-1).astype(np.int64))
+        return w(ip), w(mk)
+    assert np.all(nets["ip_len"] == 16)
+    # Network.parseMask gives 4 mask bytes up to /32: Network.maskMatch's case
+    # 1 compares those bytes only, which is the same prefix test
+    w = lambda a: torch.from_numpy(a[:, :8].copy().view(">i8").reshape(-1).astype(np.int64))
+    lo = lambda a: a[:, 8:].copy().view(">u8").reshape(-1)
+    full = np.zeros((len(mk), 16), np.uint8)
+    full[:, :mk.shape[1]] = mk
+    full[nets["mask_len"] == 4, 4:] = 0
+    assert np.all(lo(full) == 0) and np.all(lo(ip) == 0), "IPv6 prefixes longer than /64"
+    return w(ip), w(full)
+
+
+class RouteChecker:
+    """RouteTable.lookup (RouteTable.java:44-59) over one family's rule list
+    (NET_DT rows in list order)."""
+
+    def __init__(self, nets, family, dev):
+        self.family, self.dev, self.n = family, dev, len(nets)
+        width = 32 if family == 4 else 64
+        net, mk = _net_words(nets, family)
+        plen = _plen_of_masks(mk, width)
+        self.levels = _PerLength(net, plen, width, dev)
+
+    def __call__(self, dst):
+        """dst: v4 -> uint32 bits in any integer dtype [n]; v6 -> uint8 [n, 16].
+        Returns int32 list indices, -1 for null."""
+        out = []
+        for s in range(0, len(dst), CHUNK):
+            d = _t(dst[s:s + CHUNK], self.dev)
+            if self.family == 4:
+                q = _u32(d)
+            else:
+                q = _be64(d[:, :8])
+            b = _first_match(self.levels, q, self.n)
+            out.append(torch.where(b == self.n, -1, b).to(torch.int32))
+        return torch.cat(out) if out else torch.zeros(0, dtype=torch.int32, device=self.dev)
+
+
+def _be64(b):
+    """uint8 [n, 8] big-endian -> int64 [n] (two's complement bits)"""
+    b = b.to(torch.int64)
+    x = torch.zeros(b.shape[0], dtype=torch.int64, device=b.device)
+    for i in range(8):
+        x = (x << 8) | b[:, i]
+    return x
+
+
+# ---------------------------------------------------------------------------
+# SecurityGroup.allow
+# ---------------------------------------------------------------------------
+class AclChecker:
+    """SecurityGroup.allow (SecurityGroup.java:30-45) over IPv4 rule lists
+    (workloads.RULE_DT rows in list order)."""
+
+    def __init__(self, tcp, udp, default_allow, dev):
+        self.dev, self.dflt = dev, 1 if default_allow else 0
+        self.lists = []
+        for rules in (tcp, udp):
+            net, mk = _net_words(rules["net"], 4)
+            plen = _plen_of_masks(mk, 32)
+            self.lists.append(dict(
+                n=len(rules), levels=_PerLength(net, plen, 32, dev),
+                lo=_t(rules["min_port"].astype(np.int64), dev),
+                hi=_t(rules["max_port"].astype(np.int64), dev),
+                allow=_t(rules["allow"].astype(np.int64), dev)))
+
+    def _one(self, proto, src, port, valid):
+        idx = torch.full(src.shape, -1, dtype=torch.int64, device=self.dev)
+        allow = torch.full(src.shape, self.dflt, dtype=torch.int64, device=self.dev)
+        is_tcp = proto.to(torch.int64) == 6
+        for L, sel in zip(self.lists, (is_tcp, ~is_tcp)):
+            if L["n"] == 0:
+                continue
+            b = _first_match(L["levels"], src, L["n"], port, L["lo"], L["hi"], valid)
+            hit = sel & (b < L["n"])
+            bc = b.clamp(max=L["n"] - 1)
+            idx = torch.where(hit, b, idx)
+            allow = torch.where(hit, L["allow"][bc], allow)
+        return idx.to(torch.int32), allow.to(torch.uint8)
+
+    def v4(self, proto, src4, port):
+        """proto u8, src uint32 bits, port uint16 bits -> (rule idx int32, allow u8)"""
+        outs = []
+        for s in range(0, len(src4), CHUNK):
+            p = _t(proto[s:s + CHUNK], self.dev)
+            a = _u32(_t(src4[s:s + CHUNK], self.dev))
+            q = _t(port[s:s + CHUNK], self.dev).to(torch.int64) & 0xFFFF
+            outs.append(self._one(p, a, q, None))
+        return tuple(torch.cat(x) for x in zip(*outs))
+
+    def v6(self, proto, src6, port):
+        """IPv6 sources against the IPv4 rules: Network.maskMatch cases 4/5
+        (Network.java:246-277) compare the last four bytes, then
+        Utils.lowBitsV6V4(ip, 11, 10) (Utils.java:122-133) requires bytes
+        0-9 zero and bytes 10-11 both 0x00 or both 0xFF."""
+        outs = []
+        for s in range(0, len(port), CHUNK):
+            p = _t(proto[s:s + CHUNK], self.dev)
+            b = _t(src6[s:s + CHUNK], self.dev).to(torch.int64)
+            head0 = (b[:, :10] == 0).all(dim=1)
+            b10, b11 = b[:, 10], b[:, 11]
+            ok = head0 & (((b10 == 0) & (b11 == 0)) | ((b10 == 255) & (b11 == 255)))
+            a = (b[:, 12] << 24) | (b[:, 13] << 16) | (b[:, 14] << 8) | b[:, 15]
+            q = _t(port[s:s + CHUNK], self.dev).to(torch.int64) & 0xFFFF
+            outs.append(self._one(p, a, q, ok))
+        return tuple(torch.cat(x) for x in zip(*outs))
+
+
+# ---------------------------------------------------------------------------
+# Upstream.searchForGroup over host-only hints
+# ---------------------------------------------------------------------------
+_INT = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def _java_int(v):
+    """Integer.parseInt, with Annotations' failure -> 0 (Annotations.java:45-58)"""
+    if v is None:
+        return 0
+    if isinstance(v, int):
+        return v
+    if not _INT.match(v):
+        return 0
+    x = int(v)
+    return x if -2**31 <= x < 2**31 else 0
+
+
+def _anno(a, k):
+    return a.get("vproxy/hint-" + k, a.get(k))
+
+
+class HintChecker:
+    """searchForGroup for hints built by Hint.ofHost / ofHostPort."""
+
+    def __init__(self, groups):
+        self.by_host = {}          # merged hint-host bytes -> [(group index, hint-port)]
+        for i, (ha, ga) in enumerate(groups):
+            host = None
+            port = 0
+            for a in (ha or {}, ga or {}):   # Upstream.java:191: handle first
+                h = _anno(a, "host")
+                if host is None and h is not None:
+                    host = h.encode() if isinstance(h, str) else bytes(h)
+                if port == 0:
+                    port = _java_int(_anno(a, "port"))
+            if host is not None:
+                self.by_host.setdefault(host, []).append((i, port))
+
+    def _first(self, key, port):
+        for i, p in self.by_host.get(key, ()):
+            if port == 0 or p == 0 or p == port:      # Hint.java:106-108
+                return i
+        return -1
+
+    @staticmethod
+    def format_host(s):
+        """Hint.formatHost (Hint.java:57-73) for names with at most one ':'
+        (no such string parses as IPv6: without "::" IP.parseIpv6 needs 16
+        bytes of groups, with it two colons)."""
+        c = s.find(b":")
+        if c == -1:
+            return s
+        assert s.find(b":", c + 1) == -1, "checker covers names with at most one ':'"
+        h = s[:c]
+        if h.startswith(b"www."):
+            h = h[4:]
+        return h if h else None
+
+    def __call__(self, name, port=0):
+        host = self.format_host(name)
+        if host is None:
+            return -1
+        g = self._first(host, port)
+        if g >= 0:
+            return g                               # level 3 beats any other
+        best = -1
+        d = host.find(b".")
+        while d != -1:                             # every "." + annoHost suffix
+            g = self._first(host[d + 1:], port)
+            if g >= 0 and (best < 0 or g < best):
+                best = g
+            d = host.find(b".", d + 1)
+        if best >= 0:
+            return best
+        return self._first(b"*", port)
+
+    def batch(self, blob, off, ports=None):
+        blob = bytes(np.asarray(blob, np.uint8))
+        off = np.asarray(off, np.int64)
+        out = np.empty(len(off) - 1, np.int32)
+        for i in range(len(out)):
+            out[i] = self(blob[off[i]:off[i + 1]], 0 if ports is None else int(ports[i]))
+        return out

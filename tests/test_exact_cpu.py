@@ -1,0 +1,171 @@
+"""CPU tier: the whole-batch checkers of tests/exact.py against the oracle.
+
+The GPU tests compare every output of the headline batches with these
+checkers, so each is first shown equal to the oracle's linear scans
+(oracle/vc_oracle.c: vo_rt_lookup_list, vo_sg_allow, vo_search_for_group)
+on random rule sets: the 255-rule C1 route table in RouteTable.addRule
+order, a 20k-rule arbitrary-priority list with duplicate networks, IPv6
+lists with 4-byte masks and ::/0, 64- to 10k-rule ACLs with both defaults
+and every protocol, IPv6 sources against IPv4 rules (the cross-family
+cases), and Upstream groups with hint-ports, "*" and suffix chains.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_ffi as O
+from exact import AclChecker, HintChecker, RouteChecker
+from vproxy_amd import workloads as W
+
+from cases import hint_cases_random, hint_cases_shapes, rule_row, v6_edge_inputs
+
+CPU = torch.device("cpu")
+THREADS = 8
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+def test_route_c1_order_vs_oracle():
+    rng = np.random.default_rng(11)
+    ot = O.RouteTable()
+    ot.add("10.0.0.0/8")
+    plen = rng.integers(8, 31, 600)
+    net = rng.integers(0, 2**32, 600, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    added = 0
+    for i in range(600):
+        s = "%d.%d.%d.%d/%d" % (net[i] >> 24, (net[i] >> 16) & 255, (net[i] >> 8) & 255,
+                                net[i] & 255, plen[i])
+        added += bool(ot.add(s))
+        if added == 255:
+            break
+    v4, _ = O.rt_table_np(ot)
+    q = W.v4_lookups(net, plen, 200_000, 12)
+    np.testing.assert_array_equal(_np(RouteChecker(v4, 4, CPU)(q)),
+                                  O.rt_batch_v4_np(v4, q, nthreads=THREADS))
+
+
+def test_route_arbitrary_priority_vs_oracle():
+    """20k prefixes /0-/32 in random list order, some networks listed twice
+    (the earlier one must win), lookups inside and outside."""
+    rng = np.random.default_rng(21)
+    plen = rng.integers(0, 33, 20000)
+    net = rng.integers(0, 2**32, 20000, dtype=np.uint64).astype(np.uint32) & W._mask32(plen)
+    nets = W.v4_nets(net, plen)
+    nets = np.concatenate([nets, nets[rng.integers(0, len(nets), 500)]])
+    rng.shuffle(nets)
+    q = W.v4_lookups(net, plen, 200_000, 22)
+    q[:64] = [0, 0xFFFFFFFF] * 32
+    np.testing.assert_array_equal(_np(RouteChecker(nets, 4, CPU)(q)),
+                                  O.rt_batch_v4_np(nets, q, nthreads=THREADS))
+    np.testing.assert_array_equal(_np(RouteChecker(nets[:0], 4, CPU)(q[:100])),
+                                  np.full(100, -1, np.int32))
+
+
+def test_route_shortest_first_vs_oracle():
+    """The C3 generator's shape (BGP-like, shortest-first list)."""
+    net, plen = W.gen_v4_prefixes(30000, 3)
+    nets = W.v4_nets(net, plen)
+    q = W.v4_lookups(net, plen, 100_000, 4)
+    np.testing.assert_array_equal(_np(RouteChecker(nets, 4, CPU)(q)),
+                                  O.rt_batch_v4_np(nets, q, nthreads=THREADS))
+
+
+def test_route_v6_vs_oracle():
+    hi, lo, p6 = W.gen_v6_prefixes(5000, 31)
+    nets6 = np.concatenate([W.v6_nets(hi, lo, p6), W.v6_nets([0], [0], [0]),
+                            W.v6_nets(hi[:50], lo[:50], np.minimum(p6[:50], 24))])
+    rng = np.random.default_rng(3)
+    rng.shuffle(nets6)
+    assert (nets6["mask_len"] == 4).any()
+    q = W.v6_lookups(hi, lo, p6, 100_000, 23)
+    got = _np(RouteChecker(nets6, 6, CPU)(q))
+    np.testing.assert_array_equal(got, O.rt_batch_v6_np(nets6, q, nthreads=THREADS))
+    # without the ::/0 rule some lookups miss
+    keep = nets6[~((nets6["mask_len"] == 4) & (nets6["mask"][:, 0] == 0))]
+    got = _np(RouteChecker(keep, 6, CPU)(q))
+    np.testing.assert_array_equal(got, O.rt_batch_v6_np(keep, q, nthreads=THREADS))
+    assert (got == -1).any()
+
+
+@pytest.mark.parametrize("n_rules,p_range,weighted,seed", [
+    (64, 0.5, False, 1), (2000, 0.3, True, 2), (10000, 0.3, True, 3), (3000, 0.95, False, 4)])
+def test_acl_v4_vs_oracle(n_rules, p_range, weighted, seed):
+    tcp, udp = W.gen_sg_rules(n_rules, seed, p_range=p_range, weighted=weighted)
+    # a network listed several times with different port ranges (a run of
+    # equal keys the checker scans) and a catch-all late in the list
+    extra = np.concatenate([rule_row("10.1.0.0/16", lo, lo + 9, lo % 2) for lo in range(0, 200, 7)]
+                           + [rule_row("0.0.0.0/0", 0, 65535, True)])
+    tcp = np.concatenate([tcp[: len(tcp) // 2], extra, tcp[len(tcp) // 2:]])
+    proto, src, port = W.gen_acl_queries(tcp, udp, 200_000, seed + 100)
+    proto[::97] = 1                                    # not TCP: the UDP list
+    src[::89] = 0x0A010000 | (src[::89] & 0xFFFF)
+    for dflt in (False, True):
+        chk = AclChecker(tcp, udp, dflt, CPU)
+        got, allow = chk.v4(proto, src, port)
+        want, wv = O.sg_batch_v4_np(tcp, udp, dflt, proto, src, port, nthreads=THREADS)
+        np.testing.assert_array_equal(_np(got), want)
+        np.testing.assert_array_equal(_np(allow), wv)
+    for t, u in ((tcp[:0], udp), (tcp, udp[:0])):
+        got, allow = AclChecker(t, u, True, CPU).v4(proto[:5000], src[:5000], port[:5000])
+        want, wv = O.sg_batch_v4_np(t, u, True, proto[:5000], src[:5000], port[:5000])
+        np.testing.assert_array_equal(_np(got), want)
+        np.testing.assert_array_equal(_np(allow), wv)
+
+
+def test_acl_v6_sources_on_v4_rules_vs_oracle():
+    tcp, udp = W.gen_sg_rules(1500, 8)
+    extra = np.concatenate([rule_row(s, 0, 65535, a) for s, a in (
+        ("127.0.0.1/32", True), ("8.8.8.0/24", False), ("0.0.0.0/0", True))])
+    tcp = np.concatenate([extra[:2], tcp, extra[2:]])
+    udp = np.concatenate([udp, extra])
+    rng = np.random.default_rng(9)
+    src6, proto, port = v6_edge_inputs(rng, 100_000)
+    # some mapped addresses inside real rule networks
+    ip, mk = W.rule_v4_fields(tcp[2:])
+    r = rng.integers(0, len(ip), 100_000)
+    inside = (ip[r] | (rng.integers(0, 2**32, 100_000, dtype=np.uint64).astype(np.uint32) & ~mk[r]))
+    pick = (src6[:, :10] == 0).all(1) & (rng.random(100_000) < 0.5)
+    src6[pick, 12:] = W.v4_to_bytes(inside[pick])
+    for dflt in (False, True):
+        got, allow = AclChecker(tcp, udp, dflt, CPU).v6(proto, src6, port)
+        want, wv = O.sg_batch_v6_np(tcp, udp, dflt, proto, src6, port, nthreads=THREADS)
+        np.testing.assert_array_equal(_np(got), want)
+        np.testing.assert_array_equal(_np(allow), wv)
+    assert (want >= 0).mean() > 0.1
+
+
+def test_hint_dict_vs_oracle_generated():
+    groups, ghosts = W.gen_groups(3000, 17, port_frac=0.3)
+    # repeated hosts (member lists), a second "*", handle annotations
+    groups += [({}, {"host": ghosts[5]}), ({}, {"host": "*", "port": "80"}),
+               ({"host": ghosts[9]}, {"host": "zz.none"}), ({}, {"port": "443"})]
+    names = W.gen_hostnames(ghosts, 60_000, 18, port_frac=0.3)
+    names += [b"www.", b":80", b"www.:80", b"", b"*", b"a.*", b"." + ghosts[3].encode()]
+    blob, off = W.pack(names)
+    rng = np.random.default_rng(19)
+    ports = rng.choice(np.array([0, 0, 80, 443, 8080], np.uint16), len(names))
+    gp = [int(g[1]["port"]) for g in groups[:3000] if "port" in g[1]]
+    ports[::7] = rng.choice(np.array(gp, np.uint16), len(ports[::7]))
+    chk = HintChecker(groups)
+    og = O.Groups(groups)
+    for p in (None, ports):
+        want = O.hint_batch_np(og, blob, off, p, nthreads=THREADS)
+        np.testing.assert_array_equal(chk.batch(blob, off, p), want)
+    assert (want >= 0).mean() > 0.5
+
+
+def test_hint_dict_vs_oracle_edge_cases():
+    rng = np.random.default_rng(23)
+    groups, _, queries = hint_cases_random(rng, 400, 20000)
+    names = [(h, p) for h, p, _ in queries if h is not None and h.count(":") <= 1]
+    g2, n2 = hint_cases_shapes(rng, 20000)
+    chk, og = HintChecker(groups), O.Groups(groups)
+    for h, p in names:
+        assert chk(h.encode(), p) == O.search_for_group(og, h, p), (h, p)
+    chk, og = HintChecker(g2), O.Groups(g2)
+    keep = [n for n in n2 if n.count(b":") <= 1]
+    blob, off = W.pack(keep)
+    np.testing.assert_array_equal(chk.batch(blob, off), O.hint_batch_np(og, blob, off, None,
+                                                                        nthreads=THREADS))

@@ -12,6 +12,7 @@ import pytest
 
 import oracle_ffi as O
 import vproxy_amd as V
+from exact import AclChecker, RouteChecker
 from vproxy_amd import workloads as W
 from vproxy_amd.classifier import group_array, pack_strings
 
@@ -61,7 +62,8 @@ def test_acl_v4_vs_oracle(clf, n_rules, p_range, weighted, nq, seed):
 
 def test_acl_c2_full_size(clf):
     """C2: 10k-rule ACL, 64M IPv4 5-tuples resident in HBM; oracle-checked
-    sample + whole-batch properties."""
+    sample, whole-batch properties, and every output equal to the exact
+    first-match checker."""
     import torch
     tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
     compile_acl_np(clf, tcp, udp, False)
@@ -89,6 +91,36 @@ def test_acl_c2_full_size(clf):
         assert np.all((port[sel] >= lst["min_port"][r]) & (port[sel] <= lst["max_port"][r]))
         assert np.all(allow_h[sel] == lst["allow"][r])
     assert np.all(allow_h[~hit] == 0)
+    # every one of the 64M: the first match (tests/exact.py, oracle-validated)
+    want_i, want_a = AclChecker(tcp, udp, False, d[0].device).v4(*d)
+    assert torch.equal(idx, want_i), int((idx != want_i).sum())
+    assert torch.equal(allow, want_a)
+
+
+@pytest.mark.parametrize("n", [(1 << 22) + (1 << 20) + 3,        # the verdict's size
+                               4 * (11 * 131072 + 777) + 1,     # odd pass count, tail 1
+                               4 * (2 * 131072) + 2])           # just at the two-quad threshold
+def test_acl_two_quad_passes_and_tail(clf, n):
+    """vc_acl_classify_v4_dev on the C2 tables at sizes that run the
+    two-quad kernel (acl_v4_kernel<true, 2>: launch_acl_v4 picks it once
+    n / 4 >= grid x 256 x 2) with a partial last pass -- its second quad past
+    the end is searched but not stored -- and the n & 3 tail: every output
+    against the exact checker, the last 20k and a spread sample against the
+    oracle (SecurityGroup.java:30-45)."""
+    import torch
+    tcp, udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
+    compile_acl_np(clf, tcp, udp, False)
+    proto, src, port = W.gen_acl_queries(tcp, udp, n, n & 0xFFFF)
+    d = [torch.from_numpy(x).cuda() for x in (proto, src, port)]
+    idx, allow = clf.acl_v4(*d)
+    torch.cuda.synchronize()
+    want_i, want_a = AclChecker(tcp, udp, False, d[0].device).v4(*d)
+    assert torch.equal(idx, want_i), int((idx != want_i).sum())
+    assert torch.equal(allow, want_a)
+    s = np.concatenate([np.arange(n - 20000, n), np.random.default_rng(n).integers(0, n, 20000)])
+    want, wv = O.sg_batch_v4_np(tcp, udp, False, proto[s], src[s], port[s], nthreads=THREADS)
+    np.testing.assert_array_equal(idx.cpu().numpy()[s], want)
+    np.testing.assert_array_equal(allow.cpu().numpy()[s], wv)
 
 
 def test_acl_edges_and_paths(clf):
@@ -219,7 +251,8 @@ def test_route_arbitrary_priority_and_v6(clf):
 def test_route_c3_full_size(clf):
     """C3: ~1M IPv4 + 200k IPv6 prefixes inserted shortest-first through the
     RouteTable mirror (first match == LPM there); 16M device-resident
-    lookups; oracle-checked sample and LPM properties."""
+    lookups; oracle-checked sample, LPM properties, and every v4 and v6
+    output equal to the exact per-length checker."""
     import torch
     net, plen = W.gen_v4_prefixes(1000000, W.SEED + 3)
     hi, lo, p6 = W.gen_v6_prefixes(200000, W.SEED + 4)
@@ -250,10 +283,15 @@ def test_route_c3_full_size(clf):
     h = got4 >= 0
     assert np.all((q4[h] & mk[got4[h]]) == ip[got4[h]])
     assert h.mean() > 0.9
+    # every one of the 16M: the first match in list order (tests/exact.py)
+    dev = torch.device("cuda", 0)
+    want4 = RouteChecker(v4, 4, dev)(q4).cpu().numpy()
+    np.testing.assert_array_equal(got4, want4)
     q6 = W.v6_lookups(hi, lo, p6, 1 << 20, 42)
     got6 = clf.route_v6(torch.from_numpy(q6).cuda()).cpu().numpy()
     s = np.random.default_rng(2).integers(0, len(q6), 2000)
     np.testing.assert_array_equal(got6[s], O.rt_batch_v6_np(v6, q6[s], nthreads=THREADS))
+    np.testing.assert_array_equal(got6, RouteChecker(v6, 6, dev)(q6).cpu().numpy())
 
 
 # ---------------------------------------------------------------------------

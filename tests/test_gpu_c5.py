@@ -10,6 +10,12 @@ ACL (SecurityGroup.java:30-45), route (RouteTable.java:44-59) and pool
 group (Upstream.java:187-198) results; whole-batch properties; and counters
 equal to exact histograms of the outputs.
 
+Every output of every batch is compared exactly: tests/exact.py restates
+SecurityGroup.allow, RouteTable.lookup and Upstream.searchForGroup with
+per-prefix-length sorted keys and a hint-host dict (validated against the
+oracle in tests/test_exact_cpu.py), fast enough for all 16M packets and the
+whole 16M-name pool.  Oracle samples stay beside them as a second witness.
+
 Also here: DNS at C4 scale (100k groups + 50k hosts), counters fed values
 outside the counter space, and the bench's N > 1 schedule (HitCounterBucket
 fill from the library's device counters on the counting stream + an RCCL
@@ -24,6 +30,7 @@ import pytest
 import bench as B
 import oracle_ffi as O
 import vproxy_amd as V
+from exact import AclChecker, HintChecker, RouteChecker
 from vproxy_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -36,6 +43,13 @@ def c5():
     clf = V.Classifier(0)
     dev = torch.device("cuda", 0)
     t = B.c5_tables(clf, dev, 16 << 20)
+    t.acl_chk = AclChecker(t.tcp, t.udp, False, dev)
+    t.rt4_chk = RouteChecker(t.v4_list, 4, dev)
+    t.rt6_chk = RouteChecker(t.v6_list, 6, dev)
+    # the pool is 16M draws (t.pidx) from 1M distinct names: classify those
+    # with the dict checker once, then index
+    t.name_want = torch.from_numpy(HintChecker(t.groups).batch(t.nblob, t.noff)).to(dev)
+    t.pool_want = t.name_want[torch.from_numpy(t.pidx).to(dev)]
     yield clf, t, dev
     clf.close()
 
@@ -55,8 +69,15 @@ def _check_batch(clf, t, dev, pkts, outs, pool, check_counters=True):
     acl, route, grp, allow = outs
     n = len(src)
     u32 = lambda x: x.to(torch.int64) & 0xFFFFFFFF
-    # group = pool[host_id], whole batch
+    # group = pool[host_id] and the pool = searchForGroup of each name, whole batch
     assert torch.equal(grp, pool[hid.long()])
+    assert torch.equal(pool, t.pool_want)
+    # every ACL index / verdict and every route index, whole batch
+    want_acl, want_allow = t.acl_chk.v4(proto, src, dport)
+    assert torch.equal(acl, want_acl), int((acl != want_acl).sum())
+    assert torch.equal(allow, want_allow)
+    want_route = t.rt4_chk(dst)
+    assert torch.equal(route, want_route), int((route != want_route).sum())
     # whole-batch ACL properties: the index names a rule of the packet's
     # protocol that contains src and whose port range holds dport; allow is
     # that rule's bit (defaultAllow = false otherwise)
@@ -112,8 +133,9 @@ def _check_batch(clf, t, dev, pkts, outs, pool, check_counters=True):
 
 
 def test_c5_bench_tables_and_pool(c5):
-    """The bench's tables are the C5 sizes, and the classified pool matches
-    the oracle on a sample."""
+    """The bench's tables are the C5 sizes, and the classified pool equals
+    searchForGroup for all 16M names (dict checker) and the oracle on a
+    sample; the device pool blob holds exactly the drawn names' lengths."""
     import torch
     clf, t, dev = c5
     assert len(t.tcp) + len(t.udp) == 10000
@@ -121,6 +143,9 @@ def test_c5_bench_tables_and_pool(c5):
     assert len(t.groups) == 100000 and t.pool_n == 16 << 20
     pool = clf.hint_search((t.pool_blob, t.pool_off, None))
     torch.cuda.synchronize()
+    lens = torch.from_numpy(np.diff(t.noff.astype(np.int64))[t.pidx]).to(dev)
+    assert torch.equal(torch.diff(t.pool_off.long()), lens)
+    assert torch.equal(pool, t.pool_want), int((pool != t.pool_want).sum())
     s = np.random.default_rng(9).integers(0, t.pool_n, 1500)
     names = [bytes(t.nblob[t.noff[i]:t.noff[i + 1]]) for i in t.pidx[s]]
     blob, off = W.pack(names)
@@ -172,8 +197,9 @@ def test_mix_bench_batch_vs_oracle(c5):
     """The `mix` sub-bench exactly as bench.py runs it: 16M packets of
     bench.gen_mixed (15 % IPv6: IPv4-mapped and 2001:db8:: sources, 90 % of
     destinations inside a rulesV6 prefix) through vc_pipeline_dev on the C5
-    tables, counter finish on a second stream.  Oracle samples per family
-    (the `instanceof IPv4` dispatch, RouteTable.java:44-58), group =
+    tables, counter finish on a second stream.  Every ACL / verdict / route
+    output equal to the exact checkers per family (the `instanceof IPv4`
+    dispatch, RouteTable.java:44-58), oracle samples per family, group =
     pool[host_id] over the whole batch, exact route counters."""
     import torch
     clf, t, dev = c5
@@ -190,6 +216,16 @@ def test_mix_bench_batch_vs_oracle(c5):
     torch.cuda.synchronize()
     clf.counters_enable(False)
     assert torch.equal(grp, pool[hid.long()])
+    assert torch.equal(pool, t.pool_want)
+    # every packet, both families: the v4 rules see IPv6 sources through
+    # Network.maskMatch's cross-family cases (exact.AclChecker.v6)
+    is6 = fam == 6
+    a4, w4 = t.acl_chk.v4(proto, src, dport)
+    a6, w6 = t.acl_chk.v6(proto, src6, dport)
+    assert torch.equal(acl, torch.where(is6, a6, a4)), int((acl != torch.where(is6, a6, a4)).sum())
+    assert torch.equal(allow, torch.where(is6, w6, w4))
+    want_route = torch.where(is6, t.rt6_chk(dst6), t.rt4_chk(dst))
+    assert torch.equal(route, want_route), int((route != want_route).sum())
     six = (fam == 6).cpu().numpy()
     assert 0.13 < six.mean() < 0.17
     rng = np.random.default_rng(77)
