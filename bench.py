@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 import vproxy_amd as V  # noqa: E402
 from vproxy_amd import workloads as W  # noqa: E402
-from vproxy_amd.dist import HitCounterBucket, shard  # noqa: E402
+from vproxy_amd.dist import HitCounterBucket, check_replicated, shard  # noqa: E402
 
 METRIC = "M classifications/sec (ACL+LPM+host) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -644,6 +644,11 @@ def main():
     log("tables built in %.1fs (acl %d+%d, routes %d+%d, groups %d, pool %d names %.0f MB)" % (
         time.time() - t_setup, len(t.tcp), len(t.udp), t.n4, t.n6, len(t.groups), args.pool,
         t.pool_bytes / 1e6))
+    if use_dist:
+        # summed hit counters need identical tables on every rank
+        rows = check_replicated([clf.table_digest(k) for k in
+                                 (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)])
+        log("tables replicated: %d ranks, digests %s" % (len(rows), ["%016x" % d for d in rows[0]]))
     # this rank's shard of the global batch (weak scaling: N = packets x world)
     lo, hi = shard(args.packets * world, rank, world)
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)

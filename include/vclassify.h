@@ -544,6 +544,17 @@ int vc_counters_enable(vc_ctx *ctx, int on);
 int vc_counters_device(vc_ctx *ctx, int kind, uint64_t **dev_ptr, int64_t *n);
 int vc_counters_read(vc_ctx *ctx, int kind, uint64_t *host, int64_t n);
 int vc_counters_reset(vc_ctx *ctx);
+/* Replicated tables (no reference counterpart): a 64-bit
+ * digest of the compiled image of the current snapshot, kind VC_COUNTERS_ACL
+ * (SecurityGroup), _ROUTE (RouteTable) or _GROUP (Upstream).  Ranks that
+ * sum hit counters check first that they compiled identical tables; equal
+ * rule lists give equal digests on any host.  The vc_digest_* forms build
+ * the same images in host memory only (no device, no context). */
+int vc_table_digest(vc_ctx *ctx, int kind, uint64_t *digest);
+int vc_digest_acl(const vc_acl_rule *tcp, int n_tcp, const vc_acl_rule *udp, int n_udp,
+                  int default_allow, uint64_t *digest);
+int vc_digest_routes(const vc_net *v4, int n4, const vc_net *v6, int n6, uint64_t *digest);
+int vc_digest_upstream(const vc_group_annos *groups, int n, uint64_t *digest);
 /* Add the hits of an already-computed output array to the counters of the
  * current snapshot (what vc_counters_enable does automatically after each
  * classify call; exposed so callers can schedule the counting pass):

@@ -1,28 +1,43 @@
 package vproxy.component.secure;
 
+import vproxybase.util.Utils;
+
 import java.io.IOException;
 import java.nio.ByteBuffer;
 
 /**
  * JNI face of libvclassify (include/vclassify.h), selected with
- * -Dclassifier=gpu and loaded the way vfd/posix/PosixFDs.java:12-21 loads
- * vfdposix.  Every batch is a set of direct ByteBuffers (native byte order,
- * SoA, n items); results are indices into the live Java lists, -1 = null /
- * default, so callers map them back exactly as SecurityGroup.allow,
- * RouteTable.lookup and Upstream.searchForGroup would have returned them.
- * Strings are UTF-8 (include/vclassify.h "String encoding").
+ * -Dclassifier=gpu (ClassifierConfig) and loaded the way
+ * vfd/posix/PosixFDs.java:12-21 loads vfdposix.  Every batch is a set of
+ * direct ByteBuffers (native byte order, SoA, n items); results are indices
+ * into the live Java lists, -1 = null / default, so callers map them back
+ * exactly as SecurityGroup.allow, RouteTable.lookup and
+ * Upstream.searchForGroup would have returned them.  Strings are UTF-8
+ * (include/vclassify.h "String encoding").
+ *
+ * Failures: IllegalArgumentException (VC_EINVAL, a short or null buffer,
+ * offsets that decrease), IllegalStateException (VC_ESTATE: nothing compiled
+ * yet), IOException (VC_EDEVICE / VC_ENOMEM: the device failed; sticky in the
+ * HIP runtime).  GpuContext turns the last two into the Java fallback.
  * Native side: jni/vproxy_component_secure_GpuClassifier.c.
  */
 public final class GpuClassifier {
-    static {
-        try {
-            System.loadLibrary("vclassify_jni");
-        } catch (UnsatisfiedLinkError e) {
-            System.out.println("vclassify_jni not found, requires libvclassify_jni.so and "
-                + "libvclassify.so on java.library.path");
-            e.printStackTrace(System.out);
-            System.exit(1);
+    private static boolean loaded;
+
+    /** Loads the JNI library once; prints a hint and exits when it is missing (PosixFDs.java:12-21). */
+    public static synchronized void load() {
+        if (loaded) {
+            return;
         }
+        String lib = ClassifierConfig.libname;
+        try {
+            System.loadLibrary(lib);
+        } catch (UnsatisfiedLinkError e) {
+            System.out.println(lib + " not found, requires lib" + lib + ".so and libvclassify.so on java.library.path");
+            e.printStackTrace(System.out);
+            Utils.exit(1);
+        }
+        loaded = true;
     }
 
     private GpuClassifier() {

@@ -14,8 +14,16 @@
  *     (GetDirectBufferCapacity) before the library sees it;
  *   - a failing call throws (exception.h:10-31): VC_EEXIST ->
  *     AlreadyExistException, VC_ENOTFOUND -> NotFoundException, VC_EXEXC ->
- *     XException, VC_EINVAL -> IllegalArgumentException, anything else ->
- *     IOException, each with vc_last_error() as the message.
+ *     XException, VC_EINVAL -> IllegalArgumentException, VC_ESTATE (nothing
+ *     compiled yet) -> IllegalStateException, anything else (VC_EDEVICE,
+ *     VC_ENOMEM) -> IOException, each with vc_last_error() as the message.
+ *     GpuContext (jni/GpuContext.java) keys its fallback on the last two:
+ *     IllegalStateException answers that one batch with the Java
+ *     classifiers, IOException marks the context dead;
+ *   - offsets buffers are not trusted: they must be non-decreasing from a
+ *     non-negative first entry, so every item's bytes lie inside the span
+ *     the blob's capacity is checked against (the GPU reads them at those
+ *     offsets, on registered buffers straight from host memory).
  *
  * Built only where a JDK is present (jni/Makefile checks JAVA_HOME): this
  * image has no JDK, so tests/native/abi_c.c runs the same call sequence
@@ -35,6 +43,7 @@ static int jni_throw(JNIEnv *env, int rc) {
         : rc == VC_ENOTFOUND ? "vproxybase/util/exception/NotFoundException"
         : rc == VC_EXEXC     ? "vproxybase/util/exception/XException"
         : rc == VC_EINVAL    ? "java/lang/IllegalArgumentException"
+        : rc == VC_ESTATE    ? "java/lang/IllegalStateException"
         : "java/io/IOException";
     c = (*env)->FindClass(env, cls);
     if (c) (*env)->ThrowNew(env, c, vc_last_error());
@@ -45,23 +54,57 @@ static void *addr(JNIEnv *env, jobject buf) {
     return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
 }
 
+/* Throws IllegalArgumentException(msg) once per call and sets *bad. */
+static void refuse(JNIEnv *env, const char *msg, int *bad) {
+    jclass c;
+    if (*bad) return;
+    *bad = 1;
+    c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
 /* The address of direct buffer b when it holds at least `need` bytes (a
- * NULL buffer gives NULL); otherwise throws IllegalArgumentException once
- * and sets *bad, so a short buffer never lets the library read or write
- * past it into JVM memory. */
+ * NULL buffer gives NULL: the argument is optional); otherwise throws
+ * IllegalArgumentException once and sets *bad, so a short buffer never lets
+ * the library read or write past it into JVM memory. */
 static void *buf(JNIEnv *env, jobject b, int64_t need, int *bad) {
     jlong cap;
-    jclass c;
     if (*bad || !b) return NULL;
     cap = (*env)->GetDirectBufferCapacity(env, b);
     if (need >= 0 && cap >= 0 && (int64_t) cap >= need) return (*env)->GetDirectBufferAddress(env, b);
-    *bad = 1;
-    c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-    if (c) (*env)->ThrowNew(env, c, "direct buffer smaller than the batch needs");
+    refuse(env, "direct buffer smaller than the batch needs", bad);
     return NULL;
 }
 
-/* off[n] of an offsets buffer already checked to hold n + 1 ints (0 if absent) */
+/* buf() for an argument the shim reads itself: a NULL buffer is refused
+ * too when the batch needs bytes from it. */
+static void *req(JNIEnv *env, jobject b, int64_t need, int *bad) {
+    if (!*bad && !b && need > 0) refuse(env, "required direct buffer is null", bad);
+    return buf(env, b, need, bad);
+}
+
+/* An offsets buffer of n + 1 ints (NULL allowed unless `required`):
+ * off[0] >= 0 and off[i] <= off[i + 1], so item i's bytes
+ * [off[i], off[i + 1]) lie inside [0, off[n]), the span end_of() sizes the
+ * blob's capacity check by. */
+static const int32_t *offsets(JNIEnv *env, jobject b, jint n, int required, int *bad) {
+    const int32_t *o = required ? req(env, b, ((int64_t) n + 1) * 4, bad)
+                                : buf(env, b, ((int64_t) n + 1) * 4, bad);
+    jint i;
+    if (!o) return NULL;
+    if (o[0] < 0) {
+        refuse(env, "offsets must start at a non-negative value", bad);
+        return NULL;
+    }
+    for (i = 0; i < n; ++i)
+        if (o[i + 1] < o[i]) {
+            refuse(env, "offsets must be non-decreasing", bad);
+            return NULL;
+        }
+    return o;
+}
+
+/* off[n] of a validated offsets buffer (0 if absent) */
 static int64_t end_of(const int32_t *off, jint n) {
     return off && n >= 0 ? (int64_t) off[n] : 0;
 }
@@ -153,8 +196,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileVniRout
    jobject v6Off, jint n) {
     int bad = 0;
     const int32_t *k = buf(env, vni, (int64_t) n * 4, &bad);
-    const int32_t *o4 = buf(env, v4Off, ((int64_t) n + 1) * 4, &bad);
-    const int32_t *o6 = buf(env, v6Off, ((int64_t) n + 1) * 4, &bad);
+    const int32_t *o4 = offsets(env, v4Off, n, 0, &bad);
+    const int32_t *o6 = offsets(env, v6Off, n, 0, &bad);
     const vc_net *a = bad ? NULL : buf(env, v4, end_of(o4, n) * (int64_t) sizeof(vc_net), &bad);
     const vc_net *b = bad ? NULL : buf(env, v6, end_of(o6, n) * (int64_t) sizeof(vc_net), &bad);
     (void) self;
@@ -189,7 +232,7 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_lookupRouteV6
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileUpstream
   (JNIEnv *env, jclass self, jlong ctx, jobject groups, jint n, jobject strings) {
     int bad = 0;
-    const vc_group_annos *g = buf(env, groups, (int64_t) n * (int64_t) sizeof(vc_group_annos), &bad);
+    const vc_group_annos *g = req(env, groups, (int64_t) n * (int64_t) sizeof(vc_group_annos), &bad);
     const char *base = addr(env, strings);
     const int64_t cap = strings ? (int64_t) (*env)->GetDirectBufferCapacity(env, strings) : 0;
     vc_group_annos *c;
@@ -208,7 +251,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileUpstrea
         for (k = 0; k < 2; ++k) {
             const intptr_t h = (intptr_t) src[k]->host, u = (intptr_t) src[k]->uri;
             *dst[k] = *src[k];
-            if ((h >= 0 && h + src[k]->host_len > cap) || (u >= 0 && u + src[k]->uri_len > cap))
+            if ((h >= 0 && (!base || src[k]->host_len < 0 || h + src[k]->host_len > cap)) ||
+                (u >= 0 && (!base || src[k]->uri_len < 0 || u + src[k]->uri_len > cap)))
                 bad = 1;
             dst[k]->host = h < 0 ? NULL : base + h;
             dst[k]->uri = u < 0 ? NULL : base + u;
@@ -230,8 +274,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_searchHints
    jobject port, jobject uriBlob, jobject uriOff, jobject uriNull, jint n, jobject outGroup) {
     int bad = 0;
     const int64_t m = n;
-    const int32_t *ho = buf(env, hostOff, (m + 1) * 4, &bad);
-    const int32_t *uo = buf(env, uriOff, (m + 1) * 4, &bad);
+    const int32_t *ho = offsets(env, hostOff, n, hostBlob != NULL, &bad);
+    const int32_t *uo = offsets(env, uriOff, n, uriBlob != NULL, &bad);
     const uint8_t *hb = bad ? NULL : buf(env, hostBlob, end_of(ho, n), &bad);
     const uint8_t *ub = bad ? NULL : buf(env, uriBlob, end_of(uo, n), &bad);
     const uint8_t *hn = buf(env, hostNull, m, &bad);
@@ -258,8 +302,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_classifyDns
   (JNIEnv *env, jclass self, jlong ctx, jobject qBlob, jobject qOff, jint n, jobject outKind,
    jobject outValue) {
     int bad = 0;
-    const int32_t *o = buf(env, qOff, ((int64_t) n + 1) * 4, &bad);
-    const uint8_t *b = bad ? NULL : buf(env, qBlob, end_of(o, n), &bad);
+    const int32_t *o = offsets(env, qOff, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, qBlob, end_of(o, n), &bad);
     uint8_t *k = buf(env, outKind, n, &bad);
     int32_t *v = buf(env, outValue, (int64_t) n * 4, &bad);
     (void) self;
@@ -300,7 +344,7 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_pipeline
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileServers
   (JNIEnv *env, jclass self, jlong ctx, jobject servers, jobject groupOff, jint nGroups) {
     int bad = 0;
-    const int32_t *o = buf(env, groupOff, ((int64_t) nGroups + 1) * 4, &bad);
+    const int32_t *o = offsets(env, groupOff, nGroups, 0, &bad);
     const vc_server *s = bad ? NULL
                              : buf(env, servers, end_of(o, nGroups) * (int64_t) sizeof(vc_server), &bad);
     (void) self;
@@ -349,8 +393,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_parsePackets
    jobjectArray out) {
     int bad = 0;
     vc_pkt_out o;
-    const int32_t *of = buf(env, off, ((int64_t) n + 1) * 4, &bad);
-    const uint8_t *b = bad ? NULL : buf(env, blob, end_of(of, n), &bad);
+    const int32_t *of = offsets(env, off, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, blob, end_of(of, n), &bad);
     (void) self;
     pkt_out(env, out, n, &o, &bad);
     if (bad) return;
@@ -366,8 +410,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_switchClassify
     int bad = 0;
     const int64_t m = n;
     vc_pkt_out o;
-    const int32_t *of = buf(env, off, (m + 1) * 4, &bad);
-    const uint8_t *b = bad ? NULL : buf(env, blob, end_of(of, n), &bad);
+    const int32_t *of = offsets(env, off, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, blob, end_of(of, n), &bad);
     const uint8_t *rf = buf(env, remoteFamily, m, &bad);
     const uint32_t *r4 = buf(env, remote4, m * 4, &bad);
     const uint8_t *r6 = buf(env, remote6, m * 16, &bad);
@@ -393,8 +437,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_dnsDatagrams
     vc_dnsd_out o;
     void *f[6];
     int i;
-    const int32_t *of = buf(env, off, (m + 1) * 4, &bad);
-    const uint8_t *b = bad ? NULL : buf(env, blob, end_of(of, n), &bad);
+    const int32_t *of = offsets(env, off, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, blob, end_of(of, n), &bad);
     const uint8_t *rf = buf(env, remoteFamily, m, &bad);
     const uint32_t *r4 = buf(env, remote4, m * 4, &bad);
     const uint8_t *r6 = buf(env, remote6, m * 16, &bad);
@@ -412,9 +456,9 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_compileCerts
   (JNIEnv *env, jclass self, jlong ctx, jobject names, jobject off, jobject holder,
    jint nNames, jint nHolders) {
     int bad = 0;
-    const int32_t *o = buf(env, off, ((int64_t) nNames + 1) * 4, &bad);
-    const char *blob = bad ? NULL : buf(env, names, end_of(o, nNames), &bad);
-    const int32_t *h = buf(env, holder, (int64_t) nNames * 4, &bad);
+    const int32_t *o = offsets(env, off, nNames, 1, &bad);
+    const char *blob = bad ? NULL : req(env, names, end_of(o, nNames), &bad);
+    const int32_t *h = req(env, holder, (int64_t) nNames * 4, &bad);
     const char **ptrs;
     int32_t *lens;
     jint i;
@@ -441,8 +485,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_chooseCerts
   (JNIEnv *env, jclass self, jlong ctx, jobject sni, jobject off, jobject isNull, jint n,
    jobject outHolder) {
     int bad = 0;
-    const int32_t *o = buf(env, off, ((int64_t) n + 1) * 4, &bad);
-    const uint8_t *s = bad ? NULL : buf(env, sni, end_of(o, n), &bad);
+    const int32_t *o = offsets(env, off, n, 1, &bad);
+    const uint8_t *s = bad ? NULL : req(env, sni, end_of(o, n), &bad);
     const uint8_t *z = buf(env, isNull, n, &bad);
     int32_t *h = buf(env, outHolder, (int64_t) n * 4, &bad);
     (void) self;
@@ -464,8 +508,8 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_mirrorSwitch
   (JNIEnv *env, jclass self, jlong ctx, jint origin, jobject blob, jobject off, jint n,
    jint layer, jobject outMirrors) {
     int bad = 0;
-    const int32_t *o = buf(env, off, ((int64_t) n + 1) * 4, &bad);
-    const uint8_t *b = bad ? NULL : buf(env, blob, end_of(o, n), &bad);
+    const int32_t *o = offsets(env, off, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, blob, end_of(o, n), &bad);
     uint64_t *m = buf(env, outMirrors, (int64_t) n * 8, &bad);
     (void) self;
     if (bad) return;

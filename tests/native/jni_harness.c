@@ -7,13 +7,20 @@
  *   jni_harness cpu  -- no GPU: create throws IOException; a buffer shorter
  *                       than the batch throws IllegalArgumentException
  *                       before the library is called; an annotation string
- *                       outside the strings buffer is refused.
+ *                       outside the strings buffer is refused; a null
+ *                       required buffer and offsets that are negative or
+ *                       decrease are refused; injected statuses map to the
+ *                       exceptions GpuContext keys its fallback on
+ *                       (VC_EDEVICE / VC_ENOMEM -> IOException, VC_ESTATE ->
+ *                       IllegalStateException).
  *   jni_harness gpu  -- through the shim vs the C ABI directly: ACL, routes,
  *                       per-VNI routes + switch, and compileUpstream twice
  *                       on one groups buffer (rebased in a copy, so the
  *                       second compile reads the same offsets).
  * Prints "JNI OK" and exits 0 when every check holds.
  */
+#define _GNU_SOURCE
+#include <dlfcn.h>
 #include <jni.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -89,6 +96,31 @@ void J(searchHints)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject,
 void J(switchClassify)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jobject, jobject,
                        jobject, jint, jobjectArray, jobject, jobject, jobject);
 
+void J(compileCerts)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jint, jint);
+void J(classifyDns)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jobject, jobject);
+
+/* Fault injection.  The executable's definitions of these entry points
+ * preempt libvclassify's for the shim linked into it: with inject_rc set
+ * they return that status as the library would after a device error (or
+ * before anything is compiled), otherwise they forward to the library. */
+static int inject_rc;
+typedef int (*acl_fn)(vc_ctx *, const uint8_t *, const uint32_t *, const uint16_t *, int64_t,
+                      int32_t *, uint8_t *);
+int vc_acl_classify_v4(vc_ctx *ctx, const uint8_t *proto, const uint32_t *src4,
+                       const uint16_t *port, int64_t n, int32_t *out_idx, uint8_t *out_allow) {
+    static acl_fn real;
+    if (inject_rc) return inject_rc;
+    if (!real) *(void **) &real = dlsym(RTLD_NEXT, "vc_acl_classify_v4");
+    return real(ctx, proto, src4, port, n, out_idx, out_allow);
+}
+typedef int (*route_fn)(vc_ctx *, const uint32_t *, int64_t, int32_t *);
+int vc_route_lookup_v4(vc_ctx *ctx, const uint32_t *dst4, int64_t n, int32_t *out) {
+    static route_fn real;
+    if (inject_rc) return inject_rc;
+    if (!real) *(void **) &real = dlsym(RTLD_NEXT, "vc_route_lookup_v4");
+    return real(ctx, dst4, n, out);
+}
+
 static struct _jobject B(void *p, jlong cap) {
     struct _jobject o;
     o.p = p;
@@ -150,6 +182,53 @@ static void cpu_mode(void) {
     expect_throw("java/lang/IllegalArgumentException", "outside the strings buffer",
                  "annotation string past the buffer");
     CHECK((intptr_t) g.handle.host == 2, "the caller's groups buffer is left as it was");
+    /* a null groups buffer with n > 0: refused, never dereferenced */
+    J(compileUpstream)(env, NULL, 0, NULL, 1, &bstr);
+    expect_throw("java/lang/IllegalArgumentException", "required", "null groups buffer");
+    /* an annotation offset with no strings buffer at all */
+    g.handle.host = (const char *) (intptr_t) 0;
+    g.handle.host_len = 0;
+    J(compileUpstream)(env, NULL, 0, &bg, 1, NULL);
+    expect_throw("java/lang/IllegalArgumentException", "outside the strings buffer",
+                 "annotation offset without a strings buffer");
+    {   /* certificate names: offsets that decrease or start negative, a null
+         * offsets buffer -- each refused before any pointer is formed */
+        char names[8] = "abcde";
+        int32_t bad_off[3] = {0, 100000, 5}, neg_off[3] = {-4, 0, 5}, holder[2] = {0, 0};
+        struct _jobject bn = B(names, 5), bo1 = B(bad_off, 12), bo2 = B(neg_off, 12),
+                        bh = B(holder, 8);
+        J(compileCerts)(env, NULL, 0, &bn, &bo1, &bh, 2, 1);
+        expect_throw("java/lang/IllegalArgumentException", "non-decreasing", "decreasing offsets");
+        J(compileCerts)(env, NULL, 0, &bn, &bo2, &bh, 2, 1);
+        expect_throw("java/lang/IllegalArgumentException", "non-negative", "negative offset");
+        J(compileCerts)(env, NULL, 0, &bn, NULL, &bh, 2, 1);
+        expect_throw("java/lang/IllegalArgumentException", "required", "null offsets");
+        J(compileCerts)(env, NULL, 0, &bn, &bo1, NULL, 2, 1);
+        expect_throw("java/lang/IllegalArgumentException", "", "null holder buffer");
+    }
+    {   /* a batch call whose offsets decrease: refused before the library */
+        uint8_t q[16] = {0}, kind[2];
+        int32_t qoff[3] = {0, 9, 4}, val[2];
+        struct _jobject bq2 = B(q, 16), bo3 = B(qoff, 12), bk = B(kind, 2), bv = B(val, 8);
+        J(classifyDns)(env, NULL, 0, &bq2, &bo3, 2, &bk, &bv);
+        expect_throw("java/lang/IllegalArgumentException", "non-decreasing", "dns offsets");
+    }
+    /* the statuses GpuContext keys its fallback on (jni/GpuContext.java) */
+    bs.cap = 32;
+    bo.cap = 32;
+    inject_rc = VC_EDEVICE;
+    J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, 8, &bo, NULL);
+    expect_throw("java/io/IOException", "", "VC_EDEVICE -> IOException (context dead)");
+    inject_rc = VC_ENOMEM;
+    J(lookupRouteV4)(env, NULL, 0, &bs, 8, &bo);
+    expect_throw("java/io/IOException", "", "VC_ENOMEM -> IOException");
+    inject_rc = VC_ESTATE;
+    J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, 8, &bo, NULL);
+    expect_throw("java/lang/IllegalStateException", "", "VC_ESTATE -> IllegalStateException");
+    inject_rc = VC_EINVAL;
+    J(lookupRouteV4)(env, NULL, 0, &bs, 8, &bo);
+    expect_throw("java/lang/IllegalArgumentException", "", "VC_EINVAL -> IllegalArgumentException");
+    inject_rc = 0;
 }
 
 static uint32_t rnd_state = 12345;

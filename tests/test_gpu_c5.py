@@ -141,6 +141,11 @@ def test_c5_bench_tables_and_pool(c5):
     assert len(t.tcp) + len(t.udp) == 10000
     assert t.n4 == 980848 and t.n6 == 200000
     assert len(t.groups) == 100000 and t.pool_n == 16 << 20
+    # the compiled snapshots' digests equal the host-only builds (what the
+    # replica check of bench.py / dist.check_replicated compares across ranks)
+    assert clf.table_digest(V.COUNTERS_ACL) == V.digest_acl(t.tcp, t.udp, False)
+    assert clf.table_digest(V.COUNTERS_ROUTE) == V.digest_routes(t.v4_list.copy(), t.v6_list.copy())
+    assert clf.table_digest(V.COUNTERS_GROUP) == V.digest_upstream(t.groups)
     pool = clf.hint_search((t.pool_blob, t.pool_off, None))
     torch.cuda.synchronize()
     lens = torch.from_numpy(np.diff(t.noff.astype(np.int64))[t.pidx]).to(dev)

@@ -136,3 +136,73 @@ def test_cu_split_balanced_over_xcds(k):
     for share in (pick, rest):
         per_xcd = [sum(1 for c in share if c % 8 == x) for x in range(8)]
         assert len(set(per_xcd)) == 1 and per_xcd[0] % 4 == 0, per_xcd
+
+
+def _c5_digests(perturb):
+    """The C5 tables exactly as bench.c5_tables compiles them, built in host
+    memory by libvclassify's own compilers (vc_digest_*: no device)."""
+    import vproxy_amd as V
+    t = B.c5_rule_tables()
+    if perturb:                                   # one rule's port range differs
+        t.tcp = t.tcp.copy()
+        t.tcp["max_port"][17] = (int(t.tcp["max_port"][17]) + 1) % 65536
+    rt = V.RouteTable()
+    allnets = np.concatenate([W.v4_nets(t.net, t.plen), W.v6_nets(t.hi, t.lo, t.p6)])
+    arr, n_all, keep = W.as_ctypes(allnets, V._lib.VcNet)
+    rt.add_rules("bgp", arr, n=n_all)
+    a4, n4 = rt.rules_raw(4)
+    a6, n6 = rt.rules_raw(6)
+    v4 = np.frombuffer(bytes(a4)[:n4 * 40], W.NET_DT).copy()
+    v6 = np.frombuffer(bytes(a6)[:n6 * 40], W.NET_DT).copy()
+    assert n4 == 980848 and n6 == 200000
+    return [V.digest_acl(t.tcp, t.udp, False), V.digest_routes(v4, v6),
+            V.digest_upstream(t.groups)]
+
+
+def _replica_worker(rank, world, port, perturb_rank, q):
+    from vproxy_amd.dist import check_replicated
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            d = _c5_digests(rank == perturb_rank)
+        except Exception as e:                     # report, do not leave the parent waiting
+            q.put((rank, "error", repr(e)))
+            raise
+        try:
+            q.put((rank, "ok", check_replicated(d)))
+        except RuntimeError as e:
+            q.put((rank, "mismatch", str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb_rank", [-1, 1])
+def test_replicated_c5_images_are_identical(perturb_rank):
+    """Replicated tables are what make the summed hit counters meaningful:
+    two spawned ranks compile the C5-shaped tables (10k ACL rules, 980,848 +
+    200,000 routes, 100k groups) through libvclassify and the digests of
+    the compiled images agree (vproxy_amd.dist.check_replicated, which
+    bench.py runs before timing at N > 1); one differing rule on one rank is
+    caught on every rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, perturb_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    assert all(r[1] != "error" for r in res), res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if perturb_rank < 0:
+        assert [r[1] for r in res] == ["ok", "ok"]
+        rows = res[0][2]
+        assert rows[0] == rows[1] and len(set(rows[0])) == 3
+    else:
+        assert [r[1] for r in res] == ["mismatch", "mismatch"]
+        assert "[1]" in res[0][2]

@@ -14,6 +14,6 @@ from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,
                    LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6, SWITCH_NO_TABLE)
 from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
                          acl_rule_array, group_array, net_array, pack_strings, parse_ip,
-                         server_array, cn_of_dn)
+                         server_array, cn_of_dn, digest_acl, digest_routes, digest_upstream)
 
 __all__ = ["Classifier", "Network", "SecurityGroup", "RouteTable", "Annotations", "parse_ip"]

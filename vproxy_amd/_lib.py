@@ -213,6 +213,11 @@ def lib():
         L.vc_counters_read.argtypes = [vp, i32, vp, i64]
         L.vc_counters_reset.argtypes = [vp]
         L.vc_counters_add_dev.argtypes = [vp, i32, vp, vp, i32, i64, vp]
+        u64p = P(C.c_uint64)
+        L.vc_table_digest.argtypes = [vp, i32, u64p]
+        L.vc_digest_acl.argtypes = [P(VcAclRule), i32, P(VcAclRule), i32, i32, u64p]
+        L.vc_digest_routes.argtypes = [P(VcNet), i32, P(VcNet), i32, u64p]
+        L.vc_digest_upstream.argtypes = [P(VcGroupAnnos), i32, u64p]
         cpp = P(C.c_char_p)
         L.vc_prometheus_format.argtypes = [P(VcMetric), i32, cpp, cpp, i32, vp, i64, P(i64)]
         L.vc_prometheus_hits.argtypes = [vp, i32, i32, vp, i32, i32, vp, i32, C.c_char_p, vp, i64,

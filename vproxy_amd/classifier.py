@@ -801,6 +801,13 @@ class Classifier:
     def counters_reset(self):
         check(lib().vc_counters_reset(self.h))
 
+    def table_digest(self, kind):
+        """vc_table_digest: 64-bit digest of the compiled image of the current
+        snapshot (kind COUNTERS_ACL / _ROUTE / _GROUP)."""
+        d = C.c_uint64()
+        check(lib().vc_table_digest(self.h, kind, C.byref(d)))
+        return d.value
+
     def counters_prometheus(self, extra_labels=None):
         """The current hit counters as Prometheus text (vc_counters_prometheus)."""
         from .prometheus import _b as pb, _call_text
@@ -811,3 +818,31 @@ class Classifier:
         """Explicit counting pass over a device output array (torch tensor)."""
         check(lib().vc_counters_add_dev(self.h, kind, _ptr(out), _ptr(aux), family, len(out),
                                         _stream()))
+
+
+def digest_acl(tcp, udp, default_allow=False):
+    """vc_digest_acl over RULE_DT arrays (host only, no device)."""
+    from . import workloads as W
+    a, na, ka = W.as_ctypes(tcp, VcAclRule)
+    b, nb, kb = W.as_ctypes(udp, VcAclRule)
+    d = C.c_uint64()
+    check(lib().vc_digest_acl(a, na, b, nb, 1 if default_allow else 0, C.byref(d)))
+    return d.value
+
+
+def digest_routes(v4, v6):
+    """vc_digest_routes over NET_DT arrays in list order (host only)."""
+    from . import workloads as W
+    a, na, ka = W.as_ctypes(v4, VcNet)
+    b, nb, kb = W.as_ctypes(v6, VcNet)
+    d = C.c_uint64()
+    check(lib().vc_digest_routes(a, na, b, nb, C.byref(d)))
+    return d.value
+
+
+def digest_upstream(groups):
+    """vc_digest_upstream over (handle annotations, group annotations) pairs (host only)."""
+    arr, n, keep = group_array(groups)
+    d = C.c_uint64()
+    check(lib().vc_digest_upstream(arr, n, C.byref(d)))
+    return d.value

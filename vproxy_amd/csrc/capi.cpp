@@ -40,8 +40,11 @@ int hip_fail(hipError_t e, const char* what) {
 // Retired device memory.  A snapshot's last reference can drop on any
 // thread -- often an event-loop thread finishing a classify call that pinned
 // the old tables -- and hipFree waits for the whole device.  Its buffers go
-// here instead, and the control thread frees them (vc_compile_*, vc_destroy):
+// here instead, and the control thread frees them (vc_compile_*,
+// vc_servers_set_health, vc_counters_read after its device sync, vc_destroy):
 // the thread that recompiles pays the wait, the classify threads never do.
+// Retention: buffers whose last pin dropped after the publish that replaced
+// them wait for the next of those calls.
 // ---------------------------------------------------------------------------
 struct Graveyard {
     std::mutex mu;
@@ -545,6 +548,7 @@ struct Snapshot {
     std::vector<std::unique_ptr<DevBuf>> bufs;
     unsigned long long* counters = nullptr;
     int64_t n_counters = 0;
+    uint64_t digest = 0;           // vc::digest of the host-built image (vc_table_digest)
 
     void alloc_counters(Upload& up, int64_t n) {
         counters = up.zeros(*this, n);
@@ -721,6 +725,7 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
     s->img.n_tcp = b.n_tcp;
     s->img.n_udp = b.n_udp;
     s->img.default_allow = b.default_allow;
+    s->digest = vc::digest(b);
     s->alloc_counters(up, int64_t(n_tcp) + n_udp + 2);
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "ACL upload");
     ctx->publish(ctx->acl, std::shared_ptr<const AclSnap>(std::move(s)));
@@ -901,6 +906,7 @@ int vc_compile_routes(vc_ctx* ctx, const vc_net* v4, int n4, const vc_net* v6, i
     }
     s->n4 = n4;
     s->n6 = n6;
+    s->digest = vc::digest(t4, t6);
     s->alloc_counters(up, int64_t(n4) + n6 + 2);
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "route upload");
     ctx->publish(ctx->route, std::shared_ptr<const RouteSnap>(std::move(s)));
@@ -1056,6 +1062,7 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     s->img.wildcard_slot = b.wildcard_slot;
     s->img.uri_star_slot = b.uri_star_slot;
     s->img.has_uri_keys = b.has_uri_keys;
+    s->digest = vc::digest(b);
     s->alloc_counters(up, int64_t(n) + 1);
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "hint upload");
     ctx->publish(ctx->hint, std::shared_ptr<const HintSnap>(std::move(s)));
@@ -1904,7 +1911,51 @@ int vc_counters_read(vc_ctx* ctx, int kind, uint64_t* host, int64_t n) {
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess)
         e = hipMemcpy(host, s->counters, size_t(s->n_counters) * 8, hipMemcpyDeviceToHost);
+    // the device is idle here, so freeing retired snapshot buffers costs no
+    // wait: a deployment that rarely recompiles but reads its counters
+    // (Prometheus scrapes) does not keep superseded tables alive
+    if (e == hipSuccess) ctx->grave->drain();
     return e == hipSuccess ? VC_OK : hip_fail(e, "counter read");
+}
+
+int vc_table_digest(vc_ctx* ctx, int kind, uint64_t* digest) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (!digest) return fail(VC_EINVAL, "null digest");
+    std::shared_ptr<const void> keep;
+    const Snapshot* s = counter_snap(ctx, kind, &keep);
+    if (!s) return fail(VC_ESTATE, "no table compiled for this kind");
+    *digest = s->digest;
+    return VC_OK;
+}
+
+// Host-only digests: the same builds as the compile calls, no device.
+int vc_digest_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_udp,
+                  int default_allow, uint64_t* digest) {
+    if ((n_tcp && !tcp) || (n_udp && !udp) || !digest) return fail(VC_EINVAL, "null argument");
+    vc::AclBuilt b;
+    if (int rc = vc::build_acl(tcp, n_tcp, udp, n_udp, default_allow, &b)) return fail(rc, "invalid rule");
+    *digest = vc::digest(b);
+    return VC_OK;
+}
+
+int vc_digest_routes(const vc_net* v4, int n4, const vc_net* v6, int n6, uint64_t* digest) {
+    if ((n4 && !v4) || (n6 && !v6) || n4 < 0 || n6 < 0 || !digest)
+        return fail(VC_EINVAL, "bad rule arrays");
+    vc::TrieBuilt t4, t6;
+    int rc;
+    if ((rc = vc::build_trie(v4, n4, 0, &t4)) != VC_OK) return fail(rc, "invalid IPv4 route rule");
+    if ((rc = vc::build_trie(v6, n6, 1, &t6)) != VC_OK) return fail(rc, "invalid IPv6 route rule");
+    *digest = vc::digest(t4, t6);
+    return VC_OK;
+}
+
+int vc_digest_upstream(const vc_group_annos* groups, int n, uint64_t* digest) {
+    if (n < 0 || (n && !groups) || !digest) return fail(VC_EINVAL, "bad group array");
+    vc::HintBuilt b;
+    if (int rc = vc::build_hints(groups, n, &b)) return fail(rc, "invalid annotations");
+    *digest = vc::digest(b);
+    return VC_OK;
 }
 
 int vc_counters_reset(vc_ctx* ctx) {

@@ -743,4 +743,75 @@ int build_servers(const vc_server* servers, const int32_t* group_off, int n_grou
     return VC_OK;
 }
 
+namespace {
+
+struct Digest {
+    uint64_t h = 14695981039346656037ull;
+    void word(uint64_t w) { h = (h ^ w) * 1099511628211ull; }
+    void bytes(const void* p, size_t n) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        word(n);
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t w;
+            std::memcpy(&w, b + i, 8);
+            word(w);
+        }
+        uint64_t w = 0;
+        std::memcpy(&w, b + i, n - i);
+        word(w);
+    }
+    template <class T>
+    void vec(const std::vector<T>& v) { bytes(v.data(), v.size() * sizeof(T)); }
+};
+
+}  // namespace
+
+uint64_t digest(const AclBuilt& b) {
+    Digest d;
+    for (int l = 0; l < 2; ++l)
+        for (int f = 0; f < 2; ++f) {
+            const AclFamilyBuilt& x = b.fam[l][f];
+            d.vec(x.bounds4);
+            d.vec(x.bounds6);
+            d.vec(x.desc);
+            d.vec(x.rec);
+            d.vec(x.pieces);
+            d.vec(x.dir4);
+            d.word(uint64_t(uint32_t(x.nb)) | uint64_t(uint32_t(x.dir_bits)) << 32);
+        }
+    d.vec(b.allow);
+    d.word(uint64_t(uint32_t(b.n_tcp)) | uint64_t(uint32_t(b.n_udp)) << 32);
+    d.word(uint64_t(b.default_allow));
+    return d.h;
+}
+
+uint64_t digest(const TrieBuilt& t4, const TrieBuilt& t6) {
+    Digest d;
+    for (const TrieBuilt* t : {&t4, &t6}) {
+        d.vec(t->nodes);
+        d.word(uint64_t(uint32_t(t->root_bits)) | uint64_t(uint32_t(t->key_bits)) << 32);
+        d.word(uint64_t(uint32_t(t->n_rules)) | uint64_t(uint32_t(t->n_nodes)) << 32);
+        d.word(uint64_t(uint32_t(t->n_records)));
+    }
+    return d.h;
+}
+
+uint64_t digest(const HintBuilt& b) {
+    Digest d;
+    d.vec(b.blob);
+    d.vec(b.host.tags);
+    d.vec(b.host.recs);
+    d.vec(b.host.ext);
+    d.word(uint64_t(uint32_t(b.host.n)));
+    d.vec(b.uri_slots);
+    d.vec(b.uri_tags);
+    d.vec(b.lists);
+    d.vec(b.port_mins);
+    d.vec(b.groups);
+    d.word(uint64_t(uint32_t(b.n_groups)) | uint64_t(uint32_t(b.wildcard_slot)) << 32);
+    d.word(uint64_t(uint32_t(b.uri_star_slot)) | uint64_t(uint32_t(b.has_uri_keys)) << 32);
+    return d.h;
+}
+
 }  // namespace vc

@@ -111,6 +111,13 @@ struct ServersBuilt {
 int build_servers(const vc_server* servers, const int32_t* group_off, int n_groups,
                   ServersBuilt* out);
 
+// Digest of a host-built image: 64-bit FNV-1a over its 8-byte words (each
+// array prefixed by its length, scalars included), so ranks that replicate
+// the tables can check they compiled the same image (vc_table_digest).
+uint64_t digest(const AclBuilt& b);
+uint64_t digest(const TrieBuilt& t4, const TrieBuilt& t6);
+uint64_t digest(const HintBuilt& b);
+
 // 32-bit FNV-1a over bytes, forwards and right-to-left (must match device code).
 inline uint32_t fnv_fwd(const uint8_t* p, size_t n) {
     uint32_t h = 2166136261u;

@@ -71,34 +71,46 @@ private:
 // memset before reuse; slots go round-robin (kSlots launches in flight, far
 // more than the context's streams ever queue).  A launch that fails or
 // faults part-way can leave its slot nonzero, and every later launch on
-// that slot would skip work: the context marks the ring dirty on any device
-// error (capi.cpp `launched`), and the next launch re-zeroes the whole ring
-// on its stream first.
+// that slot would skip work.  The context bumps the ring's error epoch on
+// any device error (capi.cpp `launched`); a slot handed out afterwards whose
+// own epoch is older is zeroed first, with a 4-byte memset on the launching
+// stream, so it is ordered before the kernel that uses it and touches no
+// other slot: zeroing the whole ring instead could reset the counter of a
+// ticketed kernel still running on another stream (the pool pass beside the
+// pipeline, another caller's DNS launch), which would then hand its tickets
+// out twice and leave its slot nonzero.  A slot comes round again only
+// kSlots launches later, long after its previous kernel ended.
 class TicketRing {
 public:
     static constexpr uint32_t kSlots = 4096;
     hipError_t init() {
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_), kSlots * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMemset(d_, 0, kSlots * sizeof(uint32_t));
+        for (uint32_t k = 0; k < kSlots; ++k) epoch_of_[k].store(0);
         return e;
     }
     void destroy() {            // after the device is idle
         if (d_) (void)hipFree(d_);
         d_ = nullptr;
     }
-    void mark_dirty() { dirty_.store(true); }
+    void mark_dirty() { epoch_.fetch_add(1); }
     uint32_t* next(hipStream_t s) {
         if (!d_) return nullptr;
-        if (dirty_.exchange(false) &&
-            hipMemsetAsync(d_, 0, kSlots * sizeof(uint32_t), s) != hipSuccess)
-            dirty_.store(true);
-        return d_ + next_.fetch_add(1) % kSlots;
+        const uint32_t k = next_.fetch_add(1) % kSlots;
+        const uint32_t e = epoch_.load();
+        if (epoch_of_[k].load() != e) {
+            // a slot that cannot be zeroed is not used: null = the static split
+            if (hipMemsetAsync(d_ + k, 0, sizeof(uint32_t), s) != hipSuccess) return nullptr;
+            epoch_of_[k].store(e);
+        }
+        return d_ + k;
     }
 
 private:
     uint32_t* d_ = nullptr;
     std::atomic<uint32_t> next_{0};
-    std::atomic<bool> dirty_{false};
+    std::atomic<uint32_t> epoch_{0};
+    std::atomic<uint32_t> epoch_of_[kSlots];
 };
 
 struct LaunchCfg {

@@ -16,7 +16,7 @@ the north-star's "per-rule hit counters" (BASELINE.json).
 """
 import ctypes as C
 
-__all__ = ["shard", "HitCounterBucket"]
+__all__ = ["shard", "HitCounterBucket", "check_replicated"]
 
 
 def shard(n, rank, world):
@@ -91,3 +91,26 @@ class HitCounterBucket:
         import torch.distributed as dist
         dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=group)
         return self.views
+
+
+def check_replicated(digests, group=None):
+    """Summed hit counters mean something only if every rank classified
+    against the same tables.  `digests`: this rank's table digests
+    (Classifier.table_digest per counter space, or the host-only
+    vproxy_amd.digest_* forms).  All-gathers them over the process group
+    (one small collective, before any batch) and raises if any rank
+    compiled a different image.  Returns the list of every rank's digests."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([d - (1 << 64) if d >= 1 << 63 else d for d in digests],
+                        dtype=torch.int64)
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        mine = mine.cuda()
+    got = [torch.zeros_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(got, mine, group=group)
+    rows = [[int(x) & ((1 << 64) - 1) for x in g.cpu().tolist()] for g in got]
+    bad = [r for r, row in enumerate(rows) if row != rows[0]]
+    if bad:
+        raise RuntimeError("ranks %s compiled different tables than rank 0: %s" % (bad, rows))
+    return rows
