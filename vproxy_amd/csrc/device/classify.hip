@@ -45,18 +45,28 @@ __device__ __forceinline__ int fence_count(int nb, int shift) {
     return (nb + (1 << shift) - 1) >> shift;
 }
 
+// The protocol's member of a per-list pair, chosen by value.  Indexing the
+// pair with a runtime list number (a.f[tcp ? 0 : 1]) keeps the whole context
+// struct in scratch memory and reads every member through it: the two-quad
+// ACL kernel carried a 96-byte private segment that way and its speed
+// depended on the build (profiles/r03_ab_acl_quads.txt).
+// tests/test_codegen_cpu.py checks the hot kernels use no scratch.
+template <class T>
+__device__ __forceinline__ T per_list(bool tcp, T x0, T x1) { return tcp ? x0 : x1; }
+
 // kL: a.f is staged in LDS (else it is the global boundary list, shift 0)
 template <bool kL>
 __device__ __forceinline__ uint32_t acl_v4_one(const AclV4Ctx& a, bool tcp, uint32_t key,
                                                uint32_t port) {
-    const int l = tcp ? 0 : 1;
-    int j = bsearch_u32<kL>(a.f[l], a.nf[l], key);
+    int j = bsearch_u32<kL>(per_list(tcp, a.f[0], a.f[1]), per_list(tcp, a.nf[0], a.nf[1]), key);
     if (kL && a.shift) {
         const int base = j << a.shift;
-        const int rest = a.nb[l] - base;
-        j = base + bsearch_u32(a.b[l] + base, rest < (1 << a.shift) ? rest : (1 << a.shift), key);
+        const int rest = per_list(tcp, a.nb[0], a.nb[1]) - base;
+        j = base + bsearch_u32(per_list(tcp, a.b[0], a.b[1]) + base,
+                               rest < (1 << a.shift) ? rest : (1 << a.shift), key);
     }
-    return acl_value(a.rec[l], a.pieces[l], j, port);
+    return acl_value(per_list(tcp, a.rec[0], a.rec[1]), per_list(tcp, a.pieces[0], a.pieces[1]),
+                     j, port);
 }
 
 // Four lookups in lockstep (VC_ACL_LOCKSTEP, boundaries fully staged in
@@ -323,15 +333,16 @@ __device__ __forceinline__ AclV6Ctx stage_fences(const AclImage& img, uint64_t* 
 
 __device__ __forceinline__ uint32_t acl_v6_fenced(const AclV6Ctx& a, bool tcp, uint4 w,
                                                   uint32_t port) {
-    const int l = tcp ? 0 : 1;
     uint64_t hi, lo;
     v6_key(w, &hi, &lo);
-    const int k = bsearch_u128<true>(a.f[l], a.nf[l], hi, lo);
+    const int k = bsearch_u128<true>(per_list(tcp, a.f[0], a.f[1]), per_list(tcp, a.nf[0], a.nf[1]),
+                                     hi, lo);
     const int base = k << a.shift;
-    const int rest = a.nb[l] - base;
+    const int rest = per_list(tcp, a.nb[0], a.nb[1]) - base;
     const int len = rest < (1 << a.shift) ? rest : (1 << a.shift);
-    const int j = base + bsearch_u128(a.b[l] + 2 * int64_t(base), len, hi, lo);
-    return acl_value(a.rec[l], a.pieces[l], j, port);
+    const int j = base + bsearch_u128(per_list(tcp, a.b[0], a.b[1]) + 2 * int64_t(base), len, hi, lo);
+    return acl_value(per_list(tcp, a.rec[0], a.rec[1]), per_list(tcp, a.pieces[0], a.pieces[1]),
+                     j, port);
 }
 
 __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
