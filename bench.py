@@ -606,6 +606,8 @@ def main():
     ap.add_argument("--pool-cus", type=int, default=0,
                     help="CU partition: the pool pass and the counter finish on this many CUs "
                          "(a CU-masked stream), the pipeline kernel on the rest (0: no masks)")
+    ap.add_argument("--v6-frac", type=float, default=0.15,
+                    help="mix / mixhost: share of IPv6 packets (C3's mix is 0.15)")
     ap.add_argument("--dist", action="store_true",
                     help="use the process group and the counter all-reduce even at N = 1")
     args = ap.parse_args()
@@ -1289,7 +1291,8 @@ def mix_bench(args, clf, dev, rank, O):
     reads of scattered 16-byte addresses ran at 7 GB/s)."""
     t = c5_tables(clf, dev, args.pool)
     n = args.packets if args.workload == "mix" else 32 << 20
-    fam, proto, src, dst, src6, dst6, dport, hid = gen_mixed(0, n, t, t.pool_n, dev=dev)
+    fam, proto, src, dst, src6, dst6, dport, hid = gen_mixed(0, n, t, t.pool_n, dev=dev,
+                                                             v6_frac=args.v6_frac)
     pool = clf.hint_search((t.pool_blob, t.pool_off, None))
     torch.cuda.synchronize()
     n6 = int((fam == 6).sum())
@@ -1368,6 +1371,7 @@ def mix_bench(args, clf, dev, rank, O):
                         "algorithmic_bytes": unit},
            "cpu_baseline": cpu}
     res.update(extra)
+    res["v6_frac"] = args.v6_frac
     if rank == 0:
         print(json.dumps(res), flush=True)
     clf.close()

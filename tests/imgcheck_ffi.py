@@ -48,7 +48,7 @@ def acl(tcp, udp, dflt, family, proto, src, port):
     n = len(port)
     out = np.empty(n, np.int32)
     allow = np.empty(n, np.uint8)
-    stats = np.zeros(8, np.int32)
+    stats = np.zeros(10, np.int32)    # [list][family] nb, np; then v6 lookups on v4-only lists
     rc = lib().ic_acl(P(tcp), len(tcp), P(udp), len(udp), 1 if dflt else 0, family, P(proto),
                       P(src), P(port), n, P(out), P(allow), P(stats))
     assert rc == 0, rc

@@ -27,6 +27,7 @@ AclFamilyImage fam_img(const vc::AclFamilyBuilt& b) {
     f.dir_bits = b.dir_bits;
     f.nb = b.nb;
     f.np = int32_t(b.pieces.size() / 2);
+    f.v4_only = b.v4_only;
     return f;
 }
 
@@ -90,6 +91,13 @@ int ic_acl(const vc_acl_rule* tcp, int nt, const vc_acl_rule* udp, int nu, int d
             uint64_t hi, lo;
             v6_key(static_cast<const uint4*>(src)[i], &hi, &lo);
             j = bsearch_u128(f.bounds6, f.nb, hi, lo);
+            // a list of plain IPv4 rules: the kernels' shortcut through the
+            // v4 image must give the 128-bit search's answer
+            if (f.v4_only &&
+                acl6_global(f, fam_img(b.fam[l][0]), hi, lo, port[i]) !=
+                    acl_value(f.rec, f.pieces, j, port[i]))
+                return -102;
+            stats[8 + l] += f.v4_only;
         }
         // the interval's packed record, checked against (x, y) + pieces
         uint32_t v = acl_value(f.rec, f.pieces, j, port[i]);

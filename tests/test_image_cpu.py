@@ -12,7 +12,7 @@ import oracle_ffi as O
 from vproxy_amd import workloads as W
 from vproxy_amd.classifier import group_array, pack_strings
 
-from cases import acl_edge_rules, v6_edge_inputs, hint_cases_random
+from cases import acl_edge_rules, rule_row, v6_edge_inputs, hint_cases_random
 
 
 @pytest.mark.parametrize("n_rules,p_range,weighted,seed", [
@@ -59,6 +59,40 @@ def test_acl_edges_v4_v6():
         want, wv = O.sg_batch_v4_np(tcp, udp, dflt, proto6, src4, port6)
         np.testing.assert_array_equal(got, want)
         np.testing.assert_array_equal(allow, wv)
+
+
+@pytest.mark.parametrize("n_rules,seed", [(64, 1), (2000, 2), (10000, 3)])
+def test_acl_v6_sources_on_v4_only_lists(n_rules, seed):
+    """Lists of plain IPv4 rules (every bench workload's) take the kernels'
+    shortcut for IPv6 sources (acl_dev.h acl6_global, AclFamilyImage.v4_only):
+    the ::a.b.c.d / ::ffff:a.b.c.d forms classified through the v4 image on
+    their low 32 bits, every other key as no rule.  The harness checks each
+    lookup against the 128-bit search over the same list's v6 image, and the
+    results against the oracle's Network.maskMatch restatement."""
+    tcp, udp = W.gen_sg_rules(n_rules, seed)
+    rng = np.random.default_rng(seed + 50)
+    src6, proto, port = v6_edge_inputs(rng, 30000)
+    ip, mk = W.rule_v4_fields(tcp)
+    r = rng.integers(0, len(ip), 30000)
+    inside = ip[r] | (rng.integers(0, 2**32, 30000, dtype=np.uint64).astype(np.uint32) & ~mk[r])
+    pick = (src6[:, :10] == 0).all(1) & (rng.random(30000) < 0.6)
+    src6[pick, 12:] = W.v4_to_bytes(inside[pick])
+    proto[pick] = 6
+    lo, hi = tcp["min_port"][r].astype(np.int64), tcp["max_port"][r].astype(np.int64)
+    port[pick] = (lo + (rng.random(30000) * (hi - lo + 1)).astype(np.int64))[pick].astype(np.uint16)
+    for dflt in (False, True):
+        got, allow, stats = IC.acl(tcp, udp, dflt, 6, proto, src6, port)
+        want, wv = O.sg_batch_v6_np(tcp, udp, dflt, proto, src6, port)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(allow, wv)
+        assert stats[8] + stats[9] == len(port)          # every lookup took the shortcut
+    assert (want >= 0).mean() > 0.05
+    # one IPv6 rule in the TCP list turns its shortcut off (the UDP one stays)
+    tcp6 = np.concatenate([tcp, rule_row("::ffff:10.0.0.0/104", 0, 65535, True)])
+    got, allow, stats = IC.acl(tcp6, udp, False, 6, proto, src6, port)
+    want, wv = O.sg_batch_v6_np(tcp6, udp, False, proto, src6, port)
+    np.testing.assert_array_equal(got, want)
+    assert stats[8] == 0 and stats[9] == (proto != 6).sum()
 
 
 def test_acl_empty_lists():

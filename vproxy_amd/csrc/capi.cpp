@@ -720,6 +720,7 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
             fi.dir_bits = fb.dir4.empty() ? 0 : fb.dir_bits;
             fi.nb = fb.nb;
             fi.np = static_cast<int32_t>(fb.pieces.size() / 2);
+            fi.v4_only = fb.v4_only;
         }
     s->img.allow = up(*s, b.allow);
     s->img.n_tcp = b.n_tcp;

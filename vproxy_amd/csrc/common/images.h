@@ -43,7 +43,11 @@ struct AclFamilyImage {
     int32_t nb;
     int32_t np;
     int32_t dir_bits;
-    int32_t pad_;
+    // v6 image of a list whose rules are all plain IPv4 networks: an IPv6
+    // key can then only match in its ::a.b.c.d / ::ffff:a.b.c.d forms, on
+    // its low 32 bits, exactly as the list's v4 image classifies them
+    // (acl_dev.h acl6_global); bounds6 / rec stay built for that case too
+    int32_t v4_only;
 };
 
 struct AclImage {

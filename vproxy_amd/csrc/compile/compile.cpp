@@ -278,6 +278,19 @@ int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_u
             th[l * 2 + f] = std::thread(build_acl_family, l == 0 ? tcp : udp, l == 0 ? n_tcp : n_udp,
                                         f, &out->fam[l][f]);
     for (auto& t : th) t.join();
+    // Network.maskMatch (Network.java:246-277): an IPv6 input matches an
+    // IPv4 rule only through its last four bytes, and only when
+    // Utils.lowBitsV6V4 holds (bytes 0-9 zero, bytes 10-11 both 00 or both
+    // FF).  With no other kind of rule in the list, its v6 image classifies
+    // such a key like the v4 image classifies the low 32 bits, and every
+    // other key as no rule: the kernels then skip the 128-bit search.
+    for (int l = 0; l < 2; ++l) {
+        const vc_acl_rule* r = l == 0 ? tcp : udp;
+        const int n = l == 0 ? n_tcp : n_udp;
+        int only4 = 1;
+        for (int i = 0; i < n && only4; ++i) only4 = r[i].net.ip_len == 4 && r[i].net.mask_len == 4;
+        out->fam[l][1].v4_only = only4;
+    }
     return VC_OK;
 }
 
@@ -779,6 +792,7 @@ uint64_t digest(const AclBuilt& b) {
             d.vec(x.pieces);
             d.vec(x.dir4);
             d.word(uint64_t(uint32_t(x.nb)) | uint64_t(uint32_t(x.dir_bits)) << 32);
+            d.word(uint64_t(uint32_t(x.v4_only)));
         }
     d.vec(b.allow);
     d.word(uint64_t(uint32_t(b.n_tcp)) | uint64_t(uint32_t(b.n_udp)) << 32);

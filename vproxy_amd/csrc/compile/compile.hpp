@@ -21,6 +21,7 @@ struct AclFamilyBuilt {
     std::vector<uint32_t> dir4;      // v4: bucket directory (images.h AclFamilyImage)
     int32_t nb = 0;
     int32_t dir_bits = 0;
+    int32_t v4_only = 0;             // v6 image: every rule a plain IPv4 network
 };
 
 struct AclBuilt {

@@ -115,4 +115,26 @@ VC_HD uint32_t acl_value(const uint32_t* rec, const uint32_t* pieces, int j, uin
     return acl_rec_value(glb_ld(reinterpret_cast<const uint4*>(rec) + j), pieces, port);
 }
 
+// An IPv6 key (hi, lo = bytes 0-7, 8-15) in the forms an IPv4 rule can
+// match (Network.maskMatch cases 4/5, Network.java:246-277, with
+// Utils.lowBitsV6V4(ip, 11, 10), Utils.java:122-133): ::a.b.c.d or
+// ::ffff:a.b.c.d.  Such a key matches an IPv4 rule iff its low 32 bits do.
+VC_HD bool v6_v4_form(uint64_t hi, uint64_t lo) {
+    const uint32_t w = uint32_t(lo >> 32);
+    return hi == 0 && (w == 0u || w == 0xFFFFu);
+}
+
+// Rule index (or VC_NONE) of an IPv6 key on one list, from global memory:
+// f6 / f4 are the list's v6 and v4 images.  A list of plain IPv4 rules
+// (f6.v4_only) classifies the key's low 32 bits through the v4 image (its
+// bucket directory) when the key has an IPv4 form, and as no rule
+// otherwise; any other list runs the 128-bit interval search.
+VC_HD uint32_t acl6_global(const AclFamilyImage& f6, const AclFamilyImage& f4, uint64_t hi,
+                           uint64_t lo, uint32_t port) {
+    if (f6.v4_only)
+        return v6_v4_form(hi, lo) ? acl_value(f4.rec, f4.pieces, acl4_interval(f4, uint32_t(lo)), port)
+                                  : VC_NONE;
+    return acl_value(f6.rec, f6.pieces, bsearch_u128(f6.bounds6, f6.nb, hi, lo), port);
+}
+
 }  // namespace vcd

@@ -307,6 +307,7 @@ struct AclV6Ctx {
     const uint32_t* rec[2];
     const uint32_t* pieces[2];
     int nf[2], nb[2];
+    int v4only[2];                 // AclFamilyImage.v4_only of the list's v6 image
     int shift;
 };
 
@@ -319,6 +320,7 @@ __device__ __forceinline__ AclV6Ctx stage_fences(const AclImage& img, uint64_t* 
         const AclFamilyImage& f = img.fam[l][1];
         a.nb[l] = f.nb;
         a.nf[l] = fence_count(f.nb, shift);
+        a.v4only[l] = f.v4_only;
         a.b[l] = f.bounds6;
         a.rec[l] = f.rec;
         a.pieces[l] = f.pieces;
@@ -345,6 +347,23 @@ __device__ __forceinline__ uint32_t acl_v6_fenced(const AclV6Ctx& a, bool tcp, u
                      j, port);
 }
 
+// An IPv6 source on a list of plain IPv4 rules classifies like its low 32
+// bits on the v4 image when it has an IPv4 form, else as no rule
+// (acl_dev.h v6_v4_form / acl6_global); other lists take the fenced search.
+// The mixed pipeline has the v4 boundaries in LDS (kLds): the IPv6 packets
+// of a C5-style batch then cost a v4 search instead of the fence search and
+// its dependent block loads.
+template <bool kLds>
+__device__ __forceinline__ uint32_t acl_v6_any(const AclV4Ctx& a, const AclV6Ctx& a6, bool tcp,
+                                               uint4 w, uint32_t port) {
+    if (per_list(tcp, a6.v4only[0], a6.v4only[1])) {
+        uint64_t hi, lo;
+        v6_key(w, &hi, &lo);
+        return v6_v4_form(hi, lo) ? acl_v4_one<kLds>(a, tcp, uint32_t(lo), port) : VC_NONE;
+    }
+    return acl_v6_fenced(a6, tcp, w, port);
+}
+
 __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
     AclImage img, int shift, const uint8_t* __restrict__ proto,
     const uint8_t* __restrict__ src6, const uint16_t* __restrict__ port, int64_t n,
@@ -355,7 +374,16 @@ __global__ __launch_bounds__(kBlock) void acl_v6_kernel(
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool t = proto[i] == VC_PROTO_TCP;
-        const uint32_t v = acl_v6_fenced(a, t, reinterpret_cast<const uint4*>(src6)[i], port[i]);
+        const uint4 w = reinterpret_cast<const uint4*>(src6)[i];
+        uint32_t v;
+        if (per_list(t, a.v4only[0], a.v4only[1])) {
+            uint64_t hi, lo;
+            v6_key(w, &hi, &lo);
+            v = t ? acl6_global(img.fam[0][1], img.fam[0][0], hi, lo, port[i])
+                  : acl6_global(img.fam[1][1], img.fam[1][0], hi, lo, port[i]);
+        } else {
+            v = acl_v6_fenced(a, t, w, port[i]);
+        }
         acl_emit(img, t, v, allow ? allow + i : nullptr, out + i);
     }
 }
@@ -807,7 +835,7 @@ __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.dst6)[i], &hi, &lo);
         e = route6_chase(tr.n6, tr.rb6, tr.n6[hi >> (64 - tr.rb6)], hi, lo);
-        v = acl_v6_fenced(a6, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
+        v = acl_v6_any<kLds>(a, a6, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
     } else {
         const uint32_t d = in.dst4[i];
         e = route_chase(tr.n4, tr.rb4, tr.n4[d >> (32 - tr.rb4)], d);
@@ -915,9 +943,9 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
                         uint64_t hh, ll;
                         v6_key(reinterpret_cast<const uint4*>(in.dst6)[gi], &hh, &ll);
                         const uint32_t root = tr.n6[hh >> (64 - tr.rb6)];
-                        const uint32_t vv = acl_v6_fenced(a6, t6,
-                                                          reinterpret_cast<const uint4*>(in.src6)[gi],
-                                                          in.dport[gi]);
+                        const uint32_t vv = acl_v6_any<kLds>(a, a6, t6,
+                                                             reinterpret_cast<const uint4*>(in.src6)[gi],
+                                                             in.dport[gi]);
                         r6[w][lane][1] = route6_chase(tr.n6, tr.rb6, root, hh, ll);
                         r6[w][lane][0] = vv;
                     }

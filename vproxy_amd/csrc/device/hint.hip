@@ -397,10 +397,9 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
     const uint32_t port = in.rport[i];
     uint32_t v;
     if (six) {
-        const AclFamilyImage& f = acl.fam[1][1];
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
-        v = acl_value(f.rec, f.pieces, bsearch_u128(f.bounds6, f.nb, hi, lo), port);
+        v = acl6_global(acl.fam[1][1], acl.fam[1][0], hi, lo, port);
     } else {
         const AclFamilyImage& f = acl.fam[1][0];
         v = acl_value(f.rec, f.pieces, acl4_interval(f, in.r4[i]), port);

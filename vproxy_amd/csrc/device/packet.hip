@@ -121,10 +121,9 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
     const bool six = in.rfam && in.rfam[i] == 6;
     uint32_t v;
     if (six) {
-        const AclFamilyImage& f = acl.fam[1][1];
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
-        v = acl_value(f.rec, f.pieces, bsearch_u128(f.bounds6, f.nb, hi, lo), in.bind_port);
+        v = acl6_global(acl.fam[1][1], acl.fam[1][0], hi, lo, in.bind_port);
     } else {
         const AclFamilyImage& f = acl.fam[1][0];
         v = acl_value(f.rec, f.pieces, acl4_interval(f, in.r4[i]), in.bind_port);
