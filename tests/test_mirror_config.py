@@ -107,3 +107,25 @@ def test_second_values_only_with_first():
     s = load_config(cfg)
     assert s.filters == [{"origin": "o", "mirror": 0}]
     assert s.is_enabled("o") and not s.is_enabled("p")
+
+
+@pytest.mark.parametrize("filt,kind,field", [
+    # two bad fields: the one Mirror.parseAndLoadFilter reads first is reported
+    ({"mac": "zz", "port": [1, "2"]}, "invalid value", "mac"),
+    ({"port": "80", "mac": "00:00:00:00:00:01", "network": "bad"}, "invalid value", "network"),
+    ({"network": 7, "mac2": "x", "transportLayerProtocol": 5}, "type error", "network"),
+    ({"transportLayerProtocol": 5, "port": [9, 1]}, "type error", "transportLayerProtocol"),
+    ({"port": [80], "applicationLayerProtocol": 3}, "invalid value", "port"),
+    ({"port": [1, 2], "port2": [5], "applicationLayerProtocol": 3}, "invalid value", "port2"),
+    ({"mac": "00:00:00:00:00:01", "mac2": "bad", "network": "nope"}, "invalid value", "mac2"),
+])
+def test_first_bad_field_is_reported(filt, kind, field):
+    """Mirror.java:545-600 reads mac, mac2, network, network2,
+    transportLayerProtocol, port, port2, applicationLayerProtocol in that
+    order and throws at the first failure (runSub maps ClassCastException
+    to a type error, IllegalArgument- and IndexOutOfBoundsException to an
+    invalid value), naming that field."""
+    cfg = {"enabled": True, "mirrors": [{"tap": "t", "mtu": 1500, "origins": [
+        {"origin": "o", "filters": [filt]}]}]}
+    with pytest.raises(V.IllegalArgumentException, match=r"%s .*filters\[0\]\.%s$" % (kind, field)):
+        load_config(cfg)

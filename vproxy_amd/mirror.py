@@ -157,40 +157,47 @@ def load_config(cfg):
                 if not isinstance(f, dict):
                     bad("type error")
                 flt = {"origin": origin, "mirror": mi}
-                for key, kinds in (("mac", (str,)), ("network", (str,)),
-                                   ("transportLayerProtocol", (str,)), ("port", (list,)),
-                                   ("applicationLayerProtocol", (str,))):
-                    if key not in f:
-                        continue
+                # Mirror.parseAndLoadFilter (Mirror.java:545-600) field by
+                # field, each value checked before the next field is read, so
+                # the first bad field is the one reported
+                from .classifier import Network
+
+                def parsed(key, check):
                     where[3:] = [key]
-                    flt[key] = get(f, key, kinds)
-                    pair = {"mac": "mac2", "network": "network2", "port": "port2"}.get(key)
-                    if pair and pair in f:    # the second value only with the first
-                        where[3:] = [pair]
-                        flt[pair] = get(f, pair, kinds)
-                for key in ("port", "port2"):
-                    if key in flt:
-                        where[3:] = [key]
-                        arr = flt[key]
-                        if len(arr) < 2:
-                            bad("invalid value")
-                        if any(isinstance(x, bool) or not isinstance(x, int) for x in arr[:2]):
-                            bad("type error")
-                        if arr[0] > arr[1]:
-                            bad("invalid value")
-                        flt[key] = [arr[0], arr[1]]
-                try:
-                    for key in ("mac", "mac2"):
-                        if key in flt:
-                            where[3:] = [key]
-                            parse_mac(flt[key])
-                    for key in ("network", "network2"):
-                        if key in flt:
-                            where[3:] = [key]
-                            from .classifier import Network
-                            Network(flt[key])
-                except _lib.IllegalArgumentException:
-                    bad("invalid value")
+                    v = get(f, key, (str,))
+                    try:
+                        check(v)
+                    except _lib.IllegalArgumentException:
+                        bad("invalid value")
+                    flt[key] = v
+
+                def port_range(key):
+                    where[3:] = [key]
+                    arr = get(f, key, (list,))
+                    if len(arr) < 2:                  # getInt(1): IndexOutOfBounds
+                        bad("invalid value")
+                    if any(isinstance(x, bool) or not isinstance(x, int) for x in arr[:2]):
+                        bad("type error")
+                    if arr[0] > arr[1]:
+                        bad("invalid value")
+                    flt[key] = [arr[0], arr[1]]
+
+                for first, second, check in (("mac", "mac2", parse_mac),
+                                             ("network", "network2", Network)):
+                    if first in f:
+                        parsed(first, check)
+                        if second in f:
+                            parsed(second, check)
+                if "transportLayerProtocol" in f:
+                    where[3:] = ["transportLayerProtocol"]
+                    flt["transportLayerProtocol"] = get(f, "transportLayerProtocol", (str,))
+                if "port" in f:
+                    port_range("port")
+                    if "port2" in f:
+                        port_range("port2")
+                if "applicationLayerProtocol" in f:
+                    where[3:] = ["applicationLayerProtocol"]
+                    flt["applicationLayerProtocol"] = get(f, "applicationLayerProtocol", (str,))
                 del where[3:]
                 filters.append(flt)
             del where[2:]
