@@ -1301,12 +1301,18 @@ def mix_bench(args, clf, dev, rank, O):
     unit = ("B/packet: IPv4 28 (family 1 + proto 1 + src 4 + dst 4 + dport 2 + host_id 4 in, 3x "
             "int32 out), IPv6 52 (family 1 + proto 1 + src 16 + dst 16 + dport 2 + host_id 4 "
             "in, 3x int32 out); %.1f at this mix" % ((n - n6) * 28 / n + n6 * 52 / n))
+    kev = []                                       # (before, after) the classify kernel
     if args.workload == "mix":
         outs = tuple(torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3)) + (None,)
         s_cnt = hip_stream(dev)
         clf.counters_enable(True)
-        fn = lambda: clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=src6,
-                                  dst6=dst6, outs=outs, count_stream=s_cnt)
+
+        def fn():
+            k0, k1 = RawEvent(), RawEvent()
+            k0.record(torch.cuda.current_stream())
+            clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=src6, dst6=dst6,
+                         outs=outs, count_stream=s_cnt, kernel_done_event=k1.h.value)
+            kev.append((k0, k1))
         kern = "pipeline_mix_kernel (+ counter finish on a second stream)"
 
         def fin():
@@ -1342,6 +1348,23 @@ def mix_bench(args, clf, dev, rank, O):
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if args.workload == "mixhost":
         ms = el / args.steps * 1e3
+    else:
+        # the classify kernel alone, and the IPv4 kernel (vc_pipeline_v4_dev)
+        # over the same packets' IPv4 fields with the same counting: the
+        # same-conditions reference for what the IPv6 share costs
+        extra["kernel_only_ms"] = round(float(np.mean(
+            [a.elapsed_time(b) for a, b in kev[-args.steps:]])), 4)
+        ref = []
+        for r in range(args.warmup + args.steps):
+            k0, k1 = RawEvent(), RawEvent()
+            k0.record(torch.cuda.current_stream())
+            clf.pipeline_v4(proto, src, dst, dport, hid, pool, outs=outs,
+                            kernel_done_event=k1.h.value, count_stream=s_cnt)
+            fin()
+            ref.append((k0, k1))
+        torch.cuda.synchronize()
+        extra["v4_kernel_same_packets_ms"] = round(float(np.mean(
+            [a.elapsed_time(b) for a, b in ref[args.warmup:]])), 4)
     gbs = per_unit * n / (ms / 1e3) / 1e9
     cpu = None
     if O is not None:

@@ -23,6 +23,8 @@ from collections import defaultdict
 
 N = 125000000 // 8 * 8
 LAUNCHES = [(4 << 10, 1), (64 << 20, 1), (64 << 20, 2), (1 << 30, 1), (1 << 30, 2)]
+# launch 5 (round 4): the 4 KiB table again, keys read with 4-byte loads
+# (one item per lane) -- the dword-stream width of the string kernels
 
 
 def per_dispatch(d, counter):
@@ -50,9 +52,13 @@ def main():
     miss = per_dispatch(a.l2, "TCC_MISS_sum")
     hit = per_dispatch(a.l2, "TCC_HIT_sum")
     write = [x * 1024 for x in per_dispatch(a.write, "WRITE_SIZE")]
-    assert len(fetch) == len(miss) == len(write) == 5, (len(fetch), len(miss), len(write))
+    assert len(fetch) == len(miss) == len(write) in (5, 6), (len(fetch), len(miss), len(write))
     stream = 4 * N
     rows = []
+    dword = None
+    if len(fetch) == 6:
+        dword = {"fetch_bytes": fetch[5], "write_bytes": write[5], "tcc_miss": miss[5],
+                 "tcc_hit": hit[5], "stream_fetch_factor": fetch[5] / stream}
     for (tb, g), fr, m, h, w in zip(LAUNCHES, fetch, miss, hit, write):
         gm = m - miss[0]
         rows.append({"table_bytes": tb, "gathers_per_item": g, "items": N,
@@ -65,11 +71,14 @@ def main():
            "stream_fetch_factor": fetch[0] / stream,
            "stream_write_factor": write[0] / stream,
            "launches": rows,
+           "dword_stream": dword,
            "conclusion": ("a wide (16-B/lane) streamed read is counted at %.3f of its bytes; a "
                           "random 4-byte gather miss is counted at %.1f bytes (one 64-B request); "
                           "streamed stores are counted exactly" % (
                               fetch[0] / stream,
-                              sum(r["fetch_bytes_per_gather_miss"] for r in rows[1:]) / 4))}
+                              sum(r["fetch_bytes_per_gather_miss"] for r in rows[1:]) / 4)) +
+                         ("; a 4-byte-per-lane streamed read at %.3f" % dword["stream_fetch_factor"]
+                          if dword else "")}
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:

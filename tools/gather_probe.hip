@@ -178,13 +178,19 @@ int main(int argc, char** argv) {
         // stays in L2, so its launch counts only the key stream (n x 4 B,
         // 16-B loads) and the result stream (n x 4 B, 16-B stores); the others
         // add n x G uniformly random 4-byte gathers into the table.
+        // Launch 5 (round 4) streams the keys with 4-byte loads (one item per
+        // lane, consecutive lanes consecutive words), the width the string
+        // kernels stage names and read offsets with.
         printf("launch,table_KB,gathers_per_item,items,ms\n");
-        const int64_t kb[] = {4, 64 << 10, 64 << 10, 1 << 20, 1 << 20};
-        const int gs[] = {1, 1, 2, 1, 2};
-        for (int l = 0; l < 5; ++l) {
+        const int64_t kb[] = {4, 64 << 10, 64 << 10, 1 << 20, 1 << 20, 4};
+        const int gs[] = {1, 1, 2, 1, 2, 1};
+        for (int l = 0; l < 6; ++l) {
             const uint32_t mask = uint32_t(kb[l] * 1024 / 4 - 1);
             CK(hipEventRecord(a, 0));
-            if (gs[l] == 1)
+            if (l == 5)
+                hipLaunchKernelGGL((gather<1, 1>), dim3(cus * 4), dim3(512), 0, 0, keys, n, t0, t1,
+                                   mask, out);
+            else if (gs[l] == 1)
                 hipLaunchKernelGGL((gather<1, 4>), dim3(cus * 4), dim3(512), 0, 0, keys, n, t0, t1,
                                    mask, out);
             else
