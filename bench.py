@@ -460,7 +460,11 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
 
 
 def end_to_end(fn, items, reps=3):
-    """M items/s of a synchronous host-buffer call (H2D + kernels + D2H)."""
+    """M items/s of a synchronous host-buffer call (H2D + kernels + D2H).
+    VC_BENCH_NO_E2E=1 skips it (profiling passes: its chunked launches would
+    mix into the per-launch averages of the device kernel)."""
+    if os.environ.get("VC_BENCH_NO_E2E") == "1":
+        return None
     fn()
     t0 = time.perf_counter()
     for _ in range(reps):

@@ -8,6 +8,7 @@
 # Summaries on this side: scripts/pmc_traffic.py, scripts/fetch_calibration.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
+export VC_BENCH_NO_E2E=1
 O=gpurun_out/p4
 steps=()
 for w in "$@"; do
