@@ -610,6 +610,8 @@ def main():
     ap.add_argument("--pool-cus", type=int, default=0,
                     help="CU partition: the pool pass and the counter finish on this many CUs "
                          "(a CU-masked stream), the pipeline kernel on the rest (0: no masks)")
+    ap.add_argument("--compact6", action="store_true",
+                    help="mix: IPv6 addresses as one row per IPv6 packet (vc_pipeline_c6_dev)")
     ap.add_argument("--v6-frac", type=float, default=0.15,
                     help="mix / mixhost: share of IPv6 packets (C3's mix is 0.15)")
     ap.add_argument("--dist", action="store_true",
@@ -1311,13 +1313,21 @@ def mix_bench(args, clf, dev, rank, O):
         s_cnt = hip_stream(dev)
         clf.counters_enable(True)
 
+        s6, d6 = src6, dst6
+        if args.compact6:                          # one row per IPv6 packet, packet order
+            six = fam == 6
+            s6, d6 = src6[six].contiguous(), dst6[six].contiguous()
+            extra["compact6_rows"] = len(s6)
+
         def fn():
             k0, k1 = RawEvent(), RawEvent()
             k0.record(torch.cuda.current_stream())
-            clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=src6, dst6=dst6,
-                         outs=outs, count_stream=s_cnt, kernel_done_event=k1.h.value)
+            clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=s6, dst6=d6,
+                         outs=outs, count_stream=s_cnt, kernel_done_event=k1.h.value,
+                         compact6=args.compact6)
             kev.append((k0, k1))
-        kern = "pipeline_mix_kernel (+ counter finish on a second stream)"
+        kern = "pipeline_mix_kernel (+ counter finish on a second stream)" + (
+            ", compact IPv6 rows (vc_pipeline_c6_dev)" if args.compact6 else "")
 
         def fin():
             torch.cuda.current_stream().wait_stream(s_cnt)
@@ -1399,6 +1409,7 @@ def mix_bench(args, clf, dev, rank, O):
            "cpu_baseline": cpu}
     res.update(extra)
     res["v6_frac"] = args.v6_frac
+    res["compact6"] = bool(args.compact6)
     if rank == 0:
         print(json.dumps(res), flush=True)
     clf.close()

@@ -328,6 +328,18 @@ typedef struct vc_pipeline_out {
 int vc_pipeline_dev(vc_ctx *ctx, const vc_packets *in, int64_t n, const int32_t *pool_group,
                     int64_t n_pool, const vc_pipeline_out *out, void *stream, void *count_stream,
                     void *kernel_done_event);
+/* vc_pipeline_dev with the IPv6 addresses compacted: src6 / dst6 hold n6
+ * rows, row k the addresses of the batch's k-th family-6 packet (packet
+ * order); family is required.  An IPv6 packet's addresses then share cache
+ * lines with the next IPv6 packets' instead of sitting in rows no IPv4
+ * packet reads.  The arrays must be aligned as the vector kernels load them:
+ * src4 / dst4 / host_id and the int32 outputs 16 bytes, family / proto /
+ * allow 4 bytes, dport 8 bytes, src6 / dst6 16 bytes.  n6 must be the
+ * number of family-6 packets: with fewer rows the IPv6 packets past them
+ * get unspecified results (no memory outside the rows is read). */
+int vc_pipeline_c6_dev(vc_ctx *ctx, const vc_packets *in, int64_t n, int64_t n6,
+                       const int32_t *pool_group, int64_t n_pool, const vc_pipeline_out *out,
+                       void *stream, void *count_stream, void *kernel_done_event);
 /* Host pointers (every array in `in` and `out`, and pool_group), synchronous.
  * Zero-copy when every array is inside a vc_host_register'ed buffer (the
  * kernel reads and writes across PCIe directly); otherwise the batch is

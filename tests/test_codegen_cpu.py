@@ -92,7 +92,8 @@ def _one(d, part):
 HOT = {   # kernel (mangled-name fragment) -> VGPR ceiling of its launch
     "pipeline_v4_kernelILb1ELb1ELb1E": 128,   # C5: LDS ACL, vector, counting
     "pipeline_v4_kernelILb1ELb1ELb0E": 128,
-    "pipeline_mix_kernelILb1ELb1ELb1E": 128,
+    "pipeline_mix_kernelILb1ELb1ELb1ELb0E": 128,
+    "pipeline_mix_kernelILb1ELb1ELb1ELb1E": 128,   # compact IPv6 rows
     "acl_v4_kernelILb1ELi2E": 128,            # C2 (two quads per lane)
     "acl_v4_kernelILb1ELi1E": 128,
     "13acl_v6_kernelE": 128,

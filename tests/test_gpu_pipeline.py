@@ -234,3 +234,73 @@ def test_bad_arguments(setup):
         clf.pipeline(p["proto"], p["src4"], p["dst4"], p["dport"], family=p["family"])
     with pytest.raises(V.IllegalArgumentException):
         clf.pipeline(p["proto"], None, p["dst4"], p["dport"])
+
+
+def _compact(d):
+    six = d["family"] == 6
+    return d["src6"][six].contiguous(), d["dst6"][six].contiguous()
+
+
+@pytest.mark.parametrize("n,frac", [(1, 1.0), (3, 0.5), (4, 0.5), (5, 1.0), (257, 0.5),
+                                    (4099, 0.0), (4099, 1.0), (200_003, 0.5), (1 << 20, 0.15)])
+def test_compact6_rows_vs_oracle(setup, n, frac):
+    """vc_pipeline_c6_dev: src6 / dst6 with one row per IPv6 packet (packet
+    order) give every output the oracle gives the sparse batch, and the same
+    hit counters -- at sizes with partial groups of four, no IPv6 packet,
+    only IPv6 packets, and several workgroups' wave shares."""
+    import torch
+    clf, t = setup
+    p = _packets(t, n, 41 + n)
+    rng = np.random.default_rng(n)
+    p["family"] = np.where(rng.random(n) < frac, 6, 4).astype(np.uint8)
+    want = _oracle(t, p)
+    d = _dev(p)
+    pool = torch.from_numpy(t["pool"]).cuda()
+    s6, d6 = _compact(d)
+    clf.counters_enable(True)
+    clf.counters_reset()
+    got = clf.pipeline(d["proto"], d["src4"], d["dst4"], d["dport"], d["host_id"], pool,
+                       family=d["family"], src6=s6, dst6=d6, want_allow=True, compact6=True)
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    cnt = [clf.counters_read(k) for k in (V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP)]
+    for g, w, name in zip(got, want, ("acl", "route", "group", "allow")):
+        np.testing.assert_array_equal(g.cpu().numpy(), w, err_msg=name)
+    clf.counters_reset()
+    clf.counters_enable(True)
+    _call(clf, d, pool)                              # the sparse form, same counters
+    torch.cuda.synchronize()
+    clf.counters_enable(False)
+    for k, c in zip((V.COUNTERS_ACL, V.COUNTERS_ROUTE, V.COUNTERS_GROUP), cnt):
+        np.testing.assert_array_equal(clf.counters_read(k), c)
+
+
+def test_compact6_short_rows_and_alignment(setup):
+    """Fewer rows than IPv6 packets never reads outside the rows (the packets
+    past them get unspecified results; the ones before are exact), no rows at
+    all reads nothing; misaligned fields are refused."""
+    import torch
+    clf, t = setup
+    n = 50_001
+    p = _packets(t, n, 53)
+    want = _oracle(t, p)
+    d = _dev(p)
+    pool = torch.from_numpy(t["pool"]).cuda()
+    s6, d6 = _compact(d)
+    k = len(s6) // 2
+    got = clf.pipeline(d["proto"], d["src4"], d["dst4"], d["dport"], d["host_id"], pool,
+                       family=d["family"], src6=s6[:k], dst6=d6[:k], compact6=True)
+    torch.cuda.synchronize()
+    first = np.nonzero(p["family"] == 6)[0][k - 1] + 1     # packets before the k-th IPv6 one
+    for g, w in zip(got[:3], want[:3]):
+        np.testing.assert_array_equal(g.cpu().numpy()[:first], w[:first])
+    e6 = s6[:0]
+    got = clf.pipeline(d["proto"], d["src4"], d["dst4"], d["dport"], d["host_id"], pool,
+                       family=d["family"], src6=e6, dst6=e6, compact6=True)
+    torch.cuda.synchronize()
+    v4 = p["family"] == 4
+    np.testing.assert_array_equal(got[1].cpu().numpy()[v4], want[1][v4])
+    dm = _dev(p, offset=1)
+    with pytest.raises(V.IllegalArgumentException):
+        clf.pipeline(dm["proto"], dm["src4"], dm["dst4"], dm["dport"], dm["host_id"], pool,
+                     family=dm["family"], src6=s6, dst6=d6, compact6=True)

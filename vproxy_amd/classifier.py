@@ -572,13 +572,14 @@ class Classifier:
 
     def pipeline(self, proto, src4, dst4, dport, host_id=None, pool_group=None, family=None,
                  src6=None, dst6=None, outs=None, want_allow=False, kernel_done_event=None,
-                 count_stream=None):
+                 count_stream=None, compact6=False):
         """vc_pipeline(_dev): per packet SecurityGroup.allow(proto, src, dport)
         -> RouteTable.lookup(dst) (rulesV4 or rulesV6 by `family`, 4 or 6)
         -> pool_group[host_id].  torch CUDA tensors run on the device
         (asynchronous, torch's current stream); numpy arrays take the host
-        entry point (synchronous, PCIe included).  src6/dst6: n x 16 bytes.
-        Returns (acl, route, group, allow)."""
+        entry point (synchronous, PCIe included).  src6/dst6: n x 16 bytes, or
+        with compact6 (device tensors only, vc_pipeline_c6_dev) one row per
+        IPv6 packet in packet order.  Returns (acl, route, group, allow)."""
         n = len(proto)
         dev = _is_dev(proto)
         if dev:
@@ -604,7 +605,14 @@ class Classifier:
         po = _lib.VcPipelineOut(*[x.value if x is not None else None for x in
                                   (_ptr(a), _ptr(r), _ptr(g), _ptr(al))])
         n_pool = len(pool_group) if pool_group is not None else 0
-        if dev:
+        if dev and compact6:
+            check(lib().vc_pipeline_c6_dev(self.h, C.byref(pk), n, len(src6), _ptr(pool_group),
+                                           n_pool, C.byref(po), _stream(),
+                                           C.c_void_p(count_stream.cuda_stream)
+                                           if count_stream is not None else None,
+                                           C.c_void_p(kernel_done_event)
+                                           if kernel_done_event else None))
+        elif dev:
             check(lib().vc_pipeline_dev(self.h, C.byref(pk), n, _ptr(pool_group), n_pool,
                                         C.byref(po), _stream(),
                                         C.c_void_p(count_stream.cuda_stream)

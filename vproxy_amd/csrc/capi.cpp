@@ -1759,7 +1759,8 @@ static int pipeline_check(const vc_packets* in, int64_t n, const int32_t* pool_g
 
 static int pipeline_dev(vc_ctx* ctx, const vc_packets& in, int64_t n, const int32_t* pool_group,
                         int64_t n_pool, const vc_pipeline_out& out, void* stream,
-                        void* count_stream, void* kernel_done, const PipePins& pin) {
+                        void* count_stream, void* kernel_done, const PipePins& pin,
+                        int64_t n6c = -1) {
     if ((in.src6 && (reinterpret_cast<uintptr_t>(in.src6) & 15)) ||
         (in.dst6 && (reinterpret_cast<uintptr_t>(in.dst6) & 15)))
         return fail(VC_EINVAL, "src6 / dst6 must be 16-byte aligned");
@@ -1767,7 +1768,7 @@ static int pipeline_dev(vc_ctx* ctx, const vc_packets& in, int64_t n, const int3
     const bool on = ctx->counters_on;
     vc::PipeArgs p{in.family, in.proto, in.src4, in.dst4, in.src6, in.dst6, in.dport, in.host_id,
                    pool_group, in.host_id ? n_pool : 0, n, out.acl, out.route, out.group,
-                   out.allow};
+                   out.allow, n6c};
     vc::PipeCounters cnt{on ? pin.a->counters : nullptr, on ? pin.r->counters : nullptr,
                          on && pin.h && in.host_id ? pin.h->counters : nullptr,
                          pin.h ? pin.h->img.n_groups : 0};
@@ -1786,6 +1787,35 @@ int vc_pipeline_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t*
     const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
     return pipeline_dev(ctx, *in, n, pool_group, n_pool, *out, stream, count_stream,
                         kernel_done_event, pin);
+}
+
+int vc_pipeline_c6_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
+                       const int32_t* pool_group, int64_t n_pool, const vc_pipeline_out* out,
+                       void* stream, void* count_stream, void* kernel_done_event) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    // no IPv6 rows: the kernel reads none (pipe_mix_c6), so any aligned
+    // non-null pointer stands in for the empty arrays
+    alignas(16) static const uint8_t kNoRows[16] = {};
+    vc_packets m = in ? *in : vc_packets{};
+    if (in && n6 == 0) m.src6 = m.dst6 = kNoRows;
+    in = in ? &m : nullptr;
+    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
+    if (n == 0) return kernel_done_event ? (hipEventRecord(static_cast<hipEvent_t>(kernel_done_event),
+                                                           static_cast<hipStream_t>(stream)) == hipSuccess
+                                                ? VC_OK : fail(VC_EDEVICE, "event record"))
+                                         : VC_OK;
+    if (!in->family || n6 < 0 || (n6 > 0 && (!in->src6 || !in->dst6)))
+        return fail(VC_EINVAL, "compact IPv6 rows need the family array and n6 >= 0 rows");
+    auto al = [](const void* p, uintptr_t a) { return !p || (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    if (!al(in->family, 4) || !al(in->proto, 4) || !al(in->src4, 16) || !al(in->dst4, 16) ||
+        !al(in->dport, 8) || !al(in->host_id, 16) || !al(out->acl, 16) || !al(out->route, 16) ||
+        !al(out->group, 16) || !al(out->allow, 4))
+        return fail(VC_EINVAL, "vc_pipeline_c6_dev needs 16-byte aligned 4-byte fields (4-byte "
+                               "aligned family / proto / allow, 8-byte aligned dport)");
+    const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
+    return pipeline_dev(ctx, *in, n, pool_group, n_pool, *out, stream, count_stream,
+                        kernel_done_event, pin, n6);
 }
 
 int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,

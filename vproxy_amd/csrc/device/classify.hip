@@ -795,12 +795,16 @@ struct PipeIn {
     const uint8_t* proto;
     const uint32_t* src4;
     const uint32_t* dst4;
-    const uint8_t* src6;           // 16 bytes per packet, 16-byte aligned
+    const uint8_t* src6;           // 16 bytes per packet (or per IPv6 packet), 16-byte aligned
     const uint8_t* dst6;
     const uint16_t* dport;
     const uint32_t* host_id;       // null: no hostnames
     const int32_t* pool_group;
     int64_t n_pool;
+    // compact IPv6 rows (kC6): base6[wave] = IPv6 packets before the wave's
+    // sub-slice (pipe_wave_groups), n6c = rows in src6 / dst6
+    const uint32_t* base6;
+    int64_t n6c;
 };
 
 struct PipeOut {
@@ -857,6 +861,232 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Compact IPv6 rows (vc_pipeline_c6_dev): src6 / dst6 hold the addresses of
+// the batch's IPv6 packets only, in packet order, so the k-th IPv6 packet's
+// addresses are row k.  With a row per packet, an IPv6 packet's 32 address
+// bytes sit in cache lines no IPv4 packet reads: at 15 % IPv6 the mixed
+// kernel took ~2.6 more L2 misses per IPv6 packet than the IPv4 one and ran
+// 15 % longer (profiles/r04_mix_v6frac.jsonl, pmc_traffic.json `mix`).
+// Compact rows are read by consecutive lanes.  Each wave of the compact
+// kernel takes a contiguous share of its workgroup's slice (not the 4096-
+// packet interleave of the sparse form), so the rows it needs start at
+// base6[wave], counted by pipe6_count_kernel + pipe6_scan_kernel first.
+__device__ __forceinline__ void pipe_wave_groups(int64_t lo, int64_t hi, int w, int64_t* g0,
+                                                 int64_t* g1) {
+    const int64_t ng = (hi - lo + 3) >> 2;                 // groups of 4 packets
+    const int64_t per = (ng + kPipeWaves - 1) / kPipeWaves;
+    const int64_t a = int64_t(w) * per, b = a + per;
+    *g0 = a < ng ? a : ng;
+    *g1 = b < ng ? b : ng;
+}
+
+// IPv6 packets in each wave's share (launched with the pipeline's grid).
+__global__ __launch_bounds__(kPipeBlock) void pipe6_count_kernel(const uint8_t* __restrict__ family,
+                                                                 int64_t n, uint32_t* __restrict__ cnt) {
+    int64_t lo, hi, g0, g1;
+    pipe_slice(n, &lo, &hi);
+    const int w = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
+    pipe_wave_groups(lo, hi, w, &g0, &g1);
+    uint32_t c = 0;
+    for (int64_t g = g0 + lane; g < g1; g += 64) {
+        const int64_t i = lo + 4 * g;
+        if (i + 3 < hi) {
+            const uint32_t f = reinterpret_cast<const uint32_t*>(family)[i >> 2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c += ((f >> (8 * k)) & 0xFFu) == 6;
+        } else {
+            for (int64_t j = i; j < hi; ++j) c += family[j] == 6;
+        }
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane == 0) cnt[int64_t(blockIdx.x) * kPipeWaves + w] = c;
+}
+
+// Exclusive scan of the m wave counts in place (one workgroup, m <= 4 * 1024).
+__global__ __launch_bounds__(1024) void pipe6_scan_kernel(uint32_t* __restrict__ v, int m) {
+    __shared__ uint32_t part[1024];
+    uint32_t x[4], s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = int(threadIdx.x) * 4 + k;
+        x[k] = j < m ? v[j] : 0u;
+        s += x[k];
+    }
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint32_t t = int(threadIdx.x) >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = int(threadIdx.x) * 4 + k;
+        if (j < m) v[j] = run;
+        run += x[k];
+    }
+}
+
+// One wave's share of the compact form: 256 packets (4 per lane) per step,
+// the IPv6 ones queued in packet order so round r's lane l reads compact row
+// base + (packets so far) + r * 64 + l -- consecutive rows, consecutive lanes.
+template <bool kLds, bool kCount>
+__device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx& a,
+                                            const AclV6Ctx& a6, const PipeTries& tr,
+                                            const PipeIn& in, int64_t lo, int64_t hi,
+                                            const PipeOut& out, const PipeCount& pc,
+                                            const PipeLds& L, PipeTally* t, uint8_t* q6,
+                                            uint32_t (*r6)[2]) {
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const uint64_t below_me = (uint64_t(1) << lane) - 1;
+    int64_t g0, g1;
+    pipe_wave_groups(lo, hi, w, &g0, &g1);
+    int64_t row = in.base6[int64_t(blockIdx.x) * kPipeWaves + w];
+    const int64_t last = in.n6c - 1;
+    for (int64_t gb = g0; gb < g1; gb += 64) {            // uniform per wave
+        const int64_t g = gb + lane;
+        const int64_t i = lo + 4 * g;
+        const bool full = g < g1 && i + 3 < hi;
+        bool ok[4];
+        uint32_t fm = 0, pr = 0, hh4[4] = {0, 0, 0, 0};
+        uint32_t d[4] = {0, 0, 0, 0}, sk[4] = {0, 0, 0, 0}, po[4] = {0, 0, 0, 0};
+        if (full) {
+            const int64_t q = i >> 2;
+            fm = reinterpret_cast<const uint32_t*>(in.family)[q];
+            pr = reinterpret_cast<const uint32_t*>(in.proto)[q];
+            const uint2 pt = reinterpret_cast<const uint2*>(in.dport)[q];
+            const uint4 d4 = reinterpret_cast<const uint4*>(in.dst4)[q];
+            const uint4 s4 = reinterpret_cast<const uint4*>(in.src4)[q];
+            d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
+            sk[0] = s4.x; sk[1] = s4.y; sk[2] = s4.z; sk[3] = s4.w;
+            po[0] = pt.x & 0xFFFFu; po[1] = pt.x >> 16; po[2] = pt.y & 0xFFFFu; po[3] = pt.y >> 16;
+            if (in.host_id) {
+                const uint4 h4 = reinterpret_cast<const uint4*>(in.host_id)[q];
+                hh4[0] = h4.x; hh4[1] = h4.y; hh4[2] = h4.z; hh4[3] = h4.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ok[k] = true;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ok[k] = g < g1 && i + k < hi;
+                if (ok[k]) {
+                    fm |= uint32_t(in.family[i + k]) << (8 * k);
+                    pr |= uint32_t(in.proto[i + k]) << (8 * k);
+                    d[k] = in.dst4[i + k];
+                    sk[k] = in.src4[i + k];
+                    po[k] = in.dport[i + k];
+                    if (in.host_id) hh4[k] = in.host_id[i + k];
+                }
+            }
+        }
+        bool v6[4], tcp[4];
+        uint32_t e[4], v[4];
+        int32_t grp[4] = {-1, -1, -1, -1};
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v6[k] = ok[k] && ((fm >> (8 * k)) & 0xFFu) == 6;
+            tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
+            e[k] = ok[k] && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
+            v[k] = VC_NONE;
+            c += v6[k] ? 1 : 0;
+        }
+        if (in.host_id) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) grp[k] = int64_t(hh4[k]) < in.n_pool ? in.pool_group[hh4[k]] : -1;
+        }
+        // rank of each IPv6 packet among the step's IPv6 packets, packet order
+        // (lane-major): the lanes below hold sum(c) of them (c <= 4: three
+        // bit-plane ballots), then this lane's earlier slots
+        const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+        const int before = __popcll(b0 & below_me) + 2 * __popcll(b1 & below_me) +
+                           4 * __popcll(b2 & below_me);
+        const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        int pos[4];
+        int r = before;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pos[k] = r;
+            if (v6[k]) {
+                q6[r] = uint8_t(lane * 4 + k);
+                ++r;
+            }
+        }
+        if (total) {                                      // wave-uniform
+            wave_sync();
+            const int64_t wbase = lo + 4 * gb;            // the step's first packet
+            for (int r0 = 0; r0 < total; r0 += 64) {
+                if (r0 + lane < total) {
+                    const int64_t gi = wbase + q6[r0 + lane];
+                    // rows past n6c (a caller whose n6 is short) read the last
+                    // row, or the zero address when there is none: never
+                    // memory outside the rows
+                    const int64_t k6 = row + r0 + lane;
+                    const int64_t rw = k6 < last ? k6 : last;
+                    const uint4 z = make_uint4(0, 0, 0, 0);
+                    const uint4 dw = last >= 0 ? reinterpret_cast<const uint4*>(in.dst6)[rw] : z;
+                    const uint4 sw = last >= 0 ? reinterpret_cast<const uint4*>(in.src6)[rw] : z;
+                    const bool t6 = in.proto[gi] == VC_PROTO_TCP;
+                    uint64_t hh, ll;
+                    v6_key(dw, &hh, &ll);
+                    const uint32_t root = tr.n6[hh >> (64 - tr.rb6)];
+                    const uint32_t vv = acl_v6_any<kLds>(a, a6, t6, sw, in.dport[gi]);
+                    r6[lane][1] = route6_chase(tr.n6, tr.rb6, root, hh, ll);
+                    r6[lane][0] = vv;
+                }
+                wave_sync();
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (v6[k] && pos[k] >= r0 && pos[k] < r0 + 64) {
+                        v[k] = r6[pos[k] - r0][0];
+                        e[k] = r6[pos[k] - r0][1];
+                    }
+                wave_sync();
+            }
+            row += total;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ok[k] && !v6[k]) v[k] = acl_v4_one<kLds>(a, tcp[k], sk[k], po[k]);
+        int32_t oa[4], orr[4];
+        uint8_t al[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            al[k] = 0;
+            acl_emit(img, tcp[k], v[k], out.allow ? &al[k] : nullptr, &oa[k]);
+            orr[k] = out_index(v6[k] || !ok[k] ? e[k] : route_chase(tr.n4, tr.rb4, e[k], d[k]));
+        }
+        if (full) {
+            const int64_t q = i >> 2;
+            reinterpret_cast<int4*>(out.acl)[q] = make_int4(oa[0], oa[1], oa[2], oa[3]);
+            reinterpret_cast<int4*>(out.route)[q] = make_int4(orr[0], orr[1], orr[2], orr[3]);
+            reinterpret_cast<int4*>(out.group)[q] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+            if (out.allow)
+                reinterpret_cast<uint32_t*>(out.allow)[q] = uint32_t(al[0]) | uint32_t(al[1]) << 8 |
+                                                             uint32_t(al[2]) << 16 | uint32_t(al[3]) << 24;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    out.acl[i + k] = oa[k];
+                    out.route[i + k] = orr[k];
+                    out.group[i + k] = grp[k];
+                    if (out.allow) out.allow[i + k] = al[k];
+                }
+        }
+        if (kCount) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) pipe_count(pc, L.ah, L.rc, L.gc, tcp[k], v[k], v6[k], orr[k], grp[k], t);
+        }
+    }
+}
+
 // The vector path keeps IPv4 and IPv6 packets from diverging: a wave's 256
 // packets (4 per lane) are classified by family with a ballot, the IPv6
 // ones are queued in LDS and spread over all 64 lanes (one round per 64
@@ -864,7 +1094,7 @@ __device__ __forceinline__ void wave_sync() {
 // every lane finish its IPv4 packets.  Without it every wave ran the IPv6
 // path (ACL search + trie walk) once per packet slot whenever any of its
 // lanes had an IPv6 packet there -- i.e. always, at a 15 % IPv6 mix.
-template <bool kLds, bool kVec, bool kCount>
+template <bool kLds, bool kVec, bool kCount, bool kC6 = false>
 __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, PipeTries tr,
                                                                    PipeIn in, int64_t n,
                                                                    PipeOut out, PipeCount pc,
@@ -881,7 +1111,10 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
     int64_t lo, hi;
     pipe_slice(n, &lo, &hi);
     PipeTally t;
-    if (!kVec) {
+    if (kC6) {
+        pipe_mix_c6<kLds, kCount>(img, a, a6, tr, in, lo, hi, out, pc, L, &t, q6[threadIdx.x >> 6],
+                                  r6[threadIdx.x >> 6]);
+    } else if (!kVec) {
         for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
             pipe_mix_one<kLds, kCount>(img, a, a6, tr, in, i, out, pc, L, &t);
     } else {
@@ -1232,6 +1465,10 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
                aligned(p.out_route, 16) && aligned(p.out_group, 16) &&
                (!p.out_allow || aligned(p.out_allow, 4));
     if (mix) vec = vec && aligned(p.family, 4);
+    // compact IPv6 rows: the wave shares of pipe_mix_c6 (vector loads for
+    // whole groups of four)
+    const bool c6 = mix && p.n6c >= 0;
+    if (c6 && (!p.family || !vec)) return hipErrorInvalidValue;
     int64_t want = ((vec ? (n + 3) / 4 : n) + vcd::kPipeBlock - 1) / vcd::kPipeBlock;
     // Workgroups (one per CU): on an unmasked stream the IPv4 kernel takes 7/8
     // of the CUs (28 of each XCD's 32); a CU-masked stream's share is all its own.  Its rate is set by the chip's random-gather cap, which 224
@@ -1247,7 +1484,8 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     const int cus = grid_cap > 0 ? std::min(grid_cap, c.num_cus)
                   : (!mix && !c.cu_masked && c.num_cus >= 64 ? (c.num_cus * 7 / 8) & ~7
                                                                 : c.num_cus);
-    const int grid = int(want < cus ? (want < 1 ? 1 : want) : cus);
+    int grid = int(want < cus ? (want < 1 ? 1 : want) : cus);
+    if (c6 && grid > 256) grid = 256;           // pipe6_scan_kernel: <= 4096 wave shares
     // In-kernel counting where it fits the workgroup's LDS; the rest is
     // counted by separate passes over the outputs afterwards.
     size_t shmem = size_t(words) * 4;
@@ -1264,11 +1502,21 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
     const bool g_big = cnt.group && big_hist_applies(n, cnt.n_groups);
     const size_t rbytes = r_big ? big_hist_bytes(n, route_nval, grid) : 0;
     const size_t gbytes = g_big ? big_hist_bytes(n, cnt.n_groups, grid) : 0;
+    const size_t bbytes = c6 ? (size_t(grid) * vcd::kPipeWaves * 4 + 255) & ~size_t(255) : 0;
     int slot = -1;
     uint8_t* scratch = nullptr;
-    if (rbytes + gbytes)
-        e = c.scratch ? c.scratch->acquire(rbytes + gbytes, c.stream, &slot, &scratch)
+    if (rbytes + gbytes + bbytes)
+        e = c.scratch ? c.scratch->acquire(rbytes + gbytes + bbytes, c.stream, &slot, &scratch)
                       : hipErrorInvalidValue;
+    uint32_t* base6 = c6 && e == hipSuccess
+                          ? reinterpret_cast<uint32_t*>(scratch + rbytes + gbytes) : nullptr;
+    if (c6 && e == hipSuccess) {
+        hipLaunchKernelGGL(vcd::pipe6_count_kernel, dim3(grid), dim3(vcd::kPipeBlock), 0, c.stream,
+                           p.family, n, base6);
+        hipLaunchKernelGGL(vcd::pipe6_scan_kernel, dim3(1), dim3(1024), 0, c.stream, base6,
+                           grid * vcd::kPipeWaves);
+        e = hipGetLastError();
+    }
     if (cnt.acl && shmem + size_t(acl_bins) * 4 <= lds_max) {
         pc.acl = cnt.acl;
         pc.acl_bins = acl_bins;
@@ -1309,12 +1557,12 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
                            p.proto, p.src4, p.dst4, p.dport, p.host_id, p.pool_group, p.n_pool,    \
                            n, p.out_acl, p.out_route, p.out_group, p.out_allow, pc, shift);        \
     } while (0)
-#define VC_MIX(L, V, K)                                                                            \
+#define VC_MIX(L, V, K, C6)                                                                        \
     do {                                                                                           \
         if (shmem > 64 * 1024)                                                                     \
-            e = allow_lds(vcd::pipeline_mix_kernel<L, V, K>, kLdsMax - kMixStatic);                \
+            e = allow_lds(vcd::pipeline_mix_kernel<L, V, K, C6>, kLdsMax - kMixStatic);            \
         if (e != hipSuccess) break;                                                                \
-        hipLaunchKernelGGL((vcd::pipeline_mix_kernel<L, V, K>), dim3(grid),                        \
+        hipLaunchKernelGGL((vcd::pipeline_mix_kernel<L, V, K, C6>), dim3(grid),                    \
                            dim3(vcd::kPipeBlock), shmem, c.stream, acl, tr, in, n, out, pc,        \
                            fshift, fence_words, shift);                                            \
     } while (0)
@@ -1330,14 +1578,17 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
             const vcd::PipeTries tr{route.fam[0].nodes, route.fam[1].nodes, route.fam[0].root_bits,
                                     route.fam[1].root_bits};
             const vcd::PipeIn in{p.family, p.proto, p.src4, p.dst4, p.src6, p.dst6,
-                                 p.dport, p.host_id, p.pool_group, p.n_pool};
+                                 p.dport, p.host_id, p.pool_group, p.n_pool, base6, p.n6c};
             const vcd::PipeOut out{p.out_acl, p.out_route, p.out_group, p.out_allow};
-            if (count) {
-                if (vec) VC_MIX(true, true, true);
-                else VC_MIX(true, false, true);
+            if (c6) {
+                if (count) VC_MIX(true, true, true, true);
+                else VC_MIX(true, true, false, true);
+            } else if (count) {
+                if (vec) VC_MIX(true, true, true, false);
+                else VC_MIX(true, false, true, false);
             } else {
-                if (vec) VC_MIX(true, true, false);
-                else VC_MIX(true, false, false);
+                if (vec) VC_MIX(true, true, false, false);
+                else VC_MIX(true, false, false, false);
             }
         }
 #undef VC_PIPE

@@ -189,6 +189,9 @@ struct PipeArgs {
     int32_t* out_route;
     int32_t* out_group;
     uint8_t* out_allow;
+    // -1: src6 / dst6 have a row per packet; >= 0: they hold only the IPv6
+    // packets' addresses, n6c rows in packet order (vc_pipeline_c6_dev)
+    int64_t n6c = -1;
 };
 // Counter arrays of the pinned snapshots (null = not counted): ACL
 // [tcp][udp][tcp default][udp default], route [v4][v6][v4 null][v6 null],
