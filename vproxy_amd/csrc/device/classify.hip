@@ -991,14 +991,8 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         for (int k = 0; k < 4; ++k) {
             v6[k] = ok[k] && ((fm >> (8 * k)) & 0xFFu) == 6;
             tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-            e[k] = ok[k] && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
             v[k] = VC_NONE;
             c += v6[k] ? 1 : 0;
-        }
-        if (in.host_id) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (ok[k]) grp[k] = int64_t(hh4[k]) < in.n_pool ? in.pool_group[hh4[k]] : -1;
         }
         // rank of each IPv6 packet among the step's IPv6 packets, packet order
         // (lane-major): the lanes below hold sum(c) of them (c <= 4: three
@@ -1007,6 +1001,27 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         const int before = __popcll(b0 & below_me) + 2 * __popcll(b1 & below_me) +
                            4 * __popcll(b2 & below_me);
         const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        // the first round's rows are consecutive whatever packets they belong
+        // to: issue them before the IPv4 gathers, so their latency hides
+        // behind those.  Rows past n6c (a caller whose n6 is short) read the
+        // last row, or the zero address when there is none: never memory
+        // outside the rows.
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uint4 dw0 = z, sw0 = z;
+        if (lane < total && last >= 0) {
+            const int64_t k6 = row + lane;
+            const int64_t rw = k6 < last ? k6 : last;
+            dw0 = reinterpret_cast<const uint4*>(in.dst6)[rw];
+            sw0 = reinterpret_cast<const uint4*>(in.src6)[rw];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            e[k] = ok[k] && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
+        if (in.host_id) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) grp[k] = int64_t(hh4[k]) < in.n_pool ? in.pool_group[hh4[k]] : -1;
+        }
         int pos[4];
         int r = before;
 #pragma unroll
@@ -1023,14 +1038,13 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
             for (int r0 = 0; r0 < total; r0 += 64) {
                 if (r0 + lane < total) {
                     const int64_t gi = wbase + q6[r0 + lane];
-                    // rows past n6c (a caller whose n6 is short) read the last
-                    // row, or the zero address when there is none: never
-                    // memory outside the rows
-                    const int64_t k6 = row + r0 + lane;
-                    const int64_t rw = k6 < last ? k6 : last;
-                    const uint4 z = make_uint4(0, 0, 0, 0);
-                    const uint4 dw = last >= 0 ? reinterpret_cast<const uint4*>(in.dst6)[rw] : z;
-                    const uint4 sw = last >= 0 ? reinterpret_cast<const uint4*>(in.src6)[rw] : z;
+                    uint4 dw = dw0, sw = sw0;
+                    if (r0 > 0 && last >= 0) {
+                        const int64_t k6 = row + r0 + lane;
+                        const int64_t rw = k6 < last ? k6 : last;
+                        dw = reinterpret_cast<const uint4*>(in.dst6)[rw];
+                        sw = reinterpret_cast<const uint4*>(in.src6)[rw];
+                    }
                     const bool t6 = in.proto[gi] == VC_PROTO_TCP;
                     uint64_t hh, ll;
                     v6_key(dw, &hh, &ll);
