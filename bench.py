@@ -611,7 +611,8 @@ def main():
                     help="CU partition: the pool pass and the counter finish on this many CUs "
                          "(a CU-masked stream), the pipeline kernel on the rest (0: no masks)")
     ap.add_argument("--compact6", action="store_true",
-                    help="mix: IPv6 addresses as one row per IPv6 packet (vc_pipeline_c6_dev)")
+                    help="mix / mixhost: IPv6 addresses as one row per IPv6 packet "
+                         "(vc_pipeline_c6_dev / vc_pipeline_c6)")
     ap.add_argument("--v6-frac", type=float, default=0.15,
                     help="mix / mixhost: share of IPv6 packets (C3's mix is 0.15)")
     ap.add_argument("--dist", action="store_true",
@@ -1335,14 +1336,22 @@ def mix_bench(args, clf, dev, rank, O):
         hs = [x.cpu().numpy() for x in (fam, proto, src, dst, src6, dst6, dport, hid)]
         hs[2], hs[3] = hs[2].view(np.uint32), hs[3].view(np.uint32)
         hs[6], hs[7] = hs[6].view(np.uint16), hs[7].view(np.uint32)
+        if args.compact6:                          # one row per IPv6 packet, packet order
+            six = hs[0] == 6
+            hs[4], hs[5] = np.ascontiguousarray(hs[4][six]), np.ascontiguousarray(hs[5][six])
+            extra["compact6_rows"] = len(hs[4])
         hpool = pool.cpu().numpy()
         houts = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32), None)
         reg = hs + [hpool] + list(houts[:3])
         for x in reg:
-            V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
+            if x.nbytes:                           # (no rows at --v6-frac 0)
+                V.check(V.lib().vc_host_register(C.c_void_p(x.ctypes.data), x.nbytes))
         fn = lambda: clf.pipeline(hs[1], hs[2], hs[3], hs[6], hs[7], hpool, family=hs[0],
-                                  src6=hs[4], dst6=hs[5], outs=houts)
-        kern = "pipeline_mix_kernel, inputs and outputs over PCIe (chunked DMA staging), synchronous"
+                                  src6=hs[4], dst6=hs[5], outs=houts, compact6=args.compact6)
+        kern = ("pipeline_mix_kernel over registered host buffers, compact IPv6 rows "
+                "(vc_pipeline_c6, zero-copy), synchronous" if args.compact6 else
+                "pipeline_mix_kernel, inputs and outputs over PCIe (chunked DMA staging), "
+                "synchronous")
         fin = None
     for _ in range(args.warmup):
         fn()

@@ -341,12 +341,24 @@ int vc_pipeline_c6_dev(vc_ctx *ctx, const vc_packets *in, int64_t n, int64_t n6,
                        const int32_t *pool_group, int64_t n_pool, const vc_pipeline_out *out,
                        void *stream, void *count_stream, void *kernel_done_event);
 /* Host pointers (every array in `in` and `out`, and pool_group), synchronous.
- * Zero-copy when every array is inside a vc_host_register'ed buffer (the
- * kernel reads and writes across PCIe directly); otherwise the batch is
- * staged through device memory in chunks on two streams.  All chunks
- * classify against the snapshots current when the call started. */
+ * Zero-copy for an IPv4-only batch (no family array) whose every array is
+ * inside a vc_host_register'ed buffer (the kernel reads and writes across
+ * PCIe directly); otherwise the batch is staged through device memory in
+ * chunks on two streams (a mixed batch's scattered 16-byte IPv6 reads ran at
+ * 7 GB/s zero-copy).  All chunks classify against the snapshots current when
+ * the call started. */
 int vc_pipeline(vc_ctx *ctx, const vc_packets *in, int64_t n, const int32_t *pool_group,
                 int64_t n_pool, const vc_pipeline_out *out);
+/* vc_pipeline with compact IPv6 rows (as vc_pipeline_c6_dev: src6 / dst6
+ * hold n6 rows, row k the k-th family-6 packet's addresses; family
+ * required).  Zero-copy when every array is registered and aligned as
+ * vc_pipeline_c6_dev asks (the rows are read coalesced); otherwise staged
+ * in chunks, each chunk's rows found by counting its family-6 packets, and
+ * only the n6 rows cross PCIe instead of n.  The staged path checks n6
+ * against the family array: VC_EINVAL when they disagree (results are then
+ * unspecified); zero-copy trusts n6 as vc_pipeline_c6_dev does. */
+int vc_pipeline_c6(vc_ctx *ctx, const vc_packets *in, int64_t n, int64_t n6,
+                   const int32_t *pool_group, int64_t n_pool, const vc_pipeline_out *out);
 
 /* ------------------------------------------------------------------------ */
 /* Server choice after the group match, method == source:                    */

@@ -304,3 +304,63 @@ def test_compact6_short_rows_and_alignment(setup):
     with pytest.raises(V.IllegalArgumentException):
         clf.pipeline(dm["proto"], dm["src4"], dm["dst4"], dm["dport"], dm["host_id"], pool,
                      family=dm["family"], src6=s6, dst6=d6, compact6=True)
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_compact6_host_entry(setup, registered):
+    """vc_pipeline_c6 over host arrays, pageable (chunked staging: each
+    4M-packet chunk's rows found by counting its IPv6 packets; the second
+    chunk has none) or registered (zero-copy, the rows read coalesced), gives
+    the device entry point's outputs for the sparse batch; a row count that
+    disagrees with the family array is refused on the staged path."""
+    import torch
+    clf, t = setup
+    n = (9 << 20) + 5
+    p = _packets(t, n, 61)
+    rng = np.random.default_rng(61)
+    p["family"] = np.where(rng.random(n) < 0.15, 6, 4).astype(np.uint8)
+    p["family"][4 << 20:8 << 20] = 4
+    pool = np.array(t["pool"], np.int32)
+    ref = [x.cpu().numpy() for x in _call(clf, _dev(p), torch.from_numpy(pool).cuda())]
+    six = p["family"] == 6
+    s6, d6 = np.ascontiguousarray(p["src6"][six]), np.ascontiguousarray(p["dst6"][six])
+    outs = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32),
+            np.empty(n, np.uint8))
+    bufs = [p[k] for k in ("family", "proto", "src4", "dst4", "dport", "host_id")] + [
+        s6, d6, pool] + list(outs)
+    if registered:
+        for x in bufs:
+            V.check(V.lib().vc_host_register(x.ctypes.data, x.nbytes))
+    try:
+        got = clf.pipeline(p["proto"], p["src4"], p["dst4"], p["dport"], p["host_id"], pool,
+                           family=p["family"], src6=s6, dst6=d6, outs=outs, compact6=True)
+    finally:
+        if registered:
+            for x in bufs:
+                V.check(V.lib().vc_host_unregister(x.ctypes.data))
+    for g, r, name in zip(got, ref, ("acl", "route", "group", "allow")):
+        np.testing.assert_array_equal(g, r, err_msg=name)
+    if not registered:
+        for k in (len(s6) - 1, len(s6) + 1):
+            rows = np.zeros((k, 16), np.uint8)
+            with pytest.raises(V.IllegalArgumentException):
+                clf.pipeline(p["proto"], p["src4"], p["dst4"], p["dport"], p["host_id"], pool,
+                             family=p["family"], src6=rows, dst6=rows, compact6=True)
+
+
+def test_compact6_host_entry_small(setup):
+    """vc_pipeline_c6 at sizes below one chunk: no IPv6 packet (no rows),
+    only IPv6 packets, a partial group of four."""
+    clf, t = setup
+    for n, frac in ((1, 0.0), (1, 1.0), (7, 0.5), (4099, 0.0), (4099, 1.0)):
+        p = _packets(t, n, 67 + n)
+        rng = np.random.default_rng(n)
+        p["family"] = np.where(rng.random(n) < frac, 6, 4).astype(np.uint8)
+        want = _oracle(t, p)
+        six = p["family"] == 6
+        s6, d6 = np.ascontiguousarray(p["src6"][six]), np.ascontiguousarray(p["dst6"][six])
+        got = clf.pipeline(p["proto"], p["src4"], p["dst4"], p["dport"], p["host_id"],
+                           t["pool"], family=p["family"], src6=s6, dst6=d6, want_allow=True,
+                           compact6=True)
+        for g, w, name in zip(got, want, ("acl", "route", "group", "allow")):
+            np.testing.assert_array_equal(g, w, err_msg="%s n=%d frac=%s" % (name, n, frac))

@@ -185,6 +185,7 @@ def lib():
         L.vc_pipeline_c6_dev.argtypes = [vp, P(VcPackets), i64, i64, vp, i64, P(VcPipelineOut), vp,
                                          vp, vp]
         L.vc_pipeline.argtypes = [vp, P(VcPackets), i64, vp, i64, P(VcPipelineOut)]
+        L.vc_pipeline_c6.argtypes = [vp, P(VcPackets), i64, i64, vp, i64, P(VcPipelineOut)]
         L.vc_compile_servers.argtypes = [vp, P(VcServer), vp, i32]
         L.vc_servers_set_health.argtypes = [vp, vp, i64]
         for f in ("vc_source_select_v4_dev", "vc_source_select_v6_dev"):

@@ -578,8 +578,8 @@ class Classifier:
         -> pool_group[host_id].  torch CUDA tensors run on the device
         (asynchronous, torch's current stream); numpy arrays take the host
         entry point (synchronous, PCIe included).  src6/dst6: n x 16 bytes, or
-        with compact6 (device tensors only, vc_pipeline_c6_dev) one row per
-        IPv6 packet in packet order.  Returns (acl, route, group, allow)."""
+        with compact6 (vc_pipeline_c6_dev, or vc_pipeline_c6 for numpy) one
+        row per IPv6 packet in packet order.  Returns (acl, route, group, allow)."""
         n = len(proto)
         dev = _is_dev(proto)
         if dev:
@@ -619,6 +619,9 @@ class Classifier:
                                         if count_stream is not None else None,
                                         C.c_void_p(kernel_done_event)
                                         if kernel_done_event else None))
+        elif compact6:
+            check(lib().vc_pipeline_c6(self.h, C.byref(pk), n, len(src6), _ptr(pool_group),
+                                       n_pool, C.byref(po)))
         else:
             check(lib().vc_pipeline(self.h, C.byref(pk), n, _ptr(pool_group), n_pool,
                                     C.byref(po)))

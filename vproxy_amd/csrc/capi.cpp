@@ -1789,6 +1789,14 @@ int vc_pipeline_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t*
                         kernel_done_event, pin);
 }
 
+// the alignment the compact-row kernel's vector loads need
+static bool c6_aligned(const vc_packets& in, const vc_pipeline_out& out) {
+    auto al = [](const void* p, uintptr_t a) { return !p || (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    return al(in.family, 4) && al(in.proto, 4) && al(in.src4, 16) && al(in.dst4, 16) &&
+           al(in.dport, 8) && al(in.host_id, 16) && al(out.acl, 16) && al(out.route, 16) &&
+           al(out.group, 16) && al(out.allow, 4);
+}
+
 int vc_pipeline_c6_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
                        const int32_t* pool_group, int64_t n_pool, const vc_pipeline_out* out,
                        void* stream, void* count_stream, void* kernel_done_event) {
@@ -1807,10 +1815,7 @@ int vc_pipeline_c6_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
                                          : VC_OK;
     if (!in->family || n6 < 0 || (n6 > 0 && (!in->src6 || !in->dst6)))
         return fail(VC_EINVAL, "compact IPv6 rows need the family array and n6 >= 0 rows");
-    auto al = [](const void* p, uintptr_t a) { return !p || (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
-    if (!al(in->family, 4) || !al(in->proto, 4) || !al(in->src4, 16) || !al(in->dst4, 16) ||
-        !al(in->dport, 8) || !al(in->host_id, 16) || !al(out->acl, 16) || !al(out->route, 16) ||
-        !al(out->group, 16) || !al(out->allow, 4))
+    if (!c6_aligned(*in, *out))
         return fail(VC_EINVAL, "vc_pipeline_c6_dev needs 16-byte aligned 4-byte fields (4-byte "
                                "aligned family / proto / allow, 8-byte aligned dport)");
     const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
@@ -1818,12 +1823,10 @@ int vc_pipeline_c6_dev(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
                         kernel_done_event, pin, n6);
 }
 
-int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,
-                int64_t n_pool, const vc_pipeline_out* out) {
-    int rc = set_dev(ctx);
-    if (rc) return rc;
-    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
-    if (n == 0) return VC_OK;
+// The host entry points: vc_pipeline (n6 < 0: src6 / dst6 hold n rows) and
+// vc_pipeline_c6 (n6 >= 0: one row per IPv6 packet, packet order).
+static int pipeline_host(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
+                         const int32_t* pool_group, int64_t n_pool, const vc_pipeline_out* out) {
     const PipePins pin{ctx->get(ctx->acl), ctx->get(ctx->route), ctx->get(ctx->hint)};
     if (!pin.a || !pin.r) return fail(VC_ESTATE, "SecurityGroup and RouteTable must be compiled");
     const size_t un = size_t(n);
@@ -1843,29 +1846,21 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
     m.proto = static_cast<const uint8_t*>(map(in->proto, un, 1));
     m.src4 = static_cast<const uint32_t*>(map(in->src4, un * 4, 4));
     m.dst4 = static_cast<const uint32_t*>(map(in->dst4, un * 4, 4));
-    m.src6 = static_cast<const uint8_t*>(map(six ? in->src6 : nullptr, un * 16, 16));
-    m.dst6 = static_cast<const uint8_t*>(map(six ? in->dst6 : nullptr, un * 16, 16));
+    const bool c6 = n6 >= 0;
+    const size_t rows = c6 ? size_t(n6) : un;
+    m.src6 = static_cast<const uint8_t*>(map(six ? in->src6 : nullptr, rows * 16, 16));
+    m.dst6 = static_cast<const uint8_t*>(map(six ? in->dst6 : nullptr, rows * 16, 16));
+    if (c6 && !rows) m.src6 = m.dst6 = in->src6;                // never read
     m.dport = static_cast<const uint16_t*>(map(in->dport, un * 2, 2));
     m.host_id = static_cast<const uint32_t*>(map(in->host_id, un * 4, 4));
-    const auto* mpool = static_cast<const int32_t*>(map(pool_bytes ? pool_group : nullptr,
-                                                        pool_bytes, 4));
     mo.acl = static_cast<int32_t*>(map(out->acl, un * 4, 4));
     mo.route = static_cast<int32_t*>(map(out->route, un * 4, 4));
     mo.group = static_cast<int32_t*>(map(out->group, un * 4, 4));
     mo.allow = static_cast<uint8_t*>(map(out->allow, un, 1));
-    // Zero-copy only for IPv4-only batches: their SoA reads are coalesced.  A
-    // mixed batch reads 16-byte IPv6 addresses for a scattered 15 % of its
-    // packets, which across PCIe ran at 7 GB/s; staging it with DMA copies
-    // (registered memory copies at full rate) is faster.
-    if (zc && !six) {
-        rc = pipeline_dev(ctx, m, n, mpool, n_pool, mo, ctx->stream, nullptr, nullptr, pin);
-        if (rc) return rc;
-        hipError_t e = hipStreamSynchronize(ctx->stream);
-        if (e != hipSuccess) return hip_fail(e, "pipeline");
-        return ctx->sync_check ? devcheck_report("pipeline") : VC_OK;
-    }
-    // chunked staging; the hostname pool results are uploaded once, on the
-    // stager's whole-call lane, and stay there for every chunk
+    // The hostname pool results are uploaded once, on the stager's whole-call
+    // lane, and stay there for the call: pool_group[host_id] is a random
+    // 4-byte gather per packet, which across PCIe (a registered pool read
+    // zero-copy) held a compact-row batch to 8.8 GB/s.
     StagerLease lease(ctx);
     if (!lease) return hip_fail(lease.err(), "pipeline");
     Staging pst(ctx, lease.lane(2), "pool upload");
@@ -1873,17 +1868,47 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
         ? static_cast<const int32_t*>(pst.in(pool_group, pool_bytes)) : nullptr;
     if (pst.err == hipSuccess) pst.err = lease.lane(2).wait();
     if (pst.err != hipSuccess) return hip_fail(pst.err, "pool upload");
-    return host_chunks(ctx, lease, n, "pipeline", [&](Staging& st, int64_t lo, int64_t c,
-                                                      hipStream_t s) {
+    // Zero-copy for IPv4-only batches and for compact IPv6 rows: their reads
+    // are coalesced.  A mixed batch with n rows reads 16-byte IPv6 addresses
+    // for a scattered 15 % of its packets, which across PCIe ran at 7 GB/s;
+    // staging it with DMA copies (registered memory copies at full rate) is
+    // faster.  The compact kernel's vector loads need the alignment
+    // vc_pipeline_c6_dev asks for; a batch without it is staged.
+    if (zc && c6) zc = c6_aligned(m, mo);
+    if (zc && (!six || c6)) {
+        int rc = pipeline_dev(ctx, m, n, dpool, n_pool, mo, ctx->stream, nullptr, nullptr, pin,
+                              n6);
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return hip_fail(e, "pipeline");
+        return ctx->sync_check ? devcheck_report("pipeline") : VC_OK;
+    }
+    // chunked staging
+    int64_t row = 0;                                // compact rows: the chunk's first row
+    const int rc = host_chunks(ctx, lease, n, "pipeline", [&](Staging& st, int64_t lo, int64_t c,
+                                                              hipStream_t s) {
         const size_t u = size_t(lo), k = size_t(c);
         vc_packets d{};
         vc_pipeline_out o{};
+        // compact rows: the chunk's IPv6 packets are the next k6 rows (the
+        // count overlaps the previous chunk's copies and kernel)
+        int64_t k6 = 0;
+        if (c6) {
+            for (size_t i = 0; i < k; ++i) k6 += in->family[u + i] == 6;
+            if (row + k6 > n6) return fail(VC_EINVAL, "the family array has more IPv6 packets "
+                                                      "than n6 rows");
+        }
+        const size_t r0 = c6 ? size_t(row) : u, rk = c6 ? size_t(k6) : k;
         d.family = six ? static_cast<const uint8_t*>(st.in(in->family + u, k)) : nullptr;
         d.proto = static_cast<const uint8_t*>(st.in(in->proto + u, k));
         d.src4 = static_cast<const uint32_t*>(st.in(in->src4 + u, k * 4));
         d.dst4 = static_cast<const uint32_t*>(st.in(in->dst4 + u, k * 4));
-        d.src6 = six ? static_cast<const uint8_t*>(st.in(in->src6 + u * 16, k * 16)) : nullptr;
-        d.dst6 = six ? static_cast<const uint8_t*>(st.in(in->dst6 + u * 16, k * 16)) : nullptr;
+        d.src6 = six && rk ? static_cast<const uint8_t*>(st.in(in->src6 + r0 * 16, rk * 16))
+                           : nullptr;
+        d.dst6 = six && rk ? static_cast<const uint8_t*>(st.in(in->dst6 + r0 * 16, rk * 16))
+                           : nullptr;
+        if (six && !rk) d.src6 = d.dst6 = d.family;             // no rows: never read
+        row += k6;
         d.dport = static_cast<const uint16_t*>(st.in(in->dport + u, k * 2));
         d.host_id = in->host_id ? static_cast<const uint32_t*>(st.in(in->host_id + u, k * 4))
                                 : nullptr;
@@ -1892,7 +1917,8 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
         o.group = static_cast<int32_t*>(st.out(out->group, k * 4));
         o.allow = static_cast<uint8_t*>(st.out(out->allow, k));
         if (st.err != hipSuccess) return VC_OK;               // reported by host_chunks
-        int r = pipeline_dev(ctx, d, c, dpool, n_pool, o, s, nullptr, nullptr, pin);
+        int r = pipeline_dev(ctx, d, c, dpool, n_pool, o, s, nullptr, nullptr, pin,
+                             c6 ? k6 : -1);
         if (r) return r;
         st.back(out->acl + u, o.acl, k * 4);
         st.back(out->route + u, o.route, k * 4);
@@ -1900,6 +1926,33 @@ int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* poo
         if (out->allow) st.back(out->allow + u, o.allow, k);
         return VC_OK;
     });
+    if (rc == VC_OK && c6 && row != n6)
+        return fail(VC_EINVAL, "the family array has fewer IPv6 packets than n6 rows");
+    return rc;
+}
+
+int vc_pipeline(vc_ctx* ctx, const vc_packets* in, int64_t n, const int32_t* pool_group,
+                int64_t n_pool, const vc_pipeline_out* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
+    if (n == 0) return VC_OK;
+    return pipeline_host(ctx, in, n, -1, pool_group, n_pool, out);
+}
+
+int vc_pipeline_c6(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
+                   const int32_t* pool_group, int64_t n_pool, const vc_pipeline_out* out) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    alignas(16) static const uint8_t kNoRows[16] = {};
+    vc_packets m = in ? *in : vc_packets{};
+    if (in && n6 == 0) m.src6 = m.dst6 = kNoRows;
+    in = in ? &m : nullptr;
+    if ((rc = pipeline_check(in, n, pool_group, n_pool, out)) != VC_OK) return rc;
+    if (n == 0) return VC_OK;
+    if (!in->family || n6 < 0 || n6 > n)
+        return fail(VC_EINVAL, "compact IPv6 rows need the family array and 0 <= n6 <= n rows");
+    return pipeline_host(ctx, in, n, n6, pool_group, n_pool, out);
 }
 
 // ---------------------------------------------------------------------------
