@@ -92,6 +92,19 @@ public final class GpuClassifier {
                                        ByteBuffer outAllow) throws IOException;
 
     /**
+     * pipeline with compact IPv6 rows: src6 / dst6 hold n6 rows of 16 bytes, row k the addresses
+     * of the batch's k-th family-6 packet (packet order); family is required.  Runs zero-copy over
+     * registered buffers; n6 must equal the number of family-6 packets.
+     */
+    public static native void pipelineCompact6(long ctx, ByteBuffer family, ByteBuffer proto,
+                                               ByteBuffer src4, ByteBuffer dst4, ByteBuffer src6,
+                                               ByteBuffer dst6, int n6, ByteBuffer dport,
+                                               ByteBuffer hostId, ByteBuffer poolGroup, int nPool,
+                                               int n, ByteBuffer outAcl, ByteBuffer outRoute,
+                                               ByteBuffer outGroup, ByteBuffer outAllow)
+        throws IOException;
+
+    /**
      * Switch.PacketHandler.readable per datagram: bareVXLanAccess.allow on the sender, the VXLAN
      * parse (out: 12 buffers in vc_pkt_out order, null = skip) and the inner packet's route in the
      * table of its VNI.  Only datagrams VProxyEncryptedPacket.from rejected belong in the batch

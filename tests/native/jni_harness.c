@@ -98,6 +98,9 @@ void J(switchClassify)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jo
 
 void J(compileCerts)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jint, jint);
 void J(classifyDns)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jobject, jobject);
+void J(pipelineCompact6)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject,
+                        jobject, jint, jobject, jobject, jobject, jint, jint, jobject, jobject,
+                        jobject, jobject);
 
 /* Fault injection.  The executable's definitions of these entry points
  * preempt libvclassify's for the shim linked into it: with inject_rc set
@@ -213,6 +216,22 @@ static void cpu_mode(void) {
         J(classifyDns)(env, NULL, 0, &bq2, &bo3, 2, &bk, &bv);
         expect_throw("java/lang/IllegalArgumentException", "non-decreasing", "dns offsets");
     }
+    {   /* compact IPv6 rows: family required, n6 rows of src6 / dst6 */
+        uint8_t fam[8] = {4, 6, 4, 4, 6, 4, 4, 4}, rows[32] = {0};
+        int32_t r[8], g2[8];
+        struct _jobject bf = B(fam, 8), b6 = B(rows, 32), b6s = B(rows, 31), br2 = B(r, 32),
+                        bg2 = B(g2, 32);
+        J(pipelineCompact6)(env, NULL, 0, NULL, &bp, &bs, &bs, &b6, &b6, 2, &bq, NULL, NULL, 0, 8,
+                            &bo, &br2, &bg2, NULL);
+        expect_throw("java/lang/IllegalArgumentException", "required", "compact rows, null family");
+        J(pipelineCompact6)(env, NULL, 0, &bf, &bp, &bs, &bs, &b6s, &b6, 2, &bq, NULL, NULL, 0, 8,
+                            &bo, &br2, &bg2, NULL);
+        expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",
+                     "compact rows, short src6");
+        J(pipelineCompact6)(env, NULL, 0, &bf, &bp, &bs, &bs, &b6, &b6, -1, &bq, NULL, NULL, 0, 8,
+                            &bo, &br2, &bg2, NULL);
+        expect_throw("java/lang/IllegalArgumentException", "negative", "compact rows, n6 < 0");
+    }
     /* the statuses GpuContext keys its fallback on (jni/GpuContext.java) */
     bs.cap = 32;
     bo.cap = 32;
@@ -286,6 +305,49 @@ static void gpu_mode(void) {
     CHECK(vc_compile_routes(ctx, routes, NR, NULL, 0) == VC_OK, "vc_compile_routes");
     CHECK(vc_route_lookup_v4(ctx, dst, N, o2) == VC_OK, "vc_route_lookup_v4");
     CHECK(memcmp(o1, o2, sizeof o1) == 0, "routes through the shim == the C ABI");
+    {   /* the mixed pipeline with compact IPv6 rows through the shim == the
+         * sparse form through the C ABI (every 5th packet IPv6) */
+        static uint8_t fam[N], s6[N][16], d6[N][16], c6s[N][16], c6d[N][16];
+        static int32_t g1[N], g2[N], q1[N], q2[N];
+        vc_packets in;
+        vc_pipeline_out out;
+        int n6 = 0;
+        struct _jobject bf = B(fam, N), bcs = B(c6s, 16 * N), bcd = B(c6d, 16 * N),
+                        bq1 = B(q1, 4 * N), bg1 = B(g1, 4 * N);
+        for (i = 0; i < N; ++i) {
+            int k;
+            fam[i] = i % 5 == 2 ? 6 : 4;
+            for (k = 0; k < 16; ++k) {
+                s6[i][k] = (uint8_t) rnd();
+                d6[i][k] = (uint8_t) rnd();
+            }
+            if (i % 3 == 0) memset(s6[i], 0, 12);          /* ::a.b.c.d against v4 rules */
+            if (fam[i] == 6) {
+                memcpy(c6s[n6], s6[i], 16);
+                memcpy(c6d[n6], d6[i], 16);
+                ++n6;
+            }
+        }
+        J(pipelineCompact6)(env, NULL, h, &bf, &bp, &bs, &bd, &bcs, &bcd, n6, &bq, NULL, NULL, 0,
+                            N, &bo, &bq1, &bg1, &ba);
+        CHECK(!n_thrown, "pipelineCompact6");
+        memset(&in, 0, sizeof in);
+        in.family = fam;
+        in.proto = proto;
+        in.src4 = src;
+        in.dst4 = dst;
+        in.src6 = &s6[0][0];
+        in.dst6 = &d6[0][0];
+        in.dport = port;
+        out.acl = o2;
+        out.route = q2;
+        out.group = g2;
+        out.allow = a2;
+        CHECK(vc_pipeline(ctx, &in, N, NULL, 0, &out) == VC_OK, "vc_pipeline");
+        CHECK(memcmp(o1, o2, sizeof o1) == 0 && memcmp(q1, q2, sizeof q1) == 0 &&
+              memcmp(a1, a2, sizeof a1) == 0 && memcmp(g1, g2, sizeof g1) == 0,
+              "compact-row pipeline through the shim == the sparse form through the C ABI");
+    }
     {   /* per-VNI tables through the shim: the VNI-10 table is routes[0..150) */
         int32_t vni[2] = {10, 20}, off4[3] = {0, 150, NR}, off6[3] = {0, 0, 0};
         struct _jobject bv = B(vni, 8), b4o = B(off4, 12), b6o = B(off6, 12);
