@@ -358,6 +358,93 @@ def test_hint_work_tickets_wrap(clf):
         np.testing.assert_array_equal(o.cpu().numpy(), want[:n])
 
 
+def test_hint_deferred_lanes_over_slot_reuse(clf):
+    """The host-only pool pass leaves lanes that need an out-of-line step
+    (port filters over hint-port minima, IPv6 literals and other names the
+    word scan does not cover, chunks too long for the stage) to a second
+    kernel, counted in the launch's ticket slot, which that kernel resets.
+    Over 4300 launches (every slot reused) of batches with and without such
+    lanes, on two streams, every result equals the oracle's."""
+    import ctypes as C
+    import torch
+    from cases import hint_cases_shapes
+    groups, names = hint_cases_shapes(np.random.default_rng(97), 6000)
+    clf.compile_upstream(groups)
+    og = O.Groups(groups)
+    ports = np.random.default_rng(98).choice(np.array([0, 0, 80, 8080], np.uint16), len(names))
+    blob, off = W.pack(names)
+    want = O.hint_batch_np(og, blob, off, ports, nthreads=THREADS)
+    zero = O.hint_batch_np(og, blob, off, np.zeros_like(ports), nthreads=THREADS)
+    bd = torch.from_numpy(blob.astype(np.uint8)).cuda()
+    od = torch.from_numpy(off.astype(np.int32)).cuda()
+    pd = torch.from_numpy(ports.astype(np.int16)).cuda()
+    sizes = [1, 64, 65, 1025, 3000, 6000]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(4300):
+        n = sizes[k % len(sizes)]
+        s = streams[k % 2]
+        with_ports = (k // len(sizes)) % 2 == 0
+        with torch.cuda.stream(s):
+            o = torch.empty(n, dtype=torch.int32, device="cuda")
+            V.check(V.lib().vc_hint_search_dev(
+                clf.h, C.c_void_p(bd.data_ptr()), C.c_void_p(od.data_ptr()), None,
+                C.c_void_p(pd.data_ptr()) if with_ports else None, None, None, None, n,
+                C.c_void_p(o.data_ptr()), C.c_void_p(s.cuda_stream)))
+        if k % 300 < 12 or k >= 4288:
+            outs.append((n, with_ports, o))
+    torch.cuda.synchronize()
+    for n, with_ports, o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), (want if with_ports else zero)[:n])
+
+
+def test_dns_deferred_queries_over_slot_reuse(clf):
+    """dns_kernel leaves the queries that may be IP literals, carry bytes
+    >= 0x80 or have names the host scan does not cover to a second kernel
+    (counted in the launch's ticket slot, which that kernel resets).  Over
+    4300 launches of batches with and without such queries, on two streams,
+    every result equals the one-shot host call's (itself checked against the
+    oracle by test_dns_kats_and_random)."""
+    import ctypes as C
+    import torch
+    groups, ghosts = W.gen_groups(2000, 87)
+    clf.compile_upstream(groups)
+    clf.compile_hosts([(h + ".", i) for i, h in enumerate(ghosts[:40])])
+    rng = np.random.default_rng(88)
+    plain = W.gen_hostnames(ghosts, 3000, 89, dns=True)
+    odd = [b"1.2.3.4.", b"::1.", b"[::1].", b"fe80::1.", b"::ffff:1.2.3.4.", b"abc.def.",
+           b"\xc3\xa9t\xc3\xa9.com.", b"\xff.", b"a.b.c.d.e.f.g.h.i.j.", b"dead.beef."]
+    mixed = [odd[int(k)] if rng.random() < 0.1 else plain[i]
+             for i, k in enumerate(rng.integers(0, len(odd), 3000))]
+    wants = []
+    for names in (plain, mixed):
+        wants.append(clf.dns_classify(names))
+    devs = []
+    for names in (plain, mixed):
+        blob, off, _ = pack_strings(names)
+        devs.append((torch.from_numpy(blob).cuda(), torch.from_numpy(off.astype(np.int32)).cuda()))
+    sizes = [1, 65, 1025, 3000]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(4300):
+        n = sizes[k % len(sizes)]
+        which = (k // len(sizes)) % 2
+        s = streams[k % 2]
+        qb, qo = devs[which]
+        with torch.cuda.stream(s):
+            kd = torch.empty(n, dtype=torch.uint8, device="cuda")
+            vl = torch.empty(n, dtype=torch.int32, device="cuda")
+            V.check(V.lib().vc_dns_classify_dev(
+                clf.h, C.c_void_p(qb.data_ptr()), C.c_void_p(qo.data_ptr()), n,
+                C.c_void_p(kd.data_ptr()), C.c_void_p(vl.data_ptr()), C.c_void_p(s.cuda_stream)))
+        if k % 300 < 8 or k >= 4292:
+            outs.append((n, which, kd, vl))
+    torch.cuda.synchronize()
+    for n, which, kd, vl in outs:
+        np.testing.assert_array_equal(kd.cpu().numpy(), wants[which][0][:n])
+        np.testing.assert_array_equal(vl.cpu().numpy(), wants[which][1][:n])
+
+
 def test_hint_c4_scale(clf):
     """C4: 100k hint-host groups vs 1M hostnames (16M in the bench);
     oracle-checked sample (each oracle query scans all 100k groups)."""

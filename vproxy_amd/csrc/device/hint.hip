@@ -32,6 +32,12 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_HINT_PRE
 #define VC_HINT_PRE 0
 #endif
+#ifndef VC_HINT_DEFER
+#define VC_HINT_DEFER 1
+#endif
+#ifndef VC_DNS_DEFER
+#define VC_DNS_DEFER 1
+#endif
 #ifndef VC_DNS_MINW
 #define VC_DNS_MINW 6
 #endif
@@ -125,7 +131,11 @@ __device__ __forceinline__ void chunk_loop(Chunks& ch, int w, const uint8_t* blo
     }
 }
 
-template <bool kStage>
+// kDefer (no hint-uri in the batch or the image): host-only levels with no
+// call in the loop -- lanes that need an out-of-line step are written as
+// kDeferred and counted in ticket[1] for hint_defer_kernel, which runs next
+// on the stream.  Otherwise every lane is finished here (the general path).
+template <bool kStage, bool kDefer>
 __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
@@ -135,7 +145,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     Chunks ch(ticket, (n + 63) / 64);
-    const bool general = uri_blob && img.has_uri_keys;
+    const bool general = !kDefer && uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
     // pointers the compiler then knows to be global).
@@ -144,21 +154,24 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     chunk_loop<kStageBytes, true, VC_HINT_PRE>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
                                   [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         const int64_t i = c * 64 + lane;
+        int32_t r = -1;
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
             const bool has_host = host_blob && !(host_null && host_null[i]);
             const bool has_uri = uri_blob && !(uri_null && uri_null[i]);
-            int32_t r = -1;
             if (!general || !has_uri) {
                 // uri null (or no hint-uri anywhere): host-only levels
                 if (has_host) {
                     if (staged)
-                        r = host_only_fast(img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
-                                           int(e - a), p);
+                        r = host_only_fast<kDefer>(img, &slow_img,
+                                                   LdsSrc{stage[w], int(kApron + (a - a0))},
+                                                   int(e - a), p);
+                    else if (kDefer)
+                        r = kDeferred;
                     else
                         r = host_only_slow(slow_img, host_blob + a, int(e - a), p);
                 }
-            } else {
+            } else if (!kDefer) {
                 DStr h{nullptr, -1}, u{nullptr, -1};
                 if (has_host) h = DStr{host_blob + a, int(e - a)};
                 const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
@@ -167,11 +180,42 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             }
             out[i] = r;
         }
+        if (kDefer && ticket) {
+            const uint64_t dm = __ballot(i < n && r == kDeferred);
+            if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
+        }
     });
     VC_PEND();
 }
 
-template <bool kStage>
+// The lanes hint_kernel<*, true> deferred, through the reference-shaped
+// host-only search (Hint.formatHost + every dot-suffix probed in turn).
+// ctl = the launch's ticket slot: [1] deferred lanes (0: nothing to do),
+// [2] workgroups done; the last workgroup zeroes both for the slot's next
+// launch.  Without a slot every workgroup scans.
+__global__ __launch_bounds__(256) void hint_defer_kernel(
+    HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
+    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out, uint32_t* ctl) {
+    __shared__ uint32_t todo;
+    if (threadIdx.x == 0) todo = ctl ? __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                     : 1u;
+    __syncthreads();
+    if (todo) {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+             i += int64_t(gridDim.x) * blockDim.x) {
+            if (out[i] != kDeferred) continue;
+            const uint32_t a = host_off[i], e = host_off[i + 1];
+            out[i] = host_only_slow(img, host_blob + a, int(e - a), port ? int(port[i]) : 0);
+        }
+    }
+    if (ctl && threadIdx.x == 0 && atomicAdd(ctl + 2, 1u) == gridDim.x - 1) {
+        atomicExch(ctl + 1, 0u);
+        atomicExch(ctl + 2, 0u);
+    }
+}
+
+template <bool kStage, bool kDefer>
 __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
     const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
@@ -190,22 +234,60 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
         uint32_t a0 = 0;
         const bool staged = kStage && stage_wave<kStageBytes>(qblob, qoff[base], qoff[last], stage[w], &a0);
         VC_PMARK(0);
+        uint8_t kd = 0;
         if (i < n) {
             const uint32_t a = qoff[i], e = qoff[i + 1];
             VC_CHECK(a <= e && e <= qoff[n], 302, i, e);
-            uint8_t kd;
-            int32_t val;
-            if (staged)
-                dns_one(hosts, img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a), &kd, &val);
-            else
+            int32_t val = 0;
+            if (staged) {
+                dns_one<kDefer>(hosts, img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
+                                int(e - a), &kd, &val);
+            } else if (kDefer) {
+                kd = kDnsDeferred;
+            } else {
                 dns_one(hosts, img, &slow_img, PtrSrc{qblob + a}, int(e - a), &kd, &val);
+            }
             kind[i] = kd;
             value[i] = val;
+        }
+        if (kDefer && ticket) {
+            const uint64_t dm = __ballot(i < n && kd == kDnsDeferred);
+            if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
         }
         if (kStage) wave_done();
         VC_PMARK(5);
     }
     VC_PEND();
+}
+
+// The queries dns_kernel<*, true> deferred, through the complete flow
+// (out-of-line IP-literal parse, high-byte transcoding, the reference-shaped
+// host search).  ctl as hint_defer_kernel's.
+__global__ __launch_bounds__(256) void dns_defer_kernel(
+    HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
+    const uint32_t* __restrict__ qoff, int64_t n, uint8_t* __restrict__ kind,
+    int32_t* __restrict__ value, uint32_t* ctl) {
+    __shared__ uint32_t todo;
+    if (threadIdx.x == 0) todo = ctl ? __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                     : 1u;
+    __syncthreads();
+    if (todo) {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+             i += int64_t(gridDim.x) * blockDim.x) {
+            if (kind[i] != kDnsDeferred) continue;
+            const uint32_t a = qoff[i], e = qoff[i + 1];
+            uint8_t kd;
+            int32_t val;
+            dns_one(hosts, img, &img, PtrSrc{qblob + a}, int(e - a), &kd, &val);
+            kind[i] = kd;
+            value[i] = val;
+        }
+    }
+    if (ctl && threadIdx.x == 0 && atomicAdd(ctl + 2, 1u) == gridDim.x - 1) {
+        atomicExch(ctl + 1, 0u);
+        atomicExch(ctl + 2, 0u);
+    }
 }
 
 template <bool kStage>
@@ -561,19 +643,28 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                        int64_t n, int32_t* out, unsigned long long* counters) {
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    if (host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::hint_kernel<true>,
-                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<true>), vcd::kHintBlock, 0, want)),
+    const bool stage = host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0;
+    // the deferring kernel when no lane takes the general (hint-uri) path
+    const bool defer = VC_HINT_DEFER && stage && !(uri_blob && img.has_uri_keys);
+    uint32_t* ticket = c.tickets ? c.tickets->next(c.stream) : nullptr;
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
-    else
-        hipLaunchKernelGGL(vcd::hint_kernel<false>,
-                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::hint_kernel<false>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
-                           img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
-                           n, out, c.tickets ? c.tickets->next(c.stream) : nullptr);
+                           n, out, ticket);
+    };
+    if (defer) go(vcd::hint_kernel<true, true>);
+    else if (stage) go(vcd::hint_kernel<true, false>);
+    else go(vcd::hint_kernel<false, false>);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && defer) {
+        const int64_t dwant = (n + 255) / 256;
+        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        hipLaunchKernelGGL(vcd::hint_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
+                           img, host_blob, host_off, port, n, out, ticket);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, img.n_groups, 0, img.n_groups, 0,
                        counters);
@@ -584,19 +675,26 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
                       int32_t* value, unsigned long long* group_counters) {
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
-    if ((reinterpret_cast<uintptr_t>(qblob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::dns_kernel<true>,
-                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<true>), vcd::kHintBlock, 0, want)),
+    const bool stage = (reinterpret_cast<uintptr_t>(qblob) & 3) == 0;
+    const bool defer = VC_DNS_DEFER && stage;
+    uint32_t* ticket = c.tickets ? c.tickets->next(c.stream) : nullptr;
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel,
+                           dim3(resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHintBlock, 0, want)),
                            dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
-                           hosts, hints, qblob, qoff, n, kind, value,
-                           c.tickets ? c.tickets->next(c.stream) : nullptr);
-    else
-        hipLaunchKernelGGL(vcd::dns_kernel<false>,
-                           dim3(resident_grid(c, reinterpret_cast<const void*>(vcd::dns_kernel<false>), vcd::kHintBlock, 0, want)),
-                           dim3(vcd::kHintBlock), vcd::kProfLds, c.stream,
-                           hosts, hints, qblob, qoff, n, kind, value,
-                           c.tickets ? c.tickets->next(c.stream) : nullptr);
+                           hosts, hints, qblob, qoff, n, kind, value, ticket);
+    };
+    if (defer) go(vcd::dns_kernel<true, true>);
+    else if (stage) go(vcd::dns_kernel<true, false>);
+    else go(vcd::dns_kernel<false, false>);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && defer) {
+        const int64_t dwant = (n + 255) / 256;
+        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        hipLaunchKernelGGL(vcd::dns_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
+                           hosts, hints, qblob, qoff, n, kind, value, ticket);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess || !group_counters) return e;
     return launch_hist(c, VC_HIST_DNS, value, kind, n, hints.n_groups, 0, hints.n_groups, 0,
                        group_counters);

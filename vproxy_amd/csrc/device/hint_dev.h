@@ -478,6 +478,34 @@ VC_HD uint32_t wildcard_pick(const HintImage& img, int port) {
                 port);
 }
 
+// The deferring fast path (kDefer below) leaves a lane that needs an
+// out-of-line step -- the port filter over a key's distinct hint-port
+// minima, a name the word scan does not cover, an unstaged chunk -- marked
+// with kDeferred for the reference-shaped pass that follows the kernel
+// (hint.hip hint_defer_kernel), so the kernel's loop contains no call: a
+// call site inside it makes the compiler keep the loop's state in scratch
+// and spill SGPRs across the call on every chunk.
+constexpr int32_t kDeferred = INT32_MIN;
+
+template <bool kDefer>
+VC_HD uint32_t pick_or_defer(const HintImage& img, int slot, const Rec& r, int port,
+                             bool* defer) {
+    if (!kDefer) return pick(img, slot, r, port);
+    if (port == 0) return r.m.y;
+    if (!(r.m.x & VC_REC_HAS_PM)) return r.m.z;
+    *defer = true;
+    return VC_NONE;
+}
+
+template <bool kDefer>
+VC_HD uint32_t wildcard_pick_or_defer(const HintImage& img, int port, bool* defer) {
+    if (!kDefer) return wildcard_pick(img, port);
+    if (img.wildcard_slot < 0) return VC_NONE;
+    return pick_or_defer<true>(img, img.wildcard_slot,
+                               load_rec_g(img.host_recs, uint32_t(img.wildcard_slot)), port,
+                               defer);
+}
+
 // ---------------------------------------------------------------------------
 // Upstream.searchForGroup for hints whose uri is null (or when no group has
 // a hint-uri): level = hostLevel << 10, so exact (3) beats any suffix (2)
@@ -533,7 +561,7 @@ constexpr int kProbes = kMaxSuffix + 1;      // [0] = the whole host
 // loaded together, and only tag hits touch a record.  Names the scan does
 // not cover (two or more ':' -- a possible IPv6 literal -- or more than
 // kMaxSuffix labels) go to the reference-shaped slow path.
-template <class Src>
+template <bool kDefer = false, class Src>
 VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
                              int port) {
     uint32_t h[kProbes];
@@ -573,7 +601,10 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         pos -= 4;
     }
     VC_PMARK(1);
-    if (nc >= 2 || np > kMaxSuffix || n > 255) return host_only_slow(*slow_img, q.ptr(), n, port);
+    if (nc >= 2 || np > kMaxSuffix || n > 255) {
+        if (kDefer) return kDeferred;
+        return host_only_slow(*slow_img, q.ptr(), n, port);
+    }
     h[0] = vck::fin(S, uint32_t(e));
     if (nc) {
         // cut at the colon; strip "www." (then the whole host is the suffix
@@ -610,6 +641,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
     }
     VC_PMARK(2);
     uint32_t best = VC_NONE;
+    bool defer = false;
     while (hits) {
         const int k = __builtin_ctz(hits);
         hits &= hits - 1;
@@ -621,7 +653,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         const uint32_t m0 = ((tm >> (4 * k)) & 15u) | (((cont >> k) & 1u) << 4);
         const int slot = host_find(t, hk, q, sk, e - sk, &r, m0);
         if (slot < 0) continue;
-        const uint32_t v = pick(img, slot, r, port);
+        const uint32_t v = pick_or_defer<kDefer>(img, slot, r, port, &defer);
         if (k == 0) {
             if (v != VC_NONE) return int32_t(v);          // exact level wins
         } else {
@@ -629,7 +661,8 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         }
     }
     VC_PMARK(3);
-    if (best == VC_NONE) best = wildcard_pick(img, port);
+    if (best == VC_NONE) best = wildcard_pick_or_defer<kDefer>(img, port, &defer);
+    if (kDefer && defer) return kDeferred;
     return best != VC_NONE ? int32_t(best) : -1;
 }
 
@@ -763,10 +796,33 @@ VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,
     return hint_general(img, host, port, uri);
 }
 
+// kind of a DNS query the deferring kernel leaves to its second pass
+constexpr uint8_t kDnsDeferred = 0xFF;
+
+// Could [0, n) be an IP literal (IP.isIpLiteral)?  Only hex digits, '.',
+// ':', '[' and ']' occur in one; any other byte rules it out.
+template <class Src>
+VC_HD bool maybe_ip_literal(const Src& q, int n) {
+    for (int pos = 0; pos < n; pos += 4) {
+        const uint32_t w = q.word(pos, 0, n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (pos + j >= n) break;
+            const uint32_t c = (w >> (8 * j)) & 0xFFu, l = c | 0x20u;
+            if (!((c >= '0' && c <= '9') || (l >= 'a' && l <= 'f') || c == '.' || c == ':' ||
+                  c == '[' || c == ']'))
+                return false;
+        }
+    }
+    return true;
+}
+
 // DNSServer.handleRequest classification (DNSServer.java:116-166) on a
 // query name in the boundary's string encoding (UTF-8), trailing dot
-// included.
-template <class Src>
+// included.  kDefer: no out-of-line call -- a name the host scan does not
+// cover, or one that may be an IP literal, gets kind kDnsDeferred for the
+// second pass (hint.hip dns_defer_kernel).
+template <bool kDefer = false, class Src>
 VC_HD void dns_flow(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
                     const Src& q, int qn, uint8_t* kind, int32_t* value) {
     // (1) hosts.get(qname) on the raw qname (trailing dot kept), :127
@@ -784,11 +840,14 @@ VC_HD void dns_flow(const HostsImage& hosts, const HintImage& img, const HintIma
     const uint8_t* qp = q.ptr();
     const int dn = (qn > 0 && (q.word(qn - 1, qn - 1, qn) & 0xFFu) == '.') ? qn - 1 : qn;
     // (3) rrsets.searchForGroup(Hint.ofHost(domain)), :136
-    const int32_t g = host_only_fast(img, slow_img, q, dn, 0);
-    if (g >= 0) {
+    const int32_t g = host_only_fast<kDefer>(img, slow_img, q, dn, 0);
+    if (kDefer && (g == kDeferred || (g < 0 && maybe_ip_literal(q, dn)))) {
+        *kind = kDnsDeferred;
+        *value = 0;
+    } else if (g >= 0) {
         *kind = VC_DNS_GROUP;
         *value = g;
-    } else if (d_is_ip_literal(qp, dn)) {            // (4) IP literal, :140-149
+    } else if (!kDefer && d_is_ip_literal(qp, dn)) {  // (4) IP literal, :140-149
         *kind = VC_DNS_IP_LITERAL;
         *value = d_count(qp, dn, ':') ? 6 : 4;
     } else {                                          // (5) *.vproxy.local, :150-157
@@ -830,13 +889,21 @@ VC_HDN __noinline__ void dns_highbytes(const HostsImage& hosts, const HintImage*
 
 // DNSServer classification on the wire bytes of a query name
 // (Formatter.parseDomainName output, trailing dot included).
-template <class Src>
+template <bool kDefer = false, class Src>
 VC_HD void dns_one(const HostsImage& hosts, const HintImage& img, const HintImage* slow_img,
                    const Src& q, int qn, uint8_t* kind, int32_t* value) {
     uint32_t hi = 0;
     for (int pos = 0; pos < qn; pos += 4) hi |= q.word(pos, 0, qn);
-    if (hi & 0x80808080u) dns_highbytes(hosts, slow_img, q.ptr(), qn, kind, value);
-    else dns_flow(hosts, img, slow_img, q, qn, kind, value);
+    if (hi & 0x80808080u) {
+        if (kDefer) {
+            *kind = kDnsDeferred;
+            *value = 0;
+        } else {
+            dns_highbytes(hosts, slow_img, q.ptr(), qn, kind, value);
+        }
+    } else {
+        dns_flow<kDefer>(hosts, img, slow_img, q, qn, kind, value);
+    }
 }
 
 // SSLContextHolder.choose(sni) (SSLContextHolder.java:51-79) over the

@@ -83,9 +83,12 @@ private:
 class TicketRing {
 public:
     static constexpr uint32_t kSlots = 4096;
+    // words per slot: [0] the work counter; [1], [2] a follow-up kernel's
+    // (hint_defer_kernel: deferred lanes, workgroups done); [3] spare
+    static constexpr uint32_t kWords = 4;
     hipError_t init() {
-        hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_), kSlots * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemset(d_, 0, kSlots * sizeof(uint32_t));
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_), kSlots * kWords * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemset(d_, 0, kSlots * kWords * sizeof(uint32_t));
         for (uint32_t k = 0; k < kSlots; ++k) epoch_of_[k].store(0);
         return e;
     }
@@ -100,10 +103,11 @@ public:
         const uint32_t e = epoch_.load();
         if (epoch_of_[k].load() != e) {
             // a slot that cannot be zeroed is not used: null = the static split
-            if (hipMemsetAsync(d_ + k, 0, sizeof(uint32_t), s) != hipSuccess) return nullptr;
+            if (hipMemsetAsync(d_ + kWords * k, 0, kWords * sizeof(uint32_t), s) != hipSuccess)
+                return nullptr;
             epoch_of_[k].store(e);
         }
-        return d_ + k;
+        return d_ + kWords * k;
     }
 
 private:

@@ -11,6 +11,10 @@ namespace vcd {
 
 constexpr uint32_t kApron = 16;          // readable bytes before and after the items
 
+#ifndef VC_STAGE_Q
+#define VC_STAGE_Q 1
+#endif
+
 // A wave's 64 items are contiguous in the blob: copy [o0, o1) into the
 // wave's stage with coalesced dword loads once.  Item bytes then sit at
 // byte kApron + (off - a0) of the stage.  Returns false when the span does
@@ -24,6 +28,54 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
     if (o1 - a0 > kBytes) return false;
     const int lane = int(threadIdx.x & 63);
     const uint32_t full = (o1 & ~3u) - a0;         // whole dwords inside [a0, o1)
+#if VC_STAGE_Q
+    // 16-byte pieces, every load of a round (4 KiB) in flight before any LDS
+    // write: one global round trip per round.  (A dword loop compiled to
+    // batches of four loads per lane, each waited for before the next: three
+    // round trips for a pair of hint chunks.)  Piece indices are clamped to
+    // the last piece instead of predicated -- the duplicate loads and LDS
+    // writes of lanes past the end carry the same bytes to the same place --
+    // so a round is straight-line code.  The blob is only dword aligned; an
+    // unaligned dwordx4 global load is legal on gfx950.
+    typedef uint4 __attribute__((aligned(4))) q4;
+    const uint32_t nq = full >> 4;                 // whole 16-byte pieces
+    const q4* gq = reinterpret_cast<const q4*>(blob + a0);
+    uint32_t* lw = stage + kApron / 4;
+    // the bytes past the pieces: up to three whole dwords (lanes 0-2) and
+    // the partial last dword (byte loads), loaded before the first round
+    const uint32_t rw = (full >> 2) & 3u, tail = o1 & 3u;
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(blob + a0 + 16 * nq);
+    uint32_t t = 0;
+    if (uint32_t(lane) < rw) {
+        t = gw[lane];
+    } else if (uint32_t(lane) == rw && tail) {
+        for (uint32_t b = 0; b < tail; ++b) t |= uint32_t(blob[(o1 & ~3u) + b]) << (8 * b);
+    }
+    constexpr uint32_t kRound = 4;                 // pieces per lane per round
+    for (uint32_t r0 = 0; r0 < nq; r0 += 64 * kRound) {
+        const uint32_t last = nq - 1;
+        uint4 v[kRound];
+#pragma unroll
+        for (uint32_t j = 0; j < kRound; ++j) {
+            const uint32_t k = r0 + 64 * j + uint32_t(lane);
+            v[j] = gq[k < last ? k : last];
+        }
+#if VC_STAGE_Q == 2
+        __builtin_amdgcn_sched_barrier(0);         // every load issued before a write
+#endif
+#pragma unroll
+        for (uint32_t j = 0; j < kRound; ++j) {
+            const uint32_t k0 = r0 + 64 * j + uint32_t(lane), k = k0 < last ? k0 : last;
+            uint32_t* d = lw + 4 * k;
+            d[0] = v[j].x;
+            d[1] = v[j].y;
+            d[2] = v[j].z;
+            d[3] = v[j].w;
+        }
+        if (kBytes <= 64 * 16 * kRound) break;     // one round covers the stage
+    }
+    if (uint32_t(lane) < rw + (tail ? 1u : 0u)) lw[4 * nq + uint32_t(lane)] = t;
+#else
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(blob + a0);
     uint32_t* lw = stage + kApron / 4;
     for (uint32_t k = uint32_t(lane); k < full / 4; k += 64) lw[k] = gw[k];
@@ -33,6 +85,7 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
         for (uint32_t b = 0; b < tail; ++b) v |= uint32_t(blob[(o1 & ~3u) + b]) << (8 * b);
         lw[full / 4] = v;
     }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
