@@ -160,3 +160,59 @@ def test_dns_datagrams_bad_arguments():
         assert rc != 0
     finally:
         clf.close()
+
+
+def test_dns_datagrams_deferred_over_slot_reuse():
+    """The drain-loop kernel leaves datagrams with a question it does not
+    finish inline (a possible IP literal, bytes >= 0x80, a name the host scan
+    does not cover) to a second kernel, counted in the launch's ticket slot,
+    which that kernel resets.  Over 4200 launches (every slot reused) of
+    batches with and without such datagrams, on two streams, every result
+    equals the oracle's."""
+    import torch
+    prng = random.Random(31)
+    rng = np.random.default_rng(37)
+    clf = V.Classifier(0)
+    try:
+        udp = np.concatenate([rule_row(*r) for r in (
+            ("10.0.0.0/8", 0, 65535, False), ("0.0.0.0/0", 0, 65535, True))])
+        tcp = np.zeros(0, W.RULE_DT)
+        _compile_acl(clf, tcp, udp, True)
+        groups, ghosts = W.gen_groups(1000, 43)
+        clf.compile_upstream(groups)
+        hosts = [(h + ".", i) for i, h in enumerate(ghosts[:20])]
+        clf.compile_hosts(hosts)
+        plain = W.gen_hostnames(ghosts, 2000, 44, dns=True)
+        odd = plain + [b"1.2.3.4.", b"::1.", b"fe80::1.", b"dead.beef.", b"caf\xe9.com.",
+                       b"a.b.c.d.e.f.g.h.i.j.k."] * 40
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        sets = []
+        for names in (plain, odd):
+            dg = [DW.random_datagram(prng, names) for _ in range(3000)]
+            fam, r4, r6, port = _remotes(rng, len(dg))
+            blob, off = W.pack(dg)
+            want = O.dnsd_batch_np(tcp, udp, True, hosts, groups, blob, off, fam, r4, r6, port,
+                                   nthreads=16)
+            dev = ((T(blob), T(off.view(np.int32))), T(r4.view(np.int32)),
+                   T(port.view(np.int16)), T(r6), T(fam))
+            sets.append((want, dev))
+        sizes = [1, 65, 1025, 3000]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        keep = []
+        for k in range(4200):
+            n = sizes[k % len(sizes)]
+            which = (k // len(sizes)) % 2
+            want, ((b, o), r4d, pd, r6d, fd) = sets[which]
+            with torch.cuda.stream(streams[k % 2]):
+                res = clf.dns_datagrams((b, o[:n + 1]), r4d[:n], pd[:n], remote6=r6d[:n],
+                                        remote_family=fd[:n])
+            if k % 300 < 8 or k >= 4192:
+                keep.append((n, which, res))
+        torch.cuda.synchronize()
+        for n, which, res in keep:
+            got = _cpu(res)
+            got["qtype"] = got["qtype"].view(np.uint16)
+            want = {kk: v[:n] for kk, v in sets[which][0].items()}
+            _same(got, want)
+    finally:
+        clf.close()

@@ -469,11 +469,17 @@ struct DnsdOut {
     int32_t* value;
 };
 
-template <class Bytes>
-__device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImage& img,
-                                         const HintImage* slow_img, const AclImage& acl,
-                                         const DnsdIn& in, const DnsdOut& out, int64_t i,
-                                         const uint8_t* p, int n, uint32_t* name) {
+// status of a datagram the deferring dnsd kernel leaves to its second pass
+constexpr uint8_t kDnsdDeferred = 0xFF;
+
+// kDefer: a question dns_one<true> defers makes the whole datagram
+// kDnsdDeferred (status only); dnsd_defer_kernel redoes it.  Returns the
+// status written.
+template <bool kDefer>
+__device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintImage& img,
+                                            const HintImage* slow_img, const AclImage& acl,
+                                            const DnsdIn& in, const DnsdOut& out, int64_t i,
+                                            const uint8_t* p, int n, uint32_t* name) {
     // securityGroup.allow(Protocol.UDP, remote.getAddress(), remote.getPort())
     const bool six = in.rfam && in.rfam[i] == 6;
     const uint32_t port = in.rport[i];
@@ -564,7 +570,11 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
                     }
                     uint8_t kd;
                     int32_t val;
-                    dns_one(hosts, img, slow_img, LdsSrc{name, kNameApron}, len, &kd, &val);
+                    dns_one<kDefer>(hosts, img, slow_img, LdsSrc{name, kNameApron}, len, &kd, &val);
+                    if (kDefer && kd == kDnsDeferred) {
+                        st = kDnsdDeferred;
+                        break;
+                    }
                     put(q, qtype, kd, val);
                     if (kd == VC_DNS_RECURSIVE) {
                         st = VC_DNSD_RECURSIVE;
@@ -575,11 +585,13 @@ __device__ __forceinline__ void dnsd_one(const HostsImage& hosts, const HintImag
         }
     }
     out.status[i] = st;
+    if (kDefer && st == kDnsdDeferred) return st;
     if (out.nq) out.nq[i] = uint8_t(nq);
     for (int q = nq; q < VC_DNSD_MAXQ; ++q) out.kind[i * VC_DNSD_MAXQ + q] = 0;   // not evaluated
+    return st;
 }
 
-template <bool kStage>
+template <bool kStage, bool kDefer>
 __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out,
@@ -602,17 +614,53 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
         const int64_t nx = ch.next(c);
         if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kDnsdStage>(blob, o0, o1, stage[w], &a0);
+        uint8_t st = 0;
         if (i < n) {
-            if (staged)
-                dnsd_one<int>(hosts, img, &slow_img, acl, in, out, i,
-                              reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
-                              int(e - a), names[threadIdx.x]);
-            else
-                dnsd_one<int>(hosts, img, &slow_img, acl, in, out, i, blob + a, int(e - a),
-                              names[threadIdx.x]);
+            if (staged) {
+                st = dnsd_one<kDefer>(hosts, img, &slow_img, acl, in, out, i,
+                                      reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
+                                      int(e - a), names[threadIdx.x]);
+            } else if (kDefer) {
+                st = kDnsdDeferred;
+                out.status[i] = st;
+            } else {
+                st = dnsd_one<false>(hosts, img, &slow_img, acl, in, out, i, blob + a, int(e - a),
+                                     names[threadIdx.x]);
+            }
+        }
+        if (kDefer && ticket) {
+            const uint64_t dm = __ballot(i < n && st == kDnsdDeferred);
+            if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
         }
         if (kStage) wave_done();
         c = nx;
+    }
+}
+
+// The datagrams dnsd_kernel<*, true> deferred, redone whole from global
+// memory with the complete classification.  ctl as hint_defer_kernel's.
+constexpr int kDnsdDeferBlock = 128;
+__global__ __launch_bounds__(kDnsdDeferBlock) void dnsd_defer_kernel(
+    HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
+    const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out, uint32_t* ctl) {
+    __shared__ uint32_t names[kDnsdDeferBlock][kNameWords];
+    __shared__ uint32_t todo;
+    if (threadIdx.x == 0) todo = ctl ? __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                     : 1u;
+    __syncthreads();
+    if (todo) {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+             i += int64_t(gridDim.x) * blockDim.x) {
+            if (out.status[i] != kDnsdDeferred) continue;
+            const uint32_t a = off[i], e = off[i + 1];
+            dnsd_one<false>(hosts, img, &img, acl, in, out, i, blob + a, int(e - a),
+                            names[threadIdx.x]);
+        }
+    }
+    if (ctl && threadIdx.x == 0 && atomicAdd(ctl + 2, 1u) == gridDim.x - 1) {
+        atomicExch(ctl + 1, 0u);
+        atomicExch(ctl + 2, 0u);
     }
 }
 
@@ -709,19 +757,28 @@ hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kDnsdBlock - 1) / vcd::kDnsdBlock;
     const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
-    const void* k = stage ? reinterpret_cast<const void*>(vcd::dnsd_kernel<true>)
-                          : reinterpret_cast<const void*>(vcd::dnsd_kernel<false>);
-    const int grid = resident_grid(c, k, vcd::kDnsdBlock, 0, want);
+    const bool defer = VC_DNS_DEFER && stage;
     const vcd::DnsdIn in{rfam, r4, r6, rport};
     const vcd::DnsdOut o{status, out_acl, nq, qtype, kind, value};
     uint32_t* tk = VC_DNSD_TICKETS && c.tickets ? c.tickets->next(c.stream) : nullptr;
-    if (stage)
-        hipLaunchKernelGGL(vcd::dnsd_kernel<true>, dim3(grid), dim3(vcd::kDnsdBlock), 0, c.stream,
+    auto go = [&](auto kernel) {
+        const int grid = resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kDnsdBlock,
+                                       0, want);
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kDnsdBlock), 0, c.stream,
                            hosts, hints, acl, blob, off, n, in, o, tk);
-    else
-        hipLaunchKernelGGL(vcd::dnsd_kernel<false>, dim3(grid), dim3(vcd::kDnsdBlock), 0,
-                           c.stream, hosts, hints, acl, blob, off, n, in, o, tk);
-    return hipGetLastError();
+    };
+    if (defer) go(vcd::dnsd_kernel<true, true>);
+    else if (stage) go(vcd::dnsd_kernel<true, false>);
+    else go(vcd::dnsd_kernel<false, false>);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && defer) {
+        const int64_t dwant = (n + vcd::kDnsdDeferBlock - 1) / vcd::kDnsdDeferBlock;
+        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        hipLaunchKernelGGL(vcd::dnsd_defer_kernel, dim3(unsigned(dgrid)), dim3(vcd::kDnsdDeferBlock),
+                           0, c.stream, hosts, hints, acl, blob, off, n, in, o, tk);
+        e = hipGetLastError();
+    }
+    return e;
 }
 
 }  // namespace vc
