@@ -157,6 +157,10 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
         for (int al = 0; al < 4; ++al) {
             Staged st(h.p, h.n, al);
             if (host_only_fast(img, &img, st.src, h.n, p) != want) return -102;
+            // the deferring form (the pool pass's kernel): the same result,
+            // or kDeferred for the follow-up kernel
+            const int32_t d = host_only_fast<true>(img, &img, st.src, h.n, p);
+            if (d != want && d != kDeferred) return -104;
         }
     }
     return 0;
@@ -183,6 +187,10 @@ int ic_dns(const char* const* keys, const int32_t* key_lens, const int32_t* valu
             int32_t v2;
             dns_one(hosts, img, &img, st.src, qn, &k2, &v2);
             if (k2 != kind[i] || v2 != value[i]) return -103;
+            // the deferring form (dns_kernel / dnsd_kernel): the same
+            // classification, or kDnsDeferred for the follow-up kernel
+            dns_one<true>(hosts, img, &img, st.src, qn, &k2, &v2);
+            if (k2 != kDnsDeferred && (k2 != kind[i] || v2 != value[i])) return -105;
         }
     }
     return 0;
