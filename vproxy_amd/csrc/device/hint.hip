@@ -22,10 +22,12 @@ constexpr int kHintBlock = 256;
 constexpr int kWaves = kHintBlock / 64;
 constexpr uint32_t kStageBytes = 4096;   // per wave: 64 names of up to 64 B on average
 constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
-// Minimum waves per SIMD.  hint_kernel: 7 holds it at 72 VGPRs (a few
-// spills around the slow-path calls): C4 0.866 -> 0.817 ms against 5 waves at
-// 96 VGPRs.  dns_kernel: 6 (80 VGPRs); at 7 it spills in the hot path and
-// takes 1.26 ms instead of 1.07 (profiles/r02_ab_hint_occupancy.txt).
+// Minimum waves per SIMD.  hint_kernel: 7 holds it at 72 VGPRs: C4 0.866 ->
+// 0.817 ms against 5 waves at 96 VGPRs (profiles/r02_ab_hint_occupancy.txt);
+// the call-free kernel at 8 (64 VGPRs) spills 20 and loses (0.833 against
+// 0.772 ms, profiles/r04_ab_minw.txt).  dns_kernel: 7 (72 VGPRs, no spills)
+// since its loop has no call (0.913 against 0.928 ms at 6); with the calls
+// it spilled in the hot path at 7 (1.26 against 1.07 ms, round 2).
 #ifndef VC_HINT_MINW
 #define VC_HINT_MINW 7
 #endif
@@ -39,7 +41,7 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_DNS_DEFER 1
 #endif
 #ifndef VC_DNS_MINW
-#define VC_DNS_MINW 6
+#define VC_DNS_MINW 7
 #endif
 
 
