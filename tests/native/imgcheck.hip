@@ -48,6 +48,12 @@ HintImage hint_img(const vc::HintBuilt& b) {
     h.wildcard_slot = b.wildcard_slot;
     h.uri_star_slot = b.uri_star_slot;
     h.has_uri_keys = b.has_uri_keys;
+    if (b.wildcard_slot >= 0) {
+        const auto& w = b.host.recs[size_t(b.wildcard_slot)];
+        h.wild_len_pm = w.len_pm;
+        h.wild_a = w.a;
+        h.wild_b = w.b;
+    }
     return h;
 }
 // A name copied into a buffer with a 16-byte apron of junk either side, the

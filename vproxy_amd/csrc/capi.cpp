@@ -1063,6 +1063,12 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     s->img.wildcard_slot = b.wildcard_slot;
     s->img.uri_star_slot = b.uri_star_slot;
     s->img.has_uri_keys = b.has_uri_keys;
+    if (b.wildcard_slot >= 0) {
+        const auto& w = b.host.recs[size_t(b.wildcard_slot)];
+        s->img.wild_len_pm = w.len_pm;
+        s->img.wild_a = w.a;
+        s->img.wild_b = w.b;
+    }
     s->digest = vc::digest(b);
     s->alloc_counters(up, int64_t(n) + 1);
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "hint upload");

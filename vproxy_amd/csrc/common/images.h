@@ -171,6 +171,10 @@ struct HintImage {
     int32_t wildcard_slot;         // host slot of "*" or -1
     int32_t uri_star_slot;         // uri slot of "*" or -1
     int32_t has_uri_keys;          // any group with a hint-uri
+    // the "*" record's meta (len_pm, a, b; HostRec) in the kernel argument,
+    // so a miss picks the wildcard without a dependent load
+    uint32_t wild_len_pm;
+    int32_t wild_a, wild_b;
 };
 
 struct HostsImage {

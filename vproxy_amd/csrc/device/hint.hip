@@ -32,7 +32,7 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_HINT_MINW 7
 #endif
 #ifndef VC_HINT_PRE
-#define VC_HINT_PRE 0
+#define VC_HINT_PRE 2
 #endif
 #ifndef VC_HINT_DEFER
 #define VC_HINT_DEFER 1
@@ -77,9 +77,10 @@ constexpr size_t kProfLds = 0;
 // kPre 2: every offset the two chunks need (the staged span, and each
 // lane's [a, e)) is loaded together up front, so a pair costs one offset and
 // one blob round trip before its first scan instead of four dependent ones
-// (SNI 0.638 -> 0.624 ms).  kPre 0: each chunk's [a, e) is loaded at its
-// body -- the hint kernel, where live offsets spill (all four up front:
-// 0.81 -> 0.92 ms; the first chunk's only, kPre 1: 0.83 ms).
+// (SNI 0.638 -> 0.624 ms; the call-free hint kernel 0.769 -> 0.761 ms,
+// profiles/r04_ab_hint_pre.txt -- with the slow-path calls in its loop the
+// live offsets spilled: 0.81 -> 0.92 ms).  kPre 0: each chunk's [a, e) is
+// loaded at its body.
 template <uint32_t kBytes, bool kPair, int kPre, class Body>
 __device__ __forceinline__ void chunk_loop(Chunks& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,

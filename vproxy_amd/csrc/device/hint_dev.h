@@ -472,10 +472,16 @@ VC_HD int host_lookup(const HostTable& t, const Src& q, int st, int n, Rec* out)
     return host_find(t, src_khash(q, st, st + n), q, st, n, out);
 }
 
+// the "*" record's meta from the image (HintImage.wild_*: no table load)
+VC_HD Rec wildcard_rec(const HintImage& img) {
+    Rec r{};
+    r.m = uint4{img.wild_len_pm, uint32_t(img.wild_a), uint32_t(img.wild_b), 0u};
+    return r;
+}
+
 VC_HD uint32_t wildcard_pick(const HintImage& img, int port) {
     if (img.wildcard_slot < 0) return VC_NONE;
-    return pick(img, img.wildcard_slot, load_rec_g(img.host_recs, uint32_t(img.wildcard_slot)),
-                port);
+    return pick(img, img.wildcard_slot, wildcard_rec(img), port);
 }
 
 // The deferring fast path (kDefer below) leaves a lane that needs an
@@ -501,9 +507,7 @@ template <bool kDefer>
 VC_HD uint32_t wildcard_pick_or_defer(const HintImage& img, int port, bool* defer) {
     if (!kDefer) return wildcard_pick(img, port);
     if (img.wildcard_slot < 0) return VC_NONE;
-    return pick_or_defer<true>(img, img.wildcard_slot,
-                               load_rec_g(img.host_recs, uint32_t(img.wildcard_slot)), port,
-                               defer);
+    return pick_or_defer<true>(img, img.wildcard_slot, wildcard_rec(img), port, defer);
 }
 
 // ---------------------------------------------------------------------------
