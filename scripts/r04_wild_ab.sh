@@ -1,6 +1,7 @@
 #!/bin/bash
-# the "*" record's meta in the image (no dependent load for a miss) vs loaded
-# from the table: pre2 (loaded) vs wild (in the image), C4, DNS and the C5 step
+# hint pass A/B: pre2 (offset pairs up front, "*" meta loaded from the table),
+# wild ("*" meta in the image), pre3 / pre3w6 (and the next pair's offsets
+# prefetched, at 7 and 6 waves per SIMD)
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-bash scripts/ab_libs.sh "c4 dns c5" build/pre2 build/wild > gpurun_out/wild_ab.txt 2>&1
+bash scripts/ab_libs.sh "c4 dns" build/pre2 build/wild build/pre3 build/pre3w6 > gpurun_out/wild_ab.txt 2>&1
