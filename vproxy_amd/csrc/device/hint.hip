@@ -40,6 +40,16 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_DNS_DEFER
 #define VC_DNS_DEFER 1
 #endif
+// Workgroups of the follow-up (deferred-lane) kernels.  Each reads the
+// launch's deferred count and adds one to its done count, so with nothing
+// deferred the launch costs those loads and same-address atomics; with many
+// deferred lanes the grid strides over the batch.  With nothing deferred
+// the C4 follow-up takes 4.4 us at 64 workgroups, 11.7 us at 512
+// (profiles/r04_ab_defer_grid.txt); 128 keeps a heavily deferred batch (an
+// IPv6-literal Host header on every packet) on half the CUs.
+#ifndef VC_DEFER_GRID
+#define VC_DEFER_GRID 128
+#endif
 #ifndef VC_DNS_MINW
 #define VC_DNS_MINW 7
 #endif
@@ -81,11 +91,64 @@ constexpr size_t kProfLds = 0;
 // profiles/r04_ab_hint_pre.txt -- with the slow-path calls in its loop the
 // live offsets spilled: 0.81 -> 0.92 ms).  kPre 0: each chunk's [a, e) is
 // loaded at its body.
+// kPre 3: as 2, and the next pair's offsets are loaded before this pair is
+// staged, so they arrive with this pair's bytes: a pair costs one blob round
+// trip before its first scan (the ticket counter is read one pair early).
+// A lane's starts in the two chunks; its ends are the next lane's starts
+// (lane 63: the spans' ends o1, o2), taken by a lane shift when used, so the
+// prefetched pair holds two VGPRs and three SGPRs.
+struct PairOffs {
+    uint32_t A0 = 0, A1 = 0, o0 = 0, o1 = 0, o2 = 0;
+};
+
+__device__ __forceinline__ PairOffs pair_offs(const uint32_t* off, int64_t base, int64_t n) {
+    PairOffs r;
+    const int64_t i0 = base + int(threadIdx.x & 63), i1 = i0 + 64;
+    r.A0 = off[i0 < n ? i0 : n];
+    r.A1 = off[i1 < n ? i1 : n];
+    r.o0 = uint32_t(__builtin_amdgcn_readfirstlane(int(off[base])));
+    r.o1 = uint32_t(__builtin_amdgcn_readfirstlane(int(off[base + 64 < n ? base + 64 : n])));
+    r.o2 = uint32_t(__builtin_amdgcn_readfirstlane(int(off[base + 128 < n ? base + 128 : n])));
+    VC_CHECK(r.o0 <= r.o1 && r.o1 <= r.o2 && r.o2 <= off[n], 301, base, r.o2);
+    return r;
+}
+
+// the lane's end: the next lane's start, or `last` for lane 63
+__device__ __forceinline__ uint32_t lane_end(uint32_t a, uint32_t last) {
+    const uint32_t nx = uint32_t(__shfl_down(int(a), 1, 64));
+    return (threadIdx.x & 63) == 63 ? last : nx;
+}
+
 template <uint32_t kBytes, bool kPair, int kPre, class Body>
 __device__ __forceinline__ void chunk_loop(Chunks& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
     const int lane = int(threadIdx.x & 63);
+    if constexpr (kPre == 3) {
+        int64_t c = ch.first(w);
+        PairOffs cur;
+        if (c < ch.nchunks) cur = pair_offs(off, c * 64, n);
+        while (c < ch.nchunks) {
+            // a pair when chunk c + 1 is this wave's too and both fit the stage
+            const bool two = kPair && blob && ch.paired(c) &&
+                             cur.o2 - (cur.o0 & ~3u) <= kBytes;
+            const int nsub = two ? 2 : 1;
+            const int64_t cn = ch.next(c + nsub - 1);
+            PairOffs nxt;
+            if (cn < ch.nchunks) nxt = pair_offs(off, cn * 64, n);
+            uint32_t a0 = 0;
+            const bool staged = blob && stage_wave<kBytes>(blob, cur.o0, two ? cur.o2 : cur.o1,
+                                                           stage, &a0);
+            VC_PMARK(0);
+            body(c, staged, a0, cur.A0, lane_end(cur.A0, cur.o1));
+            if (two) body(c + 1, staged, a0, cur.A1, lane_end(cur.A1, cur.o2));
+            wave_done();
+            VC_PMARK(5);
+            c = cn;
+            cur = nxt;
+        }
+        return;
+    }
     for (int64_t c = ch.first(w); c < ch.nchunks;) {
         const int64_t base = c * 64;
         const bool pair = kPair && ch.paired(c);
@@ -711,7 +774,7 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && defer) {
         const int64_t dwant = (n + 255) / 256;
-        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        const int64_t dgrid = dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID;
         hipLaunchKernelGGL(vcd::hint_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
                            img, host_blob, host_off, port, n, out, ticket);
         e = hipGetLastError();
@@ -741,7 +804,7 @@ hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintIma
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && defer) {
         const int64_t dwant = (n + 255) / 256;
-        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        const int64_t dgrid = dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID;
         hipLaunchKernelGGL(vcd::dns_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
                            hosts, hints, qblob, qoff, n, kind, value, ticket);
         e = hipGetLastError();
@@ -776,7 +839,7 @@ hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && defer) {
         const int64_t dwant = (n + vcd::kDnsdDeferBlock - 1) / vcd::kDnsdDeferBlock;
-        const int64_t dgrid = dwant < int64_t(c.num_cus) * 2 ? dwant : int64_t(c.num_cus) * 2;
+        const int64_t dgrid = dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID;
         hipLaunchKernelGGL(vcd::dnsd_defer_kernel, dim3(unsigned(dgrid)), dim3(vcd::kDnsdDeferBlock),
                            0, c.stream, hosts, hints, acl, blob, off, n, in, o, tk);
         e = hipGetLastError();
