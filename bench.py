@@ -263,7 +263,8 @@ class C5Steps:
     """
 
     def __init__(self, clf, t, packets, dev, bucket=False, serial=False, counters="fused",
-                 finish="stream", inflight=3, overlap="finish", gate=False, pool_cus=0):
+                 finish="stream", inflight=3, overlap="finish", gate=False, pool_cus=0,
+                 pool_stream="pipe"):
         self.clf, self.t, self.dev = clf, t, dev
         self.proto, self.src, self.dst, self.dport, self.hid = packets
         self.B = len(self.src)
@@ -294,6 +295,10 @@ class C5Steps:
             self.s_cnt = hip_stream(dev, small)
         else:
             self.s_pipe, self.s_hint, self.s_cnt = (hip_stream(dev) for _ in range(3))
+            if pool_stream == "pipe" and overlap == "finish":
+                # in order behind the previous pipeline kernel: no cross-stream
+                # event wait between the two kernels of a step
+                self.s_hint = self.s_pipe
         self.ev_hint, self.ev_pipe, self.ev_cnt, self.kdone = {}, {}, {}, {}
         self.timing = []
         self.host_ms = {"hint": 0.0, "pipe": 0.0, "counters": 0.0}   # host time issuing
@@ -607,6 +612,10 @@ def main():
                          "finish (which then overlaps only the pool pass)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight (output and pool buffers)")
+    ap.add_argument("--pool-stream", choices=["own", "pipe"], default="pipe",
+                    help="the pool pass in order on the pipeline stream (default: no "
+                         "cross-stream event wait between a step's two kernels; 6.076 against "
+                         "6.115 ms, profiles/r04_ab_pool_stream.jsonl) or on its own stream")
     ap.add_argument("--pool-cus", type=int, default=0,
                     help="CU partition: the pool pass and the counter finish on this many CUs "
                          "(a CU-masked stream), the pipeline kernel on the rest (0: no masks)")
@@ -663,7 +672,8 @@ def main():
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
     steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
                     counters=args.counters, finish=args.finish, inflight=args.inflight,
-                    overlap=args.overlap, gate=args.gate, pool_cus=args.pool_cus)
+                    overlap=args.overlap, gate=args.gate, pool_cus=args.pool_cus,
+                    pool_stream=args.pool_stream)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
@@ -769,7 +779,10 @@ def main():
                                             args.inflight, "counter finish" if
                                             args.overlap == "finish" else "pipeline kernel") +
                                         (", pool pass and finish on %d CUs, pipeline on the "
-                                         "rest" % args.pool_cus if args.pool_cus else ""))},
+                                         "rest" % args.pool_cus if args.pool_cus else "") +
+                                        (", pool pass in order on the pipeline stream"
+                                         if args.pool_stream == "pipe" and not args.pool_cus
+                                         and args.overlap == "finish" else ""))},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     clf.close()
