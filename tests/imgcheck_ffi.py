@@ -24,6 +24,7 @@ def lib():
                              vp, vp]
         L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp, C.c_int]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
+        L.ic_hint_deferred.restype = C.c_int64
         L.ic_dns.argtypes = [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int64, vp, vp]
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
         L.ic_mirror.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
@@ -76,6 +77,12 @@ def hint(group_arr, ng, hosts, ports, uris):
                        P(out))
     assert rc == 0, rc
     return out
+
+
+def hint_deferred():
+    """names of the last hint() call the deferring fast path left to the
+    follow-up kernel (hint_defer_kernel)"""
+    return int(lib().ic_hint_deferred())
 
 
 def is_ipv6(s):

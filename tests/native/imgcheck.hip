@@ -138,6 +138,11 @@ int ic_route(const vc_net* rules, int nr, int family, const void* keys, int64_t 
     return 0;
 }
 
+// names the deferring fast path left to the follow-up kernel in the last
+// ic_hint call
+static int64_t g_hint_deferred = 0;
+int64_t ic_hint_deferred() { return g_hint_deferred; }
+
 int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* ho,
             const uint8_t* hn, const uint16_t* port, const uint8_t* ub, const uint32_t* uo,
             const uint8_t* un, int64_t n, int32_t* out) {
@@ -145,6 +150,7 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
     int rc = vc::build_hints(g, ng, &b);
     if (rc) return rc;
     HintImage img = hint_img(b);
+    g_hint_deferred = 0;
     for (int64_t i = 0; i < n; ++i) {
         DStr h{nullptr, -1}, u{nullptr, -1};
         if (hb && !(hn && hn[i])) h = DStr{hb + ho[i], int(ho[i + 1] - ho[i])};
@@ -167,6 +173,7 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
             // or kDeferred for the follow-up kernel
             const int32_t d = host_only_fast<true>(img, &img, st.src, h.n, p);
             if (d != want && d != kDeferred) return -104;
+            if (al == 0 && d == kDeferred) ++g_hint_deferred;
         }
     }
     return 0;
