@@ -336,6 +336,12 @@ template <class Src>
 VC_HD bool rec_match(const HostRec* recs, uint32_t s, const uint8_t* blob, const Src& q, int st,
                      int n, uint4* meta) {
     const uint4* p = reinterpret_cast<const uint4*>(recs + s);
+#if defined(VC_ABL_NOREC)          // timing ablation only: no record load
+    if (s != 0xFFFFFFFFu) {
+        *meta = uint4{uint32_t(n), 0u, 0u, 0u};
+        return true;
+    }
+#endif
     const uint4 m = gload(p), k0 = gload(p + 1), k1 = gload(p + 2);
     int rn = int(m.x & ~VC_REC_HAS_PM);
     if (rn != n) return false;
@@ -391,6 +397,10 @@ VC_HD T gload(const T* p) {
 }
 
 VC_HD uint4 tag_group(const uint32_t* tags, uint32_t mask, uint32_t h) {
+#if defined(VC_ABL_NOTAG)          // timing ablation only: every probe misses
+    if (h == 0x12345u) return gload(reinterpret_cast<const uint4*>(tags));
+    return uint4{0u, 0u, 0u, 0u};
+#endif
     return gload(reinterpret_cast<const uint4*>(tags + (h & mask & ~3u)));
 }
 
@@ -568,6 +578,9 @@ constexpr int kProbes = kMaxSuffix + 1;      // [0] = the whole host
 template <bool kDefer = false, class Src>
 VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
                              int port) {
+#if defined(VC_ABL_NOSCAN)         // timing ablation only: stage, no scan
+    if (n != 0x7FFFFFFF) return int32_t(q.word(0, 0, n) & 1u) - 1;
+#endif
     uint32_t h[kProbes];
     uint64_t stp = 0;                 // suffix starts, a byte each: [k] at bits 8k
     int e = n, np = 0, nc = 0;
