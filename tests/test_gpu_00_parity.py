@@ -328,8 +328,8 @@ def test_hint_work_tickets_wrap(clf):
     """The string kernels take work tickets from a ring of 4096 per-launch
     device counters (launch.h TicketRing) that each launch's last wave
     resets: over 4500 launches (every slot reused) of sizes around the
-    64-item chunk and 1024-item ticket edges, on two streams, every result
-    equals the oracle's."""
+    64-item chunk and the tail- and big-ticket edges, on two streams, every
+    result equals the oracle's."""
     import ctypes as C
     import torch
     groups, hosts, queries = hint_cases_random(np.random.default_rng(43), 300, 7000)
@@ -340,7 +340,9 @@ def test_hint_work_tickets_wrap(clf):
     blob, off, _ = pack_strings(hs)
     bd = torch.from_numpy(blob).cuda()
     od = torch.from_numpy(off.astype(np.int32)).cuda()
-    sizes = [1, 63, 64, 65, 1023, 1024, 1025, 3000, 6000]
+    # chunk (64 items), tail-ticket (8 chunks) and big-ticket (24 chunks)
+    # edges (chunks.h)
+    sizes = [1, 63, 64, 65, 511, 512, 513, 1535, 1536, 1537, 3000, 6000]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     outs = []
     for k in range(4500):

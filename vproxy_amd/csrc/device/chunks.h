@@ -24,7 +24,15 @@ namespace vcd {
 // tickets per wave).  Tails of 4-chunk tickets, two per wave: C4 0.813 ->
 // 0.803 ms, DNS 1.10 -> 1.06, the C5 step 6.13 -> 6.03-6.06 ms; 1- and
 // 2-chunk tails lose to their extra atomics, 8-chunk ones end too coarsely
-// (profiles/r03_ab_ticket.txt).
+// (profiles/r03_ab_ticket.txt).  Round 4, once the hint / DNS kernels had no
+// call in their loops and a chunk cost less: 24-chunk big tickets and one
+// round of 8-chunk tail tickets -- C4 0.762 -> 0.705 ms, SNI 0.635 -> 0.580,
+// mirror 2.495 -> 2.397, DNS 0.892 -> 0.880 (profiles/r04_ab_ticket_sweep*.txt;
+// 32-chunk tickets lose on every kernel).  With little work per chunk the
+// single counter itself is the cost: the C4 pass without its scan ran 0.474
+// ms on tickets against 0.317 ms on the static split (r04_ab_hint_ablation.txt),
+// and eight counters on separate lines lost to the one counter once the scan
+// was back (r04_ab_part_tickets.txt).
 // Every wave takes exactly one out-of-range ticket (its last), so the wave
 // holding ticket ntickets + nwaves - 1 is the last taker of the launch and
 // resets the counter for the slot's next launch.
@@ -33,35 +41,36 @@ namespace vcd {
 #define VC_DNSD_TICKETS 1
 #endif
 #ifndef VC_TICKET_CHUNKS
-#define VC_TICKET_CHUNKS 16
+#define VC_TICKET_CHUNKS 24
 #endif
 #ifndef VC_TICKET_TAIL
-#define VC_TICKET_TAIL 4
+#define VC_TICKET_TAIL 8
 #endif
 constexpr int64_t kPerTicket = VC_TICKET_CHUNKS;
 constexpr int64_t kTailChunks = VC_TICKET_TAIL;     // 0: big tickets to the end
 #ifndef VC_TICKET_TAIL_ROUNDS
-#define VC_TICKET_TAIL_ROUNDS 2
+#define VC_TICKET_TAIL_ROUNDS 1
 #endif
 constexpr int64_t kTailRounds = VC_TICKET_TAIL_ROUNDS;
 
 // Ticket t -> its chunk run: big tickets [B t, B t + B) up to chunk head,
 // then tail tickets of kTailChunks.  `end` is the end of the wave's current
 // run (wave-uniform).
-struct Chunks {
+template <int64_t P = kPerTicket, int64_t T = kTailChunks, int64_t R = kTailRounds>
+struct ChunksT {
     uint32_t* ticket;
     int64_t nchunks;
     int64_t head = 0;              // chunks covered by big tickets
     int64_t nbig = 0;              // big tickets
     int64_t ntickets = 0;
     int64_t end = 0;
-    __device__ Chunks(uint32_t* t, int64_t nc) : ticket(t), nchunks(nc) {
+    __device__ ChunksT(uint32_t* t, int64_t nc) : ticket(t), nchunks(nc) {
         const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-        const int64_t tail = kTailChunks ? nwaves * kTailChunks * kTailRounds : 0;
-        head = nc > tail ? (nc - tail) / kPerTicket * kPerTicket : 0;
-        if (!kTailChunks) head = nc;
-        nbig = (head + kPerTicket - 1) / kPerTicket;
-        ntickets = nbig + (kTailChunks ? (nc - head + kTailChunks - 1) / kTailChunks : 0);
+        const int64_t tail = T ? nwaves * T * R : 0;
+        head = nc > tail ? (nc - tail) / P * P : 0;
+        if (!T) head = nc;
+        nbig = (head + P - 1) / P;
+        ntickets = nbig + (T ? (nc - head + T - 1) / T : 0);
     }
     __device__ int64_t take() {
         uint32_t t = 0;
@@ -75,11 +84,11 @@ struct Chunks {
         const int64_t tk = int64_t(__shfl(t, 0, 64));
         int64_t start;
         if (tk < nbig) {
-            start = tk * kPerTicket;
-            end = start + kPerTicket < head ? start + kPerTicket : head;
+            start = tk * P;
+            end = start + P < head ? start + P : head;
         } else {
-            start = head + (tk - nbig) * (kTailChunks ? kTailChunks : 1);
-            end = start + kTailChunks;
+            start = head + (tk - nbig) * (T ? T : 1);
+            end = start + T;
         }
         if (end > nchunks) end = nchunks;
         return start < nchunks ? start : nchunks;
@@ -94,6 +103,9 @@ struct Chunks {
     // c + 1 is this wave's next chunk (same ticket)
     __device__ bool paired(int64_t c) const { return ticket && c + 1 < end; }
 };
+
+// the string and frame kernels' layout (the constants above)
+using Chunks = ChunksT<>;
 
 }  // namespace vcd
 

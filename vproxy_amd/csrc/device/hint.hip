@@ -34,6 +34,9 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_HINT_PRE
 #define VC_HINT_PRE 2
 #endif
+#ifndef VC_HINT_TICKETS                 // 0: static split (A/B only)
+#define VC_HINT_TICKETS 1
+#endif
 #ifndef VC_HINT_DEFER
 #define VC_HINT_DEFER 1
 #endif
@@ -666,9 +669,12 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     __shared__ uint32_t names[kDnsdBlock][kNameWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     HintImage slow_img = img;
-    // 64-datagram chunks from the work tickets (Chunks), or the static
-    // grid-stride sequence without them
-    Chunks ch(ticket, (n + 63) / 64);
+    // 64-datagram chunks from the work tickets, or the static grid-stride
+    // sequence without them.  16-chunk big tickets and two rounds of 4-chunk
+    // tail tickets: the drain loop's chunks cost more than the other string
+    // kernels', and their 24 / 8 / 1 layout ran it 3.99 against 3.94 ms
+    // (profiles/r04_ab_ticket_confirm.txt)
+    ChunksT<16, 4, 2> ch(ticket, (n + 63) / 64);
     int64_t c = ch.first(w);
     LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
     while (c < ch.nchunks) {
@@ -760,7 +766,7 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
     const bool stage = host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0;
     // the deferring kernel when no lane takes the general (hint-uri) path
     const bool defer = VC_HINT_DEFER && stage && !(uri_blob && img.has_uri_keys);
-    uint32_t* ticket = c.tickets ? c.tickets->next(c.stream) : nullptr;
+    uint32_t* ticket = VC_HINT_TICKETS && c.tickets ? c.tickets->next(c.stream) : nullptr;
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel,
                            dim3(resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHintBlock, 0, want)),

@@ -28,6 +28,9 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
     if (o1 - a0 > kBytes) return false;
     const int lane = int(threadIdx.x & 63);
     const uint32_t full = (o1 & ~3u) - a0;         // whole dwords inside [a0, o1)
+#if defined(VC_ABL_NOSTAGE)                        // timing ablation only: no copy
+    if (full != 0xFFFFFFFFu) return true;
+#endif
 #if VC_STAGE_Q
     // 16-byte pieces, every load of a round (4 KiB) in flight before any LDS
     // write: one global round trip per round.  (A dword loop compiled to
