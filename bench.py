@@ -773,8 +773,8 @@ def main():
                            "global_batch": args.packets * world,
                            "parallelism": "dp%d" % world,
                            "schedule": ("serial, one stream" if args.serial else
-                                        "%d batches in flight: pool / pipeline / counters on 3 "
-                                        "HIP streams, counter finish on the counters stream, "
+                                        "%d batches in flight: pool pass, pipeline and counter "
+                                        "finish on HIP streams (the counter finish on its own), "
                                         "next pool pass beside the %s" % (
                                             args.inflight, "counter finish" if
                                             args.overlap == "finish" else "pipeline kernel") +
