@@ -14,6 +14,8 @@ hot kernel, from the AMDGPU metadata and the disassembly:
   private segment size would show if they reached memory);
 - VGPRs within what the launch keeps resident (4 waves per SIMD for the
   1024-thread pipeline workgroup and two 512-thread ACL workgroups per CU);
+- the hint / DNS / DNS drain-loop kernels make no call (no `s_swappc`):
+  their rare paths run in follow-up kernels;
 - the two-quad ACL kernel's lockstep search loop issues its 8 LDS reads
   (two quads of four tuples) per step with one branch, and the one-quad
   loop 4 (acl_v4_four in device/classify.hip).
@@ -105,6 +107,15 @@ HOT = {   # kernel (mangled-name fragment) -> VGPR ceiling of its launch
     "hist_kernelILb1E": 128,
 }
 
+# string kernels without a call in their loops (device/hint.hip: rare lanes
+# go to a follow-up kernel); a call site there brought back a private
+# segment, scratch spills of the loop state and SGPR spills on every chunk
+HOT_STRING = {
+    "hint_kernelILb1ELb1E": 72,               # 7 waves per SIMD
+    "dns_kernelILb1ELb1E": 72,
+    "dnsd_kernelILb1ELb1E": 128,
+}
+
 
 def test_hot_kernels_use_no_scratch(tmp_path):
     k = _kernels(_code_object("classify", tmp_path))
@@ -115,6 +126,20 @@ def test_hot_kernels_use_no_scratch(tmp_path):
         assert m["private_segment_fixed_size"] == 0, (part, m)
         assert m["vgpr_spill_count"] == 0, (part, m)
         assert m["vgpr_count"] <= vmax, (part, m)
+
+
+def test_string_kernels_have_no_call_in_their_loops(tmp_path):
+    co = _code_object("hint", tmp_path)
+    k = _kernels(co)
+    f = _functions(co)
+    for part, vmax in HOT_STRING.items():
+        name = _one(k, part)
+        m = k[name]
+        assert m["private_segment_fixed_size"] == 0, (part, m)
+        assert m["vgpr_spill_count"] == 0, (part, m)
+        assert m["vgpr_count"] <= vmax, (part, m)
+        ins = f[_one(f, part)]
+        assert not any(t.startswith("s_swappc") for _, t in ins), part
 
 
 @pytest.mark.parametrize("quads", [1, 2])
