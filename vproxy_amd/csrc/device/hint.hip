@@ -122,8 +122,8 @@ __device__ __forceinline__ uint32_t lane_end(uint32_t a, uint32_t last) {
     return (threadIdx.x & 63) == 63 ? last : nx;
 }
 
-template <uint32_t kBytes, bool kPair, int kPre, class Body>
-__device__ __forceinline__ void chunk_loop(Chunks& ch, int w, const uint8_t* blob,
+template <uint32_t kBytes, bool kPair, int kPre, class Body, class Ch>
+__device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
     const int lane = int(threadIdx.x & 63);
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    Chunks ch(ticket, (n + 63) / 64);
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, 60> ch(ticket, (n + 63) / 64);
     const bool general = !kDefer && uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     int32_t* __restrict__ value, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    Chunks ch(ticket, (n + 63) / 64);
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, 50> ch(ticket, (n + 63) / 64);
     HintImage slow_img = img;
     VC_PBEGIN();
     // one chunk per stage: staging two (chunk_loop) adds live registers
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    Chunks ch(ticket, (n + 63) / 64);
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);
     VC_PBEGIN();
     chunk_loop<kStageBytes, true, 2>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
                                   [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
@@ -673,8 +673,9 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     // sequence without them.  16-chunk big tickets and two rounds of 4-chunk
     // tail tickets: the drain loop's chunks cost more than the other string
     // kernels', and their 24 / 8 / 1 layout ran it 3.99 against 3.94 ms
-    // (profiles/r04_ab_ticket_confirm.txt)
-    ChunksT<16, 4, 2> ch(ticket, (n + 63) / 64);
+    // (profiles/r04_ab_ticket_confirm.txt); 60 % of the chunks static
+    // (chunks.h ChunksT)
+    ChunksT<16, 4, 2, 60> ch(ticket, (n + 63) / 64);
     int64_t c = ch.first(w);
     LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
     while (c < ch.nchunks) {

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     __shared__ uint32_t stage[kStage ? kMirrorWaves : 1][kStage ? kMirrorStageWords : 1];
     const MirrorImage& fi = img;
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    Chunks ch(ticket, (n + 63) / 64);              // chunks.h: work tickets or static
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);   // chunks.h
     int64_t c = ch.first(w);
     LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
     while (c < ch.nchunks) {
