@@ -31,6 +31,15 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_HINT_MINW
 #define VC_HINT_MINW 7
 #endif
+#ifndef VC_HINT_SWAP
+#define VC_HINT_SWAP 1
+#endif
+#ifndef VC_CERT_SWAP
+#define VC_CERT_SWAP 1
+#endif
+#ifndef VC_DNS_PAIR
+#define VC_DNS_PAIR 0
+#endif
 #ifndef VC_HINT_PRE
 #define VC_HINT_PRE 2
 #endif
@@ -116,13 +125,18 @@ __device__ __forceinline__ PairOffs pair_offs(const uint32_t* off, int64_t base,
     return r;
 }
 
+// kSwap (kPre 2): each lane runs the shorter of its two items in the pair's
+// first body call and the longer in the second.  A body's scan runs to its
+// wave's longest name, so the first call ends near the lanes' upper
+// quantile of the shorter names instead of the longest of 64.
+
 // the lane's end: the next lane's start, or `last` for lane 63
 __device__ __forceinline__ uint32_t lane_end(uint32_t a, uint32_t last) {
     const uint32_t nx = uint32_t(__shfl_down(int(a), 1, 64));
     return (threadIdx.x & 63) == 63 ? last : nx;
 }
 
-template <uint32_t kBytes, bool kPair, int kPre, class Body, class Ch>
+template <uint32_t kBytes, bool kPair, int kPre, bool kSwap = false, class Body, class Ch>
 __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
                                            Body body) {
@@ -143,8 +157,8 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
             const bool staged = blob && stage_wave<kBytes>(blob, cur.o0, two ? cur.o2 : cur.o1,
                                                            stage, &a0);
             VC_PMARK(0);
-            body(c, staged, a0, cur.A0, lane_end(cur.A0, cur.o1));
-            if (two) body(c + 1, staged, a0, cur.A1, lane_end(cur.A1, cur.o2));
+            body(c * 64 + lane, staged, a0, cur.A0, lane_end(cur.A0, cur.o1));
+            if (two) body(c * 64 + 64 + lane, staged, a0, cur.A1, lane_end(cur.A1, cur.o2));
             wave_done();
             VC_PMARK(5);
             c = cn;
@@ -185,6 +199,13 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
             if (!staged) staged = stage_wave<kBytes>(blob, o0, o1, stage, &a0);
         }
         VC_PMARK(0);
+        // the lane's shorter item first (see kSwap above); a lane mask, so
+        // the items' indices stay a scalar base plus the lane
+        const bool sw = kSwap && kPre == 2 && nsub == 2 && E1 - A1 < E0 - A0;
+        if (sw) {
+            const uint32_t ta = A0, te = E0;
+            A0 = A1; E0 = E1; A1 = ta; E1 = te;
+        }
         for (int sub = 0; sub < nsub; ++sub) {
             if (off && (kPre == 0 || (kPre == 1 && sub == 1))) {
                 const int64_t i = base + 64 * sub + lane;
@@ -192,7 +213,7 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
                 E0 = off[i + 1 < n ? i + 1 : n];
             }
             VC_CHECK(!off || (A0 <= E0 && E0 <= off[n]), 303, base, E0);
-            body(c + sub, staged, a0, kPre == 2 && sub ? A1 : A0, kPre == 2 && sub ? E1 : E0);
+            body(base + ((sub != 0) != sw ? 64 : 0) + lane, staged, a0, kPre == 2 && sub ? A1 : A0, kPre == 2 && sub ? E1 : E0);
         }
         wave_done();
         VC_PMARK(5);
@@ -220,9 +241,8 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true, VC_HINT_PRE>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
-                                  [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
-        const int64_t i = c * 64 + lane;
+    chunk_loop<kStageBytes, true, VC_HINT_PRE, bool(VC_HINT_SWAP)>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
+                                  [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         int32_t r = -1;
         if (i < n) {
             const int p = port ? int(port[i]) : 0;
@@ -294,6 +314,30 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     ChunksT<kPerTicket, kTailChunks, kTailRounds, 50> ch(ticket, (n + 63) / 64);
     HintImage slow_img = img;
     VC_PBEGIN();
+#if VC_DNS_PAIR
+    // two chunks per stage, as hint_kernel (once the loop had no call in it)
+    chunk_loop<kStageBytes, true, 2, bool(VC_HINT_SWAP)>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
+                                  [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
+        uint8_t kd = 0;
+        if (i < n) {
+            int32_t val = 0;
+            if (staged) {
+                dns_one<kDefer>(hosts, img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
+                                int(e - a), &kd, &val);
+            } else if (kDefer) {
+                kd = kDnsDeferred;
+            } else {
+                dns_one(hosts, img, &slow_img, PtrSrc{qblob + a}, int(e - a), &kd, &val);
+            }
+            kind[i] = kd;
+            value[i] = val;
+        }
+        if (kDefer && ticket) {
+            const uint64_t dm = __ballot(i < n && kd == kDnsDeferred);
+            if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
+        }
+    });
+#else
     // one chunk per stage: staging two (chunk_loop) adds live registers
     // that spill in this kernel's hot path (DNS 1.08 -> 1.21 ms)
     for (int64_t c = ch.first(w); c < ch.nchunks; c = ch.next(c)) {
@@ -326,6 +370,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
         if (kStage) wave_done();
         VC_PMARK(5);
     }
+#endif
     VC_PEND();
 }
 
@@ -365,12 +410,11 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     const uint8_t* __restrict__ null, int64_t n, int32_t* __restrict__ out,
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
-    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const int w = int(threadIdx.x >> 6);
     ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);
     VC_PBEGIN();
-    chunk_loop<kStageBytes, true, 2>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
-                                  [&](int64_t c, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
-        const int64_t i = c * 64 + lane;
+    chunk_loop<kStageBytes, true, 2, bool(VC_CERT_SWAP)>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
+                                  [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         if (i < n) {
             const bool is_null = null && null[i];
             out[i] = staged ? cert_one(certs, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a),
