@@ -40,6 +40,9 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_DNS_PAIR
 #define VC_DNS_PAIR 0
 #endif
+#ifndef VC_DNS_PRE
+#define VC_DNS_PRE 2
+#endif
 #ifndef VC_HINT_PRE
 #define VC_HINT_PRE 2
 #endif
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     VC_PBEGIN();
 #if VC_DNS_PAIR
     // two chunks per stage, as hint_kernel (once the loop had no call in it)
-    chunk_loop<kStageBytes, true, 2, bool(VC_HINT_SWAP)>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
+    chunk_loop<kStageBytes, true, VC_DNS_PRE, bool(VC_HINT_SWAP) && VC_DNS_PRE == 2>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
                                   [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         uint8_t kd = 0;
         if (i < n) {
