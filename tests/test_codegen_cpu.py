@@ -110,10 +110,12 @@ HOT = {   # kernel (mangled-name fragment) -> VGPR ceiling of its launch
 # string kernels without a call in their loops (device/hint.hip: rare lanes
 # go to a follow-up kernel); a call site there brought back a private
 # segment, scratch spills of the loop state and SGPR spills on every chunk
+# (VGPR bound, spilled dwords allowed): dns_kernel on chunk pairs at 6 waves
+# puts one dword, the lane's stage address, in scratch (read once per stage)
 HOT_STRING = {
-    "hint_kernelILb1ELb1E": 72,               # 7 waves per SIMD
-    "dns_kernelILb1ELb1E": 72,
-    "dnsd_kernelILb1ELb1E": 128,
+    "hint_kernelILb1ELb1E": (72, 0),          # 7 waves per SIMD
+    "dns_kernelILb1ELb1E": (80, 1),           # 6
+    "dnsd_kernelILb1ELb1E": (128, 0),
 }
 
 
@@ -132,11 +134,11 @@ def test_string_kernels_have_no_call_in_their_loops(tmp_path):
     co = _code_object("hint", tmp_path)
     k = _kernels(co)
     f = _functions(co)
-    for part, vmax in HOT_STRING.items():
+    for part, (vmax, spill) in HOT_STRING.items():
         name = _one(k, part)
         m = k[name]
-        assert m["private_segment_fixed_size"] == 0, (part, m)
-        assert m["vgpr_spill_count"] == 0, (part, m)
+        assert m["private_segment_fixed_size"] <= 4 * spill + 4 * bool(spill), (part, m)
+        assert m["vgpr_spill_count"] <= spill, (part, m)
         assert m["vgpr_count"] <= vmax, (part, m)
         ins = f[_one(f, part)]
         assert not any(t.startswith("s_swappc") for _, t in ins), part

@@ -27,7 +27,11 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 // the call-free kernel at 8 (64 VGPRs) spills 20 and loses (0.833 against
 // 0.772 ms, profiles/r04_ab_minw.txt).  dns_kernel: 7 (72 VGPRs, no spills)
 // since its loop has no call (0.913 against 0.928 ms at 6); with the calls
-// it spilled in the hot path at 7 (1.26 against 1.07 ms, round 2).
+// it spilled in the hot path at 7 (1.26 against 1.07 ms, round 2).  On
+// chunk pairs (VC_DNS_PAIR): 6 (80 VGPRs; one dword, the lane's stage
+// address, goes to scratch and is read once per stage): 0.78 ms against 0.78
+// at 7 (72 VGPRs, 11 spilled) and 0.83 at 5 (90, none), against 0.807 on
+// single chunks (profiles/r04_ab_dns_pair.txt).
 #ifndef VC_HINT_MINW
 #define VC_HINT_MINW 7
 #endif
@@ -38,10 +42,13 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_CERT_SWAP 1
 #endif
 #ifndef VC_DNS_PAIR
-#define VC_DNS_PAIR 0
+#define VC_DNS_PAIR 1
 #endif
 #ifndef VC_DNS_PRE
 #define VC_DNS_PRE 2
+#endif
+#ifndef VC_DNS_SWAP
+#define VC_DNS_SWAP VC_HINT_SWAP
 #endif
 #ifndef VC_HINT_PRE
 #define VC_HINT_PRE 2
@@ -66,7 +73,7 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #define VC_DEFER_GRID 128
 #endif
 #ifndef VC_DNS_MINW
-#define VC_DNS_MINW 7
+#define VC_DNS_MINW 6
 #endif
 
 
@@ -318,8 +325,9 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     HintImage slow_img = img;
     VC_PBEGIN();
 #if VC_DNS_PAIR
-    // two chunks per stage, as hint_kernel (once the loop had no call in it)
-    chunk_loop<kStageBytes, true, VC_DNS_PRE, bool(VC_HINT_SWAP) && VC_DNS_PRE == 2>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
+    // two chunks per stage, as hint_kernel, once the loop had no call in it
+    // (0.807 -> 0.78 ms)
+    chunk_loop<kStageBytes, true, VC_DNS_PRE, bool(VC_DNS_SWAP) && VC_DNS_PRE == 2>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
                                   [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         uint8_t kd = 0;
         if (i < n) {
