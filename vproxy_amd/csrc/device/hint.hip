@@ -47,6 +47,10 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_DNS_PRE
 #define VC_DNS_PRE 2
 #endif
+// dns_kernel's static share (chunks.h ChunksT S)
+#ifndef VC_DNS_STATIC
+#define VC_DNS_STATIC 50
+#endif
 #ifndef VC_DNS_SWAP
 #define VC_DNS_SWAP VC_HINT_SWAP
 #endif
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     int32_t* __restrict__ value, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    ChunksT<kPerTicket, kTailChunks, kTailRounds, 50> ch(ticket, (n + 63) / 64);
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, VC_DNS_STATIC> ch(ticket, (n + 63) / 64);
     HintImage slow_img = img;
     VC_PBEGIN();
 #if VC_DNS_PAIR
