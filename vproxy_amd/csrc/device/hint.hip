@@ -47,7 +47,10 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_DNS_PRE
 #define VC_DNS_PRE 2
 #endif
-// dns_kernel's static share (chunks.h ChunksT S)
+// hint_kernel's and dns_kernel's static shares (chunks.h ChunksT S)
+#ifndef VC_HINT_STATIC
+#define VC_HINT_STATIC 60
+#endif
 #ifndef VC_DNS_STATIC
 #define VC_DNS_STATIC 50
 #endif
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    ChunksT<kPerTicket, kTailChunks, kTailRounds, 60> ch(ticket, (n + 63) / 64);
+    ChunksT<kPerTicket, kTailChunks, kTailRounds, VC_HINT_STATIC> ch(ticket, (n + 63) / 64);
     const bool general = !kDefer && uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
