@@ -110,11 +110,10 @@ HOT = {   # kernel (mangled-name fragment) -> VGPR ceiling of its launch
 # string kernels without a call in their loops (device/hint.hip: rare lanes
 # go to a follow-up kernel); a call site there brought back a private
 # segment, scratch spills of the loop state and SGPR spills on every chunk
-# (VGPR bound, spilled dwords allowed): dns_kernel on chunk pairs at 6 waves
-# puts one dword, the lane's stage address, in scratch (read once per stage)
+# (VGPR bound, spilled dwords allowed)
 HOT_STRING = {
     "hint_kernelILb1ELb1E": (72, 0),          # 7 waves per SIMD
-    "dns_kernelILb1ELb1E": (80, 1),           # 6
+    "dns_kernelILb1ELb1E": (80, 0),           # 6
     "dnsd_kernelILb1ELb1E": (128, 0),
 }
 

@@ -28,10 +28,11 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 // 0.772 ms, profiles/r04_ab_minw.txt).  dns_kernel: 7 (72 VGPRs, no spills)
 // since its loop has no call (0.913 against 0.928 ms at 6); with the calls
 // it spilled in the hot path at 7 (1.26 against 1.07 ms, round 2).  On
-// chunk pairs (VC_DNS_PAIR): 6 (80 VGPRs; one dword, the lane's stage
-// address, goes to scratch and is read once per stage): 0.78 ms against 0.78
-// at 7 (72 VGPRs, 11 spilled) and 0.83 at 5 (90, none), against 0.807 on
-// single chunks (profiles/r04_ab_dns_pair.txt).
+// chunk pairs (VC_DNS_PAIR): 6 (80 VGPRs): 0.78 ms against 0.78 at 7 (72
+// VGPRs, 11 spilled) and 0.83 at 5 (90, none), against 0.807 on single
+// chunks (profiles/r04_ab_dns_pair.txt); with its results stored in item
+// order (VC_DNS_ORDERED) it keeps nothing in scratch and runs 0.764 against
+// 0.776 ms (profiles/r04_ab_dns_ordered.txt).
 #ifndef VC_HINT_MINW
 #define VC_HINT_MINW 7
 #endif
@@ -46,6 +47,10 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #endif
 #ifndef VC_DNS_PRE
 #define VC_DNS_PRE 2
+#endif
+// VC_DNS_ORDERED: dns_kernel's results stored in item order (chunk_loop store)
+#ifndef VC_DNS_ORDERED
+#define VC_DNS_ORDERED 1
 #endif
 // hint_kernel's and dns_kernel's static shares (chunks.h ChunksT S)
 #ifndef VC_HINT_STATIC
@@ -153,10 +158,21 @@ __device__ __forceinline__ uint32_t lane_end(uint32_t a, uint32_t last) {
     return (threadIdx.x & 63) == 63 ? last : nx;
 }
 
-template <uint32_t kBytes, bool kPair, int kPre, bool kSwap = false, class Body, class Ch>
+// store (optional; kPre 2): the body returns its item's result and
+// store(i, r) writes the pair's results after both calls, in item order, so
+// the lane swap does not split each output line over two partial writes.
+struct NoStore {
+    template <class R>
+    __device__ void operator()(int64_t, R) const {}
+};
+
+template <uint32_t kBytes, bool kPair, int kPre, bool kSwap = false, class Body, class Ch,
+          class Store = NoStore>
 __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
                                            const uint32_t* off, int64_t n, uint32_t* stage,
-                                           Body body) {
+                                           Body body, Store store = Store{}) {
+    constexpr bool kOrdered = !std::is_same_v<Store, NoStore>;
+    static_assert(!kOrdered || kPre == 2, "ordered stores need both spans up front");
     const int lane = int(threadIdx.x & 63);
     if constexpr (kPre == 3) {
         int64_t c = ch.first(w);
@@ -223,7 +239,20 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
             const uint32_t ta = A0, te = E0;
             A0 = A1; E0 = E1; A1 = ta; E1 = te;
         }
-        for (int sub = 0; sub < nsub; ++sub) {
+        if constexpr (kOrdered) {
+            const int64_t i = base + lane;
+            VC_CHECK(!off || (A0 <= E0 && E0 <= off[n]), 303, base, E0);
+            const auto r0 = body(sw ? i + 64 : i, staged, a0, A0, E0);
+            if (nsub == 1) {
+                if (i < n) store(i, r0);
+            } else {
+                VC_CHECK(!off || (A1 <= E1 && E1 <= off[n]), 303, base, E1);
+                const auto r1 = body(sw ? i : i + 64, staged, a0, A1, E1);
+                if (i < n) store(i, sw ? r1 : r0);
+                if (i + 64 < n) store(i + 64, sw ? r0 : r1);
+            }
+        }
+        for (int sub = 0; sub < (kOrdered ? 0 : nsub); ++sub) {
             if (off && (kPre == 0 || (kPre == 1 && sub == 1))) {
                 const int64_t i = base + 64 * sub + lane;
                 A0 = off[i < n ? i : n];
@@ -321,6 +350,12 @@ __global__ __launch_bounds__(256) void hint_defer_kernel(
     }
 }
 
+// one query's answer (chunk_loop's ordered stores)
+struct DnsRes {
+    int32_t value;
+    uint8_t kind;
+};
+
 template <bool kStage, bool kDefer>
 __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     HostsImage hosts, HintImage img, const uint8_t* __restrict__ qblob,
@@ -337,8 +372,8 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
     chunk_loop<kStageBytes, true, VC_DNS_PRE, bool(VC_DNS_SWAP) && VC_DNS_PRE == 2>(ch, w, kStage ? qblob : nullptr, qoff, n, stage[w],
                                   [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
         uint8_t kd = 0;
+        int32_t val = 0;
         if (i < n) {
-            int32_t val = 0;
             if (staged) {
                 dns_one<kDefer>(hosts, img, &slow_img, LdsSrc{stage[w], int(kApron + (a - a0))},
                                 int(e - a), &kd, &val);
@@ -347,14 +382,24 @@ __global__ __launch_bounds__(kHintBlock, VC_DNS_MINW) void dns_kernel(
             } else {
                 dns_one(hosts, img, &slow_img, PtrSrc{qblob + a}, int(e - a), &kd, &val);
             }
+#if !VC_DNS_ORDERED
             kind[i] = kd;
             value[i] = val;
+#endif
         }
         if (kDefer && ticket) {
             const uint64_t dm = __ballot(i < n && kd == kDnsDeferred);
             if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
         }
-    });
+        return DnsRes{val, kd};
+    }
+#if VC_DNS_ORDERED
+    , [&](int64_t i, DnsRes r) {
+        kind[i] = r.kind;
+        value[i] = r.value;
+    }
+#endif
+    );
 #else
     // one chunk per stage: staging two (chunk_loop) adds live registers
     // that spill in this kernel's hot path (DNS 1.08 -> 1.21 ms)
