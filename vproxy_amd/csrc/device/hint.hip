@@ -52,6 +52,9 @@ constexpr uint32_t kStageWords = (kStageBytes + 2 * kApron) / 4;
 #ifndef VC_DNS_ORDERED
 #define VC_DNS_ORDERED 1
 #endif
+#ifndef VC_CERT_ORDERED
+#define VC_CERT_ORDERED 1
+#endif
 // hint_kernel's and dns_kernel's static shares (chunks.h ChunksT S)
 #ifndef VC_HINT_STATIC
 #define VC_HINT_STATIC 60
@@ -478,13 +481,22 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
     VC_PBEGIN();
     chunk_loop<kStageBytes, true, 2, bool(VC_CERT_SWAP)>(ch, w, kStage ? blob : nullptr, off, n, stage[w],
                                   [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
+        int32_t r = -1;
         if (i < n) {
             const bool is_null = null && null[i];
-            out[i] = staged ? cert_one(certs, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a),
-                                       is_null)
-                            : cert_one(certs, PtrSrc{blob + a}, int(e - a), is_null);
+            r = staged ? cert_one(certs, LdsSrc{stage[w], int(kApron + (a - a0))}, int(e - a),
+                                  is_null)
+                       : cert_one(certs, PtrSrc{blob + a}, int(e - a), is_null);
+#if !VC_CERT_ORDERED
+            out[i] = r;
+#endif
         }
-    });
+        return r;
+    }
+#if VC_CERT_ORDERED
+    , [&](int64_t i, int32_t r) { out[i] = r; }
+#endif
+    );
     VC_PEND();
 }
 
