@@ -404,6 +404,107 @@ class C5Steps:
         return float(np.mean([r[key][0].elapsed_time(r[key][1]) for r in self.timing]))
 
 
+# ---------------------------------------------------------------------------
+# rank launcher: `python bench.py --gpus N` without torch.distributed.run
+# ---------------------------------------------------------------------------
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv, script=None, env=None, poll_s=0.2, grace_s=20.0):
+    """Run `script argv` as n rank processes (RANK = LOCAL_RANK = 0..n-1,
+    WORLD_SIZE = n, MASTER_ADDR 127.0.0.1 and one MASTER_PORT), the layout
+    torch.distributed.run gives them.  Children, never exec: the caller must
+    not have touched the GPU (this process only counts devices).  Rank 0's
+    stdout is inherited, so its JSON line is the job's.  Returns 0 when every
+    rank exits 0; otherwise the first failing rank's status (128 + signal for
+    a signal), after terminating the ranks still running -- a rank waiting
+    in a collective for a dead peer would otherwise hang the job."""
+    import signal
+    import subprocess
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in base:
+        base["MASTER_PORT"] = str(_free_port())
+    procs = []
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signum, frame):          # the driver's time limit: pass it on
+        stop_all(signum)
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                     LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0")
+            procs.append(subprocess.Popen([sys.executable, "-u", script or __file__] + list(argv),
+                                          env=e))
+        rc = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                c = bad[0]
+                rc = 128 - c if c < 0 else c
+                stop_all()
+                t0 = time.time()
+                while any(p.poll() is None for p in procs) and time.time() - t0 < grace_s:
+                    time.sleep(poll_s)
+                stop_all(signal.SIGKILL)
+                for p in procs:
+                    p.wait()
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+        return rc
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
+def resolve_world(gpus, environ=None, shared=False, device_count=None):
+    """What `--gpus N` means for this process: ("run", world) when it is one
+    rank of a launched job (WORLD_SIZE set, and equal to N) or N == 1;
+    ("launch", N) when N > 1 and nothing launched it (bench.py spawns the N
+    ranks itself).  Raises SystemExit(2) when WORLD_SIZE disagrees with
+    --gpus, or when N ranks need more GPUs than the node shows -- never a
+    silent one-GPU run labelled N."""
+    environ = os.environ if environ is None else environ
+    ws = environ.get("WORLD_SIZE")
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1 (got %d)" % gpus)
+    if ws is not None and ws != "":
+        if int(ws) != gpus:
+            print("bench.py: --gpus %d but WORLD_SIZE=%s: the launcher and the flag disagree"
+                  % (gpus, ws), file=sys.stderr)
+            raise SystemExit(2)
+        return "run", gpus
+    if gpus == 1:
+        return "run", 1
+    if not shared:
+        if device_count is None:
+            device_count = torch.cuda.device_count()     # counts only: no HIP context
+        if device_count < gpus:
+            print("bench.py: --gpus %d but %d GPU(s) visible" % (gpus, device_count),
+                  file=sys.stderr)
+            raise SystemExit(2)
+    return "launch", gpus
+
+
 def max_over_ranks(x, dev):
     """MAX of a float over the process group (the step time the job sees)."""
     import torch.distributed as dist
@@ -429,9 +530,29 @@ def cpu_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    quota = cgroup_cpu_max()
+    # every core this process may run on (all host cores);
+    # a cgroup quota below that is recorded, not used to shrink the pool
     return {"nproc": os.cpu_count(), "affinity": avail, "cpu_model": model,
-            "threads_all": max(1, min(share, avail, 64))}
+            "cgroup_cpu_max": quota[0], "quota_cpus": quota[1],
+            "threads_all": max(1, avail)}
+
+
+def cgroup_cpu_max(path="/sys/fs/cgroup/cpu.max"):
+    """(raw `cpu.max` text, CPUs it allows or None when unlimited/absent):
+    cgroup v2 "quota period", e.g. "1600000 100000" = 16 CPUs."""
+    try:
+        with open(path) as f:
+            raw = f.read().strip()
+    except OSError:
+        return None, None
+    parts = raw.split()
+    if len(parts) == 2 and parts[0] != "max":
+        try:
+            return raw, round(int(parts[0]) / int(parts[1]), 2)
+        except ValueError:
+            pass
+    return raw, None
 
 
 def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
@@ -458,7 +579,9 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
            "sample": "%s; all-core: %d items in %.1f s on %d threads; 1 core: %d items in %.1f s"
                      % (what, na, ta, info["threads_all"], n1, t1),
            "one_core": {"value": n1 / t1 / 1e6, "cores": 1},
-           "nproc": info["nproc"], "cpu_model": info["cpu_model"]}
+           "nproc": info["nproc"], "affinity": info["affinity"],
+           "cgroup_cpu_max": info["cgroup_cpu_max"], "quota_cpus": info["quota_cpus"],
+           "cpu_model": info["cpu_model"]}
     if note:
         out["note"] = note
     return out
@@ -583,7 +706,7 @@ def load_traffic(workload, kernel):
 
 
 # ---------------------------------------------------------------------------
-def main():
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -626,17 +749,33 @@ def main():
                     help="mix / mixhost: share of IPv6 packets (C3's mix is 0.15)")
     ap.add_argument("--dist", action="store_true",
                     help="use the process group and the counter all-reduce even at N = 1")
-    args = ap.parse_args()
+    return ap
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+
+def make_c5_steps(clf, t, packets, dev, args, bucket):
+    """The C5 schedule exactly as main() times it (also run, at the timed
+    size, by tests/test_gpu_c5.py::test_c5_timed_launch_exact)."""
+    return C5Steps(clf, t, packets, dev, bucket=bucket, serial=args.serial,
+                   counters=args.counters, finish=args.finish, inflight=args.inflight,
+                   overlap=args.overlap, gate=args.gate, pool_cus=args.pool_cus,
+                   pool_stream=args.pool_stream)
+
+
+def main():
+    args = build_parser().parse_args()
+
     # VC_BENCH_SHARED_GPU=1: rehearsal of the multi-rank path on a one-GPU
     # box -- every rank on cuda:0 and gloo for the collectives (RCCL refuses
     # two ranks on one device).  The timing is then not a scaling result.
     shared = os.environ.get("VC_BENCH_SHARED_GPU") == "1"
+    mode, world = resolve_world(args.gpus, shared=shared)
+    if mode == "launch":
+        # `python bench.py --gpus N` with no launcher: spawn the N ranks here
+        # (nothing above touched the GPU) and exit with their status
+        log("launching %d ranks (no WORLD_SIZE in the environment)" % world)
+        sys.exit(launch_ranks(world, sys.argv[1:]))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if shared:
         local = 0
     torch.cuda.set_device(local)
@@ -670,10 +809,7 @@ def main():
     # this rank's shard of the global batch (weak scaling: N = packets x world)
     lo, hi = shard(args.packets * world, rank, world)
     packets = gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
-    steps = C5Steps(clf, t, packets, dev, bucket=use_dist, serial=args.serial,
-                    counters=args.counters, finish=args.finish, inflight=args.inflight,
-                    overlap=args.overlap, gate=args.gate, pool_cus=args.pool_cus,
-                    pool_stream=args.pool_stream)
+    steps = make_c5_steps(clf, t, packets, dev, args, bucket=use_dist)
     torch.cuda.synchronize()
     log("packets generated (%d of %d, shard [%d, %d)), setup %.1fs" % (
         hi - lo, args.packets * world, lo, hi, time.time() - t_setup))
@@ -811,6 +947,25 @@ def _time(fn, steps, warmup):
     return el, float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
+def hosts_text(n=50_000):
+    """The DNS workloads' hosts file: n lines "10.0.x.y hN.hosts.local"."""
+    return "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i) for i in range(n))
+
+
+def c4_workload(dns, n=16 << 20):
+    """The `c4` / `dns` sub-benches' inputs (also checked whole by
+    tests/test_gpu_c5.py): 100k hint-host groups, the 50k-line hosts file
+    (dns), 1M distinct hostnames (DNS-flavoured with trailing dots for dns)
+    and the n seeded draws from them that form the batch."""
+    groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+    if dns:
+        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
+    else:
+        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
+    pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
+    return groups, hosts_text() if dns else None, names, pidx
+
+
 def dnsd_tables(clf, n_templates=1 << 20):
     """The `dnsd` workload's tables, compiled into clf: 100k hint-host
     groups, a 50k-line hosts file, a 10k-rule SecurityGroup (default allow);
@@ -821,8 +976,7 @@ def dnsd_tables(clf, n_templates=1 << 20):
     t = types.SimpleNamespace()
     t.groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
     clf.compile_upstream(t.groups)
-    t.hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
-                        for i in range(50_000))
+    t.hosts = hosts_text()
     clf.compile_hosts_text(t.hosts)
     t.tcp, t.udp = W.gen_sg_rules(10000, W.SEED + 2, p_range=0.3)
     a, na, ka = W.as_ctypes(t.tcp, V._lib.VcAclRule)
@@ -835,6 +989,7 @@ def dnsd_tables(clf, n_templates=1 << 20):
     dgs = [DW.header(qd=1, ar=int(e), ident=i & 0xFFFF) + DW.question(q, int(qt_)) +
            (DW.opt_record() if e else b"") for i, (q, qt_, e) in enumerate(zip(qn, qt, edns))]
     t.dblob, t.doff = W.pack(dgs)
+    t.qnames, t.qtypes = qn, qt
     return t
 
 
@@ -946,7 +1101,8 @@ def sub_bench(args, clf, dev, rank, world):
                        "sample": "the full C1 batch (%d tuples, ACL + route), oracle linear "
                                  "scans" % n,
                        "one_core": {"value": cpu[1], "cores": 1}, "nproc": info["nproc"],
-                       "cpu_model": info["cpu_model"]}
+                       "affinity": info["affinity"], "cgroup_cpu_max": info["cgroup_cpu_max"],
+                       "quota_cpus": info["quota_cpus"], "cpu_model": info["cpu_model"]}
             else:
                 cpu = cpu_rates(run, "M items/s", 4.0, "first tuples of the C2 batch, oracle "
                                 "first-match scan over 10k rules")
@@ -1004,19 +1160,13 @@ def sub_bench(args, clf, dev, rank, world):
             cpu = cpu_rates(run, "M items/s", 4.0, "85/15 v4/v6 lookups of the C3 workload, "
                             "oracle first-match scans over the RouteTable lists")
     elif args.workload in ("c4", "dns"):
-        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
-        clf.compile_upstream(groups)
         dns = args.workload == "dns"
-        if dns:
-            hosts = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
-                              for i in range(50_000))
-            clf.compile_hosts_text(hosts)
-            names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
-        else:
-            names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
-        nblob, noff = W.pack(names)
         n = 16 << 20
-        pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
+        groups, hosts, names, pidx = c4_workload(dns, n)
+        clf.compile_upstream(groups)
+        if dns:
+            clf.compile_hosts_text(hosts)
+        nblob, noff = W.pack(names)
         blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
         hblob, hoff = blob.cpu().numpy(), off.cpu().numpy().view(np.uint32)
         P = lambda x: C.c_void_p(x.ctypes.data)

@@ -354,9 +354,9 @@ int vc_pipeline(vc_ctx *ctx, const vc_packets *in, int64_t n, const int32_t *poo
  * required).  Zero-copy when every array is registered and aligned as
  * vc_pipeline_c6_dev asks (the rows are read coalesced); otherwise staged
  * in chunks, each chunk's rows found by counting its family-6 packets, and
- * only the n6 rows cross PCIe instead of n.  The staged path checks n6
- * against the family array: VC_EINVAL when they disagree (results are then
- * unspecified); zero-copy trusts n6 as vc_pipeline_c6_dev does. */
+ * only the n6 rows cross PCIe instead of n.  Both paths first count the
+ * family array's IPv6 packets and return VC_EINVAL, before any output is
+ * written, when that count is not n6. */
 int vc_pipeline_c6(vc_ctx *ctx, const vc_packets *in, int64_t n, int64_t n6,
                    const int32_t *pool_group, int64_t n_pool, const vc_pipeline_out *out);
 

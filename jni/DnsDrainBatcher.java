@@ -51,7 +51,9 @@ import java.nio.ByteBuffer;
  * Handler's readable becomes {@code batcher.readable(ctx)}; the UDP list of
  * {@code securityGroup}, the rrsets Upstream and the hosts map are compiled
  * into {@code gpu} after each change (GpuContext.compileSecurityGroup /
- * compileUpstream, GpuClassifier.compileHostsText).
+ * compileUpstream / compileHostsText).  A batch's outputs are acted on
+ * inside GpuContext.batch, so the group indices and hosts values it hands
+ * to Host.answer belong to the snapshot the call classified against.
  */
 public final class DnsDrainBatcher {
     public static final int ANSWER = 0, RECURSIVE = 1, RESPONSE = 2, REJECTED = 3,
@@ -78,8 +80,10 @@ public final class DnsDrainBatcher {
     private final Host host;
     private final int cap = ClassifierConfig.batch;
 
-    // one batch, SoA, registered once so the calls run zero-copy
-    private final ByteBuffer blob = GpuContext.direct((long) cap * 512);
+    // one batch, SoA, registered once so the calls run zero-copy; the blob
+    // holds at least one largest datagram, so fill() always makes progress
+    // whatever -Dclassifier_batch says
+    private final ByteBuffer blob = GpuContext.direct(Math.max((long) cap * 512, MAX_DATAGRAM));
     private final ByteBuffer off = GpuContext.direct(4L * (cap + 1));
     private final ByteBuffer family = GpuContext.direct(cap);
     private final ByteBuffer remote4 = GpuContext.direct(4L * cap);
@@ -170,8 +174,13 @@ public final class DnsDrainBatcher {
     private boolean dispatch() {
         final int m = n;
         pack(m);
-        boolean ok = gpu.call(c -> GpuClassifier.dnsDatagrams(c, blob, off, m, family, remote4, remote6,
-            remotePort, out));
+        // the native call and every group index of this batch resolve against
+        // one snapshot: a recompile waits for the batch (GpuContext.batch)
+        return gpu.batch(c -> GpuClassifier.dnsDatagrams(c, blob, off, m, family, remote4, remote6,
+            remotePort, out), ok -> act(m, ok));
+    }
+
+    private boolean act(int m, boolean ok) {
         for (int i = 0; i < m; ++i) {
             head = i + 1;
             if (!ok) {

@@ -16,6 +16,8 @@ import java.nio.ByteOrder;
 import java.nio.charset.StandardCharsets;
 import java.util.ArrayList;
 import java.util.List;
+import java.util.concurrent.locks.ReentrantReadWriteLock;
+import java.util.function.Function;
 
 /**
  * One libvclassify context (one GPU) with the fallback INTEGRATION.md
@@ -38,8 +40,13 @@ import java.util.List;
  * The Java lists stay live and authoritative: the library only holds
  * compiled snapshots of them, so the fallback needs no state transfer.  The
  * compile helpers pack the lists in the vclassify.h layouts and keep the
- * list each index refers to, so a result maps back to the rule object of
- * the snapshot that produced it.
+ * list each index refers to.  A result maps back to the rule object of the
+ * snapshot that produced it because publishing is one critical section:
+ * compile* hold the write side of {@code snap} across the native compile
+ * and the list swap, and {@link #batch} holds the read side across a
+ * batch's native call and its index mapping (aclRule / route / group), so
+ * no recompile can land between the two.  Batches on different event-loop
+ * threads share the read side and never wait for each other.
  */
 public final class GpuContext {
     // include/vclassify.h struct sizes (tests/test_jni_shim.py checks them
@@ -63,6 +70,9 @@ public final class GpuContext {
     private volatile List<RouteTable.RouteRule> routesV4 = List.of();
     private volatile List<RouteTable.RouteRule> routesV6 = List.of();
     private volatile List<Upstream.ServerGroupHandle> handles = List.of();
+
+    // write: a compile + list swap; read: a batch's call + index mapping
+    private final ReentrantReadWriteLock snap = new ReentrantReadWriteLock();
 
     private GpuContext(long ctx, String name) {
         this.ctx = ctx;
@@ -113,9 +123,39 @@ public final class GpuContext {
         }
     }
 
+    /**
+     * One batch: the native call, then {@code map} with its outcome (true =
+     * the outputs are valid; false = answer the batch with the Java
+     * classifiers), both under the read side of the snapshot lock, so every
+     * aclRule / route / group lookup inside {@code map} sees the lists of
+     * the snapshot the call classified against.
+     */
+    public <T> T batch(Call c, Function<Boolean, T> map) {
+        snap.readLock().lock();
+        try {
+            return map.apply(call(c));
+        } finally {
+            snap.readLock().unlock();
+        }
+    }
+
     /** A control-plane call (compile, register): false when it failed and the context is not usable for it. */
     public boolean control(Call c) {
         return call(c);
+    }
+
+    /** A compile and the swap of the lists its indices refer to, as one publish (see the class comment). */
+    private boolean publish(Call compile, Runnable swap) {
+        snap.writeLock().lock();
+        try {
+            boolean ok = control(compile);
+            if (ok) {
+                swap.run();
+            }
+            return ok;
+        } finally {
+            snap.writeLock().unlock();
+        }
     }
 
     // ------------------------------------------------------------------
@@ -148,12 +188,10 @@ public final class GpuContext {
             (r.protocol == Protocol.TCP ? tcp : udp).add(r);
         }
         ByteBuffer t = packRules(tcp), u = packRules(udp);
-        boolean ok = control(c -> GpuClassifier.compileAcl(c, t, tcp.size(), u, udp.size(), sg.defaultAllow));
-        if (ok) {
+        return publish(c -> GpuClassifier.compileAcl(c, t, tcp.size(), u, udp.size(), sg.defaultAllow), () -> {
             tcpRules = tcp;
             udpRules = udp;
-        }
-        return ok;
+        });
     }
 
     private static ByteBuffer packRules(List<SecurityGroupRule> rules) {
@@ -175,12 +213,10 @@ public final class GpuContext {
             (r.rule.getIp() instanceof IPv4 ? v4 : v6).add(r);
         }
         ByteBuffer a = packNets(v4), b = packNets(v6);
-        boolean ok = control(c -> GpuClassifier.compileRoutes(c, a, v4.size(), b, v6.size()));
-        if (ok) {
+        return publish(c -> GpuClassifier.compileRoutes(c, a, v4.size(), b, v6.size()), () -> {
             routesV4 = v4;
             routesV6 = v6;
-        }
-        return ok;
+        });
     }
 
     private static ByteBuffer packNets(List<RouteTable.RouteRule> rules) {
@@ -201,11 +237,16 @@ public final class GpuContext {
             putAnnos(g, h.group.getAnnotations(), strings);
         }
         ByteBuffer s = strings.toDirect();
-        boolean ok = control(c -> GpuClassifier.compileUpstream(c, g, hs.size(), s));
-        if (ok) {
-            handles = hs;
-        }
-        return ok;
+        return publish(c -> GpuClassifier.compileUpstream(c, g, hs.size(), s), () -> handles = hs);
+    }
+
+    /**
+     * The hosts map -> compileHostsText (Resolver.getHosts' text); a hosts
+     * value is the index of the file's valid line, so {@code swap} installs
+     * the caller's line -> IP list of the same text under the same publish.
+     */
+    public boolean compileHostsText(ByteBuffer text, int len, Runnable swap) {
+        return publish(c -> GpuClassifier.compileHostsText(c, text, len), swap);
     }
 
     /** vc_annos with string slots as offsets into `strings` (-1 = null). */
@@ -229,7 +270,8 @@ public final class GpuContext {
     }
 
     // ------------------------------------------------------------------
-    // results -> the Java objects of the compiled snapshot
+    // results -> the Java objects of the compiled snapshot (call these
+    // inside batch(): the read side pins the lists to the call's snapshot)
     // ------------------------------------------------------------------
     public SecurityGroupRule aclRule(Protocol p, int idx) {
         return idx < 0 ? null : (p == Protocol.TCP ? tcpRules : udpRules).get(idx);

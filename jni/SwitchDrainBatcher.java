@@ -71,8 +71,10 @@ public final class SwitchDrainBatcher {
     private final int cap = ClassifierConfig.batch;
     private final ByteBuffer recv = ByteBuffer.allocate(MAX_DATAGRAM);
 
-    // the bare datagrams of the batch (SoA, registered once: zero-copy calls)
-    private final ByteBuffer blob = GpuContext.direct((long) cap * 256);
+    // the bare datagrams of the batch (SoA, registered once: zero-copy calls);
+    // the blob holds at least one largest datagram, so every pass of the
+    // drain loop receives one whatever -Dclassifier_batch says
+    private final ByteBuffer blob = GpuContext.direct(Math.max((long) cap * 256, MAX_DATAGRAM));
     private final ByteBuffer off = GpuContext.direct(4L * (cap + 1));
     private final ByteBuffer family = GpuContext.direct(cap);
     private final ByteBuffer remote4 = GpuContext.direct(4L * cap);
@@ -161,8 +163,20 @@ public final class SwitchDrainBatcher {
 
     private void dispatch(SelectorEventLoop loop, int n, int nb) {
         final int m = nb;
-        boolean ok = m == 0 || gpu.call(c -> GpuClassifier.switchClassify(c, blob, off, m, LAYER_VXLAN, family,
-            remote4, remote6, host.bindPort(), pktOut, outAcl, outAllow, outRoute));
+        if (m == 0) {
+            act(loop, n, true);
+            return;
+        }
+        // route indices resolve against the snapshot that produced them: a
+        // recompile waits for this batch (GpuContext.batch)
+        gpu.batch(c -> GpuClassifier.switchClassify(c, blob, off, m, LAYER_VXLAN, family,
+            remote4, remote6, host.bindPort(), pktOut, outAcl, outAllow, outRoute), ok -> {
+            act(loop, n, ok);
+            return null;
+        });
+    }
+
+    private void act(SelectorEventLoop loop, int n, boolean ok) {
         for (int i = 0; i < n; ++i) {
             String uuid = host.newHandlingUUID();
             if (decrypted[i] != null) {

@@ -480,17 +480,22 @@ static void parallel_for(int64_t n, int nthreads, range_fn fn, void *ctx)
         fn(ctx, 0, n);
         return;
     }
-    if (nthreads > 256) nthreads = 256;
-    pthread_t th[256];
-    range_job jobs[256];
+    if (nthreads > 1024) nthreads = 1024;
+    if (nthreads > n) nthreads = (int)n;
+    pthread_t th[1024];
+    range_job jobs[1024];
+    int started[1024];
     for (int t = 0; t < nthreads; ++t) {
         jobs[t].fn = fn;
         jobs[t].ctx = ctx;
         jobs[t].lo = n * t / nthreads;
         jobs[t].hi = n * (t + 1) / nthreads;
-        pthread_create(&th[t], NULL, range_thread, &jobs[t]);
+        /* a thread the system refuses runs its range here instead */
+        started[t] = pthread_create(&th[t], NULL, range_thread, &jobs[t]) == 0;
+        if (!started[t]) fn(ctx, jobs[t].lo, jobs[t].hi);
     }
-    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; ++t)
+        if (started[t]) pthread_join(th[t], NULL);
 }
 
 typedef struct {

@@ -35,6 +35,10 @@ kernels or the table compiler.
   any "."-suffix of it (host.endsWith("." + annoHost)), level 1 = "*"; the
   strict ">" of searchForGroup makes the answer the earliest group of the
   best level.
+- DnsChecker: DNSServer.handleRequest's classification (DNSServer.java:
+  116-166) -- a dict restatement of Resolver.getHosts' dual-key map
+  (Resolver.java:62-153), then HintChecker on the dot-stripped name, then
+  the IP-literal / .vproxy.local / recursive tail.
 """
 import re
 
@@ -321,3 +325,84 @@ class HintChecker:
         for i in range(len(out)):
             out[i] = self(blob[off[i]:off[i + 1]], 0 if ports is None else int(ports[i]))
         return out
+
+
+# ---------------------------------------------------------------------------
+# DNSServer.handleRequest classification
+# ---------------------------------------------------------------------------
+DNS_HOSTS, DNS_GROUP, DNS_IP_LITERAL, DNS_INTERNAL, DNS_RECURSIVE = 1, 2, 3, 4, 5   # VC_DNS_*
+
+
+def hosts_map(text, is_ip):
+    """Resolver.getHosts (Resolver.java:62-153) restated with Python's str
+    and dict: per line (\\n, \\r or \\r\\n), cut at the first '#', skip blank
+    lines, split on ' ' / '\\t' and drop empty tokens; the first token must
+    be an IP literal (`is_ip`: IP.parseIpString != null), and the line's
+    entry index counts the lines that pass.  Each name d1 adds d1 and its
+    dot-twin d2 (trailing '.' removed or added) unless either is already a
+    key -- the first line naming a host wins (:130-141).  Returns {name bytes: entry index}."""
+    if isinstance(text, bytes):
+        text = text.decode("latin-1")
+    ret, entry = {}, 0
+    for line in re.split(r"\r\n|\r|\n", text):
+        if "#" in line:
+            line = line[:line.index("#")]
+        if not line.strip(" \t\n\x0b\f\r\x1c\x1d\x1e\x1f"):    # String.isBlank (ASCII)
+            continue
+        toks = [s.strip("".join(chr(c) for c in range(33))) for s in re.split(r"[ \t]", line)]
+        toks = [s for s in toks if s]
+        if len(toks) < 2 or not is_ip(toks[0].encode("latin-1")):
+            continue
+        for d1 in toks[1:]:
+            d2 = d1[:-1] if d1.endswith(".") else d1 + "."
+            k1, k2 = d1.encode("latin-1"), d2.encode("latin-1")
+            if k1 in ret or k2 in ret:
+                continue
+            ret[k1] = entry
+            ret[k2] = entry
+        entry += 1
+    return ret
+
+
+class DnsChecker:
+    """DNSServer.handleRequest's classification of one A/AAAA/SRV qname
+    (DNSServer.java:116-166): the hosts map on the raw qname (trailing dot
+    included; both key forms, Resolver.java:130-141), else strip one
+    trailing dot and Upstream.searchForGroup(Hint.ofHost(domain)) through
+    HintChecker, else IP.isIpLiteral -> the literal's family, else
+    `.vproxy.local` -> internal, else recursive.  `is_ip`: the IP-literal
+    predicate (IP.java:112-300) -- the oracle's strict parser, consulted only
+    for the few names no hosts entry and no group took; `fallback(name)`
+    answers the rare names HintChecker does not cover (two or more ':')."""
+
+    def __init__(self, hosts_text, groups, is_ip, fallback=None):
+        self.is_ip = is_ip
+        self.hosts = hosts_map(hosts_text, is_ip) if hosts_text else {}
+        self.hint = HintChecker(groups)
+        self.fallback = fallback
+
+    def __call__(self, q):
+        assert max(q, default=0) < 0x80, "checker covers ASCII qnames"
+        v = self.hosts.get(q)
+        if v is not None:
+            return DNS_HOSTS, v
+        d = q[:-1] if q.endswith(b".") else q
+        if d.count(b":") > 1:
+            return self.fallback(q)
+        g = self.hint(d)
+        if g >= 0:
+            return DNS_GROUP, g
+        if self.is_ip(d):
+            return DNS_IP_LITERAL, 6 if b":" in d else 4
+        if d.endswith(b".vproxy.local"):
+            return DNS_INTERNAL, 0
+        return DNS_RECURSIVE, 0
+
+    def batch(self, blob, off):
+        blob = bytes(np.asarray(blob, np.uint8))
+        off = np.asarray(off, np.int64)
+        kind = np.empty(len(off) - 1, np.uint8)
+        val = np.empty(len(off) - 1, np.int32)
+        for i in range(len(kind)):
+            kind[i], val[i] = self(blob[off[i]:off[i + 1]])
+        return kind, val

@@ -169,3 +169,55 @@ def test_hint_dict_vs_oracle_edge_cases():
     blob, off = W.pack(keep)
     np.testing.assert_array_equal(chk.batch(blob, off), O.hint_batch_np(og, blob, off, None,
                                                                         nthreads=THREADS))
+
+
+def _dns_oracle_fallback(oh, og):
+    return lambda q: O.dns_classify(oh, og, q)
+
+
+def test_hosts_map_vs_oracle_parser():
+    """exact.hosts_map (dict restatement of Resolver.getHosts) equals the
+    oracle's parser on comments, CRLF, tabs, invalid IPs, dot-twins and
+    first-occurrence-wins lines, and on the kats.json hosts texts."""
+    import json
+    import os
+    from exact import hosts_map
+    texts = [("# comment\n127.0.0.1 localhost localhost.localdomain\n"
+              "10.0.0.1\tdb.example.com. db # trailing\n"
+              "bad line\n::1 localhost ip6-localhost\r\n\n10.0.0.2 db\n"
+              "300.1.1.1 nope.example\n  \t\n10.1.1.1   spaced.example\t\ttab.example.\r"
+              "fe80::1%eth0 scoped.example\n10.2.2.2 db. fresh.example # x\n01.2.3.4 lead.zero\n")]
+    with open(os.path.join(os.path.dirname(__file__), "golden", "kats.json")) as f:
+        texts += [c["text"] for c in json.load(f)["hosts_text"]]
+    for text in texts:
+        pairs, _ = O.hosts_parse(text)
+        want = {}
+        for k, v in pairs:
+            want.setdefault(k.encode(), v)
+        assert hosts_map(text, O.is_ip_literal) == want
+
+
+def test_dns_checker_vs_oracle():
+    """DnsChecker against vo_dns_classify on the DNS-flavoured C4 names
+    (trailing dots), hosts keys in both forms, IP literals, .vproxy.local
+    names and misses, with and without a "*" group."""
+    from exact import DnsChecker
+    groups, ghosts = W.gen_groups(2000, 31, port_frac=0.1)
+    hosts = "\n".join("10.0.%d.%d h%d.hosts.local%s" % (i >> 8 & 255, i & 255, i,
+                                                         "." if i % 3 == 0 else "")
+                      for i in range(3000)) + "\n# c\n::1 six.hosts.local\n"
+    names = W.gen_hostnames(ghosts, 20000, 32, dns=True, port_frac=0)
+    names += [b"h%d.hosts.local" % i for i in range(0, 3000, 7)]
+    names += [b"h%d.hosts.local." % i for i in range(1, 3000, 7)]
+    names += [b"1.2.3.4", b"1.2.3.4.", b"::1", b"::1.", b"[::1]", b"2001:db8::1.",
+              b"a.vproxy.local.", b"vproxy.local", b"x.vproxy.local", b"six.hosts.local.",
+              b"01.2.3.4.", b"", b".", b"..", b"miss.nowhere.", b"www.x:80", b"1.2.3.256."]
+    for gs in (groups, [g for g in groups if g[1].get("host") != "*"]):
+        oh, og = O.Hosts(O.hosts_parse(hosts)[0]), O.Groups(gs)
+        chk = DnsChecker(hosts, gs, O.is_ip_literal, _dns_oracle_fallback(oh, og))
+        blob, off = W.pack(names)
+        kind, val = chk.batch(blob, off)
+        wk, wv = O.dns_batch_np(oh, og, blob, off, nthreads=THREADS)
+        np.testing.assert_array_equal(kind, wk)
+        np.testing.assert_array_equal(val, wv)
+        assert len(set(wk.tolist())) >= (2 if gs is groups else 4)

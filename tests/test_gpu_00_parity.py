@@ -12,7 +12,7 @@ import pytest
 
 import oracle_ffi as O
 import vproxy_amd as V
-from exact import AclChecker, RouteChecker
+from exact import AclChecker, HintChecker, RouteChecker
 from vproxy_amd import workloads as W
 from vproxy_amd.classifier import group_array, pack_strings
 
@@ -448,8 +448,9 @@ def test_dns_deferred_queries_over_slot_reuse(clf):
 
 
 def test_hint_c4_scale(clf):
-    """C4: 100k hint-host groups vs 1M hostnames (16M in the bench);
-    oracle-checked sample (each oracle query scans all 100k groups)."""
+    """C4: 100k hint-host groups (5 % with a hint-port) vs 1M hostnames with
+    hint ports on 20 %: every result equal to exact.HintChecker, plus an
+    oracle sample (each oracle query scans all 100k groups)."""
     groups, ghosts = W.gen_groups(100000, W.SEED + 5)
     clf.compile_upstream(groups)
     names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, pool=1 << 18)
@@ -463,11 +464,15 @@ def test_hint_c4_scale(clf):
     exp = np.bincount(np.where(got >= 0, got, len(groups)), minlength=len(groups) + 1)
     np.testing.assert_array_equal(cg, exp.astype(np.uint64))
     clf.counters_enable(False)
+    # every name, hint-port filter included (Hint.java:124-128): exact.HintChecker
+    blob, off = W.pack(names)
+    np.testing.assert_array_equal(got, HintChecker(groups).batch(blob, off, ports))
     og = O.Groups(groups)
-    s = rng.integers(0, len(names), 1500)
+    s = rng.integers(0, len(names), 500)
     want = [O.search_for_group(og, names[i], int(ports[i]), None) for i in s]
     np.testing.assert_array_equal(got[s], np.array(want, np.int32))
     assert (got >= 0).mean() > 0.5
+    assert (ports > 0).mean() > 0.15
 
 
 def test_hint_shapes(clf):

@@ -30,7 +30,7 @@ import pytest
 import bench as B
 import oracle_ffi as O
 import vproxy_amd as V
-from exact import AclChecker, HintChecker, RouteChecker
+from exact import AclChecker, DnsChecker, HintChecker, RouteChecker
 from vproxy_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -198,6 +198,73 @@ def test_c5_pipeline_count_stream(c5):
     _check_batch(clf, t, dev, pk, outs, pool)
 
 
+def test_c5_timed_launch_exact(c5):
+    """The launch the headline times, at its size: bench.main's C5 schedule
+    (make_c5_steps with the default arguments: 125M packets per GPU, 3
+    batches in flight, fused counters with the finish on the counting
+    stream, the pool pass in order on the pipeline stream) run for 3 warmup
+    + 2 timed steps over rank 0's shard.  Every ACL, route and group output
+    of every in-flight buffer equal to the exact checkers
+    (SecurityGroup.java:30-45, RouteTable.java:44-59, Upstream.java:187-198),
+    every pool buffer equal to searchForGroup of all 16M names, and the
+    counters equal to 5 x the per-step histograms."""
+    import torch
+    clf, t, dev = c5
+    args = B.build_parser().parse_args([])
+    assert args.packets == 125_000_000 and args.inflight == 3 and args.counters == "fused"
+    lo, hi = B.shard(args.packets, 0, 1)
+    pk = B.gen_packets(lo, hi - lo, t, t.pool_n, dev=dev)
+    clf.counters_reset()
+    steps = B.make_c5_steps(clf, t, pk, dev, args, bucket=False)
+    nw, nk = 3, 2
+    steps.run(0, nw, False)
+    torch.cuda.synchronize()
+    steps.reset_events()
+    steps.run(nw, nk, True)
+    torch.cuda.synchronize()
+    assert steps.span("pipe") > 0
+    last = (nw + nk - 1) % steps.nbuf
+    acl, route, grp, _ = steps.outsb[last]
+    assert acl.shape[0] == 125_000_000
+    for pool in steps.pools:
+        assert torch.equal(pool, t.pool_want)
+    proto, src, dst, dport, hid = pk
+    assert torch.equal(grp, t.pool_want[hid.long()])
+    want_acl, _ = t.acl_chk.v4(proto, src, dport)
+    assert torch.equal(acl, want_acl), int((acl != want_acl).sum())
+    del want_acl
+    want_route = t.rt4_chk(dst)
+    assert torch.equal(route, want_route), int((route != want_route).sum())
+    del want_route
+    for b in range(steps.nbuf):                   # every buffer holds a full step
+        if b != last:
+            for x, y in zip(steps.outsb[b][:3], steps.outsb[last][:3]):
+                assert torch.equal(x, y)
+    steps_run = nw + nk
+    nt, nu = len(t.tcp), len(t.udp)
+    a = acl.long()
+    is_tcp = proto == 6
+    bins = torch.where(a >= 0, torch.where(is_tcp, a, nt + a),
+                       torch.where(is_tcp, nt + nu, nt + nu + 1))
+    exp = steps_run * torch.bincount(bins, minlength=nt + nu + 2)
+    del a, bins
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ACL),
+                                  exp.cpu().numpy().astype(np.uint64))
+    nn = t.n4 + t.n6
+    r = route.long()
+    exp = steps_run * torch.bincount(torch.where(r >= 0, r, nn), minlength=nn + 2)
+    del r
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE),
+                                  exp.cpu().numpy().astype(np.uint64))
+    ng = len(t.groups)
+    g = grp.long()
+    exp = steps_run * torch.bincount(torch.where(g >= 0, g, ng), minlength=ng + 1)
+    np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP),
+                                  exp.cpu().numpy().astype(np.uint64))
+    del steps, pk
+    torch.cuda.empty_cache()
+
+
 def test_mix_bench_batch_vs_oracle(c5):
     """The `mix` sub-bench exactly as bench.py runs it: 16M packets of
     bench.gen_mixed (15 % IPv6: IPv4-mapped and 2001:db8:: sources, 90 % of
@@ -269,18 +336,24 @@ def test_generator_device_equals_host(c5):
         assert torch.equal(x.cpu(), y)
 
 
+def _dns_checker(text, groups):
+    oh = O.Hosts(O.hosts_parse(text)[0])
+    og = O.Groups(groups)
+    return DnsChecker(text, groups, O.is_ip_literal, lambda q: O.dns_classify(oh, og, q)), oh, og
+
+
 def test_dns_c4_scale():
     """DNSServer classification at C4 scale: 100k groups + 50k hosts-file
-    names (the bench's DNS workload), oracle sample + group counters."""
+    names (the bench's DNS workload, with hosts keys in both forms and IPv4
+    literals mixed in): every one of the 1M results equal to DnsChecker
+    (DNSServer.java:116-166 over Resolver.java:130-141's dual-key map), an
+    oracle sample beside it, and exact group counters."""
     import torch
     clf = V.Classifier(0)
     try:
-        groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+        groups, text, names, _ = B.c4_workload(True, 0)
         clf.compile_upstream(groups)
-        text = "\n".join("10.0.%d.%d h%d.hosts.local" % (i >> 8 & 255, i & 255, i)
-                         for i in range(50_000))
         clf.compile_hosts_text(text)
-        names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6, dns=True, port_frac=0)
         names[::50] = [b"h%d.hosts.local." % i for i in range(0, len(names[::50]))]
         names[7::97] = [b"h%d.hosts.local" % i for i in range(0, len(names[7::97]))]
         names[3::211] = [b"1.2.3.%d." % (i & 255) for i in range(len(names[3::211]))]
@@ -293,13 +366,16 @@ def test_dns_c4_scale():
         torch.cuda.synchronize()
         clf.counters_enable(False)
         kind, val = kind.cpu().numpy(), val.cpu().numpy()
-        oh = O.Hosts(O.hosts_parse(text)[0])
-        og = O.Groups(groups)
-        s = np.random.default_rng(4).integers(0, len(names), 1200)
+        chk, oh, og = _dns_checker(text, groups)
+        wk, wv = chk.batch(blob, off)
+        np.testing.assert_array_equal(kind, wk)
+        np.testing.assert_array_equal(val, wv)
+        s = np.random.default_rng(4).integers(0, len(names), 300)
         want = [O.dns_classify(oh, og, names[i]) for i in s]
         assert [(int(kind[i]), int(val[i])) for i in s] == want
         # the "*" group (W.gen_groups) takes every name the hosts map does not
         assert {int(k) for k in np.unique(kind)} == {V.DNS_HOSTS, V.DNS_GROUP}
+        assert (kind == V.DNS_HOSTS).sum() >= len(names[::50]) + len(names[7::97])
         g = val[kind == V.DNS_GROUP]
         exp = np.bincount(g, minlength=len(groups) + 1).astype(np.uint64)
         np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp)
@@ -307,28 +383,80 @@ def test_dns_c4_scale():
         clf.close()
 
 
+def test_dns_bench_batch():
+    """The `dns` sub-bench's batch exactly as bench.py builds it
+    (bench.c4_workload: 16M seeded draws from 1M DNS-flavoured names, 100k
+    groups, 50k hosts lines) through vc_dns_classify_dev: every one of the
+    16M (kind, value) pairs equal to DnsChecker."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        n = 16 << 20
+        groups, text, names, pidx = B.c4_workload(True, n)
+        clf.compile_upstream(groups)
+        clf.compile_hosts_text(text)
+        nblob, noff = W.pack(names)
+        blob, off, _ = B.gather_strings_dev(nblob, noff, pidx, "cuda")
+        kind, val = clf.dns_classify((blob, off))
+        torch.cuda.synchronize()
+        wk, wv = _dns_checker(text, groups)[0].batch(nblob, noff)
+        pi = torch.from_numpy(pidx).cuda()
+        wk = torch.from_numpy(wk).cuda()[pi]
+        wv = torch.from_numpy(wv).cuda()[pi]
+        assert kind.shape[0] == n
+        assert torch.equal(kind, wk), int((kind != wk).sum())
+        assert torch.equal(val, wv), int((val != wv).sum())
+    finally:
+        clf.close()
+
+
 def test_dnsd_bench_workload():
     """The `dnsd` sub-bench exactly as bench.py builds it (bench.dnsd_tables /
     dnsd_batch: 10k-rule SecurityGroup, 100k groups, 50k hosts, 4M of its
-    datagrams from random IPv4 senders): every status, rule and question
-    result of an oracle sample (DNSServer drain loop, vo_dnsd_batch), and
-    whole-batch properties -- every allowed datagram answered, the rejected
-    ones exactly the senders the UDP list denies."""
+    datagrams from random IPv4 senders).  Every datagram: the UDP rule and
+    verdict of the sender (exact.AclChecker, SecurityGroup.java:30-45 with
+    DNSServer.java:469's source port), the status, the question count, and
+    the answered question's type, kind and value (DnsChecker over the
+    templates' qnames, DNSServer.java:116-166).  An oracle sample of the
+    whole drain loop (vo_dnsd_batch) beside it."""
     import torch
     clf = V.Classifier(0)
     try:
         t = B.dnsd_tables(clf)
         n = 4 << 20
         blob, off, nbytes, r4, rport, pidx = B.dnsd_batch(t, n, "cuda")
-        res = {k: v.cpu().numpy() for k, v in clf.dns_datagrams(
-            (blob, off), r4, rport).items()}
-        res["qtype"] = res["qtype"].view(np.uint16)
+        res = clf.dns_datagrams((blob, off), r4, rport)
         torch.cuda.synchronize()
+        dev = torch.device("cuda", 0)
+        # every datagram against the exact checkers
+        proto = torch.full((n,), 17, dtype=torch.uint8, device=dev)
+        want_acl, want_allow = AclChecker(t.tcp, t.udp, True, dev).v4(proto, r4, rport)
+        assert torch.equal(res["acl"], want_acl), int((res["acl"] != want_acl).sum())
+        qb, qo = W.pack(t.qnames)
+        qk, qv = _dns_checker(t.hosts, t.groups)[0].batch(qb, qo)
+        pi = torch.from_numpy(pidx).to(dev)
+        qk = torch.from_numpy(qk).to(dev)[pi]
+        qv = torch.from_numpy(qv).to(dev)[pi]
+        qt = torch.from_numpy(t.qtypes.astype(np.int64)).to(dev)[pi]
+        ok = want_allow == 1
+        full = lambda v: torch.full((n,), v, dtype=torch.uint8, device=dev)
+        want_status = torch.where(~ok, full(V.DNSD_REJECTED),
+                                  torch.where(qk == V.DNS_RECURSIVE, full(V.DNSD_RECURSIVE),
+                                              full(V.DNSD_ANSWER)))
+        assert torch.equal(res["status"], want_status), int((res["status"] != want_status).sum())
+        assert torch.equal(res["nq"], ok.to(torch.uint8))
+        assert torch.equal(res["qtype"][:, 0][ok].long() & 0xFFFF, qt[ok])
+        assert torch.equal(res["kind"][:, 0][ok], qk[ok])
+        assert torch.equal(res["value"][:, 0][ok], qv[ok])
+        assert 0 < int((~ok).sum()) < n
+        # oracle sample of the drain loop
+        res = {k: v.cpu().numpy() for k, v in res.items()}
+        res["qtype"] = res["qtype"].view(np.uint16)
         h4 = r4.cpu().numpy().view(np.uint32)
         hp = rport.cpu().numpy().view(np.uint16)
         og = O.Groups(t.groups)
         oh = O.Hosts(O.hosts_parse(t.hosts)[0])
-        s = np.sort(np.random.default_rng(5).choice(n, 3000, replace=False))
+        s = np.sort(np.random.default_rng(5).choice(n, 1500, replace=False))
         sb, so = W.pack([bytes(t.dblob[t.doff[j]:t.doff[j + 1]]) for j in pidx[s]])
         want = O.dnsd_batch_np(t.tcp, t.udp, True, oh, og, sb, so, None, h4[s], None, hp[s],
                                nthreads=16)
@@ -339,17 +467,6 @@ def test_dnsd_bench_workload():
         for k in ("qtype", "kind", "value"):
             np.testing.assert_array_equal(res[k][s, 0][live].astype(want[k].dtype),
                                           want[k][live, 0], err_msg=k)
-        # whole batch: answered or rejected, one question, and the rule equal
-        # to the ACL kernel's (LDS-staged boundaries, not the bucket
-        # directory) over all 4M senders, rejected iff that rule denies
-        st = res["status"]
-        assert set(np.unique(st)) <= {V.DNSD_ANSWER, V.DNSD_REJECTED}
-        assert np.all(res["nq"][st == V.DNSD_ANSWER] == 1)
-        proto = torch.full((n,), 17, dtype=torch.uint8, device="cuda")
-        idx, allow = clf.acl_v4(proto, r4, rport)
-        np.testing.assert_array_equal(res["acl"], idx.cpu().numpy())
-        np.testing.assert_array_equal(st == V.DNSD_REJECTED, allow.cpu().numpy() == 0)
-        assert 0 < (st == V.DNSD_REJECTED).sum() < n
     finally:
         clf.close()
 

@@ -330,6 +330,21 @@ def _ptr(x):
     return C.c_void_p(x.ctypes.data)
 
 
+def _rows16(x, what):
+    """Row count of an IPv6 address array: [m, 16] bytes, or flat bytes of a
+    length divisible by 16 (m = len / 16).  Anything else is refused before
+    a kernel is handed a row count its buffer does not hold."""
+    shape = tuple(x.shape)
+    itemsize = x.element_size() if hasattr(x, "element_size") else x.itemsize
+    if itemsize != 1:
+        raise IllegalArgumentException("%s: uint8 bytes expected" % what)
+    if len(shape) == 2 and shape[1] == 16:
+        return shape[0]
+    if len(shape) == 1 and shape[0] % 16 == 0:
+        return shape[0] // 16
+    raise IllegalArgumentException("%s: shape %s is not rows of 16 bytes" % (what, shape))
+
+
 def _stream():
     import torch
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -582,6 +597,20 @@ class Classifier:
         row per IPv6 packet in packet order.  Returns (acl, route, group, allow)."""
         n = len(proto)
         dev = _is_dev(proto)
+        n6 = 0
+        if src6 is not None or dst6 is not None:
+            if src6 is None or dst6 is None:
+                raise IllegalArgumentException("src6 and dst6 come together")
+            n6 = _rows16(src6, "src6")
+            if _rows16(dst6, "dst6") != n6:
+                raise IllegalArgumentException("src6 has %d rows, dst6 %d" % (n6, _rows16(dst6, "dst6")))
+            if not compact6 and n6 != n:
+                raise IllegalArgumentException("src6/dst6: %d rows for %d packets (one row per "
+                                               "packet without compact6)" % (n6, n))
+            if compact6 and n6 > n:
+                raise IllegalArgumentException("compact6: %d IPv6 rows for %d packets" % (n6, n))
+        elif compact6 and family is not None:
+            raise IllegalArgumentException("compact6 needs src6 / dst6 rows")
         if dev:
             import torch
             mk = lambda dt: torch.empty(n, dtype=dt, device=proto.device)
@@ -606,7 +635,7 @@ class Classifier:
                                   (_ptr(a), _ptr(r), _ptr(g), _ptr(al))])
         n_pool = len(pool_group) if pool_group is not None else 0
         if dev and compact6:
-            check(lib().vc_pipeline_c6_dev(self.h, C.byref(pk), n, len(src6), _ptr(pool_group),
+            check(lib().vc_pipeline_c6_dev(self.h, C.byref(pk), n, n6, _ptr(pool_group),
                                            n_pool, C.byref(po), _stream(),
                                            C.c_void_p(count_stream.cuda_stream)
                                            if count_stream is not None else None,
@@ -620,7 +649,7 @@ class Classifier:
                                         C.c_void_p(kernel_done_event)
                                         if kernel_done_event else None))
         elif compact6:
-            check(lib().vc_pipeline_c6(self.h, C.byref(pk), n, len(src6), _ptr(pool_group),
+            check(lib().vc_pipeline_c6(self.h, C.byref(pk), n, n6, _ptr(pool_group),
                                        n_pool, C.byref(po)))
         else:
             check(lib().vc_pipeline(self.h, C.byref(pk), n, _ptr(pool_group), n_pool,

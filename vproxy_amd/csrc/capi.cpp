@@ -1958,6 +1958,16 @@ int vc_pipeline_c6(vc_ctx* ctx, const vc_packets* in, int64_t n, int64_t n6,
     if (n == 0) return VC_OK;
     if (!in->family || n6 < 0 || n6 > n)
         return fail(VC_EINVAL, "compact IPv6 rows need the family array and 0 <= n6 <= n rows");
+    // One rule for both host paths (zero-copy and staged), checked before any
+    // output is written: n6 is the number of IPv6 packets.  A vectorised
+    // byte count over the host family array, small beside the batch's PCIe
+    // traffic.
+    int64_t six = 0;
+    const uint8_t* fam = in->family;
+    for (int64_t i = 0; i < n; ++i) six += fam[i] == 6;
+    if (six != n6)
+        return fail(VC_EINVAL, "the family array has " + std::to_string(six) +
+                                   " IPv6 packets but n6 = " + std::to_string(n6) + " rows");
     return pipeline_host(ctx, in, n, n6, pool_group, n_pool, out);
 }
 
