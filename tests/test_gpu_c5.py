@@ -375,7 +375,8 @@ def test_dns_c4_scale():
         assert [(int(kind[i]), int(val[i])) for i in s] == want
         # the "*" group (W.gen_groups) takes every name the hosts map does not
         assert {int(k) for k in np.unique(kind)} == {V.DNS_HOSTS, V.DNS_GROUP}
-        assert (kind == V.DNS_HOSTS).sum() >= len(names[::50]) + len(names[7::97])
+        assert (kind == V.DNS_HOSTS).sum() == sum(1 for q in names if q.endswith(
+            (b".hosts.local", b".hosts.local.")))
         g = val[kind == V.DNS_GROUP]
         exp = np.bincount(g, minlength=len(groups) + 1).astype(np.uint64)
         np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_GROUP), exp)
