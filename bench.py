@@ -531,11 +531,17 @@ def cpu_info():
     except AttributeError:
         avail = os.cpu_count() or 1
     quota = cgroup_cpu_max()
-    # every core this process may run on (all host cores);
-    # a cgroup quota below that is recorded, not used to shrink the pool
+    # all host cores this process may use: the affinity
+    # set, or the cgroup CPU quota when that is smaller -- threads past the
+    # quota only take turns (on the GPU box 256 threads under a 16-CPU quota
+    # ran the C5 sample at half the 16-thread rate).  The affinity-wide rate
+    # is reported beside it (cpu_rates: `affinity_all`).
+    share = avail
+    if quota[1]:
+        share = max(1, min(avail, int(quota[1])))
     return {"nproc": os.cpu_count(), "affinity": avail, "cpu_model": model,
             "cgroup_cpu_max": quota[0], "quota_cpus": quota[1],
-            "threads_all": max(1, avail)}
+            "threads_all": share}
 
 
 def cgroup_cpu_max(path="/sys/fs/cgroup/cpu.max"):
@@ -561,7 +567,10 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
     at most `cap` items (the sample the caller holds)."""
     info = cpu_info()
     res = {}
-    for threads in (info["threads_all"], 1):
+    legs = [info["threads_all"], 1]
+    if info["affinity"] > info["threads_all"]:
+        legs.append(info["affinity"])
+    for threads in legs:
         # grow the sample until it runs at least half the budget (a short
         # probe is dominated by thread start-up), or reaches the cap
         n = max(threads * 4, 64)
@@ -582,6 +591,10 @@ def cpu_rates(run, unit, budget_s, what, note=None, cap=None):
            "nproc": info["nproc"], "affinity": info["affinity"],
            "cgroup_cpu_max": info["cgroup_cpu_max"], "quota_cpus": info["quota_cpus"],
            "cpu_model": info["cpu_model"]}
+    if info["affinity"] > info["threads_all"]:
+        nx, tx = res[info["affinity"]]
+        out["affinity_all"] = {"value": nx / tx / 1e6, "cores": info["affinity"],
+                               "sample": "%d items in %.1f s" % (nx, tx)}
     if note:
         out["note"] = note
     return out

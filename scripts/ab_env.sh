@@ -24,7 +24,9 @@ print(json.dumps({"cfg": sys.argv[1], "round": int(sys.argv[2]),
                   "ms_per_step": d["ms_per_step"], "value": d["M_items_per_s"] if sub else d["value"],
                   "kernel_ms": d["kernel_ms"] if sub else d["roofline"].get("kernel_ms"),
                   "pipe_ms": o.get("pipeline_v4_kernel"),
-                  "hint_ms": o.get("hint_kernel"), "count_ms": o.get("kernel_end_to_counters_done")}))
+                  "hint_ms": o.get("hint_kernel"), "count_ms": o.get("kernel_end_to_counters_done"),
+                  "kernel_only_ms": d.get("kernel_only_ms"), "v4_ms": d.get("v4_ms"),
+                  "v6_ms": d.get("v6_ms"), "v4_same_ms": d.get("v4_kernel_same_packets_ms")}))
 PY
     tail -1 $OUT
   done

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-dispatch SQ issue counters of scripts/prof_sq_r03.sh, for the
+"""Per-dispatch SQ issue counters of scripts/prof.sh (PASSES=sq), for the
 dispatches of one kernel at its largest grid: instructions per wave, and the
 VALU issue share of the kernel's own cycles.  GRBM_GUI_ACTIVE is summed over
 the 8 XCDs (MI355X_MICROARCH.md), so cycles = GRBM_GUI_ACTIVE / 8; a CU

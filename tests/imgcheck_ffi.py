@@ -60,7 +60,9 @@ def route(rules, family, keys, root_bits=0):
     """root_bits 0: the library's default for the table size"""
     n = len(keys)
     out = np.empty(n, np.int32)
-    stats = np.zeros(3, np.int32)     # root bits, node units, one-prefix records
+    # root bits, node units, one-prefix records, IPv6 keys the wide root
+    # answers in one load (every IPv6 key is also checked through it: rc -201)
+    stats = np.zeros(4, np.int32)
     rc = lib().ic_route(P(rules), len(rules), family, P(keys), n, P(out), P(stats), root_bits)
     assert rc == 0, rc
     return out, stats

@@ -209,7 +209,9 @@ def test_route_one_prefix_records():
     records (images.h VC_ONE).  Edges: length 64 (the record limit) and 65
     (nodes), a covering shorter prefix listed before and after the long one
     (the record's match value is the min), slots with two long prefixes
-    (nodes), and queries one bit inside / outside each prefix."""
+    (nodes), and queries one bit inside / outside each prefix.  Every IPv6
+    key is also looked up through the wide root (images.h TrieImage.wide,
+    built per slot by route_dev.h wide_entry) and must get the same answer."""
     rng = np.random.default_rng(51)
     n = 1500
     plen = rng.choice(np.array([25, 30, 32, 40, 47, 48, 56, 63, 64, 65, 80]), n)
@@ -243,6 +245,9 @@ def test_route_one_prefix_records():
     got, stats = IC.route(big, 6, qb)
     np.testing.assert_array_equal(got, O.rt_batch_v6_np(big, qb, nthreads=4))
     assert stats[0] == 24 and stats[2] > 500, stats
+    # the IPv6 wide root (every key above also went through it, harness rc
+    # -201 otherwise) answers the one-prefix slots' keys in one load
+    assert stats[3] > len(qb) // 4, stats
     # IPv4 with a 16-bit root: /17-/32 prefixes alone in their slot
     p4 = rng.integers(17, 33, 2000)
     n4 = rng.integers(0, 2**32, 2000, dtype=np.uint64).astype(np.uint32) & W._mask32(p4)

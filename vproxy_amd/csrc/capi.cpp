@@ -905,6 +905,21 @@ int vc_compile_routes(vc_ctx* ctx, const vc_net* v4, int n4, const vc_net* v6, i
         s->img.fam[f].key_bits = tb[f]->key_bits;
         s->img.fam[f].n_rules = tb[f]->n_rules;
     }
+    // the IPv6 wide root (images.h TrieImage.wide), expanded on the device
+    // from the uploaded root and records; VC_ROUTE6_WIDE=0 leaves it out
+    static const bool wide6 = [] {
+        const char* w = std::getenv("VC_ROUTE6_WIDE");
+        return !(w && std::strcmp(w, "0") == 0);
+    }();
+    if (wide6 && n6 > 0) {
+        const size_t bytes = (size_t(1) << t6.root_bits) * 16;
+        auto* w = static_cast<uint32_t*>(up.dev(*s, bytes));
+        if (w && up.err == hipSuccess) {
+            up.L().busy = true;
+            up.err = vc::build_wide_root(s->img.fam[1].nodes, t6.root_bits, w, up.L().s);
+            s->img.fam[1].wide = w;
+        }
+    }
     s->n4 = n4;
     s->n6 = n6;
     s->digest = vc::digest(t4, t6);

@@ -75,11 +75,24 @@ struct AclImage {
 //                             entry's address range (VC_NONE if none).
 // "min list index" is RouteTable.lookup's first-match (list order), not LPM.
 // ---------------------------------------------------------------------------
+//
+// IPv6 wide root (`wide`, built on the device from the root at compile time,
+// route_dev.h wide_entry): 4 words per root slot, so the first access of a
+// walk answers a one-prefix slot by itself --
+//   a one-prefix record's subtree: the record, inline (its word 3 has
+//                             len << 24 with len > root_bits: nonzero)
+//   any other slot:           {root entry, 0, 0, 0}
+// IPv6 prefixes are /32-/64 on top of a 2^24 root, so without it a lookup
+// inside a prefix read the root entry and then the record: two dependent
+// misses.  The array is 16x the root's bytes, but only the slots under the
+// address ranges in use are ever read (2000::/3 is 1/8 of them).
 struct TrieImage {
     const uint32_t* nodes;
+    const uint32_t* wide;         // IPv6 only: 4 words per root slot, or null
     int32_t root_bits;
     int32_t key_bits;             // 32 (v4) or 128 (v6)
     int32_t n_rules;
+    int32_t pad_;
 };
 
 struct RouteImage {

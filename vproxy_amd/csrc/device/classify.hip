@@ -434,13 +434,26 @@ __global__ __launch_bounds__(kBlock) void route_v4_kernel_scalar(
         route_emit(trie_v4(nodes, rb, dst[i]), out + i);
 }
 
+// The IPv6 wide root (images.h TrieImage.wide) from the root and its
+// one-prefix records, one slot per thread, at compile time.
+__global__ __launch_bounds__(kBlock) void wide_root_kernel(const uint32_t* __restrict__ nodes,
+                                                           uint32_t slots,
+                                                           uint4* __restrict__ wide) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += stride) {
+        uint32_t w[4];
+        wide_entry(nodes, s, w);
+        wide[s] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 // 4 IPv6 lookups per lane: the trie walk is a chain of dependent gathers
 // (root, then one 8-bit stride per level down to /48 or /64), so four
 // independent walks advance level by level together to keep four gathers in
 // flight per lane.
 __global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
-    const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
-    int32_t* __restrict__ out) {
+    const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ wide, int rb,
+    const uint8_t* __restrict__ dst6, int64_t n, int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     const int64_t n4 = n >> 2;
     const uint32_t root = 1u << rb;
@@ -453,8 +466,14 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
             v6_key(reinterpret_cast<const uint4*>(dst6)[4 * g + k], &hi[k], &lo[k]);
             bits[k] = rb;
         }
+        if (wide) {                               // one load answers a one-prefix slot
 #pragma unroll
-        for (int k = 0; k < 4; ++k) e[k] = nodes[hi[k] >> (64 - rb)];
+            for (int k = 0; k < 4; ++k)
+                e[k] = wide_first(reinterpret_cast<const uint4*>(wide)[hi[k] >> (64 - rb)], hi[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) e[k] = nodes[hi[k] >> (64 - rb)];
+        }
         for (;;) {
             bool any = false;
 #pragma unroll
@@ -478,18 +497,18 @@ __global__ __launch_bounds__(kBlock) void route_v6_kernel_x4(
         const int64_t i = (n4 << 2) + threadIdx.x;
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(dst6)[i], &hi, &lo);
-        route_emit(trie_v6(nodes, rb, hi, lo), out + i);
+        route_emit(trie_v6w(nodes, wide, rb, hi, lo), out + i);
     }
 }
 
 __global__ __launch_bounds__(kBlock) void route_v6_kernel(
-    const uint32_t* __restrict__ nodes, int rb, const uint8_t* __restrict__ dst6, int64_t n,
-    int32_t* __restrict__ out) {
+    const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ wide, int rb,
+    const uint8_t* __restrict__ dst6, int64_t n, int32_t* __restrict__ out) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(dst6)[i], &hi, &lo);
-        route_emit(trie_v6(nodes, rb, hi, lo), out + i);
+        route_emit(trie_v6w(nodes, wide, rb, hi, lo), out + i);
     }
 }
 
@@ -540,6 +559,49 @@ __device__ __forceinline__ void stream_st(uint32_t* p, uint32_t v) {
     *p = v;
 #endif
 }
+// Random table gathers (route roots, pool results) of the mixed-family
+// kernels; with VC_GATHER_NT they carry the nontemporal hint, so the lines
+// they pull through L2 do not evict the small tables the IPv6 packets read
+// next (one-prefix records, ACL records).
+#ifndef VC_GATHER_NT
+#define VC_GATHER_NT 0
+#endif
+template <class T>
+__device__ __forceinline__ T gather_ld(const T* p) {
+#if VC_GATHER_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+// The compact-row kernel's SoA streams through stream_ld / stream_st too
+// (VC_C6_NT = 0: plain loads and stores, the round-4 form).
+#ifndef VC_C6_NT
+#define VC_C6_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T c6_ld(const T* p) {
+#if VC_C6_NT
+    return stream_ld(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void c6_st(int4* p, int4 v) {
+#if VC_C6_NT
+    stream_st(p, v);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void c6_st(uint32_t* p, uint32_t v) {
+#if VC_C6_NT
+    stream_st(p, v);
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ uint32_t route_chase(const uint32_t* nodes, int rb, uint32_t e,
                                                 uint32_t d) {
     int bits = rb;
@@ -818,7 +880,16 @@ struct PipeTries {
     const uint32_t* n4;
     const uint32_t* n6;
     int32_t rb4, rb6;
+    const uint32_t* w6;            // IPv6 wide root, or null
 };
+
+// First entry of an IPv6 packet's route walk: the wide root's answer for a
+// one-prefix slot (one gather), else the root entry.
+__device__ __forceinline__ uint32_t route6_first(const PipeTries& tr, uint64_t hh) {
+    if (tr.w6) return wide_first(gather_ld(reinterpret_cast<const uint4*>(tr.w6) +
+                                           (hh >> (64 - tr.rb6))), hh);
+    return gather_ld(tr.n6 + (hh >> (64 - tr.rb6)));
+}
 
 template <bool kLds, bool kCount>
 __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx& a,
@@ -838,7 +909,7 @@ __device__ __forceinline__ void pipe_mix_one(const AclImage& img, const AclV4Ctx
     if (v6) {
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.dst6)[i], &hi, &lo);
-        e = route6_chase(tr.n6, tr.rb6, tr.n6[hi >> (64 - tr.rb6)], hi, lo);
+        e = route6_chase(tr.n6, tr.rb6, route6_first(tr, hi), hi, lo);
         v = acl_v6_any<kLds>(a, a6, tcp, reinterpret_cast<const uint4*>(in.src6)[i], port);
     } else {
         const uint32_t d = in.dst4[i];
@@ -955,16 +1026,16 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         uint32_t d[4] = {0, 0, 0, 0}, sk[4] = {0, 0, 0, 0}, po[4] = {0, 0, 0, 0};
         if (full) {
             const int64_t q = i >> 2;
-            fm = reinterpret_cast<const uint32_t*>(in.family)[q];
-            pr = reinterpret_cast<const uint32_t*>(in.proto)[q];
-            const uint2 pt = reinterpret_cast<const uint2*>(in.dport)[q];
-            const uint4 d4 = reinterpret_cast<const uint4*>(in.dst4)[q];
-            const uint4 s4 = reinterpret_cast<const uint4*>(in.src4)[q];
+            fm = c6_ld(reinterpret_cast<const uint32_t*>(in.family) + q);
+            pr = c6_ld(reinterpret_cast<const uint32_t*>(in.proto) + q);
+            const uint2 pt = c6_ld(reinterpret_cast<const uint2*>(in.dport) + q);
+            const uint4 d4 = c6_ld(reinterpret_cast<const uint4*>(in.dst4) + q);
+            const uint4 s4 = c6_ld(reinterpret_cast<const uint4*>(in.src4) + q);
             d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
             sk[0] = s4.x; sk[1] = s4.y; sk[2] = s4.z; sk[3] = s4.w;
             po[0] = pt.x & 0xFFFFu; po[1] = pt.x >> 16; po[2] = pt.y & 0xFFFFu; po[3] = pt.y >> 16;
             if (in.host_id) {
-                const uint4 h4 = reinterpret_cast<const uint4*>(in.host_id)[q];
+                const uint4 h4 = c6_ld(reinterpret_cast<const uint4*>(in.host_id) + q);
                 hh4[0] = h4.x; hh4[1] = h4.y; hh4[2] = h4.z; hh4[3] = h4.w;
             }
 #pragma unroll
@@ -1011,16 +1082,16 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         if (lane < total && last >= 0) {
             const int64_t k6 = row + lane;
             const int64_t rw = k6 < last ? k6 : last;
-            dw0 = reinterpret_cast<const uint4*>(in.dst6)[rw];
-            sw0 = reinterpret_cast<const uint4*>(in.src6)[rw];
+            dw0 = c6_ld(reinterpret_cast<const uint4*>(in.dst6) + rw);
+            sw0 = c6_ld(reinterpret_cast<const uint4*>(in.src6) + rw);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            e[k] = ok[k] && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
+            e[k] = ok[k] && !v6[k] ? gather_ld(tr.n4 + (d[k] >> (32 - tr.rb4))) : 0u;   // root gathers
         if (in.host_id) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (ok[k]) grp[k] = int64_t(hh4[k]) < in.n_pool ? in.pool_group[hh4[k]] : -1;
+                if (ok[k]) grp[k] = int64_t(hh4[k]) < in.n_pool ? gather_ld(in.pool_group + hh4[k]) : -1;
         }
         int pos[4];
         int r = before;
@@ -1034,22 +1105,31 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         }
         if (total) {                                      // wave-uniform
             wave_sync();
-            const int64_t wbase = lo + 4 * gb;            // the step's first packet
+            const uint32_t pa = po[0] | po[1] << 16, pb = po[2] | po[3] << 16;
             for (int r0 = 0; r0 < total; r0 += 64) {
+                // the queued packet's protocol and port come from the lane
+                // that loaded them (three cross-lane reads), not from memory
+                const int qe = r0 + lane < total ? int(q6[r0 + lane]) : 0;
+                const int sl = qe >> 2, ks = qe & 3;
+                const uint32_t prs = __shfl(pr, sl, 64);
+                // every lane takes part in both reads (a lane outside a
+                // divergent read's mask supplies no data to it)
+                const uint32_t wa = __shfl(pa, sl, 64), wb = __shfl(pb, sl, 64);
+                const uint32_t pw = ks < 2 ? wa : wb;
                 if (r0 + lane < total) {
-                    const int64_t gi = wbase + q6[r0 + lane];
                     uint4 dw = dw0, sw = sw0;
                     if (r0 > 0 && last >= 0) {
                         const int64_t k6 = row + r0 + lane;
                         const int64_t rw = k6 < last ? k6 : last;
-                        dw = reinterpret_cast<const uint4*>(in.dst6)[rw];
-                        sw = reinterpret_cast<const uint4*>(in.src6)[rw];
+                        dw = c6_ld(reinterpret_cast<const uint4*>(in.dst6) + rw);
+                        sw = c6_ld(reinterpret_cast<const uint4*>(in.src6) + rw);
                     }
-                    const bool t6 = in.proto[gi] == VC_PROTO_TCP;
+                    const bool t6 = ((prs >> (8 * ks)) & 0xFFu) == VC_PROTO_TCP;
+                    const uint32_t port6 = (ks & 1) ? pw >> 16 : pw & 0xFFFFu;
                     uint64_t hh, ll;
                     v6_key(dw, &hh, &ll);
-                    const uint32_t root = tr.n6[hh >> (64 - tr.rb6)];
-                    const uint32_t vv = acl_v6_any<kLds>(a, a6, t6, sw, in.dport[gi]);
+                    const uint32_t root = route6_first(tr, hh);
+                    const uint32_t vv = acl_v6_any<kLds>(a, a6, t6, sw, port6);
                     r6[lane][1] = route6_chase(tr.n6, tr.rb6, root, hh, ll);
                     r6[lane][0] = vv;
                 }
@@ -1077,12 +1157,13 @@ __device__ __forceinline__ void pipe_mix_c6(const AclImage& img, const AclV4Ctx&
         }
         if (full) {
             const int64_t q = i >> 2;
-            reinterpret_cast<int4*>(out.acl)[q] = make_int4(oa[0], oa[1], oa[2], oa[3]);
-            reinterpret_cast<int4*>(out.route)[q] = make_int4(orr[0], orr[1], orr[2], orr[3]);
-            reinterpret_cast<int4*>(out.group)[q] = make_int4(grp[0], grp[1], grp[2], grp[3]);
+            c6_st(reinterpret_cast<int4*>(out.acl) + q, make_int4(oa[0], oa[1], oa[2], oa[3]));
+            c6_st(reinterpret_cast<int4*>(out.route) + q, make_int4(orr[0], orr[1], orr[2], orr[3]));
+            c6_st(reinterpret_cast<int4*>(out.group) + q, make_int4(grp[0], grp[1], grp[2], grp[3]));
             if (out.allow)
-                reinterpret_cast<uint32_t*>(out.allow)[q] = uint32_t(al[0]) | uint32_t(al[1]) << 8 |
-                                                             uint32_t(al[2]) << 16 | uint32_t(al[3]) << 24;
+                c6_st(reinterpret_cast<uint32_t*>(out.allow) + q,
+                      uint32_t(al[0]) | uint32_t(al[1]) << 8 | uint32_t(al[2]) << 16 |
+                          uint32_t(al[3]) << 24);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -1160,7 +1241,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
             for (int k = 0; k < 4; ++k) {
                 v6[k] = act && ((fm >> (8 * k)) & 0xFFu) == 6;
                 tcp[k] = ((pr >> (8 * k)) & 0xFFu) == VC_PROTO_TCP;
-                e[k] = act && !v6[k] ? tr.n4[d[k] >> (32 - tr.rb4)] : 0u;   // root gathers
+                e[k] = act && !v6[k] ? gather_ld(tr.n4 + (d[k] >> (32 - tr.rb4))) : 0u;   // root gathers
                 v[k] = VC_NONE;
             }
             if (act && in.host_id) {
@@ -1168,7 +1249,7 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
                 const uint32_t h[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    grp[k] = int64_t(h[k]) < in.n_pool ? in.pool_group[h[k]] : -1;
+                    grp[k] = int64_t(h[k]) < in.n_pool ? gather_ld(in.pool_group + h[k]) : -1;
             }
             // queue this wave's IPv6 packets (slot-major, then lane order)
             int pos[4];
@@ -1184,15 +1265,22 @@ __global__ __launch_bounds__(kPipeBlock) void pipeline_mix_kernel(AclImage img, 
                 wave_sync();
                 const int64_t wbase = lo + it * per_iter + 256 * int64_t(w);
                 for (int r0 = 0; r0 < total; r0 += 64) {
+                    // protocol and port from the lane that loaded them
+                    const int qe = r0 + lane < total ? int(q6[w][r0 + lane]) : 0;
+                    const int sl = qe >> 2, ks = qe & 3;
+                    const uint32_t prs = __shfl(pr, sl, 64);
+                    const uint32_t wa = __shfl(pt.x, sl, 64), wb = __shfl(pt.y, sl, 64);
+                    const uint32_t pw = ks < 2 ? wa : wb;
                     if (r0 + lane < total) {
-                        const int64_t gi = wbase + q6[w][r0 + lane];
-                        const bool t6 = in.proto[gi] == VC_PROTO_TCP;
+                        const int64_t gi = wbase + qe;
+                        const bool t6 = ((prs >> (8 * ks)) & 0xFFu) == VC_PROTO_TCP;
+                        const uint32_t port6 = (ks & 1) ? pw >> 16 : pw & 0xFFFFu;
                         uint64_t hh, ll;
                         v6_key(reinterpret_cast<const uint4*>(in.dst6)[gi], &hh, &ll);
-                        const uint32_t root = tr.n6[hh >> (64 - tr.rb6)];
+                        const uint32_t root = route6_first(tr, hh);
                         const uint32_t vv = acl_v6_any<kLds>(a, a6, t6,
                                                              reinterpret_cast<const uint4*>(in.src6)[gi],
-                                                             in.dport[gi]);
+                                                             port6);
                         r6[w][lane][1] = route6_chase(tr.n6, tr.rb6, root, hh, ll);
                         r6[w][lane][0] = vv;
                     }
@@ -1445,14 +1533,24 @@ hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t
     if (!aligned(dst6, 16)) return hipErrorInvalidValue;
     if (aligned(out, 16))
         hipLaunchKernelGGL(vcd::route_v6_kernel_x4, dim3(grid_for(c, (n + 3) / 4, 8)),
-                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.root_bits, dst6, n, out);
+                           dim3(vcd::kBlock), 0, c.stream, t.nodes, t.wide, t.root_bits, dst6, n,
+                           out);
     else
         hipLaunchKernelGGL(vcd::route_v6_kernel, dim3(grid_for(c, n, 8)), dim3(vcd::kBlock), 0,
-                           c.stream, t.nodes, t.root_bits, dst6, n, out);
+                           c.stream, t.nodes, t.wide, t.root_bits, dst6, n, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !counters) return e;
     return launch_hist(c, VC_HIST_PLAIN, out, nullptr, n, t.n_rules, rule_base, none_at, 0,
                        counters);
+}
+
+hipError_t build_wide_root(const uint32_t* nodes, int root_bits, uint32_t* wide,
+                           hipStream_t stream) {
+    const uint32_t slots = 1u << root_bits;
+    const uint32_t blocks = std::min<uint32_t>((slots + vcd::kBlock - 1) / vcd::kBlock, 4096u);
+    hipLaunchKernelGGL(vcd::wide_root_kernel, dim3(blocks), dim3(vcd::kBlock), 0, stream, nodes,
+                       slots, reinterpret_cast<uint4*>(wide));
+    return hipGetLastError();
 }
 
 hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteImage& route,
@@ -1590,7 +1688,7 @@ hipError_t launch_pipeline(const LaunchCfg& c, const AclImage& acl, const RouteI
             }
         } else {
             const vcd::PipeTries tr{route.fam[0].nodes, route.fam[1].nodes, route.fam[0].root_bits,
-                                    route.fam[1].root_bits};
+                                    route.fam[1].root_bits, route.fam[1].wide};
             const vcd::PipeIn in{p.family, p.proto, p.src4, p.dst4, p.src6, p.dst6,
                                  p.dport, p.host_id, p.pool_group, p.n_pool, base6, p.n6c};
             const vcd::PipeOut out{p.out_acl, p.out_route, p.out_group, p.out_allow};

@@ -159,6 +159,10 @@ hipError_t launch_route_v4(const LaunchCfg& c, const TrieImage& t, const uint32_
 hipError_t launch_route_v6(const LaunchCfg& c, const TrieImage& t, const uint8_t* dst6, int64_t n,
                            int32_t* out, unsigned long long* counters, int64_t rule_base,
                            int64_t none_at);
+// images.h TrieImage.wide from a device copy of the trie (root + records):
+// 4 words per root slot, on `stream`
+hipError_t build_wide_root(const uint32_t* nodes, int root_bits, uint32_t* wide,
+                           hipStream_t stream);
 hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* host_blob,
                        const uint32_t* host_off, const uint8_t* host_null, const uint16_t* port,
                        const uint8_t* uri_blob, const uint32_t* uri_off, const uint8_t* uri_null,

@@ -55,6 +55,42 @@ VC_HD uint32_t v6_sub(uint64_t hi, uint64_t lo, int bits, int s) {
     return bits < 64 ? uint32_t((hi >> (64 - bits - s)) & m) : uint32_t((lo >> (128 - bits - s)) & m);
 }
 
+// Wide-root entry of root slot s (images.h TrieImage.wide): the one-prefix
+// record inline, or {root entry, 0, 0, 0}.
+VC_HD void wide_entry(const uint32_t* nodes, uint32_t s, uint32_t out[4]) {
+    const uint32_t e = nodes[s];
+    if ((e & VC_PTR) && (e & VC_ONE)) {
+        const uint32_t* r = nodes + 4u * (e & ~(VC_PTR | VC_ONE));
+        out[0] = r[0]; out[1] = r[1]; out[2] = r[2]; out[3] = r[3];
+    } else {
+        out[0] = e; out[1] = 0u; out[2] = 0u; out[3] = 0u;
+    }
+}
+
+// First step of an IPv6 walk from a wide-root entry: the answer of a
+// one-prefix slot, else the root entry (a value or a node pointer).
+VC_HD uint32_t wide_first(uint4 w, uint64_t hi) {
+    return (w.w >> 24) ? one_match(w, hi) : w.x;
+}
+
+VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo);
+
+// trie_v6 through the wide root when the image has one (one load for a
+// one-prefix slot instead of two dependent ones).
+VC_HD uint32_t trie_v6w(const uint32_t* nodes, const uint32_t* wide, int rb, uint64_t hi,
+                        uint64_t lo) {
+    if (!wide) return trie_v6(nodes, rb, hi, lo);
+    uint32_t e = wide_first(reinterpret_cast<const uint4*>(wide)[hi >> (64 - rb)], hi);
+    int bits = rb;
+    const uint32_t root = 1u << rb;
+    while (e & VC_PTR) {
+        const int s = trie_stride(bits);
+        e = trie_next(nodes, root, e, v6_sub(hi, lo, bits, s), hi);
+        bits += s;
+    }
+    return e;
+}
+
 VC_HD uint32_t trie_v6(const uint32_t* nodes, int rb, uint64_t hi, uint64_t lo) {
     uint32_t e = nodes[hi >> (64 - rb)];
     int bits = rb;
