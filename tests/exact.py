@@ -35,6 +35,9 @@ kernels or the table compiler.
   any "."-suffix of it (host.endsWith("." + annoHost)), level 1 = "*"; the
   strict ">" of searchForGroup makes the answer the earliest group of the
   best level.
+- HintLevelChecker: searchForGroup with the whole matchLevel -- hint-uri
+  levels (prefix / equal / "*", UTF-16 length, cap 1023), port filter,
+  host levels -- visiting only the groups a host or uri dict lookup finds.
 - DnsChecker: DNSServer.handleRequest's classification (DNSServer.java:
   116-166) -- a dict restatement of Resolver.getHosts' dual-key map
   (Resolver.java:62-153), then HintChecker on the dot-stripped name, then
@@ -325,6 +328,139 @@ class HintChecker:
         for i in range(len(out)):
             out[i] = self(blob[off[i]:off[i + 1]], 0 if ports is None else int(ports[i]))
         return out
+
+
+# ---------------------------------------------------------------------------
+# Upstream.searchForGroup over full hints (host, port, uri)
+# ---------------------------------------------------------------------------
+def format_uri(u):
+    """Hint.formatUri (Hint.java:75-90): cut at the first '?', "/" stays,
+    else one trailing '/' goes."""
+    if u is None:
+        return None
+    q = u.find(b"?")
+    if q != -1:
+        u = u[:q]
+    if u == b"/":
+        return u
+    return u[:-1] if u.endswith(b"/") else u
+
+
+class HintLevelChecker:
+    """Upstream.searchForGroup (Upstream.java:187-198) with the whole of
+    Hint.matchLevel (Hint.java:100-160): level = hostLevel << 10 + uriLevel,
+    the port filter, strict '>' over the handle list.  Only groups that can
+    score above 0 are considered:
+    - host candidates, whose merged hint-host equals the formatted host, one
+      of its dot-suffixes or "*" (host dict): level computed exactly;
+    - uri candidates, whose merged hint-uri is the uri, a prefix of it or
+      "*" (uri dict, every prefix probed).  Scored as if hostLevel were 0,
+      all groups of one hint-uri share one level, so only the earliest one
+      the port filter lets through counts (precomputed per uri and port).
+      A group that also matches the host scores >= 1024 on the host side,
+      above any uri-only level (<= 1023), so the underestimate never wins.
+    Any other group scores 0.  ASCII strings (UTF-16 length = byte length).
+    `fallback(host, port, uri)` answers names with two or more ':'
+    (IP.isIpv6 in formatHost)."""
+
+    def __init__(self, groups, fallback=None):
+        self.fallback = fallback
+        self.g = []                 # merged (host, port, uri) per handle
+        self.by_host, self.by_uri = {}, {}
+        for i, (ha, ga) in enumerate(groups):
+            host, port, uri = None, 0, None
+            for a in (ha or {}, ga or {}):       # handle annotations first (Upstream.java:191)
+                h, u = _anno(a, "host"), _anno(a, "uri")
+                if host is None and h is not None:
+                    host = h.encode() if isinstance(h, str) else bytes(h)
+                if port == 0:
+                    port = _java_int(_anno(a, "port"))
+                if uri is None and u is not None:
+                    uri = u.encode() if isinstance(u, str) else bytes(u)
+            for x in (host, uri):
+                assert x is None or max(x, default=0) < 0x80, "checker covers ASCII annotations"
+            self.g.append((host, port, uri))
+            if host is not None:
+                self.by_host.setdefault(host, []).append(i)
+            if uri is not None:
+                # per hint-uri: (earliest handle with no hint-port, earliest
+                # handle per hint-port); indices ascend, so setdefault keeps
+                # the first
+                e = self.by_uri.setdefault(uri, [None, {}, i])     # [2]: earliest of all
+                if port == 0:
+                    if e[0] is None:
+                        e[0] = i
+                else:
+                    e[1].setdefault(port, i)
+
+    def level(self, i, host, port, uri):
+        """Hint.matchLevel of handle i (Hint.java:100-160)."""
+        H, P, U = self.g[i]
+        if H is None and P == 0 and U is None:
+            return 0
+        if port != 0 and P != 0 and port != P:
+            return 0
+        hl = 0
+        if H is not None and host is not None:
+            if host == H:
+                hl = 3
+            elif host.endswith(b"." + H):
+                hl = 2
+            elif H == b"*":
+                hl = 1
+        ul = 0
+        if U is not None and uri is not None:
+            if uri == U:
+                ul = len(uri) + 1
+            elif uri.startswith(U):
+                ul = len(U) + 1
+            elif U == b"*":
+                ul = 1
+        return (hl << 10) + min(ul, 1023)
+
+    def __call__(self, name, port=0, uri=None):
+        """Hint.ofHostPortUri(name, port, uri) (name / uri may be None)."""
+        if name is not None and name.count(b":") > 1:
+            return self.fallback(name, port, uri)
+        host = None if name is None else HintChecker.format_host(name)
+        uri = format_uri(uri)
+        best, lv = -1, 0
+
+        def take(i, l):
+            nonlocal best, lv
+            if l > lv or (l == lv and l > 0 and i < best):
+                best, lv = i, l
+
+        if host is not None:
+            cand = set(self.by_host.get(host, ()))
+            d = host.find(b".")
+            while d != -1:
+                cand.update(self.by_host.get(host[d + 1:], ()))
+                d = host.find(b".", d + 1)
+            cand.update(self.by_host.get(b"*", ()))
+            for i in cand:
+                take(i, self.level(i, host, port, uri))
+        if uri is not None:
+            keys = {uri[:k] for k in range(len(uri) + 1)} | {b"*"}
+            for U in keys:
+                e = self.by_uri.get(U)
+                if e is None:
+                    continue
+                if uri == U:
+                    ul = len(uri) + 1
+                elif uri.startswith(U):
+                    ul = len(U) + 1
+                else:                                   # U == "*"
+                    ul = 1
+                ul = min(ul, 1023)
+                p0, per, first = e
+                if port == 0:                           # every hint-port passes
+                    take(first, ul)
+                else:
+                    idx = [x for x in (p0, per.get(port)) if x is not None]
+                    if idx:
+                        take(min(idx), ul)
+        return best
 
 
 # ---------------------------------------------------------------------------

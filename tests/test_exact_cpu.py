@@ -221,3 +221,39 @@ def test_dns_checker_vs_oracle():
         np.testing.assert_array_equal(kind, wk)
         np.testing.assert_array_equal(val, wv)
         assert len(set(wk.tolist())) >= (2 if gs is groups else 4)
+
+
+def test_hint_level_checker_vs_oracle():
+    """HintLevelChecker (searchForGroup with hint-uri levels, the port filter
+    and every host level) against vo_search_for_group: the random edge-case
+    groups and queries of cases.hint_cases_random (overlapping hosts,
+    handle/group merging, ports, uris with '?', '/', '*', nulls), and the
+    generated C4 groups with hint-uris added."""
+    from exact import HintLevelChecker
+    rng = np.random.default_rng(71)
+    groups, _, queries = hint_cases_random(rng, 400, 20000)
+    og = O.Groups(groups)
+    fb = lambda h, p, u: O.search_for_group(og, h, p, u)
+    chk = HintLevelChecker(groups, fb)
+    enc = lambda x: None if x is None else x.encode()
+    for h, p, u in queries:
+        assert chk(enc(h), p, enc(u)) == O.search_for_group(og, h, p, u), (h, p, u)
+    # generated groups with uris (a quarter), uri-only groups, queries with paths
+    g2, hosts = W.gen_groups(3000, 72, port_frac=0.1)
+    paths = ["/", "/api", "/api/v1", "/api/v1/users", "/static", "/static/img/a.png", "*",
+             "/api/", "/x?y=1"]
+    for i in range(0, len(g2), 4):
+        g2[i][1]["uri"] = paths[i % len(paths)]
+    g2 += [({}, {"uri": p}) for p in paths]
+    names = W.gen_hostnames(hosts, 20000, 73, port_frac=0.2)
+    qp = rng.choice(np.array([0, 0, 80, 443]), len(names))
+    qu = [None if rng.random() < 0.2 else
+          paths[int(rng.integers(0, len(paths)))] + ("/" + str(int(rng.integers(0, 5)))
+                                                      if rng.random() < 0.5 else "")
+          for _ in names]
+    og2 = O.Groups(g2)
+    chk2 = HintLevelChecker(g2, lambda h, p, u: O.search_for_group(og2, h, p, u))
+    got = [chk2(n, int(p), enc(u)) for n, p, u in zip(names, qp, qu)]
+    want = [O.search_for_group(og2, n, int(p), u) for n, p, u in zip(names, qp, qu)]
+    assert got == want
+    assert len(set(want)) > 1000

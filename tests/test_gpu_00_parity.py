@@ -475,6 +475,42 @@ def test_hint_c4_scale(clf):
     assert (ports > 0).mean() > 0.15
 
 
+def test_hint_uri_levels_at_scale(clf):
+    """R9 at scale with hint-uris: 100k C4 groups, a fifth with a hint-uri
+    (paths, prefixes of each other, '*'), 200 uri-only groups, 5 % with a
+    hint-port; 500k hostnames with ports on 20 % and uris on 80 % (formatUri
+    cases: '?', trailing '/').  Every result equal to exact.HintLevelChecker
+    (the whole Hint.matchLevel, Hint.java:100-160, and searchForGroup's
+    strict '>', Upstream.java:187-198), plus an oracle sample."""
+    from exact import HintLevelChecker
+    groups, ghosts = W.gen_groups(100000, W.SEED + 5)
+    paths = ["/", "/api", "/api/v1", "/api/v1/users", "/api/v2", "/static", "/static/img",
+             "/static/img/a.png", "*", "/login", "/a/b/c/d/e/f"]
+    rng = np.random.default_rng(81)
+    for i in np.nonzero(rng.random(len(groups)) < 0.2)[0]:
+        groups[i][1]["uri"] = paths[int(rng.integers(0, len(paths)))]
+    groups += [({}, {"uri": paths[k % len(paths)] + ("/u%d" % k if k > len(paths) else "")})
+               for k in range(200)]
+    clf.compile_upstream(groups)
+    names = W.gen_hostnames(ghosts, 500_000, W.SEED + 6, pool=1 << 18)
+    ports = np.where(rng.random(len(names)) < 0.2, rng.integers(1, 65536, len(names)), 0)
+    ports = ports.astype(np.uint16)
+    tails = ["", "/", "/x", "?q=1", "/?q=2", "/users/7"]
+    uris = [None if rng.random() < 0.2 else
+            (paths[int(rng.integers(0, len(paths)))] + tails[int(rng.integers(0, len(tails)))])
+            for _ in range(len(names))]
+    got = clf.hint_search([n.decode() for n in names], ports, uris)
+    og = O.Groups(groups)
+    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    enc = lambda x: None if x is None else x.encode()
+    want = np.array([chk(n, int(p), enc(u)) for n, p, u in zip(names, ports, uris)], np.int32)
+    np.testing.assert_array_equal(got, want)
+    s = rng.integers(0, len(names), 300)
+    np.testing.assert_array_equal(got[s], [O.search_for_group(og, names[i], int(ports[i]), uris[i])
+                                           for i in s])
+    assert (got >= 0).mean() > 0.5 and len(np.unique(got)) > 10000
+
+
 def test_hint_shapes(clf):
     """Fast-path shapes (lengths mod 4, > 6 labels, waves whose names
     overflow the LDS stage, ':port' / 'www.' / IPv6 forms) vs the oracle,
