@@ -80,10 +80,10 @@ public final class DnsDrainBatcher {
     private final Host host;
     private final int cap = ClassifierConfig.batch;
 
-    // one batch, SoA, registered once so the calls run zero-copy; the blob
-    // holds at least one largest datagram, so fill() always makes progress
-    // whatever -Dclassifier_batch says
-    private final ByteBuffer blob = GpuContext.direct(Math.max((long) cap * 512, MAX_DATAGRAM));
+    // one batch, SoA, registered once so the calls run zero-copy; room for
+    // cap datagrams of 512 bytes plus one largest datagram, so fill() always
+    // makes progress whatever -Dclassifier_batch says
+    private final ByteBuffer blob = GpuContext.direct((long) cap * 512 + MAX_DATAGRAM);
     private final ByteBuffer off = GpuContext.direct(4L * (cap + 1));
     private final ByteBuffer family = GpuContext.direct(cap);
     private final ByteBuffer remote4 = GpuContext.direct(4L * cap);

@@ -72,9 +72,10 @@ public final class SwitchDrainBatcher {
     private final ByteBuffer recv = ByteBuffer.allocate(MAX_DATAGRAM);
 
     // the bare datagrams of the batch (SoA, registered once: zero-copy calls);
-    // the blob holds at least one largest datagram, so every pass of the
-    // drain loop receives one whatever -Dclassifier_batch says
-    private final ByteBuffer blob = GpuContext.direct(Math.max((long) cap * 256, MAX_DATAGRAM));
+    // room for cap datagrams of 256 bytes plus one largest datagram, so
+    // every pass of the drain loop receives at least one whatever
+    // -Dclassifier_batch says (tests/native/switch_loop.c replays this rule)
+    private final ByteBuffer blob = GpuContext.direct((long) cap * 256 + MAX_DATAGRAM);
     private final ByteBuffer off = GpuContext.direct(4L * (cap + 1));
     private final ByteBuffer family = GpuContext.direct(cap);
     private final ByteBuffer remote4 = GpuContext.direct(4L * cap);
