@@ -979,6 +979,18 @@ def c4_workload(dns, n=16 << 20):
     return groups, hosts_text() if dns else None, names, pidx
 
 
+def sni_workload(n=16 << 20):
+    """The `sni` sub-bench's inputs (also checked whole by
+    tests/test_gpu_certs.py): 100k certificate holders, each a plain name
+    and a "*." wildcard (200k names), 1M distinct SNIs from the C4 name
+    generator (ports cut), and the n seeded draws that form the batch."""
+    _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
+    holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]
+    names = [x.split(b":")[0] for x in W.gen_hostnames(hosts, 1 << 20, W.SEED + 10)]
+    pidx = np.random.default_rng(W.SEED + 11).integers(0, len(names), n)
+    return holders, names, pidx
+
+
 def dnsd_tables(clf, n_templates=1 << 20):
     """The `dnsd` workload's tables, compiled into clf: 100k hint-host
     groups, a 50k-line hosts file, a 10k-rule SecurityGroup (default allow);
@@ -1282,13 +1294,10 @@ def sub_bench(args, clf, dev, rank, world):
                             "SecurityGroup scan (10k rules) + parsePackets + hosts lookup and "
                             "searchForGroup scan over 100k groups", cap=n)
     elif args.workload == "sni":
-        _, hosts = W.gen_groups(200_000, W.SEED + 9, wildcard=False)
-        holders = [[hosts[i], "*." + hosts[i + 1]] for i in range(0, len(hosts), 2)]
-        clf.compile_certs(holders)
-        names = [x.split(b":")[0] for x in W.gen_hostnames(hosts, 1 << 20, W.SEED + 10)]
-        nblob, noff = W.pack(names)
         n = 16 << 20
-        pidx = np.random.default_rng(W.SEED + 11).integers(0, len(names), n)
+        holders, names, pidx = sni_workload(n)
+        clf.compile_certs(holders)
+        nblob, noff = W.pack(names)
         blob, off, nbytes = gather_strings_dev(nblob, noff, pidx, dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         fn = lambda: V.check(V.lib().vc_cert_choose_dev(

@@ -38,6 +38,9 @@ kernels or the table compiler.
 - HintLevelChecker: searchForGroup with the whole matchLevel -- hint-uri
   levels (prefix / equal / "*", UTF-16 length, cap 1023), port filter,
   host levels -- visiting only the groups a host or uri dict lookup finds.
+- CertChecker: SSLContextHolder.choose (SSLContextHolder.java:50-79,
+  171-186) -- a plain-name dict and a wildcard-suffix dict, since a "*.S"
+  name can only match an SNI through its suffix from the first dot.
 - DnsChecker: DNSServer.handleRequest's classification (DNSServer.java:
   116-166) -- a dict restatement of Resolver.getHosts' dual-key map
   (Resolver.java:62-153), then HintChecker on the dot-stripped name, then
@@ -542,3 +545,48 @@ class DnsChecker:
         for i in range(len(kind)):
             kind[i], val[i] = self(blob[off[i]:off[i + 1]])
         return kind, val
+
+
+# ---------------------------------------------------------------------------
+# SSLContextHolder.choose (SNI -> certificate holder)
+# ---------------------------------------------------------------------------
+class CertChecker:
+    """SSLContextHolder.choose(sni) (SSLContextHolder.java:50-79) with
+    compare (:171-186): one holder -> it; none -> null (-1); a null SNI or
+    no match -> the first holder; else the first holder (add() order) with
+    a name equal to the SNI, or a "*.S" name where the SNI ends with ".S"
+    and the rest before it is non-empty with no '.': that rest ends at the
+    SNI's first dot, so one dict probe on the SNI and one on its suffix
+    from the first dot cover every name."""
+
+    def __init__(self, holders):
+        self.n = len(holders)
+        self.plain, self.wild = {}, {}
+        for h, names in enumerate(holders):
+            for nm in names:
+                b = nm.encode() if isinstance(nm, str) else bytes(nm)
+                if b.startswith(b"*."):
+                    self.wild.setdefault(b[1:], h)        # ".S", first holder wins
+                else:
+                    self.plain.setdefault(b, h)
+
+    def __call__(self, sni):
+        if self.n == 1:
+            return 0
+        if self.n == 0:
+            return -1
+        if sni is None:
+            return 0
+        best = self.plain.get(sni, self.n)
+        d = sni.find(b".")
+        if d >= 1:
+            best = min(best, self.wild.get(sni[d:], self.n))
+        return best if best < self.n else 0
+
+    def batch(self, blob, off, null=None):
+        blob = bytes(np.asarray(blob, np.uint8))
+        off = np.asarray(off, np.int64)
+        out = np.empty(len(off) - 1, np.int32)
+        for i in range(len(out)):
+            out[i] = self(None if null is not None and null[i] else blob[off[i]:off[i + 1]])
+        return out

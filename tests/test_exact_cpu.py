@@ -257,3 +257,25 @@ def test_hint_level_checker_vs_oracle():
     want = [O.search_for_group(og2, n, int(p), u) for n, p, u in zip(names, qp, qu)]
     assert got == want
     assert len(set(want)) > 1000
+
+
+def test_cert_checker_vs_oracle():
+    """CertChecker against vo_cert_choose: generated holders with plain,
+    wildcard and shared names, SNIs that hit plain names, wildcard depths
+    (one extra label, two, none), empty labels and nulls; one- and
+    zero-holder tables."""
+    from exact import CertChecker
+    _, hosts = W.gen_groups(6000, 61, wildcard=False)
+    holders = [[hosts[i], "*." + hosts[i + 1], "shared%d.example" % (i % 37)]
+               for i in range(0, len(hosts), 2)]
+    holders += [["*.x.example", "a.x.example"], ["*.example", "*"], [""], ["*."]]
+    names = W.gen_hostnames(hosts, 20000, 62)
+    snis = [n.split(b":")[0] for n in names]
+    snis += [b"a." + h.encode() for h in hosts[1:400:2]] + [b"a.b." + h.encode() for h in hosts[1:200:2]]
+    snis += [b"x.example", b"q.x.example", b".x.example", b"a.example", b"", b".", b"*", b"*.",
+             b"shared3.example", b"a.shared3.example"]
+    for hs in (holders, holders[:1], []):
+        chk, oc = CertChecker(hs), O.Certs(hs)
+        got = [chk(s) for s in snis] + [chk(None)]
+        want = [oc.choose(s) for s in snis] + [oc.choose(None)]
+        assert got == want

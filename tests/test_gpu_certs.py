@@ -9,6 +9,7 @@ import pytest
 
 import oracle_ffi as O
 import vproxy_amd as V
+from vproxy_amd import workloads as W
 from test_certs_cpu import HOLDERS, VECTORS, _random_case
 
 pytestmark = pytest.mark.gpu
@@ -62,6 +63,31 @@ def test_large_table_device_paths(clf):
                                torch.from_numpy(nul).cuda()))
         torch.cuda.synchronize()
         np.testing.assert_array_equal(dev.cpu().numpy(), got)
+
+
+def test_sni_bench_batch(clf):
+    """The `sni` sub-bench's batch exactly as bench.py builds it
+    (bench.sni_workload: 100k holders = 200k names, 16M seeded draws from
+    1M SNIs) through vc_cert_choose_dev: every one of the 16M results equal
+    to exact.CertChecker (SSLContextHolder.choose, SSLContextHolder.java:
+    50-79,171-186), with an oracle sample."""
+    import torch
+    import bench as B
+    from exact import CertChecker
+    n = 16 << 20
+    holders, names, pidx = B.sni_workload(n)
+    clf.compile_certs(holders)
+    nblob, noff = W.pack(names)
+    blob, off, _ = B.gather_strings_dev(nblob, noff, pidx, "cuda")
+    got = clf.cert_choose((blob, off, None))
+    torch.cuda.synchronize()
+    want = torch.from_numpy(CertChecker(holders).batch(nblob, noff)).cuda()[
+        torch.from_numpy(pidx).cuda()]
+    assert torch.equal(got, want), int((got != want).sum())
+    c = O.Certs(holders)
+    s = np.random.default_rng(3).integers(0, n, 300)
+    np.testing.assert_array_equal(got.cpu().numpy()[s], [c.choose(names[pidx[i]]) for i in s])
+    assert (want > 0).float().mean() > 0.3
 
 
 def test_errors(clf):
