@@ -979,6 +979,45 @@ def c4_workload(dns, n=16 << 20):
     return groups, hosts_text() if dns else None, names, pidx
 
 
+def frames_workload(n=32 << 20):
+    """The frame sub-benches' inputs (`parse`, `switch`, `mirror`; also
+    checked whole by tests/test_gpu_frames_scale.py): 64K seeded VXLAN
+    frames and the n seeded draws from them that form the batch."""
+    frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
+    pidx = np.random.default_rng(W.SEED + 13).integers(0, len(frames), n)
+    return frames, pidx
+
+
+def switch_senders(n, dev):
+    """The `switch` sub-bench's datagram senders: n uniform IPv4 addresses."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(19)
+    return dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
+
+
+def compile_switch_acl(clf, t):
+    """The `switch` sub-bench's bareVXLanAccess: the C5 SecurityGroup with a
+    last UDP rule 0.0.0.0/0 port 4789 allow, so the senders no earlier rule
+    decides reach the parse's inner route (with defaultAllow false alone the
+    bench's uniform senders were nearly all denied).  Compiled into clf;
+    returns the (tcp, udp) lists."""
+    last = np.zeros(1, W.RULE_DT)
+    last["net"] = W.v4_nets(np.array([0], np.uint32), np.array([0]))
+    last["min_port"] = last["max_port"] = 4789
+    last["allow"] = 1
+    udp = np.concatenate([t.udp, last])
+    a, na, ka = W.as_ctypes(t.tcp, V._lib.VcAclRule)
+    b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+    V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
+    return t.tcp, udp
+
+
+# the `mirror` sub-bench's 17 filters (Mirror.switchPacket over the switch origin)
+MIRROR_FILTERS = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
+                   "network2": "10.0.0.0/8"} for i in range(16)] + \
+                 [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}]
+
+
 def sni_workload(n=16 << 20):
     """The `sni` sub-bench's inputs (also checked whole by
     tests/test_gpu_certs.py): 100k certificate holders, each a plain name
@@ -1315,10 +1354,9 @@ def sub_bench(args, clf, dev, rank, world):
             cpu = cpu_rates(run, "M items/s", 3.0, "SNIs of the workload, oracle "
                             "SSLContextHolder.choose scan over 100k holders (200k names)", cap=n)
     elif args.workload in ("parse", "mirror", "switch"):
-        frames = W.gen_vxlan_frames(1 << 16, W.SEED + 12)
-        fblob, foff = W.pack(frames)
         n = 32 << 20
-        pidx = np.random.default_rng(W.SEED + 13).integers(0, len(frames), n)
+        frames, pidx = frames_workload(n)
+        fblob, foff = W.pack(frames)
         blob, off, nbytes = gather_strings_dev(fblob, foff, pidx, dev)
         if args.workload == "parse":
             res = {k: torch.empty((n, w) if w > 1 else (n,), dtype={"u8": torch.uint8,
@@ -1344,9 +1382,8 @@ def sub_bench(args, clf, dev, rank, world):
             # over the C5 SecurityGroup and route tables; only the route
             # index and the verdict leave the kernel
             t = c5_tables(clf, dev, 1 << 20)
-            g = torch.Generator(device=dev)
-            g.manual_seed(19)
-            r4 = dev_u32(torch.randint(0, 2**32, (n,), generator=g, device=dev))
+            sw_tcp, sw_udp = compile_switch_acl(clf, t)
+            r4 = switch_senders(n, dev)
             out_route = torch.empty(n, dtype=torch.int32, device=dev)
             out_allow = torch.empty(n, dtype=torch.uint8, device=dev)
             none = V._lib.VcPktOut()
@@ -1356,7 +1393,8 @@ def sub_bench(args, clf, dev, rank, world):
                 C.c_void_p(out_allow.data_ptr()), C.c_void_p(out_route.data_ptr()), S()))
             per_unit = nbytes / n + 4 + 4 + 5
             unit = ("B/datagram (frame bytes + 4 offset + 4 sender in; 4 route + 1 verdict out), "
-                    "10k-rule SecurityGroup, 980,848 + 200,000 routes")
+                    "10k-rule SecurityGroup + a last allow rule for the VXLAN port, "
+                    "980,848 + 200,000 routes")
             kern = "switch_kernel"
             if O is not None:
                 r4h = r4[:1 << 20].cpu().numpy().view(np.uint32)
@@ -1364,16 +1402,14 @@ def sub_bench(args, clf, dev, rank, world):
                 def run(k, threads):
                     sb, so = sample_blob(fblob, foff, pidx[:k])
                     t0 = time.perf_counter()
-                    O.switch_batch_np(t.tcp, t.udp, False, sb, so, r4h[:k], 4789, t.v4_list,
+                    O.switch_batch_np(sw_tcp, sw_udp, False, sb, so, r4h[:k], 4789, t.v4_list,
                                       t.v6_list, nthreads=threads)
                     return time.perf_counter() - t0
                 cpu = cpu_rates(run, "M items/s", 4.0, "datagrams of the workload, oracle parse + "
                                 "SecurityGroup.allow scan + RouteTable.lookup scan of the inner "
                                 "destination", cap=1 << 20)
         else:
-            filters = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1),
-                        "network2": "10.0.0.0/8"} for i in range(16)] + \
-                      [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}]
+            filters = MIRROR_FILTERS
             mf = clf.compile_mirror(filters)
             out = torch.empty(n, dtype=torch.int64, device=dev)
             oid = mf.id_of("switch", create=False)

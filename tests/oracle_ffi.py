@@ -246,7 +246,10 @@ def sg_allow(tcp, udp, default_allow, proto, ip_bytes, port):
 
 
 def _ptr(a):
-    return C.c_void_p(a.ctypes.data) if a is not None else None
+    # data_as keeps a reference to the array in the pointer, so a converted
+    # temporary (e.g. _ptr(np.ascontiguousarray(x, np.uint32))) lives until
+    # the C call that takes the pointer returns
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
 def sg_allow_batch_v4(tcp, udp, default_allow, proto, src4, port, nthreads=1):
