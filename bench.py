@@ -1018,6 +1018,20 @@ MIRROR_FILTERS = [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" 
                  [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}]
 
 
+def source_workload(n, dev):
+    """The `source` sub-bench's inputs (also checked whole by
+    tests/test_gpu_source.py): 10k groups of 1-31 IPv4 servers (90 %
+    healthy), and n (group, client address) pairs generated on the device."""
+    rng = np.random.default_rng(W.SEED + 14)
+    groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
+               for _ in range(int(rng.integers(1, 32)))] for _ in range(10_000)]
+    g = torch.Generator(device=dev)
+    g.manual_seed(15)
+    grp = torch.randint(0, len(groups), (n,), generator=g, device=dev, dtype=torch.int32)
+    src = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, device=dev, dtype=torch.int32)
+    return groups, grp, src
+
+
 def sni_workload(n=16 << 20):
     """The `sni` sub-bench's inputs (also checked whole by
     tests/test_gpu_certs.py): 100k certificate holders, each a plain name
@@ -1432,15 +1446,9 @@ def sub_bench(args, clf, dev, rank, world):
                 cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle "
                                 "Mirror.switchPacket over the 17 filters", cap=1 << 22)
     elif args.workload == "source":
-        rng = np.random.default_rng(W.SEED + 14)
-        groups = [[(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1, rng.random() < 0.9)
-                   for _ in range(int(rng.integers(1, 32)))] for _ in range(10_000)]
-        clf.compile_servers(groups)
         n = 128 << 20
-        g = torch.Generator(device=dev)
-        g.manual_seed(15)
-        grp = torch.randint(0, len(groups), (n,), generator=g, device=dev, dtype=torch.int32)
-        src = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, device=dev, dtype=torch.int32)
+        groups, grp, src = source_workload(n, dev)
+        clf.compile_servers(groups)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         fn = lambda: V.check(V.lib().vc_source_select_v4_dev(
             clf.h, C.c_void_p(grp.data_ptr()), C.c_void_p(src.data_ptr()), n, 0,

@@ -41,6 +41,10 @@ kernels or the table compiler.
 - CertChecker: SSLContextHolder.choose (SSLContextHolder.java:50-79,
   171-186) -- a plain-name dict and a wildcard-suffix dict, since a "*.S"
   name can only match an SNI through its suffix from the first dot.
+- SourceChecker: ServerGroup's source hashing (ServerGroup.java:377-490,
+  620-664) as tensor arithmetic: the sdbm hash of the signed address bytes
+  per item, and per group a table of the first healthy list position at
+  or after each position (the probe), so an item is two gathers.
 - DnsChecker: DNSServer.handleRequest's classification (DNSServer.java:
   116-166) -- a dict restatement of Resolver.getHosts' dual-key map
   (Resolver.java:62-153), then HintChecker on the dot-stripped name, then
@@ -590,3 +594,65 @@ class CertChecker:
         for i in range(len(out)):
             out[i] = self(None if null is not None and null[i] else blob[off[i]:off[i + 1]])
         return out
+
+
+# ---------------------------------------------------------------------------
+# ServerGroup source hashing (method source)
+# ---------------------------------------------------------------------------
+def _signed_key(ip):
+    return tuple(b - 256 if b >= 128 else b for b in ip)
+
+
+class SourceChecker:
+    """ServerGroup.next(source) for method source over IPv4 clients
+    (ServerGroup.java:422-490): the group's sourceReset list (:620-664:
+    servers with weight > 0 of the view, sorted stably by address length,
+    then signed address bytes, then port), hash = Math.abs(sdbm of the
+    client's signed address bytes) (:387-397, Math.abs(MIN_VALUE) taken as
+    0 as the oracle does), idx = hash % size, then forward (wrapping) to the
+    first healthy server; none healthy -> null (-1).  Results are indices
+    into the group's own server list, as the library returns them.
+    groups: list of server lists [(ip bytes, port, weight, healthy)]."""
+
+    def __init__(self, groups, dev, view=0):
+        base, size, nxt = [], [], []
+        for g in groups:
+            keep = [i for i, (ip, port, w, h) in enumerate(g)
+                    if w > 0 and (view == 0 or (view == 4) == (len(ip) == 4))]
+            order = sorted(keep, key=lambda i: (len(g[i][0]), _signed_key(g[i][0]), g[i][1]))
+            base.append(len(nxt))
+            size.append(len(order))
+            for p in range(len(order)):       # first healthy position at or after p
+                r = -1
+                for q in range(len(order)):
+                    c = order[(p + q) % len(order)]
+                    if g[c][3]:
+                        r = c
+                        break
+                nxt.append(r)
+        T = lambda x: torch.tensor(x, dtype=torch.int64, device=dev)
+        self.base, self.size, self.nxt = T(base), T(size), T(nxt if nxt else [-1])
+        self.dev = dev
+
+    @staticmethod
+    def hash_v4(src):
+        """Math.abs(sdbm(bytes)) of uint32 v4 keys (int64 tensor), Java int math"""
+        x = _u32(src)
+        h = torch.zeros_like(x)
+        for sh in (24, 16, 8, 0):
+            b = (x >> sh) & 0xFF
+            b = torch.where(b >= 128, b - 256, b)
+            h = (b + (h << 6) + (h << 16) - h) & 0xFFFFFFFF
+        h = torch.where(h >= 2**31, h - 2**32, h)            # to Java int
+        return torch.where(h == -2**31, torch.zeros_like(h), h.abs())
+
+    def v4(self, grp, src):
+        outs = []
+        for s in range(0, len(grp), CHUNK):
+            g = _t(grp[s:s + CHUNK], self.dev).long()
+            h = self.hash_v4(_t(src[s:s + CHUNK], self.dev))
+            sz = self.size[g]
+            idx = self.base[g] + h % sz.clamp(min=1)
+            outs.append(torch.where(sz > 0, self.nxt[idx.clamp(max=len(self.nxt) - 1)],
+                                    torch.full_like(g, -1)).to(torch.int32))
+        return torch.cat(outs)

@@ -279,3 +279,30 @@ def test_cert_checker_vs_oracle():
         got = [chk(s) for s in snis] + [chk(None)]
         want = [oc.choose(s) for s in snis] + [oc.choose(None)]
         assert got == want
+
+
+def test_source_checker_vs_oracle():
+    """SourceChecker against vo_source_batch: groups of 0-31 servers with
+    duplicate addresses (the stable sort), zero weights, IPv6 servers in the
+    all-view, unhealthy runs (the forward probe) and all-unhealthy groups;
+    clients with high-bit bytes (signed sdbm), 0 and 255.255.255.255."""
+    from exact import SourceChecker
+    rng = np.random.default_rng(83)
+    groups = []
+    for k in range(600):
+        g = []
+        for _ in range(int(rng.integers(0, 32))):
+            ip = bytes(rng.integers(0, 256, 4 if rng.random() < 0.9 else 16).astype(np.uint8))
+            if g and rng.random() < 0.1:
+                ip = g[int(rng.integers(0, len(g)))][0]           # duplicate address
+            g.append((ip, int(rng.choice([80, 443, 8080])), int(rng.random() < 0.9),
+                      bool(rng.random() < (0.0 if k % 50 == 0 else 0.7))))
+        groups.append(g)
+    n = 200_000
+    grp = rng.integers(0, len(groups), n).astype(np.int32)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    src[:4] = [0, 0xFFFFFFFF, 0x80000000, 0x7F000001]
+    got = SourceChecker(groups, CPU).v4(grp, src).numpy()
+    want = O.source_batch_np(groups, 0, grp, src, nthreads=THREADS)
+    np.testing.assert_array_equal(got, want)
+    assert (want >= 0).mean() > 0.5 and (want < 0).any()

@@ -99,3 +99,27 @@ def test_source_errors(clf):
         clf.set_server_health(np.ones(2, np.uint8))
     with pytest.raises(V.IllegalArgumentException):
         clf.source_select(np.zeros(1, np.int32), np.zeros(1, np.uint32), view=5)
+
+
+def test_source_bench_batch(clf):
+    """The `source` sub-bench's batch exactly as bench.py builds it
+    (bench.source_workload: 10k groups, 128M device-generated clients)
+    through vc_source_select_v4_dev: every one of the 128M results equal to
+    exact.SourceChecker (ServerGroup.java:377-490,620-664), plus an oracle
+    sample."""
+    import torch
+    import bench as B
+    from exact import SourceChecker
+    dev = torch.device("cuda", 0)
+    n = 128 << 20
+    groups, grp, src = B.source_workload(n, dev)
+    clf.compile_servers(groups)
+    got = clf.source_select(grp, src)
+    torch.cuda.synchronize()
+    want = SourceChecker(groups, dev).v4(grp, src)
+    assert torch.equal(got, want), int((got != want).sum())
+    s = np.random.default_rng(5).integers(0, n, 20000)
+    gh, sh = grp.cpu().numpy()[s], src.cpu().numpy()[s].view(np.uint32)
+    np.testing.assert_array_equal(got.cpu().numpy()[s], O.source_batch_np(groups, 0, gh, sh,
+                                                                           nthreads=16))
+    assert float((got >= 0).float().mean()) > 0.9
