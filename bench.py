@@ -1032,6 +1032,34 @@ def source_workload(n, dev):
     return groups, grp, src
 
 
+def c3_workload(clf, dev, n=256 << 20, rank=0):
+    """The `c3` sub-bench (also checked whole by tests/test_gpu_c5.py): the
+    ~1M IPv4 + 200k IPv6 BGP-like prefixes through the RouteTable mirror,
+    shortest first, compiled into clf; n lookups, 85 % IPv4 (90 % inside a
+    prefix, generated on the device) and 15 % IPv6 (host-generated)."""
+    c = types.SimpleNamespace()
+    c.net, c.plen = W.gen_v4_prefixes(1_000_000, W.SEED + 3)
+    c.hi, c.lo, c.p6 = W.gen_v6_prefixes(200_000, W.SEED + 4)
+    c.rt = V.RouteTable()
+    allnets = np.concatenate([W.v4_nets(c.net, c.plen), W.v6_nets(c.hi, c.lo, c.p6)])
+    arr, n_all, keep = W.as_ctypes(allnets, V._lib.VcNet)
+    c.rt.add_rules("bgp", arr, n=n_all)
+    clf.compile_route_table(c.rt)
+    c.n4 = int(n * 0.85)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7 + rank)
+    netd = torch.from_numpy(c.net.astype(np.int64)).to(dev)
+    mkd = torch.from_numpy(W._mask32(c.plen).astype(np.int64)).to(dev)
+    r = torch.randint(0, len(c.net), (c.n4,), generator=g, device=dev)
+    q = torch.randint(0, 2**32, (c.n4,), generator=g, device=dev)
+    c.q4 = dev_u32(torch.where(torch.rand(c.n4, generator=g, device=dev) < 0.9,
+                               netd[r] | (q & (~mkd[r] & 0xFFFFFFFF)), q))
+    del r, q
+    c.q6h = W.v6_lookups(c.hi, c.lo, c.p6, n - c.n4, 8 + rank)
+    c.q6 = torch.from_numpy(c.q6h).to(dev)
+    return c
+
+
 def sni_workload(n=16 << 20):
     """The `sni` sub-bench's inputs (also checked whole by
     tests/test_gpu_certs.py): 100k certificate holders, each a plain name
@@ -1185,26 +1213,10 @@ def sub_bench(args, clf, dev, rank, world):
                 cpu = cpu_rates(run, "M items/s", 4.0, "first tuples of the C2 batch, oracle "
                                 "first-match scan over 10k rules")
     elif args.workload == "c3":
-        net, plen = W.gen_v4_prefixes(1_000_000, W.SEED + 3)
-        hi, lo, p6 = W.gen_v6_prefixes(200_000, W.SEED + 4)
-        rt = V.RouteTable()
-        allnets = np.concatenate([W.v4_nets(net, plen), W.v6_nets(hi, lo, p6)])
-        arr, n_all, keep = W.as_ctypes(allnets, V._lib.VcNet)
-        rt.add_rules("bgp", arr, n=n_all)
-        clf.compile_route_table(rt)
         n = 256 << 20
-        n4 = int(n * 0.85)
-        g = torch.Generator(device=dev)
-        g.manual_seed(7 + rank)
-        netd = torch.from_numpy(net.astype(np.int64)).to(dev)
-        mkd = torch.from_numpy(W._mask32(plen).astype(np.int64)).to(dev)
-        r = torch.randint(0, len(net), (n4,), generator=g, device=dev)
-        q = torch.randint(0, 2**32, (n4,), generator=g, device=dev)
-        q4 = dev_u32(torch.where(torch.rand(n4, generator=g, device=dev) < 0.9,
-                                 netd[r] | (q & (~mkd[r] & 0xFFFFFFFF)), q))
-        del r, q
-        q6h = W.v6_lookups(hi, lo, p6, n - n4, 8 + rank)
-        q6 = torch.from_numpy(q6h).to(dev)
+        c3 = c3_workload(clf, dev, n, rank)
+        rt, net, plen, hi, lo, p6 = c3.rt, c3.net, c3.plen, c3.hi, c3.lo, c3.p6
+        q4, q6h, q6, n4 = c3.q4, c3.q6h, c3.q6, c3.n4
         o4 = torch.empty(n4, dtype=torch.int32, device=dev)
         o6 = torch.empty(n - n4, dtype=torch.int32, device=dev)
         fn = lambda: (clf.route_v4(q4, out=o4), clf.route_v6(q6, out=o6))

@@ -266,7 +266,7 @@ def test_c5_timed_launch_exact(c5):
 
 
 def test_mix_bench_batch_vs_oracle(c5):
-    """The `mix` sub-bench exactly as bench.py runs it: 16M packets of
+    """The `mix` sub-bench exactly as bench.py runs it: 125M packets of
     bench.gen_mixed (15 % IPv6: IPv4-mapped and 2001:db8:: sources, 90 % of
     destinations inside a rulesV6 prefix) through vc_pipeline_dev on the C5
     tables, counter finish on a second stream.  Every ACL / verdict / route
@@ -276,7 +276,7 @@ def test_mix_bench_batch_vs_oracle(c5):
     import torch
     clf, t, dev = c5
     pool = clf.hint_search((t.pool_blob, t.pool_off, None))
-    n = 16 << 20
+    n = B.build_parser().parse_args([]).packets          # the bench's 125M
     fam, proto, src, dst, src6, dst6, dport, hid = B.gen_mixed(0, n, t, t.pool_n, dev=dev)
     s_cnt = torch.cuda.Stream()
     torch.cuda.synchronize()
@@ -305,7 +305,7 @@ def test_mix_bench_batch_vs_oracle(c5):
     acl_h, route_h, allow_h = h(acl), h(route), h(allow)
     proto_h, dport_h = h(proto), h(dport).view(np.uint16)
     for is6, k in ((False, 8000), (True, 3000)):
-        s = rng.choice(np.nonzero(six == is6)[0], k, replace=False)
+        s = rng.choice(np.nonzero(six == is6)[0], k)              # with replacement: O(k)
         if is6:
             want, wv = O.sg_batch_v6_np(t.tcp, t.udp, False, proto_h[s], h(src6)[s], dport_h[s],
                                         nthreads=THREADS)
@@ -324,6 +324,45 @@ def test_mix_bench_batch_vs_oracle(c5):
                        torch.where(fam == 6, nn + 1, nn))
     exp = torch.bincount(bins, minlength=nn + 2).cpu().numpy().astype(np.uint64)
     np.testing.assert_array_equal(clf.counters_read(V.COUNTERS_ROUTE), exp)
+    del bins, rr
+    # the `mix --compact6` form of the same batch (vc_pipeline_c6_dev): the
+    # same outputs with the IPv6 addresses as one row per IPv6 packet
+    six = fam == 6
+    s6, d6 = src6[six].contiguous(), dst6[six].contiguous()
+    c = clf.pipeline(proto, src, dst, dport, hid, pool, family=fam, src6=s6, dst6=d6,
+                     want_allow=True, compact6=True)
+    torch.cuda.synchronize()
+    for x, y, name in zip(c, (acl, route, grp, allow), ("acl", "route", "group", "allow")):
+        assert torch.equal(x, y), name
+
+
+def test_c3_bench_batch():
+    """The `c3` sub-bench exactly as bench.py builds it (bench.c3_workload:
+    980,848 + 200,000 prefixes shortest-first, 256M lookups, 85 % IPv4):
+    every one of the 217.6M IPv4 and 38.4M IPv6 results equal to
+    exact.RouteChecker (RouteTable.java:44-59), the IPv6 ones through the
+    wide root."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        dev = torch.device("cuda", 0)
+        c = B.c3_workload(clf, dev)
+        o4 = clf.route_v4(c.q4)
+        o6 = clf.route_v6(c.q6)
+        torch.cuda.synchronize()
+        a4, k4 = c.rt.rules_raw(4)
+        a6, k6 = c.rt.rules_raw(6)
+        v4 = np.frombuffer(bytes(a4)[:k4 * 40], W.NET_DT)
+        v6 = np.frombuffer(bytes(a6)[:k6 * 40], W.NET_DT)
+        w4 = RouteChecker(v4, 4, dev)(c.q4)
+        assert torch.equal(o4, w4), int((o4 != w4).sum())
+        del w4
+        w6 = RouteChecker(v6, 6, dev)(c.q6)
+        assert torch.equal(o6, w6), int((o6 != w6).sum())
+        assert len(c.q4) + len(c.q6) == 256 << 20
+        assert float((o6 >= 0).float().mean()) > 0.85
+    finally:
+        clf.close()
 
 
 def test_generator_device_equals_host(c5):
