@@ -452,7 +452,7 @@ def test_dns_bench_batch():
 
 def test_dnsd_bench_workload():
     """The `dnsd` sub-bench exactly as bench.py builds it (bench.dnsd_tables /
-    dnsd_batch: 10k-rule SecurityGroup, 100k groups, 50k hosts, 4M of its
+    dnsd_batch: 10k-rule SecurityGroup, 100k groups, 50k hosts, its 16M
     datagrams from random IPv4 senders).  Every datagram: the UDP rule and
     verdict of the sender (exact.AclChecker, SecurityGroup.java:30-45 with
     DNSServer.java:469's source port), the status, the question count, and
@@ -463,7 +463,7 @@ def test_dnsd_bench_workload():
     clf = V.Classifier(0)
     try:
         t = B.dnsd_tables(clf)
-        n = 4 << 20
+        n = 16 << 20                                   # the bench's batch
         blob, off, nbytes, r4, rport, pidx = B.dnsd_batch(t, n, "cuda")
         res = clf.dns_datagrams((blob, off), r4, rport)
         torch.cuda.synchronize()
