@@ -115,3 +115,34 @@ def test_switch_bench_batch(frames):
         assert int((route >= 0).sum()) > N // 10
     finally:
         clf.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 4097, 100_003, 800_001, 2_000_003])
+def test_frames_ragged_sizes(frames, n):
+    """The frame kernels' chunk schedule (chunks.h) at the chunk and pair
+    edges and across the work-ticket regimes: the first n frames of the
+    bench batch through parse and mirror, every result equal to its frame's
+    oracle-checked template result."""
+    import torch
+    fr, pidx, tmpl, batch, pi = frames
+    clf = V.Classifier(0)
+    try:
+        t = clf.parse_packets(tmpl, V.LAYER_VXLAN)
+        clf.compile_mirror(B.MIRROR_FILTERS)
+        tm = clf.mirror_switch("switch", tmpl)
+        torch.cuda.synchronize()
+        sub = (batch[0], batch[1][:n + 1])
+        res = clf.parse_packets(sub, V.LAYER_VXLAN)
+        m = clf.mirror_switch("switch", sub)
+        torch.cuda.synchronize()
+        for k, v in res.items():
+            assert torch.equal(v, t[k][pi[:n]]), (k, n)
+        assert torch.equal(m, tm[pi[:n]]), n
+        if n <= 129:                                 # and the oracle on each frame
+            uns = {np.dtype(np.int16): np.uint16, np.dtype(np.int32): np.uint32}
+            rh = {k: (lambda a: a.view(uns.get(a.dtype, a.dtype)))(v.cpu().numpy())
+                  for k, v in res.items()}
+            for i in range(n):
+                assert _rows(rh, i) == O.parse_packet(fr[pidx[i]], V.LAYER_VXLAN), (n, i)
+    finally:
+        clf.close()
