@@ -44,6 +44,7 @@ from vproxy_amd.dist import HitCounterBucket, check_replicated, shard  # noqa: E
 
 METRIC = "M classifications/sec (ACL+LPM+host) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+HBM_ACHIEVABLE_GBS = 6290.0    # the same table: a float4 copy kernel, measured (79 % of spec)
 PROFILES = os.path.join(ROOT, "profiles")
 PACKET_SEED = 1234
 
@@ -505,6 +506,29 @@ def resolve_world(gpus, environ=None, shared=False, device_count=None):
     return "launch", gpus
 
 
+def copy_bandwidth(dev, nbytes=1 << 30, reps=5):
+    """torch's device-to-device copy rate on this GPU (read + written bytes
+    over the copy's time, best of `reps` after one warmup) with 1 GiB
+    tensors, far past the 256 MB Infinity Cache -- printed beside the
+    guide's float4-copy figure (HBM_ACHIEVABLE_GBS) that the roofline is
+    also quoted against."""
+    a = torch.ones(nbytes // 4, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return 2.0 * nbytes / (best / 1e3) / 1e9
+
+
 def max_over_ranks(x, dev):
     """MAX of a float over the process group (the step time the job sees)."""
     import torch.distributed as dist
@@ -883,8 +907,19 @@ def main():
                           "this run's ms_per_step, against the rate the two-gather probe over "
                           "64 MB tables reaches (tools/gather_probe.hip; the cap sits past the "
                           "CUs, tools/gather_paths.hip)" % r_commit}
+    copy_gbs = copy_bandwidth(dev)
+    traffic_gbs = traffic / (ms / 1e3) / 1e9 if traffic else None
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            # SURVEY.md §8(d)'s second number: the measured (PMC) bytes of the
+            # kernel over its time, against the spec and this GPU's copy rate
+            "traffic_GBps": round(traffic_gbs, 1) if traffic_gbs else None,
+            "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
+            "achievable_GBps": HBM_ACHIEVABLE_GBS,
+            "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 5),
+            "traffic_frac_of_achievable": round(traffic_gbs / HBM_ACHIEVABLE_GBS, 4)
+            if traffic_gbs else None,
+            "torch_copy_GBps": round(copy_gbs, 1),
             "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE + the "
                               "wide streamed reads' uncounted half (15 B/packet) + WRITE_SIZE "
                               "per launch, taken at commit %s; random-gather misses are "

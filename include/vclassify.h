@@ -20,6 +20,8 @@
  *    NULL = HIP's null stream); they are asynchronous and ordered on it.  The
  *    plain variants take HOST pointers and are synchronous (H2D + kernel +
  *    D2H, or zero-copy over buffers registered with vc_host_register).
+ *  - A batch of n = 0 items is a no-op that returns VC_OK without reading or
+ *    writing any array (its pointers may be NULL); n < 0 is VC_EINVAL.
  *  - IPv4 addresses are uint32 in IP.ipv4Bytes2Int order (big-endian value,
  *    vfd/IP.java:476-478); IPv6 addresses are 16 raw bytes per item.
  *  - Strings are packed in a byte blob with uint32 offsets (n+1 entries, item
