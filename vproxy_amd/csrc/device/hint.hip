@@ -134,6 +134,22 @@ constexpr size_t kProfLds = 0;
 // A lane's starts in the two chunks; its ends are the next lane's starts
 // (lane 63: the spans' ends o1, o2), taken by a lane shift when used, so the
 // prefetched pair holds two VGPRs and three SGPRs.
+// VC_OFF_NT: the chunk loop's offset loads carry the nontemporal hint (a
+// streamed array, like the staged blob).  Off: each offset is read twice (a
+// lane's start and the previous lane's end, a chunk's span ends), and the
+// hinted lines are gone before the second read -- C4 0.598 -> 0.607 ms, DNS
+// 0.745 -> 0.757, SNI 0.521 -> 0.532 (profiles/r05_ab_off_nt_rejected.jsonl)
+#ifndef VC_OFF_NT
+#define VC_OFF_NT 0
+#endif
+__device__ __forceinline__ uint32_t off_ld(const uint32_t* p) {
+#if VC_OFF_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 struct PairOffs {
     uint32_t A0 = 0, A1 = 0, o0 = 0, o1 = 0, o2 = 0;
 };
@@ -212,16 +228,16 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
         if (off) {
             const int64_t i0 = base + lane, i1 = i0 + 64;
             if (kPre >= 1) {
-                A0 = off[i0 < n ? i0 : n];
-                E0 = off[i0 + 1 < n ? i0 + 1 : n];
+                A0 = off_ld(off + (i0 < n ? i0 : n));
+                E0 = off_ld(off + (i0 + 1 < n ? i0 + 1 : n));
             }
             if (kPre >= 2) {
-                A1 = off[i1 < n ? i1 : n];
-                E1 = off[i1 + 1 < n ? i1 + 1 : n];
+                A1 = off_ld(off + (i1 < n ? i1 : n));
+                E1 = off_ld(off + (i1 + 1 < n ? i1 + 1 : n));
             }
-            o0 = off[base];
-            o1 = off[base + 64 < n ? base + 64 : n];
-            o2 = off[base + 128 < n ? base + 128 : n];
+            o0 = off_ld(off + base);
+            o1 = off_ld(off + (base + 64 < n ? base + 64 : n));
+            o2 = off_ld(off + (base + 128 < n ? base + 128 : n));
             VC_CHECK(o0 <= o1 && o1 <= o2 && o2 <= off[n], 301, base, o2);
         }
         uint32_t a0 = 0;

@@ -14,6 +14,13 @@ constexpr uint32_t kApron = 16;          // readable bytes before and after the 
 #ifndef VC_STAGE_Q
 #define VC_STAGE_Q 1
 #endif
+// VC_STAGE_NT: the staged copy's loads carry the nontemporal hint, so the
+// streamed blob does not displace the probed tables from L2: C4 0.613 ->
+// 0.602 ms, DNS 0.757 -> 0.746, SNI 0.531 -> 0.519, the C5 pool pass in the
+// schedule 0.770 -> 0.761 (profiles/r05_ab_stage_nt.jsonl)
+#ifndef VC_STAGE_NT
+#define VC_STAGE_NT 1
+#endif
 
 // A wave's 64 items are contiguous in the blob: copy [o0, o1) into the
 // wave's stage with coalesced dword loads once.  Item bytes then sit at
@@ -41,6 +48,7 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
     // so a round is straight-line code.  The blob is only dword aligned; an
     // unaligned dwordx4 global load is legal on gfx950.
     typedef uint4 __attribute__((aligned(4))) q4;
+    typedef uint32_t __attribute__((ext_vector_type(4), aligned(4))) v4a;
     const uint32_t nq = full >> 4;                 // whole 16-byte pieces
     const q4* gq = reinterpret_cast<const q4*>(blob + a0);
     uint32_t* lw = stage + kApron / 4;
@@ -61,7 +69,13 @@ __device__ __forceinline__ bool stage_wave(const uint8_t* blob, uint32_t o0, uin
 #pragma unroll
         for (uint32_t j = 0; j < kRound; ++j) {
             const uint32_t k = r0 + 64 * j + uint32_t(lane);
+#if VC_STAGE_NT
+            const v4a t4 = __builtin_nontemporal_load(
+                reinterpret_cast<const v4a*>(gq + (k < last ? k : last)));
+            v[j] = make_uint4(t4.x, t4.y, t4.z, t4.w);
+#else
             v[j] = gq[k < last ? k : last];
+#endif
         }
 #if VC_STAGE_Q == 2
         __builtin_amdgcn_sched_barrier(0);         // every load issued before a write
