@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the string kernels' chunk-loop offset loads nontemporal (VC_OFF_NT)
-# against plain loads (both with the nontemporal staged copy); interleaved.
+# Round 5: the frame kernels (parse, mirror, switch, dnsd) with the staged
+# copy's nontemporal loads (base, the default) against plain loads; interleaved.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-ROUNDS=2 bash scripts/ab_libs.sh "c4;dns;sni;c5" build/base build/offnt
+ROUNDS=2 bash scripts/ab_libs.sh "parse;mirror;switch;dnsd" build/base build/plain

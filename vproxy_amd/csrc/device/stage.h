@@ -17,7 +17,9 @@ constexpr uint32_t kApron = 16;          // readable bytes before and after the 
 // VC_STAGE_NT: the staged copy's loads carry the nontemporal hint, so the
 // streamed blob does not displace the probed tables from L2: C4 0.613 ->
 // 0.602 ms, DNS 0.757 -> 0.746, SNI 0.531 -> 0.519, the C5 pool pass in the
-// schedule 0.770 -> 0.761 (profiles/r05_ab_stage_nt.jsonl)
+// schedule 0.770 -> 0.761 (profiles/r05_ab_stage_nt.jsonl); the DNS drain
+// loop 3.935 -> 3.849 ms, parse / mirror / switch unchanged
+// (r05_ab_stage_nt_frames.jsonl)
 #ifndef VC_STAGE_NT
 #define VC_STAGE_NT 1
 #endif
