@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the frame kernels (parse, mirror, switch, dnsd) with the staged
-# copy's nontemporal loads (base, the default) against plain loads; interleaved.
+# Round 5: C2 with the ACL interval search removed (timing-only ablation,
+# VC_ABL_NOSEARCH) against the real kernel: the most any faster search can gain.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-ROUNDS=2 bash scripts/ab_libs.sh "parse;mirror;switch;dnsd" build/base build/plain
+ROUNDS=2 bash scripts/ab_libs.sh "c2" build/base build/nosearch

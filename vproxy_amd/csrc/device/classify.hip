@@ -108,6 +108,11 @@ __device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[kN
         len[k] = tcp[k] ? a.nf[0] : a.nf[1];
         lo[k] = 0;
     }
+#if defined(VC_ABL_NOSEARCH)        // timing ablation only: no interval search
+#pragma unroll
+    for (int k = 0; k < kN; ++k) lo[k] = int(key[k] % uint32_t(len[k]));
+    if (steps > 0) goto records;
+#endif
     for (int s = 0; s < steps; ++s) {
         uint32_t x[kN];
         int half[kN];
@@ -122,6 +127,9 @@ __device__ __forceinline__ void acl_v4_four(const AclV4Ctx& a, const bool tcp[kN
             len[k] -= half[k];
         }
     }
+#if defined(VC_ABL_NOSEARCH)
+records:
+#endif
     uint4 r[kN];
 #pragma unroll
     for (int k = 0; k < kN; ++k)
