@@ -340,12 +340,26 @@ def test_compact6_host_entry(setup, registered):
                 V.check(V.lib().vc_host_unregister(x.ctypes.data))
     for g, r, name in zip(got, ref, ("acl", "route", "group", "allow")):
         np.testing.assert_array_equal(g, r, err_msg=name)
-    if not registered:
-        for k in (len(s6) - 1, len(s6) + 1):
-            rows = np.zeros((k, 16), np.uint8)
+    # a row count that disagrees with the family array is refused before any
+    # output is written, on the staged and the zero-copy path alike
+    for k in (len(s6) - 1, len(s6) + 1):
+        rows = np.zeros((k, 16), np.uint8)
+        mark = [np.full(n, -7, np.int32) for _ in range(3)] + [np.full(n, 9, np.uint8)]
+        regs = [rows] + [p[k2] for k2 in ("family", "proto", "src4", "dst4", "dport",
+                                           "host_id")] + [pool] + mark
+        if registered:
+            for x in regs:
+                V.check(V.lib().vc_host_register(x.ctypes.data, x.nbytes))
+        try:
             with pytest.raises(V.IllegalArgumentException):
                 clf.pipeline(p["proto"], p["src4"], p["dst4"], p["dport"], p["host_id"], pool,
-                             family=p["family"], src6=rows, dst6=rows, compact6=True)
+                             family=p["family"], src6=rows, dst6=rows, outs=tuple(mark),
+                             compact6=True)
+        finally:
+            if registered:
+                for x in regs:
+                    V.check(V.lib().vc_host_unregister(x.ctypes.data))
+        assert all((m == m.flat[0]).all() for m in mark), "outputs written before the refusal"
 
 
 def test_compact6_host_entry_small(setup):

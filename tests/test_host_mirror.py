@@ -189,3 +189,19 @@ def test_no_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(V.DeviceError):
         V.Classifier(0)
+
+
+def test_ipv6_row_shapes():
+    """classifier._rows16: IPv6 address arrays are [m, 16] bytes or flat bytes
+    of a length divisible by 16; anything else is refused before a kernel is
+    handed a row count its buffer does not hold (vc_pipeline_c6 trusts n6)."""
+    import torch
+    from vproxy_amd.classifier import _rows16
+    assert _rows16(np.zeros((5, 16), np.uint8), "x") == 5
+    assert _rows16(np.zeros(48, np.uint8), "x") == 3
+    assert _rows16(np.zeros((0, 16), np.uint8), "x") == 0
+    assert _rows16(torch.zeros((7, 16), dtype=torch.uint8), "x") == 7
+    for bad in (np.zeros(47, np.uint8), np.zeros((5, 8), np.uint8), np.zeros((5, 4), np.int32),
+                np.zeros(12, np.uint32), np.zeros((2, 16, 1), np.uint8)):
+        with pytest.raises(V.IllegalArgumentException):
+            _rows16(bad, "x")

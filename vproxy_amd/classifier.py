@@ -18,8 +18,8 @@ import ipaddress
 import numpy as np
 
 from . import _lib
-from ._lib import (DNSD_MAXQ, PROTO_TCP, PROTO_UDP, VcAclRule, VcAnnos, VcDnsdOut,
-                   VcGroupAnnos, VcNet, VcPktOut, VcServer, check, lib)
+from ._lib import (DNSD_MAXQ, PROTO_TCP, PROTO_UDP, IllegalArgumentException, VcAclRule,
+                   VcAnnos, VcDnsdOut, VcGroupAnnos, VcNet, VcPktOut, VcServer, check, lib)
 
 HINT_HOST = "vproxy/hint-host"   # AnnotationKeys.ServerGroup_HintHost
 HINT_PORT = "vproxy/hint-port"   # AnnotationKeys.ServerGroup_HintPort
