@@ -205,3 +205,26 @@ def test_ipv6_row_shapes():
                 np.zeros(12, np.uint32), np.zeros((2, 16, 1), np.uint8)):
         with pytest.raises(V.IllegalArgumentException):
             _rows16(bad, "x")
+
+
+def test_pipeline_argument_errors_before_any_call():
+    """Classifier.pipeline refuses inconsistent IPv6 arguments before it
+    touches the library (so this runs without a device)."""
+    from vproxy_amd.classifier import Classifier
+    c = object.__new__(Classifier)          # no context: a library call would fail differently
+    n = 8
+    z = lambda dt: np.zeros(n, dt)
+    base = (z(np.uint8), z(np.uint32), z(np.uint32), z(np.uint16), z(np.uint32),
+            np.zeros(4, np.int32))
+    rows = np.zeros((n, 16), np.uint8)
+    cases = [dict(src6=rows),                                        # dst6 missing
+             dict(dst6=rows),                                        # src6 missing
+             dict(src6=rows, dst6=rows[:3]),                         # row counts differ
+             dict(src6=rows[:3], dst6=rows[:3]),                     # not one row per packet
+             dict(src6=np.zeros(40, np.uint8), dst6=np.zeros(40, np.uint8)),   # not 16-byte rows
+             dict(src6=np.zeros((n + 1, 16), np.uint8), dst6=np.zeros((n + 1, 16), np.uint8),
+                  compact6=True),                                    # more rows than packets
+             dict(family=z(np.uint8), compact6=True)]                # compact without rows
+    for kw in cases:
+        with pytest.raises(V.IllegalArgumentException):
+            c.pipeline(*base, **kw)
