@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 5: C2 with the ACL interval search removed (timing-only ablation,
-# VC_ABL_NOSEARCH) against the real kernel: the most any faster search can gain.
+# Round 5: the source-hash kernel through the per-position pick table with
+# four items per lane (the tree) against the probing kernel (build/base).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-ROUNDS=2 bash scripts/ab_libs.sh "c2" build/base build/nosearch
+mkdir -p build/head && cp vproxy_amd/libvclassify.so build/head/
+ROUNDS=2 bash scripts/ab_libs.sh "source" build/base build/head

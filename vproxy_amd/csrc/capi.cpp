@@ -600,6 +600,8 @@ struct ServerSnap : Snapshot {
     // (kept alive through `lists`), so a batch keeps one health view for all
     // of its chunks.
     std::shared_ptr<const ServerSnap> lists;
+    // the host-built lists, for the pick table a health update rebuilds
+    std::shared_ptr<const vc::ServersBuilt> host;
 };
 
 }  // namespace
@@ -1405,9 +1407,11 @@ int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* gro
     s->img.order = up(*s, b.order);
     s->img.healthy = up(*s, b.healthy);
     s->img.group_base = up(*s, b.group_base);
+    s->img.pick = up(*s, b.pick);
     s->img.n_groups = b.n_groups;
     s->img.n_servers = b.n_servers;
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "server upload");
+    s->host = std::make_shared<const vc::ServersBuilt>(std::move(b));
     ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(s)));
     return VC_OK;
 }
@@ -1426,8 +1430,12 @@ int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers
     auto ns = std::make_shared<ServerSnap>();
     ns->img = s->img;
     ns->lists = s->lists ? s->lists : s;
+    ns->host = s->host;
+    std::vector<int32_t> pick;
+    vc::source_pick_table(*s->host, h.data(), &pick);
     Upload up(ctx);
     ns->img.healthy = up(*ns, h);
+    ns->img.pick = up(*ns, pick);
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "health upload");
     ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(ns)));
     return VC_OK;

@@ -249,14 +249,19 @@ struct MirrorImage {
 // server indices (all / IPv4 / IPv6 servers with weight > 0, in
 // sourceReset's sort order).  view_off holds (offset, count) into order[]
 // for [group][view 0..2]; order[] holds global server indices; healthy[]
-// is per global server (updated in place by vc_servers_set_health);
-// group_base[g] is the global index of group g's first server.
+// is per global server (a new snapshot per vc_servers_set_health);
+// group_base[g] is the global index of group g's first server.  pick[]
+// holds, per order[] entry, sourceHashGet's answer when hash % size lands
+// there: the first healthy server from that position on, cyclically within
+// the list, as an index within its group (-1: none healthy) -- rebuilt on
+// the host with every health update (compile.cpp source_pick_table).
 // ---------------------------------------------------------------------------
 struct ServerImage {
     const uint32_t* view_off;      // 6 words per group
     const int32_t* order;
     const uint8_t* healthy;
     const int32_t* group_base;
+    const int32_t* pick;
     int32_t n_groups;
     int32_t n_servers;
 };

@@ -753,7 +753,29 @@ int build_servers(const vc_server* servers, const int32_t* group_off, int n_grou
     out->group_base[n_groups] = total;
     if (out->order.empty()) out->order.push_back(0);
     if (out->view_off.empty()) out->view_off.assign(6, 0);
+    source_pick_table(*out, out->healthy.data(), &out->pick);
     return VC_OK;
+}
+
+// sourceHashGet's probe (ServerGroup.java:479-490): from idx = hash % size
+// it takes the first healthy server at idx, idx + 1, ... cyclically, null
+// after a whole round.  That depends only on idx, so each list position
+// gets its answer once per health state: a backward pass over the list
+// doubled carries the nearest healthy server at or after each position.
+void source_pick_table(const ServersBuilt& b, const uint8_t* healthy, std::vector<int32_t>* pick) {
+    pick->assign(b.order.size(), -1);
+    for (int g = 0; g < b.n_groups; ++g) {
+        for (int v = 0; v < 3; ++v) {
+            const uint32_t off = b.view_off[size_t(g) * 6 + 2 * v];
+            const int64_t size = b.view_off[size_t(g) * 6 + 2 * v + 1];
+            int32_t next = -1;
+            for (int64_t k = 2 * size - 1; k >= 0; --k) {
+                const int32_t s = b.order[off + size_t(k % size)];
+                if (healthy[s]) next = s - b.group_base[g];
+                if (k < size) (*pick)[off + size_t(k)] = next;
+            }
+        }
+    }
 }
 
 namespace {

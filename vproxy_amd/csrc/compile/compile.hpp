@@ -105,12 +105,16 @@ struct ServersBuilt {
     std::vector<int32_t> order;
     std::vector<uint8_t> healthy;
     std::vector<int32_t> group_base;
+    std::vector<int32_t> pick;           // per order[] entry (images.h ServerImage)
     int32_t n_groups = 0;
     int32_t n_servers = 0;
 };
 
 int build_servers(const vc_server* servers, const int32_t* group_off, int n_groups,
                   ServersBuilt* out);
+
+// ServerImage.pick for the lists of `b` under `healthy` (one byte per server)
+void source_pick_table(const ServersBuilt& b, const uint8_t* healthy, std::vector<int32_t>* pick);
 
 // Digest of a host-built image: 64-bit FNV-1a over its 8-byte words (each
 // array prefixed by its length, scalars included), so ranks that replicate
