@@ -1,6 +1,5 @@
 #!/bin/bash
-# Round 5: the switch kernel with the inner IPv4 route's root entry loaded
-# before the bare-VXLAN ACL (the tree) against the serial chain (build/base).
+# Round 5: the DNS drain loop without its UDP ACL search (timing-only
+# ablation VC_ABL_NOACL) against the real kernel: the ACL chain's share.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-mkdir -p build/head && cp vproxy_amd/libvclassify.so build/head/
-ROUNDS=2 bash scripts/ab_libs.sh "switch" build/base build/head
+ROUNDS=2 bash scripts/ab_libs.sh "dnsd" build/base build/noacl

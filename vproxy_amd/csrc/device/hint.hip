@@ -688,6 +688,11 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
     const bool six = in.rfam && in.rfam[i] == 6;
     const uint32_t port = in.rport[i];
     uint32_t v;
+#if defined(VC_ABL_NOACL)          // timing ablation only: no ACL search (default verdict)
+    if (port != 0x7FFFFFFF) {
+        v = VC_NONE;
+    } else
+#endif
     if (six) {
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
