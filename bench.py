@@ -977,6 +977,22 @@ def main():
 # ---------------------------------------------------------------------------
 # sub-benchmarks (DESIGN.md / BASELINE.md numbers, not the headline)
 # ---------------------------------------------------------------------------
+def replicas(res, world, dev):
+    """A sub-bench at N > 1: every rank runs the same workload on its own GPU
+    (replicas: the classifiers share nothing, so there is no collective in
+    the timed work); the line reports the slowest rank's times and the items
+    all N ranks classified.  Every rank must call it (max-over-ranks)."""
+    res["n_gpus"] = world
+    if world > 1:
+        ms = max_over_ranks(res["kernel_ms"], dev)
+        res["kernel_ms"] = round(ms, 4)
+        res["ms_per_step"] = round(max_over_ranks(res["ms_per_step"], dev), 3)
+        res["items_per_gpu"] = res["items"]
+        res["items"] = res["items"] * world
+        res["M_items_per_s"] = round(res["items"] / (ms / 1e3) / 1e6, 1)
+        res["scaling"] = "weak (replicas)"
+
+
 def _time(fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -1152,7 +1168,7 @@ def sub_bench(args, clf, dev, rank, world):
     dominant kernel's algorithmic bytes over its event-timed duration) and,
     unless --no-cpu-baseline, the oracle's all-core and 1-core rates on a
     sample of the same workload."""
-    O = None if args.no_cpu_baseline else _oracle()
+    O = None if args.no_cpu_baseline or rank > 0 else _oracle()
     cpu = None
     extra = {}
     S = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -1514,7 +1530,7 @@ def sub_bench(args, clf, dev, rank, world):
                             "sourceHashGet over each group's sourceReset order (built once per "
                             "call for all 10k groups, as Java caches it per group)", cap=1 << 22)
     else:
-        return mix_bench(args, clf, dev, rank, O)
+        return mix_bench(args, clf, dev, rank, O, world)
     el, ms = _time(fn, args.steps, args.warmup)
     gbs = per_unit * n / (ms / 1e3) / 1e9
     res = {"workload": args.workload, "items": n, "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -1524,6 +1540,7 @@ def sub_bench(args, clf, dev, rank, world):
                         "algorithmic_bytes": unit},
            "cpu_baseline": cpu}
     res.update(extra)
+    replicas(res, world, dev)
     if rank == 0:
         print(json.dumps(res), flush=True)
     clf.close()
@@ -1564,7 +1581,7 @@ def gen_mixed(lo, n, t, pool_n, v6_frac=0.15, seed=PACKET_SEED + 1, dev="cpu"):
     return fam, proto, src, dst, src6, dst6, dport, hid
 
 
-def mix_bench(args, clf, dev, rank, O):
+def mix_bench(args, clf, dev, rank, O, world=1):
     """The general pipeline (vc_pipeline_dev / vc_pipeline) on the C5 tables
     over a mixed batch: 85 % IPv4 / 15 % IPv6 packets as in C3, per-packet
     family dispatch (RouteTable.java:44-58).  `mix`: device-resident
@@ -1695,6 +1712,7 @@ def mix_bench(args, clf, dev, rank, O):
     res.update(extra)
     res["v6_frac"] = args.v6_frac
     res["compact6"] = bool(args.compact6)
+    replicas(res, world, dev)
     if rank == 0:
         print(json.dumps(res), flush=True)
     clf.close()
