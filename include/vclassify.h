@@ -384,7 +384,9 @@ int vc_compile_servers(vc_ctx *ctx, const vc_server *servers, const int32_t *gro
 /* Health-check result changed: healthy[i] for every server (same indexing
  * as vc_compile_servers).  Publishes a new snapshot (copy-on-write): batches
  * issued afterwards see it, a batch already in flight -- every chunk of a
- * chunked host call included -- keeps the health it started with. */
+ * chunked host call included -- keeps the health it started with.  The call
+ * rebuilds the lists' per-position answers on the host (O(servers)) and
+ * uploads them, so a classify call's probe is one table read. */
 int vc_servers_set_health(vc_ctx *ctx, const uint8_t *healthy, int64_t n_servers);
 #define VC_SOURCE_ALL   0   /* ServerGroup.next(source)      :422-434 */
 #define VC_SOURCE_IPV4  4   /* ServerGroup.nextIPv4(source)  :436-448 */
