@@ -123,3 +123,41 @@ def test_source_bench_batch(clf):
     np.testing.assert_array_equal(got.cpu().numpy()[s], O.source_batch_np(groups, 0, gh, sh,
                                                                            nthreads=16))
     assert float((got >= 0).float().mean()) > 0.9
+
+
+@pytest.mark.parametrize("healthy_frac", [0.5, 0.05, 0.0])
+def test_source_health_updates_at_scale(clf, healthy_frac):
+    """vc_servers_set_health rebuilds the lists' per-position answers
+    (compile.cpp source_pick_table): after each update every one of 32M
+    results equals exact.SourceChecker over the new health, in all three
+    views -- half the servers down, nearly all down (long probe runs), all
+    down (null everywhere) -- and the snapshot taken before the update
+    still answers with the old health."""
+    import torch
+    import bench as B
+    from exact import SourceChecker
+    dev = torch.device("cuda", 0)
+    n = 32 << 20
+    groups, grp, src = B.source_workload(n, dev)
+    clf.compile_servers(groups)
+    before = clf.source_select(grp, src)
+    rng = np.random.default_rng(int(healthy_frac * 100) + 7)
+    flat = [s for g in groups for s in g]
+    h = rng.random(len(flat)) < healthy_frac
+    clf.set_server_health(h.astype(np.uint8))
+    sick, k = [], 0
+    for g in groups:
+        sick.append([(a, p, w, bool(h[k + j])) for j, (a, p, w, _) in enumerate(g)])
+        k += len(g)
+    for view in (V.SOURCE_ALL, V.SOURCE_IPV4, V.SOURCE_IPV6):
+        got = clf.source_select(grp, src, view=view)
+        torch.cuda.synchronize()
+        want = SourceChecker(sick, dev, view=view).v4(grp, src)
+        assert torch.equal(got, want), (view, int((got != want).sum()))
+    if healthy_frac == 0.0:
+        assert bool((got == -1).all())
+    # the compile's own health, through a fresh compile, is the first answer
+    clf.compile_servers(groups)
+    again = clf.source_select(grp, src)
+    torch.cuda.synchronize()
+    assert torch.equal(again, before)
