@@ -4,9 +4,11 @@
 //   sourceHashGet     ServerGroup.java:464-490
 //   sourceReset       ServerGroup.java:620-664 (host side: compile.cpp)
 //
-// One lane per item: the sdbm hash of the client address bytes (Java int
-// arithmetic on sign-extended bytes), then the first healthy server from
-// hash % size on, probing forward as the Java recursion does.
+// Per item: the sdbm hash of the client address bytes (Java int arithmetic
+// on sign-extended bytes), then one read of the list's pick table at
+// hash % size -- the first healthy server from there on, which is where the
+// Java recursion's forward probe ends (images.h ServerImage.pick).  IPv4:
+// four items per lane.
 #include "dev_common.h"
 #include "launch.h"
 
