@@ -101,6 +101,9 @@ void J(classifyDns)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jobject, jo
 void J(pipelineCompact6)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject,
                         jobject, jint, jobject, jobject, jobject, jint, jint, jobject, jobject,
                         jobject, jobject);
+void J(compileServers)(JNIEnv *, jclass, jlong, jobject, jobject, jint);
+void J(setServerHealth)(JNIEnv *, jclass, jlong, jobject, jint);
+void J(selectSourceV4)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jobject);
 
 /* Fault injection.  The executable's definitions of these entry points
  * preempt libvclassify's for the shim linked into it: with inject_rc set
@@ -418,6 +421,44 @@ static void gpu_mode(void) {
         CHECK(memcmp(r1, r2, sizeof r1) == 0 && memcmp(r3, r2, sizeof r2) == 0,
               "hints through the shim (twice) == the C ABI");
         CHECK(r2[0] == 0 && r2[3] == -1, "a.example.com -> group 0, nope.org -> null");
+    }
+    {   /* source hashing through the shim: compile, health update, select ==
+         * the C ABI; a short health buffer is refused */
+        enum { NG = 40, NS = 200 };
+        static vc_server sv[NS];
+        static int32_t goff[NG + 1], grp[N], s1[N], s2[N];
+        static uint8_t hl[NS];
+        struct _jobject bsv = B(sv, sizeof sv), bgo = B(goff, sizeof goff), bgr = B(grp, 4 * N),
+                        bsr = B(src, 4 * N), bh = B(hl, NS), bout = B(s1, 4 * N);
+        for (i = 0; i < NS; ++i) {
+            const uint32_t a = rnd();
+            memset(&sv[i], 0, sizeof sv[i]);
+            sv[i].ip[0] = (uint8_t) (a >> 24);
+            sv[i].ip[1] = (uint8_t) (a >> 16);
+            sv[i].ip[2] = (uint8_t) (a >> 8);
+            sv[i].ip[3] = (uint8_t) a;
+            sv[i].ip_len = 4;
+            sv[i].port = 80;
+            sv[i].weight = 1;
+            sv[i].healthy = 1;
+            hl[i] = (uint8_t) (rnd() % 3 != 0);
+        }
+        for (i = 0; i <= NG; ++i) goff[i] = i * NS / NG;
+        for (i = 0; i < N; ++i) grp[i] = (int32_t) (rnd() % NG);
+        J(compileServers)(env, NULL, h, &bsv, &bgo, NG);
+        CHECK(!n_thrown, "compileServers");
+        J(setServerHealth)(env, NULL, h, &bh, NS);
+        CHECK(!n_thrown, "setServerHealth");
+        J(selectSourceV4)(env, NULL, h, &bgr, &bsr, N, 0, &bout);
+        CHECK(!n_thrown, "selectSourceV4");
+        CHECK(vc_compile_servers(ctx, sv, goff, NG) == VC_OK, "vc_compile_servers");
+        CHECK(vc_servers_set_health(ctx, hl, NS) == VC_OK, "vc_servers_set_health");
+        CHECK(vc_source_select_v4(ctx, grp, src, N, 0, s2) == VC_OK, "vc_source_select_v4");
+        CHECK(memcmp(s1, s2, sizeof s1) == 0, "source hashing through the shim == the C ABI");
+        bh.cap = NS - 1;
+        J(setServerHealth)(env, NULL, h, &bh, NS);
+        expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",
+                     "short health buffer");
     }
     J(destroy)(env, NULL, h);
     vc_destroy(ctx);
