@@ -1,7 +1,6 @@
 #!/bin/bash
-# Round 5: the pool pass without its record loads (timing-only ablation
-# VC_ABL_NOREC: every tag hit taken as a match) against the real kernel, on
-# C4 and the C5 step: the most a smaller / denser record layout can give.
+# Round 5: the deferring DNS drain-loop kernel with 96-char qname buffers
+# (longer names deferred; seven workgroups per CU) against 128-char ones.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p build/head && cp vproxy_amd/libvclassify.so build/head/
-ROUNDS=2 bash scripts/ab_libs.sh "c4;c5" build/head build/norec
+ROUNDS=2 bash scripts/ab_libs.sh "dnsd" build/base build/head

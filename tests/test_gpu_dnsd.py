@@ -216,3 +216,58 @@ def test_dns_datagrams_deferred_over_slot_reuse():
             _same(got, want)
     finally:
         clf.close()
+
+
+def test_dns_datagram_qname_lengths():
+    """Decoded qnames of 1 .. 140 chars, around the deferring kernel's
+    96-char buffers (longer names go to dnsd_defer_kernel, whose buffers
+    hold 128) and the contract's 128 (longer: VC_DNSD_HOST, the Java path):
+    hint-host, hosts-file and unknown names of every length, one and two
+    questions, through the staged and unstaged kernels, equal to the oracle."""
+    import torch
+    rng = np.random.default_rng(31)
+    clf = V.Classifier(0)
+    try:
+        tcp = np.concatenate([rule_row("0.0.0.0/0", 0, 65535, False)])
+        udp = np.concatenate([rule_row("0.0.0.0/0", 0, 65535, True)])
+        _compile_acl(clf, tcp, udp, True)
+
+        def label_name(total):
+            """a dotted name of exactly `total` chars, trailing dot included
+            (30-char labels)"""
+            c = list("".join(rng.choice(list("abcdefghij"), total - 1)))
+            for p in range(30, total - 2, 31):
+                c[p] = "."
+            return "".join(c) + "."
+        names = [label_name(L) for L in range(2, 141)]
+        assert all(len(n) == L for n, L in zip(names, range(2, 141)))
+        groups = [({}, {"host": n.rstrip(".")}) for n in names[::3]]
+        hosts = [(n, 100 + i) for i, n in enumerate(names[1::3])]
+        clf.compile_upstream(groups)
+        clf.compile_hosts(hosts)
+        dg = []
+        for n in names:
+            dg.append(DW.query([(n, DW.A)]))
+            dg.append(DW.query([("x.org.", DW.A), (n, DW.AAAA)]))
+        N = len(dg)
+        fam = np.full(N, 4, np.uint8)
+        r4 = np.full(N, 0x08080808, np.uint32)
+        r6 = np.zeros((N, 16), np.uint8)
+        port = np.full(N, 53, np.uint16)
+        blob, off = W.pack(dg)
+        want = O.dnsd_batch_np(tcp, udp, True, hosts, groups, blob, off, fam, r4, r6, port)
+        lens = np.array([len(n) - 1 for n in names])
+        assert (lens > 96).sum() > 20 and (lens > 128).sum() > 5
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        for shift in (0, 1):
+            dblob = torch.zeros(len(blob) + 16, dtype=torch.uint8, device="cuda")
+            dblob[shift:shift + len(blob)] = T(blob)
+            res = _cpu(clf.dns_datagrams((dblob[shift:], T(off.view(np.int32))),
+                                         T(r4.view(np.int32)), T(port.view(np.int16)),
+                                         remote6=T(r6), remote_family=T(fam)))
+            res["qtype"] = res["qtype"].view(np.uint16)
+            _same(res, want)
+        st = want["status"]
+        assert (st == V.DNSD_HOST).sum() > 0 and (st == V.DNSD_ANSWER).sum() > 0
+    finally:
+        clf.close()

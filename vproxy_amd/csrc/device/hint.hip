@@ -541,15 +541,28 @@ constexpr int kDnsdWaves = kDnsdBlock / 64;
 // (profiles/r02_ab_dnsd_residency.txt).
 constexpr uint32_t kDnsdStage = 4096;
 constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
-constexpr int kNameCap = 128;                 // decoded qname chars a lane classifies
+constexpr int kNameCap = 128;                 // decoded qname chars classified (contract)
+// The deferring kernel's per-lane buffer holds kFastCap chars; a datagram
+// with a longer qname (up to kNameCap) is left to dnsd_defer_kernel, whose
+// buffers hold kNameCap.  96-char buffers make the workgroup 21.6 KiB, seven
+// per CU instead of six: 3.83 -> 3.51 ms for the bench's 16.7M datagrams
+// (profiles/r05_ab_dnsd_cap96.jsonl); the bench's names are under 60 chars.
+#ifndef VC_DNSD_FAST_CAP
+#define VC_DNSD_FAST_CAP 96
+#endif
+constexpr int kFastCap = VC_DNSD_FAST_CAP;
 // Readable bytes around a qname: LdsSrc reads the aligned word pair that
 // holds [pos, pos + 4) for pos in [-3, len + 3].
 constexpr int kNameApron = 4;
 // an odd stride in words: lane l's word k sits in bank (35 l + k) mod 64, so
 // the lanes' buffers do not collide when they read the same word index
 // (an even stride of 40 words put them on 8 banks)
-constexpr int kNameWords = (kNameCap + 2 * kNameApron) / 4 + 1;
+constexpr int name_words(int cap) { return (cap + 2 * kNameApron) / 4 + 1; }
+constexpr int kNameWords = name_words(kNameCap);
+constexpr int kFastWords = name_words(kFastCap);
 static_assert((kNameApron + kNameCap + 3) / 4 + 1 < kNameWords, "qname buffer too short");
+static_assert((kNameApron + kFastCap + 3) / 4 + 1 < kFastWords, "qname buffer too short");
+static_assert(kFastCap <= kNameCap && (kNameWords & 1) && (kFastWords & 1), "odd strides");
 constexpr int kMaxPtr = 16;
 
 enum : int { kNameOk = 0, kNameBad = 1, kNameHost = 2 };
@@ -679,7 +692,7 @@ constexpr uint8_t kDnsdDeferred = 0xFF;
 // kDefer: a question dns_one<true> defers makes the whole datagram
 // kDnsdDeferred (status only); dnsd_defer_kernel redoes it.  Returns the
 // status written.
-template <bool kDefer>
+template <bool kDefer, int kCap = kDefer ? kFastCap : kNameCap>
 __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintImage& img,
                                             const HintImage* slow_img, const AclImage& acl,
                                             const DnsdIn& in, const DnsdOut& out, int64_t i,
@@ -760,7 +773,7 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
                 for (int q = 0; q < qd; ++q) {
                     int used = 0, len = 0;
                     parse_name(p, n, at, n - at, &used, [&](int b) {
-                        if (len < kNameCap) nb[len] = uint8_t(b);
+                        if (len < kCap) nb[len] = uint8_t(b);
                         ++len;
                     });
                     at += used;
@@ -775,6 +788,10 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
                     if (len > kNameCap) {               // the Java path decides
                         st = VC_DNSD_HOST;
                         nq = 0;
+                        break;
+                    }
+                    if (kDefer && len > kCap) {         // longer than this kernel's buffer
+                        st = kDnsdDeferred;
                         break;
                     }
                     uint8_t kd;
@@ -806,7 +823,7 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out,
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kDnsdWaves : 1][kStage ? kDnsdStageWords : 1];
-    __shared__ uint32_t names[kDnsdBlock][kNameWords];
+    __shared__ uint32_t names[kDnsdBlock][kDefer ? kFastWords : kNameWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     HintImage slow_img = img;
     // 64-datagram chunks from the work tickets, or the static grid-stride
