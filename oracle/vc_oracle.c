@@ -1802,3 +1802,173 @@ void vo_dnsd_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int n
                         remote4, remote6, remote_port, out};
     parallel_for(n, nthreads, dnsd_range, &c);
 }
+
+/* ------------------------------------------------------------------------ */
+/* HTTP/1 request head -> connection hint -> group                          */
+/* HttpSubContext.java:394-534, HttpContext.java:55-71                      */
+/* ------------------------------------------------------------------------ */
+
+/* The parser builds its strings with sb.append((char) b) of Java bytes: a
+ * byte c >= 0x80 is the char U+FF00 | c (as in Formatter.parseDomainName);
+ * here as its UTF-8 bytes EF (BC | c >> 6) (80 | c & 3F). */
+static int jchars_utf8(const unsigned char *s, int n, char *out)
+{
+    int k = 0;
+    for (int i = 0; i < n; ++i) {
+        unsigned char c = s[i];
+        if (c < 0x80) {
+            out[k++] = (char)c;
+        } else {
+            out[k++] = (char)0xEF;
+            out[k++] = (char)(0xBC | (c >> 6));
+            out[k++] = (char)(0x80 | (c & 0x3F));
+        }
+    }
+    return k;
+}
+
+/* String.trim(): chars <= ' ' off both ends (every char of a byte >= 0x80 is
+ * above ' ') */
+static void j_trim(const unsigned char *s, int n, int *from, int *to)
+{
+    int a = 0, e = n;
+    while (a < e && s[a] <= ' ') ++a;
+    while (e > a && s[e - 1] <= ' ') --e;
+    *from = a;
+    *to = e;
+}
+
+int vo_http_extract(const uint8_t *p, int n, uint8_t *uri, int *uri_len, uint8_t *host,
+                    int *host_len)
+{
+    unsigned char *key = malloc((size_t)n + 1), *val = malloc((size_t)n + 1);
+    int ul = 0, kl = 0, vl = 0, hl = 0;
+    int uri_set = 0, host_set = 0;     /* theUri / theHostHeader != null */
+    int header = 0;                    /* the HeaderBuilder exists */
+    int state = 0;
+    for (int i = 0; i < n && state != 9; ++i) {
+        const unsigned char b = p[i];
+    again:
+        switch (state) {
+        case 0:                                        /* :394-404 (frontend) */
+            state = 1;
+            goto again;
+        case 1:                                        /* method :406-412 */
+            if (b == ' ') state = 2;
+            break;
+        case 2:                                        /* uri :414-426 */
+            if (b == ' ') {
+                uri_set = 1;
+                state = 3;
+            } else if (b == '\r') {
+            } else if (b == '\n') {
+                uri_set = 1;
+                state = 4;
+            } else {
+                uri[ul++] = b;
+            }
+            break;
+        case 3:                                        /* version :428-439 */
+            if (b == '\n') state = 4;
+            break;
+        case 4:                                        /* end-first-line :441-451 */
+            if (b == '\r') {
+            } else if (b == '\n') {
+                state = 9;
+            } else {
+                state = 5;
+                goto again;
+            }
+            break;
+        case 5:                                        /* header-key :453-464 */
+            if (!header) {
+                header = 1;
+                kl = vl = 0;
+            }
+            if (b == ':') state = 7;                   /* state6(':') -> 7, :466-472 */
+            else key[kl++] = b;
+            break;
+        case 7:                                        /* header-value :474-484 */
+            if (b == '\r') {
+            } else if (b == '\n') {
+                state = 8;
+            } else if (b != ' ' || vl != 0) {
+                val[vl++] = b;
+            }
+            break;
+        case 8:                                        /* end-one-header :486-534 */
+            if (header) {
+                int a, e;
+                j_trim(key, kl, &a, &e);               /* key.trim().toLowerCase() */
+                if (e - a == 4 && (key[a] | 0x20) == 'h' && (key[a + 1] | 0x20) == 'o' &&
+                    (key[a + 2] | 0x20) == 's' && (key[a + 3] | 0x20) == 't') {
+                    int va, ve;
+                    j_trim(val, vl, &va, &ve);         /* theHostHeader = value.trim() */
+                    hl = ve - va;
+                    memcpy(host, val + va, (size_t)hl);
+                    host_set = 1;
+                }
+                header = 0;
+            }
+            if (b == '\r') {
+            } else if (b == '\n') {
+                state = 9;
+            } else {
+                state = 5;
+                goto again;
+            }
+            break;
+        }
+    }
+    free(key);
+    free(val);
+    *uri_len = ul;
+    *host_len = hl;
+    return (host_set ? VO_HTTP_HOST : 0) | (uri_set ? VO_HTTP_URI : 0);
+}
+
+int vo_http_hint(const vo_group *g, int ng, const uint8_t *p, int n, int *kind)
+{
+    unsigned char *uri = malloc((size_t)n + 1), *host = malloc((size_t)n + 1);
+    int ul = 0, hl = 0;
+    /* HttpContext.connectionHint, :55-71 */
+    const int k = vo_http_extract(p, n, uri, &ul, host, &hl);
+    const int host_set = (k & VO_HTTP_HOST) != 0, uri_set = (k & VO_HTTP_URI) != 0;
+    int out = -1;
+    if (k) {
+        char *hu = malloc((size_t)hl * 3 + 1), *uu = malloc((size_t)ul * 3 + 1);
+        const int hn = host_set ? jchars_utf8(host, hl, hu) : 0;
+        const int un = uri_set ? jchars_utf8(uri, ul, uu) : 0;
+        vo_hint h = vo_hint_of(host_set ? hu : NULL, hn, 0, uri_set ? uu : NULL, un);
+        out = vo_search_for_group(g, ng, &h);
+        free(hu);
+        free(uu);
+    }
+    free(uri);
+    free(host);
+    *kind = k;
+    return out;
+}
+
+typedef struct {
+    const vo_group *g; int ng; const uint8_t *blob; const uint32_t *off;
+    uint8_t *kind; int32_t *group;
+} http_batch_ctx;
+
+static void http_range(void *p, int64_t lo, int64_t hi)
+{
+    http_batch_ctx *c = (http_batch_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        int k = 0;
+        c->group[i] = vo_http_hint(c->g, c->ng, c->blob + c->off[i],
+                                   (int)(c->off[i + 1] - c->off[i]), &k);
+        if (c->kind) c->kind[i] = (uint8_t)k;
+    }
+}
+
+void vo_http_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off, int64_t n,
+                   uint8_t *kind, int32_t *group, int nthreads)
+{
+    http_batch_ctx c = {g, ng, blob, off, kind, group};
+    parallel_for(n, nthreads, http_range, &c);
+}

@@ -25,6 +25,22 @@
 
 #ifdef __cplusplus
 extern "C" {
+/* ---- HTTP/1 request head -> Hint -> Upstream.searchForGroup ----
+ * HttpSubContext.feed over the request line and headers (states 0-8,
+ * base/.../processor/http1/HttpSubContext.java:394-534; parsing stops at
+ * the end of the headers, state 9), then HttpContext.connectionHint
+ * (HttpContext.java:55-71) and Upstream.searchForGroup.  *kind: 0 = no hint
+ * (null), 1 = Hint.ofUri, 2 = Hint.ofHost, 3 = Hint.ofHostUri.  Returns the
+ * group index, -1 for none (and for a null hint). */
+enum { VO_HTTP_NONE = 0, VO_HTTP_URI = 1, VO_HTTP_HOST = 2, VO_HTTP_HOST_URI = 3 };
+int vo_http_hint(const vo_group *g, int ng, const uint8_t *head, int n, int *kind);
+/* theUri / theHostHeader as the parser leaves them (raw bytes, one per Java
+ * char; buffers of n bytes); returns the kind bits (1 uri set, 2 host set) */
+int vo_http_extract(const uint8_t *head, int n, uint8_t *uri, int *uri_len, uint8_t *host,
+                    int *host_len);
+void vo_http_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off, int64_t n,
+                   uint8_t *kind, int32_t *group, int nthreads);
+
 #endif
 
 /* ---- IP parsing: base/src/main/java/vfd/IP.java ---- */
@@ -261,6 +277,22 @@ void vo_source_batch(const vo_server *servers, const int32_t *goff, int n_groups
 
 #ifdef __cplusplus
 }
+/* ---- HTTP/1 request head -> Hint -> Upstream.searchForGroup ----
+ * HttpSubContext.feed over the request line and headers (states 0-8,
+ * base/.../processor/http1/HttpSubContext.java:394-534; parsing stops at
+ * the end of the headers, state 9), then HttpContext.connectionHint
+ * (HttpContext.java:55-71) and Upstream.searchForGroup.  *kind: 0 = no hint
+ * (null), 1 = Hint.ofUri, 2 = Hint.ofHost, 3 = Hint.ofHostUri.  Returns the
+ * group index, -1 for none (and for a null hint). */
+enum { VO_HTTP_NONE = 0, VO_HTTP_URI = 1, VO_HTTP_HOST = 2, VO_HTTP_HOST_URI = 3 };
+int vo_http_hint(const vo_group *g, int ng, const uint8_t *head, int n, int *kind);
+/* theUri / theHostHeader as the parser leaves them (raw bytes, one per Java
+ * char; buffers of n bytes); returns the kind bits (1 uri set, 2 host set) */
+int vo_http_extract(const uint8_t *head, int n, uint8_t *uri, int *uri_len, uint8_t *host,
+                    int *host_len);
+void vo_http_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off, int64_t n,
+                   uint8_t *kind, int32_t *group, int nthreads);
+
 #endif
 
 /* DNSServer's drain loop per datagram (DNSServer.java:457-500, Formatter.
@@ -285,5 +317,21 @@ void vo_dnsd_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int n
                    const uint8_t *blob, const uint32_t *off, int64_t n, const uint8_t *family,
                    const uint32_t *remote4, const uint8_t *remote6, const uint16_t *remote_port,
                    vo_dnsd_out *out, int nthreads);
+
+/* ---- HTTP/1 request head -> Hint -> Upstream.searchForGroup ----
+ * HttpSubContext.feed over the request line and headers (states 0-8,
+ * base/.../processor/http1/HttpSubContext.java:394-534; parsing stops at
+ * the end of the headers, state 9), then HttpContext.connectionHint
+ * (HttpContext.java:55-71) and Upstream.searchForGroup.  *kind: 0 = no hint
+ * (null), 1 = Hint.ofUri, 2 = Hint.ofHost, 3 = Hint.ofHostUri.  Returns the
+ * group index, -1 for none (and for a null hint). */
+enum { VO_HTTP_NONE = 0, VO_HTTP_URI = 1, VO_HTTP_HOST = 2, VO_HTTP_HOST_URI = 3 };
+int vo_http_hint(const vo_group *g, int ng, const uint8_t *head, int n, int *kind);
+/* theUri / theHostHeader as the parser leaves them (raw bytes, one per Java
+ * char; buffers of n bytes); returns the kind bits (1 uri set, 2 host set) */
+int vo_http_extract(const uint8_t *head, int n, uint8_t *uri, int *uri_len, uint8_t *host,
+                    int *host_len);
+void vo_http_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off, int64_t n,
+                   uint8_t *kind, int32_t *group, int nthreads);
 
 #endif

@@ -537,8 +537,72 @@ def dns_datagrams():
                        "nq": nq, "questions": qs} for w, d, r, port, st, nq, qs in cases]}
 
 
+# ---------------------------------------------------------------------------
+# HTTP/1 request heads -> theUri / theHostHeader (HttpContext.connectionHint)
+# ---------------------------------------------------------------------------
+def http1():
+    """The request heads of TestHttp1Parser (test/src/test/java/vproxy/test/
+    cases/TestHttp1Parser.java) with the uri and Host value its assertions
+    hold, then quirk KATs hand-derived from HttpSubContext.java's states
+    (base/src/main/java/vproxybase/processor/http1/HttpSubContext.java):
+    uri/host None = the Java field stays null."""
+    H = "GET /hello/url HTTP/1.1\r\n"
+    ref = [
+        ("simpleRequest :39-44, :64, :68", H + "Host: www.example.com\r\nHello: World\r\n\r\n",
+         "/hello/url", "www.example.com"),
+        ("noHeaderRequest :114-117, :129", H + "\r\n", "/hello/url", None),
+        ("noVersionRequest :173-178, :198, :202",
+         "GET /hello/url\r\nHost: www.example.com\r\nHello: World\r\n\r\n",
+         "/hello/url", "www.example.com"),
+        ("noHeaderNorVersionRequest :217-220, :232", "GET /hello/url\r\n\r\n", "/hello/url", None),
+        ("normalRequest :247-253, :273, :277",
+         "PUT /hello/url HTTP/1.1\r\nHost: www.example.com\r\nHello: World\r\n"
+         "Content-Length: 10\r\n\r\n", "/hello/url", "www.example.com"),
+        ("chunk request :340-346, :366, :370",
+         "POST /hello/url HTTP/1.1\r\nHost: www.example.com\r\nHello: World\r\n"
+         "Transfer-Encoding: chunked\r\n\r\n", "/hello/url", "www.example.com"),
+    ]
+    derived = [
+        # state2 :414-426: '\r' inside the uri is dropped; ' ' or '\n' ends it
+        ("uri CR dropped (:418)", "GET /a\rb?x=1 HTTP/1.1\r\n\r\n", "/ab?x=1", None),
+        ("uri ends at LF (:420-422)", "GET /a\nHost: h\r\n\r\n", "/a", "h"),
+        ("empty uri (double space, :415-417)", "GET  /a HTTP/1.1\r\nHost: h\r\n\r\n", "", "h"),
+        ("the method runs to the first space (:406-412)", "GET\r\nHost: h\r\n\r\n", "h", None),
+        ("empty head", "", None, None),
+        ("method only", "GET ", None, None),
+        ("uri cut short (no terminator)", "GET /abc", None, None),
+        # state8 :486-534: a header is stored on the byte after its LF
+        ("last header not finalised", "GET /a HTTP/1.1\r\nHost: h\r\n", "/a", None),
+        ("finalised by the next byte", "GET /a HTTP/1.1\r\nHost: h\r\n\r", "/a", "h"),
+        # key.trim().toLowerCase() (:499), value.trim() (:502), leading
+        # spaces skipped and CR dropped in the value (:475-481)
+        ("key case and trim", "GET /a HTTP/1.1\r\n hOsT\t: \t h.example \r\n\r\n", "/a",
+         "h.example"),
+        ("value CR inside", "GET /a HTTP/1.1\r\nHost: a\rb.c\r\n\r\n", "/a", "ab.c"),
+        ("the last Host wins", "GET /a HTTP/1.1\r\nHost: one\r\nHost: two\r\n\r\n", "/a", "two"),
+        ("Host-like keys", "GET /a HTTP/1.1\r\nHosts: x\r\nX-Host: y\r\n\r\n", "/a", None),
+        ("empty Host value", "GET /a HTTP/1.1\r\nHost:\r\n\r\n", "/a", ""),
+        ("colon in value", "GET /a HTTP/1.1\r\nHost: h:8080\r\n\r\n", "/a", "h:8080"),
+        # state5 :453-464: the key runs to the next ':' across line ends
+        ("key spans lines", "GET /a HTTP/1.1\r\nX\r\nHost: h\r\n\r\n", "/a", None),
+        # state4 / state8: headers end at an empty line; later bytes unread
+        ("bytes after the head", "GET /a HTTP/1.1\r\nHost: h\r\n\r\nGET /b HTTP/1.1\r\n"
+         "Host: z\r\n\r\n", "/a", "h"),
+        ("bare LF line ends", "GET /a HTTP/1.1\nHost: h\n\n", "/a", "h"),
+        # (char) b of a Java byte: bytes >= 0x80 kept one per char
+        ("non-ASCII bytes", "GET /\u00e4 HTTP/1.1\r\nHost: \u00e4.example\r\n\r\n", "/\u00e4",
+         "\u00e4.example"),
+    ]
+    enc = lambda t: t.encode("latin-1").hex() if t is not None else None
+    dump("http1.json", {
+        "source": "TestHttp1Parser.java (request heads) + HttpSubContext.java states 0-8",
+        "cases": [{"what": w, "head": enc(h), "uri": enc(u), "host": enc(o)}
+                  for w, h, u, o in ref + derived]})
+
+
 if __name__ == "__main__":
     netmask()
     ip_parser()
     route_table()
     kats()
+    http1()

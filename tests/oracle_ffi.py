@@ -134,6 +134,9 @@ def lib():
                                      C.c_int]
         vp, i64 = C.c_void_p, C.c_int64
         L.vo_dns_batch.argtypes = [P(VoHosts), P(VoGroup), C.c_int, vp, vp, i64, vp, vp, C.c_int]
+        L.vo_http_extract.argtypes = [vp, C.c_int, vp, P(C.c_int), vp, P(C.c_int)]
+        L.vo_http_hint.argtypes = [P(VoGroup), C.c_int, vp, C.c_int, P(C.c_int)]
+        L.vo_http_batch.argtypes = [P(VoGroup), C.c_int, vp, vp, i64, vp, vp, C.c_int]
         L.vo_parse_batch.argtypes = [vp, vp, i64, C.c_int, P(VoPkt), C.c_int]
         L.vo_switch_batch.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int, vp, vp,
                                       i64, vp, C.c_int, P(VoNet), C.c_int, P(VoNet), C.c_int, vp,
@@ -617,6 +620,38 @@ def dns_batch_np(hosts, groups, blob, off, nthreads=1):
     lib().vo_dns_batch(C.byref(h.h), g.arr, g.n, _ptr(np.ascontiguousarray(blob, np.uint8)),
                        _ptr(_u32a(off)), n, _ptr(kind), _ptr(value), nthreads)
     return kind, value
+
+
+def http_extract(head):
+    """HttpSubContext's theUri / theHostHeader after feeding `head` (bytes):
+    (uri or None, host or None), raw bytes (one per Java char)."""
+    head = bytes(head)
+    n = len(head)
+    hb = C.create_string_buffer(head, max(1, n))
+    ub, hob = C.create_string_buffer(max(1, n)), C.create_string_buffer(max(1, n))
+    ul, hl = C.c_int(), C.c_int()
+    k = lib().vo_http_extract(C.cast(hb, C.c_void_p), n, C.cast(ub, C.c_void_p), C.byref(ul),
+                              C.cast(hob, C.c_void_p), C.byref(hl))
+    return (ub.raw[:ul.value] if k & 1 else None), (hob.raw[:hl.value] if k & 2 else None)
+
+
+def http_hint(groups, head):
+    """-> (group, kind) of HttpContext.connectionHint + Upstream.searchForGroup"""
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    head = bytes(head)
+    hb = C.create_string_buffer(head, max(1, len(head)))
+    k = C.c_int()
+    r = lib().vo_http_hint(g.arr, g.n, C.cast(hb, C.c_void_p), len(head), C.byref(k))
+    return r, k.value
+
+
+def http_batch_np(groups, blob, off, nthreads=1):
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    n = len(off) - 1
+    kind, group = np.empty(n, np.uint8), np.empty(n, np.int32)
+    lib().vo_http_batch(g.arr, g.n, _ptr(np.ascontiguousarray(blob, np.uint8)), _ptr(_u32a(off)),
+                        n, _ptr(kind), _ptr(group), nthreads)
+    return kind, group
 
 
 def parse_batch_np(blob, off, layer, nthreads=1):

@@ -195,3 +195,40 @@ def test_source_kats():
         servers = [(_ip_bytes(ip), port, w, h) for ip, port, w, h in case["servers"]]
         for client, view, want in case["queries"]:
             assert O.source_select(servers, view, _ip_bytes(client)) == want, case["source"]
+
+
+def _hx(v):
+    return bytes.fromhex(v) if v is not None else None
+
+
+def test_http1_heads():
+    """HttpSubContext's theUri / theHostHeader (TestHttp1Parser's request
+    heads and the derived state-machine KATs, tests/golden/http1.json)."""
+    for c in load("http1.json")["cases"]:
+        assert O.http_extract(_hx(c["head"])) == (_hx(c["uri"]), _hx(c["host"])), c["what"]
+
+
+def test_http1_connection_hint():
+    """HttpContext.connectionHint (HttpContext.java:55-71): the hint kind
+    follows which fields are set, and Upstream.searchForGroup sees the
+    formatted host (port and 'www.' cut, Hint.java:57-73) and uri ('?' cut,
+    trailing '/' cut, :75-90)."""
+    groups = [({"host": "example.com"}, {}), ({"uri": "/hello"}, {}),
+              ({"host": "*"}, {"uri": "/api"})]
+    cases = [
+        (b"GET /hello/url HTTP/1.1\r\nHost: www.example.com:8080\r\n\r\n", 0, 3),
+        (b"GET /hello/url HTTP/1.1\r\n\r\n", 1, 1),
+        (b"GET /api/?q=1 HTTP/1.1\r\nHost: other\r\n\r\n", 2, 3),
+        (b"GET /none HTTP/1.1\r\nHost: other\r\n\r\n", 2, 3),      # "*" host: level 1 << 10
+        (b"GET /none HTTP/1.1\r\n\r\n", -1, 1),
+        (b"", -1, 0),
+        (b"GET /hello/url HTTP/1.1\r\nHost: :80\r\n\r\n", 1, 3),   # formatHost -> null
+    ]
+    for head, group, kind in cases:
+        assert O.http_hint(groups, head) == (group, kind), head
+    # the batch form equals the single form
+    blob = b"".join(h for h, _, _ in cases)
+    import numpy as np
+    off = np.cumsum([0] + [len(h) for h, _, _ in cases]).astype(np.uint32)
+    kind, grp = O.http_batch_np(groups, np.frombuffer(blob, np.uint8), off, nthreads=2)
+    assert list(grp) == [g for _, g, _ in cases] and list(kind) == [k for _, _, k in cases]
