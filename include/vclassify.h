@@ -206,6 +206,28 @@ int vc_dns_classify_dev(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff,
 int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int64_t n,
                     uint8_t *out_kind, int32_t *out_value);
 
+/* ------------------------------------------------------------------------ */
+/* The upstream group of an HTTP/1 request (HttpLB's frontend): for request
+ * head i = blob[off[i], off[i+1]), HttpSubContext's request-line and header
+ * states (HttpSubContext.java:394-534, parsing stops at the empty line that
+ * ends the headers), HttpContext.connectionHint (HttpContext.java:55-71:
+ * theUri and the last Host header's trimmed value; Hint.ofUri / ofHost /
+ * ofHostUri) and Upstream.searchForGroup on the compiled Upstream.
+ * out_group = handle index, -1 for no group and for a null hint; out_kind
+ * (optional) = VC_HTTP_* of the hint.  Heads are bytes as they came off the
+ * socket; the _dev form needs blob_bytes >= off[n] (it sizes the scratch
+ * that heads with CR or non-ASCII bytes in their uri / Host are rewritten
+ * into). */
+/* ------------------------------------------------------------------------ */
+#define VC_HTTP_NONE      0  /* no uri and no Host header: the hint is null */
+#define VC_HTTP_URI       1  /* Hint.ofUri(theUri) */
+#define VC_HTTP_HOST      2  /* Hint.ofHost(theHostHeader) */
+#define VC_HTTP_HOST_URI  3  /* Hint.ofHostUri(theHostHeader, theUri) */
+int vc_http_hint_dev(vc_ctx *ctx, const uint8_t *blob, int64_t blob_bytes, const uint32_t *off,
+                     int64_t n, int32_t *out_group, uint8_t *out_kind, void *stream);
+int vc_http_hint(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
+                 int32_t *out_group, uint8_t *out_kind);
+
 /* DNSServer's drain loop per datagram (DNSServer.java:457-500): for UDP
  * payload i = blob[off[i], off[i+1]) from the remote address (family 4/6,
  * remote4 in IP.ipv4Bytes2Int order or 16 remote6 bytes, 16-byte aligned)

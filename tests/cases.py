@@ -361,3 +361,63 @@ def mirror_frames(rng, n):
             f[34:38] = bytes([10, int(rng.integers(0, 3)), 2, 3])
         frames.append(bytes(f))
     return frames
+
+
+def http_heads_random(rng, n, hosts, uris):
+    """HTTP/1 request heads (bytes) for HttpContext.connectionHint: request
+    lines with and without a version, bare-LF lines, Host headers in any
+    case with blanks and tabs around key and value, ':port' and 'www.'
+    forms, two Host headers, Host-like keys, CR or non-ASCII bytes inside
+    the uri or the Host value, keys running across lines, heads cut short
+    at any byte and bodies or a second request after the empty line."""
+    methods = [b"GET", b"POST", b"PUT", b"HEAD", b"OPTIONS"]
+    out = []
+    pick = lambda xs: xs[int(rng.integers(0, len(xs)))]
+    for _ in range(n):
+        eol = b"\r\n" if rng.random() < 0.9 else b"\n"
+        u = pick(uris)
+        u = b"" if u is None else (u.encode() if isinstance(u, str) else u)
+        r = rng.random()
+        if r < 0.03:
+            u = u + b"\r" + b"x"
+        elif r < 0.05:
+            u = u + b"\xe4\xff"
+        line = pick(methods) + (b"  " if rng.random() < 0.02 else b" ") + u
+        line += (b" HTTP/1.1" if rng.random() < 0.85 else b"") + eol
+        hdrs = []
+        if rng.random() < 0.5:
+            hdrs.append(b"User-Agent: curl/8.0")
+        if rng.random() < 0.05:
+            hdrs.append(b"Hosts: " + pick(hosts).encode())
+        if rng.random() < 0.05:
+            hdrs.append(b"X-Host: " + pick(hosts).encode())
+        nh = 0 if rng.random() < 0.1 else (2 if rng.random() < 0.05 else 1)
+        for _ in range(nh):
+            key = pick([b"Host", b"host", b"HOST", b"hOsT", b" Host", b"Host\t", b"\tHOST "])
+            v = pick(hosts).encode()
+            if rng.random() < 0.15:
+                v = b"www." + v
+            if rng.random() < 0.2:
+                v += b":" + str(int(rng.choice([80, 8080, 443]))).encode()
+            r = rng.random()
+            if r < 0.03:
+                v = v[:1] + b"\r" + v[1:]
+            elif r < 0.05:
+                v = b"\xc3" + v
+            pre = pick([b" ", b"", b"  ", b"\t", b" \t"])
+            post = pick([b"", b"", b" ", b"\t", b" \r"])
+            hdrs.insert(int(rng.integers(0, len(hdrs) + 1)), key + b":" + pre + v + post)
+        if rng.random() < 0.02:
+            hdrs.insert(0, b"Broken-Line")                  # the key runs to the next ':'
+        if rng.random() < 0.3:
+            hdrs.append(b"Accept: */*")
+        head = line + b"".join(h + eol for h in hdrs) + eol
+        r = rng.random()
+        if r < 0.08:
+            head = head[:int(rng.integers(0, len(head) + 1))]
+        elif r < 0.12:
+            head += b"GET /second HTTP/1.1" + eol + b"Host: second.example" + eol + eol
+        elif r < 0.15:
+            head += b"x" * int(rng.integers(1, 64))
+        out.append(head)
+    return out

@@ -177,6 +177,8 @@ def lib():
         L.vc_compile_hosts_text.argtypes = [vp, C.c_char_p, i64]
         L.vc_dns_classify_dev.argtypes = [vp, vp, vp, i64, vp, vp, vp]
         L.vc_dns_classify.argtypes = [vp, vp, vp, i64, vp, vp]
+        L.vc_http_hint_dev.argtypes = [vp, vp, i64, vp, i64, vp, vp, vp]
+        L.vc_http_hint.argtypes = [vp, vp, vp, i64, vp, vp]
         L.vc_pipeline_v4_dev.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
         L.vc_pipeline_v4_dev_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                             vp, vp]

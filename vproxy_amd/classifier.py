@@ -533,6 +533,28 @@ class Classifier:
         check(lib().vc_dns_classify(self.h, _ptr(qb), _ptr(qo), n, _ptr(kind), _ptr(val)))
         return kind, val
 
+    def http_hint(self, heads):
+        """HttpContext.connectionHint + Upstream.searchForGroup per HTTP/1
+        request head (vc_http_hint[_dev], HttpContext.java:55-71 over
+        HttpSubContext's request line and headers) -> (group, kind): group =
+        handle index or -1, kind = VC_HTTP_* (0: null hint).  heads: a list
+        of bytes, or (blob, off) torch CUDA tensors (int32 off, n + 1)."""
+        if isinstance(heads, tuple) and _is_dev(heads[0]):
+            import torch
+            hb, ho = heads[0], heads[1]
+            n = len(ho) - 1
+            grp = torch.empty(n, dtype=torch.int32, device=hb.device)
+            kind = torch.empty(n, dtype=torch.uint8, device=hb.device)
+            check(lib().vc_http_hint_dev(self.h, _ptr(hb), hb.numel(), _ptr(ho), n, _ptr(grp),
+                                         _ptr(kind), _stream()))
+            return grp, kind
+        n = len(heads)
+        hb, ho, _ = pack_strings(heads)
+        grp = np.empty(n, np.int32)
+        kind = np.empty(n, np.uint8)
+        check(lib().vc_http_hint(self.h, _ptr(hb), _ptr(ho), n, _ptr(grp), _ptr(kind)))
+        return grp, kind
+
     def dns_datagrams(self, datagrams, remote4, remote_port, remote6=None, remote_family=None):
         """DNSServer's drain loop per datagram (vc_dns_datagrams[_dev],
         DNSServer.java:457-500): securityGroup.allow(UDP, remote, remote

@@ -1211,6 +1211,44 @@ int vc_dns_classify(vc_ctx* ctx, const uint8_t* qblob, const uint32_t* qoff, int
 }
 
 // ---------------------------------------------------------------------------
+// HTTP/1 request heads -> HttpContext.connectionHint -> Upstream.searchForGroup
+// ---------------------------------------------------------------------------
+int vc_http_hint_dev(vc_ctx* ctx, const uint8_t* blob, int64_t blob_bytes, const uint32_t* off,
+                     int64_t n, int32_t* out_group, uint8_t* out_kind, void* stream) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n < 0 || blob_bytes < 0 || (n > 0 && (!blob || !off || !out_group)))
+        return fail(VC_EINVAL, "bad batch arguments");
+    auto h = ctx->get(ctx->hint);
+    if (!h) return fail(VC_ESTATE, "no Upstream compiled");
+    hipError_t e = vc::launch_http_hint(ctx->cfg(stream), h->img, blob, blob_bytes, off, n,
+                                        out_group, out_kind);
+    return launched(ctx, e, stream, "http launch");
+}
+
+int vc_http_hint(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
+                 int32_t* out_group, uint8_t* out_kind) {
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? VC_OK : fail(VC_EINVAL, "negative n");
+    if (!blob || !off || !out_group) return fail(VC_EINVAL, "bad batch arguments");
+    StagerLease lease(ctx);
+    if (!lease) return hip_fail(lease.err(), "http hint");
+    Staging st(ctx, lease.lane(0), "http hint");
+    hipStream_t s = st.stream();
+    auto* db = static_cast<uint8_t*>(st.in(blob, off[n]));
+    auto* dof = static_cast<uint32_t*>(st.in(off, size_t(n + 1) * 4));
+    auto* dg = static_cast<int32_t*>(st.out(out_group, size_t(n) * 4));
+    auto* dk = out_kind ? static_cast<uint8_t*>(st.out(out_kind, size_t(n))) : nullptr;
+    if (st.err != hipSuccess) return hip_fail(st.err, "staging");
+    rc = vc_http_hint_dev(ctx, db, int64_t(off[n]), dof, n, dg, dk, s);
+    if (rc) return rc;
+    st.back(out_group, dg, size_t(n) * 4);
+    if (dk) st.back(out_kind, dk, size_t(n));
+    return st.finish();
+}
+
+// ---------------------------------------------------------------------------
 // SSLContextHolder certificate choice by SNI
 // ---------------------------------------------------------------------------
 int vc_compile_certs(vc_ctx* ctx, const char* const* names, const int32_t* name_lens,

@@ -1023,3 +1023,5 @@ extern "C" int vc_debug_hint_prof(unsigned long long* out) {
 #endif
 
 VC_DEVCHECK_READER(hint)
+
+#include "http_dev.h"

@@ -170,6 +170,11 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
 hipError_t launch_dns(const LaunchCfg& c, const HostsImage& hosts, const HintImage& hints,
                       const uint8_t* qblob, const uint32_t* qoff, int64_t n, uint8_t* kind,
                       int32_t* value, unsigned long long* group_counters);
+// HttpContext.connectionHint + Upstream.searchForGroup over HTTP/1 request
+// heads (http.hip); blob_bytes >= off[n] sizes the launch's scratch
+hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* blob,
+                            int64_t blob_bytes, const uint32_t* off, int64_t n, int32_t* out_group,
+                            uint8_t* out_kind);
 // SSLContextHolder.choose over a batch of SNI names (hint.hip)
 hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
                         const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out);
