@@ -749,8 +749,8 @@ def build_parser():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
-                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "dnsd", "sni", "parse",
-                             "switch", "source", "mirror", "mix", "mixhost"])
+                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "dnsd", "sni", "http",
+                             "parse", "switch", "source", "mirror", "mix", "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1028,6 +1028,34 @@ def c4_workload(dns, n=16 << 20):
         names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
     pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
     return groups, hosts_text() if dns else None, names, pidx
+
+
+def http_workload(n=8 << 20, n_templates=1 << 18):
+    """The `http` sub-bench's inputs (also checked whole by
+    tests/test_gpu_http.py): the C4 groups, a fifth of them with a hint-uri;
+    n_templates seeded HTTP/1 request heads (request line with a path and
+    query, Host with 'www.' / ':port' forms on some, user agent, accept,
+    optional cookie) and the n seeded draws from them that form the batch."""
+    groups, ghosts = W.gen_groups(100_000, W.SEED + 5)
+    paths = ["/", "/api", "/api/v1", "/api/v1/users", "/api/v2", "/static", "/static/img",
+             "/static/img/a.png", "*", "/login", "/a/b/c/d/e/f"]
+    rng = np.random.default_rng(W.SEED + 20)
+    for i in np.nonzero(rng.random(len(groups)) < 0.2)[0]:
+        groups[i][1]["uri"] = paths[int(rng.integers(0, len(paths)))]
+    names = W.gen_hostnames(ghosts, n_templates, W.SEED + 21, port_frac=0.1)
+    tails = ["", "/", "/x", "?q=1", "/?q=2", "/users/7", "/index.html?a=1&b=2"]
+    agents = [b"curl/8.5.0", b"Mozilla/5.0 (X11; Linux x86_64; rv:128.0) Gecko/20100101 Firefox/128.0",
+              b"python-requests/2.32.3", b"Go-http-client/1.1"]
+    heads = []
+    for k in range(n_templates):
+        path = paths[int(rng.integers(0, len(paths)))] + tails[int(rng.integers(0, len(tails)))]
+        h = [b"GET " + path.encode() + b" HTTP/1.1", b"Host: " + names[k],
+             b"User-Agent: " + agents[int(rng.integers(0, len(agents)))], b"Accept: */*"]
+        if rng.random() < 0.3:
+            h.append(b"Cookie: sid=%016x" % int(rng.integers(0, 2**62)))
+        heads.append(b"\r\n".join(h) + b"\r\n\r\n")
+    pidx = np.random.default_rng(W.SEED + 22).integers(0, n_templates, n)
+    return groups, heads, pidx
 
 
 def frames_workload(n=32 << 20):
@@ -1430,6 +1458,38 @@ def sub_bench(args, clf, dev, rank, world):
                 return time.perf_counter() - t0
             cpu = cpu_rates(run, "M items/s", 3.0, "SNIs of the workload, oracle "
                             "SSLContextHolder.choose scan over 100k holders (200k names)", cap=n)
+    elif args.workload == "http":
+        n = 8 << 20
+        groups, heads, pidx = http_workload(n)
+        clf.compile_upstream(groups)
+        hblob_t, hoff_t = W.pack(heads)
+        blob, off, nbytes = gather_strings_dev(hblob_t, hoff_t, pidx, dev)
+        grp = torch.empty(n, dtype=torch.int32, device=dev)
+        kind = torch.empty(n, dtype=torch.uint8, device=dev)
+        fn = lambda: V.check(V.lib().vc_http_hint_dev(
+            clf.h, C.c_void_p(blob.data_ptr()), nbytes, C.c_void_p(off.data_ptr()), n,
+            C.c_void_p(grp.data_ptr()), C.c_void_p(kind.data_ptr()), S()))
+        per_unit, unit, kern = nbytes / n + 9, "B/request head (bytes + 4 offset + 4 group + " \
+                                                "1 kind)", "http_hint_kernel"
+        hb, ho = blob.cpu().numpy(), off.cpu().numpy().view(np.uint32)
+        P = lambda x: C.c_void_p(x.ctypes.data)
+        hg, hk = np.empty(n, np.int32), np.empty(n, np.uint8)
+        extra["end_to_end_host_buffers_M_per_s"] = end_to_end(
+            lambda: V.check(V.lib().vc_http_hint(clf.h, P(hb), P(ho), n, P(hg), P(hk))), n)
+        extra["end_to_end_note"] = ("vc_http_hint on pageable host arrays (heads + offsets in, "
+                                    "group + kind out): chunked H2D + kernel + D2H, synchronous")
+        del hb, ho
+        if O is not None:
+            og = O.Groups(groups)
+
+            def run(k, threads):
+                sb, so = sample_blob(hblob_t, hoff_t, pidx[:k])
+                t0 = time.perf_counter()
+                O.http_batch_np(og, sb, so, nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 4.0, "request heads of the workload, oracle "
+                            "HttpSubContext state machine + searchForGroup scan over 100k groups",
+                            cap=n)
     elif args.workload in ("parse", "mirror", "switch"):
         n = 32 << 20
         frames, pidx = frames_workload(n)

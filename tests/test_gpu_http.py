@@ -88,3 +88,36 @@ def test_edges(clf):
     assert len(g) == 0 and len(k) == 0
     g, k = clf.http_hint([b"", b"G", b"GET /x HTTP/1.1\r\nHost: a.com\r\n\r\n"])
     assert list(g) == [-1, -1, 0] and list(k) == [0, 0, 3]
+
+
+def test_http_bench_batch_whole(clf):
+    """The `http` sub-bench's whole batch (bench.http_workload: 8M draws of
+    262k request heads over the C4 groups, a fifth with hint-uris): every
+    group and kind equal to the oracle's extraction (vo_http_extract) scored
+    by exact.HintLevelChecker (Hint.matchLevel + searchForGroup's strict
+    '>', Upstream.java:187-198), itself checked against vo_http_hint on a
+    sample of the heads."""
+    import torch
+    import bench as B
+    from exact import HintLevelChecker
+    n = 8 << 20
+    groups, heads, pidx = B.http_workload(n)
+    clf.compile_upstream(groups)
+    tb, to = B.W.pack(heads)
+    blob, off, nbytes = B.gather_strings_dev(tb, to, pidx, "cuda")
+    grp, kind = clf.http_hint((blob, off))
+    torch.cuda.synchronize()
+    og = O.Groups(groups)
+    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    want_g = np.empty(len(heads), np.int32)
+    want_k = np.empty(len(heads), np.uint8)
+    for t, h in enumerate(heads):
+        u, host = O.http_extract(h)
+        want_k[t] = (2 if host is not None else 0) | (1 if u is not None else 0)
+        want_g[t] = chk(host, 0, u) if want_k[t] else -1
+    rng = np.random.default_rng(5)
+    for t in rng.integers(0, len(heads), 200):
+        assert O.http_hint(og, heads[t]) == (want_g[t], want_k[t])
+    np.testing.assert_array_equal(grp.cpu().numpy(), want_g[pidx])
+    np.testing.assert_array_equal(kind.cpu().numpy(), want_k[pidx])
+    assert (want_g >= 0).mean() > 0.5

@@ -792,16 +792,24 @@ __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr
         if (img.wildcard_slot >= 0) consider_host_slot(img, img.wildcard_slot, host, port, uri, &b);
     }
     if (uri.n >= 0) {
+        // Members of one hint-uri share its uri level c, so member g scores
+        // (hostLevel(g) << 10) + c.  With port 0 no hint-port excludes any,
+        // and a member with hostLevel > 0 sits in a host slot probed above,
+        // scored exactly there; so the list's first member (scored exactly)
+        // decides what the list can add: HTTP hints (port 0) under a "/" or
+        // "*" hint-uri shared by thousands of groups no longer scan them all.
         KeySlot k;
         uint32_t h = kFnvBasis;
         for (int j = 0; j <= uri.n; ++j) {
             if (uri_probe(img, h, uri.p, j, &k) >= 0)
-                consider_members(img, k.list_off, k.list_cnt, host, port, uri, &b);
+                consider_members(img, k.list_off, port == 0 && k.list_cnt ? 1u : k.list_cnt,
+                                 host, port, uri, &b);
             if (j < uri.n) h = fnv_step(h, uri.p[j]);
         }
         if (img.uri_star_slot >= 0) {
             const KeySlot u = load_slot(img.uri_slots, uint32_t(img.uri_star_slot));
-            consider_members(img, u.list_off, u.list_cnt, host, port, uri, &b);
+            consider_members(img, u.list_off, port == 0 && u.list_cnt ? 1u : u.list_cnt, host,
+                             port, uri, &b);
         }
     }
     return b.idx;
