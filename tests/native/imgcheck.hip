@@ -48,6 +48,8 @@ HintImage hint_img(const vc::HintBuilt& b) {
     h.wildcard_slot = b.wildcard_slot;
     h.uri_star_slot = b.uri_star_slot;
     h.has_uri_keys = b.has_uri_keys;
+    h.uri_len_lo = uint32_t(b.uri_len_mask);
+    h.uri_len_hi = uint32_t(b.uri_len_mask >> 32);
     if (b.wildcard_slot >= 0) {
         const auto& w = b.host.recs[size_t(b.wildcard_slot)];
         h.wild_len_pm = w.len_pm;

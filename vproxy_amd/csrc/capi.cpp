@@ -1080,6 +1080,8 @@ int vc_compile_upstream(vc_ctx* ctx, const vc_group_annos* groups, int n) {
     s->img.wildcard_slot = b.wildcard_slot;
     s->img.uri_star_slot = b.uri_star_slot;
     s->img.has_uri_keys = b.has_uri_keys;
+    s->img.uri_len_lo = uint32_t(b.uri_len_mask);
+    s->img.uri_len_hi = uint32_t(b.uri_len_mask >> 32);
     if (b.wildcard_slot >= 0) {
         const auto& w = b.host.recs[size_t(b.wildcard_slot)];
         s->img.wild_len_pm = w.len_pm;

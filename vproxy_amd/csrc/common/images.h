@@ -188,6 +188,9 @@ struct HintImage {
     // so a miss picks the wildcard without a dependent load
     uint32_t wild_len_pm;
     int32_t wild_a, wild_b;
+    // hint-uri key lengths present: bit l (l < 63) for length l, bit 63 for
+    // any length >= 63 (the general search probes only those prefixes)
+    uint32_t uri_len_lo, uri_len_hi;
 };
 
 struct HostsImage {

@@ -545,6 +545,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         }
         if (U) {
             out->has_uri_keys = 1;
+            out->uri_len_mask |= uint64_t(1) << (Un < 63 ? Un : 63);
             std::string k(U, Un);
             auto it = urik.find(k);
             if (it == urik.end()) {
@@ -847,6 +848,7 @@ uint64_t digest(const HintBuilt& b) {
     d.vec(b.groups);
     d.word(uint64_t(uint32_t(b.n_groups)) | uint64_t(uint32_t(b.wildcard_slot)) << 32);
     d.word(uint64_t(uint32_t(b.uri_star_slot)) | uint64_t(uint32_t(b.has_uri_keys)) << 32);
+    d.word(b.uri_len_mask);
     return d.h;
 }
 

@@ -78,6 +78,7 @@ struct HintBuilt {
     std::vector<int32_t> groups;         // 8 words per GroupRec
     int32_t n_groups = 0;
     int32_t wildcard_slot = -1, uri_star_slot = -1, has_uri_keys = 0;
+    uint64_t uri_len_mask = 0;           // HintImage.uri_len_lo / _hi
 };
 
 int build_hints(const vc_group_annos* groups, int n, HintBuilt* out);

@@ -800,8 +800,9 @@ __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr
         // "*" hint-uri shared by thousands of groups no longer scan them all.
         KeySlot k;
         uint32_t h = kFnvBasis;
+        const uint64_t lens = uint64_t(img.uri_len_hi) << 32 | img.uri_len_lo;
         for (int j = 0; j <= uri.n; ++j) {
-            if (uri_probe(img, h, uri.p, j, &k) >= 0)
+            if (((lens >> (j < 63 ? j : 63)) & 1u) && uri_probe(img, h, uri.p, j, &k) >= 0)
                 consider_members(img, k.list_off, port == 0 && k.list_cnt ? 1u : k.list_cnt,
                                  host, port, uri, &b);
             if (j < uri.n) h = fnv_step(h, uri.p[j]);

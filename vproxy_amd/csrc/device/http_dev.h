@@ -13,12 +13,12 @@
 // stores a header on the next byte).  Parsing stops at the empty line that
 // ends the headers (state 9); bytes after it are not read.
 //
-// A span that is plain ASCII with no CR inside is matched in place.  Any
-// other is rewritten first into the launch's scratch, in the region three
-// times the span's offset: CR bytes dropped and every byte >= 0x80 as the
-// UTF-8 of the Java char (char) b = U+FF00 | b (EF, BC | b >> 6,
-// 80 | b & 3F), as the compiled annotations hold Java strings in UTF-8
-// (the DNS path does the same, hint_dev.h).
+// The two strings are then written out for the search -- CR bytes dropped
+// and every byte >= 0x80 as the UTF-8 of the Java char (char) b = U+FF00 | b
+// (EF, BC | b >> 6, 80 | b & 3F), as the compiled annotations hold Java
+// strings in UTF-8 (the DNS path does the same, hint_dev.h) -- into the
+// lane's LDS buffer, or when longer than it into the launch's scratch, in
+// the region three times the span's offset.
 // Included once, at the end of hint.hip (hint_dev.h's out-of-line
 // functions belong to that translation unit).
 #pragma once
@@ -26,14 +26,20 @@
 namespace vcd {
 
 constexpr int kHttpBlock = 256;
+constexpr int kHttpWaves = kHttpBlock / 64;
+constexpr uint32_t kHttpStage = 10240;     // bytes of heads staged per wave (64 heads)
 
-// Byte i of an item through 16-byte aligned loads, one block cached.  An
-// aligned block holding a byte of the item lies inside that byte's page, so
-// the bytes around the item it also reads cannot fault.
+// Byte i of an item in global memory through 16-byte aligned loads, one
+// block cached.  An aligned block holding a byte of the item lies inside
+// that byte's page, so the bytes around the item it also reads cannot
+// fault.  (Used for chunks the stage cannot hold and for unaligned blobs.)
 struct HeadCur {
     uintptr_t base;
     uintptr_t blk = ~uintptr_t(0);
     uint4 v{0, 0, 0, 0};
+    __device__ __forceinline__ const uint8_t* ptr() const {
+        return reinterpret_cast<const uint8_t*>(base);
+    }
     __device__ __forceinline__ uint32_t at(int i) {
         const uintptr_t a = base + uintptr_t(i);
         const uintptr_t b = a & ~uintptr_t(15);
@@ -47,6 +53,13 @@ struct HeadCur {
     }
 };
 
+// A head staged in the wave's LDS copy.
+struct StagedCur {
+    const uint8_t* p;
+    __device__ __forceinline__ const uint8_t* ptr() const { return p; }
+    __device__ __forceinline__ uint32_t at(int i) { return p[i]; }
+};
+
 struct HttpFields {
     int us = 0, ue = 0;        // theUri: [us, ue) minus CR
     int hs = 0, he = 0;        // theHostHeader: [hs, he) minus CR (already trimmed)
@@ -56,7 +69,8 @@ struct HttpFields {
 __device__ __forceinline__ bool ws(uint32_t b) { return b <= 0x20u; }   // String.trim
 
 // The request line and headers of one head (HttpSubContext states 0-8).
-__device__ HttpFields http_fields(HeadCur& c, int n) {
+template <class Cur>
+__device__ HttpFields http_fields(Cur& c, int n) {
     HttpFields f;
     int i = 0;
     while (i < n && c.at(i) != ' ') ++i;             // state 1: method
@@ -101,14 +115,18 @@ __device__ HttpFields http_fields(HeadCur& c, int n) {
 }
 
 // The Java string of head bytes [s, e) minus CR: in place when plain ASCII
-// without CR, else rewritten into out (3 * (e - s) bytes at most).
-__device__ DStr http_str(HeadCur& c, const uint8_t* head, int s, int e, uint8_t* out) {
+// without CR; else written to out (3 * (e - s) bytes at most) -- CR dropped
+// and every byte >= 0x80 as the UTF-8 of the Java char (char) b =
+// U+FF00 | b (EF, BC | b >> 6, 80 | b & 3F), as the compiled annotations
+// hold Java strings in UTF-8 (the DNS path does the same, hint_dev.h).
+template <class Cur>
+__device__ DStr http_str(Cur& c, int s, int e, uint8_t* out) {
     bool plain = true;
     for (int j = s; j < e; ++j) {
         const uint32_t b = c.at(j);
-        if (b == '\r' || b >= 0x80u) plain = false;
+        plain = plain && b != '\r' && b < 0x80u;
     }
-    if (plain) return DStr{head + s, e - s};
+    if (plain) return DStr{c.ptr() + s, e - s};
     int k = 0;
     for (int j = s; j < e; ++j) {
         const uint32_t b = c.at(j);
@@ -124,28 +142,58 @@ __device__ DStr http_str(HeadCur& c, const uint8_t* head, int s, int e, uint8_t*
     return DStr{out, k};
 }
 
+// One head: (group, kind).  Rewritten strings go to the launch's scratch,
+// in the region three times the span's blob offset `a + s`.
+template <class Cur>
+__device__ __forceinline__ int32_t http_one(const HintImage& img, Cur& c, int n, uint32_t a,
+                                            uint8_t* scratch, uint8_t* kind_out, int abl) {
+    const HttpFields f = http_fields(c, n);
+    const uint8_t kind = uint8_t((f.host ? 2 : 0) | (f.uri ? 1 : 0));
+    *kind_out = kind;
+    if (!kind || abl == 1) return -1;
+    // HttpContext.connectionHint: ofUri / ofHost / ofHostUri, port 0
+    DStr host{nullptr, -1}, uri{nullptr, -1};
+    if (f.host) host = format_host(http_str(c, f.hs, f.he, scratch + 3 * (int64_t(a) + f.hs)));
+    if (f.uri) uri = format_uri(http_str(c, f.us, f.ue, scratch + 3 * (int64_t(a) + f.us)));
+    if (abl == 2) return host.n + uri.n;
+    return search_for_group(img, host, 0, uri);
+}
+
+// kStage: each wave takes 64 consecutive heads at a time and copies their
+// bytes into its LDS stage with coalesced loads (stage.h), so a lane walks
+// its head in LDS: reading each head from global memory lane by lane made
+// the wave wait on a load whenever any lane crossed into a new 16-byte
+// block -- nearly every byte.  A chunk whose heads exceed the stage is read
+// from global memory.  The blob must be dword aligned (launch_http_hint).
+template <bool kStage>
 __global__ __launch_bounds__(kHttpBlock) void http_hint_kernel(
     HintImage img, const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n,
-    uint8_t* __restrict__ scratch, int32_t* __restrict__ out_group, uint8_t* __restrict__ out_kind) {
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-         i += int64_t(gridDim.x) * blockDim.x) {
-        const uint32_t a = off[i], z = off[i + 1];
-        const uint8_t* head = blob + a;
-        HeadCur c{reinterpret_cast<uintptr_t>(head)};
-        const HttpFields f = http_fields(c, int(z - a));
-        const uint8_t kind = uint8_t((f.host ? 2 : 0) | (f.uri ? 1 : 0));
+    uint8_t* __restrict__ scratch, int32_t* __restrict__ out_group, uint8_t* __restrict__ out_kind,
+    int abl) {
+    __shared__ uint32_t stage[kStage ? kHttpWaves : 1][kStage ? (kHttpStage + 2 * kApron) / 4 : 1];
+    const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    const int64_t nchunks = (n + 63) / 64;
+    const int64_t waves = int64_t(gridDim.x) * kHttpWaves;
+    for (int64_t ch = int64_t(blockIdx.x) * kHttpWaves + w; ch < nchunks; ch += waves) {
+        const int64_t base = ch * 64, i = base + lane;
+        const LaneSpan sp = lane_span(off, base, n);
+        uint32_t o0, o1, a0 = 0;
+        span_of(sp, base, n, &o0, &o1);
+        const bool staged = kStage && stage_wave<kHttpStage>(blob, o0, o1, stage[w], &a0);
+        uint8_t kind = 0;
         int32_t g = -1;
-        if (kind) {
-            // HttpContext.connectionHint: ofUri / ofHost / ofHostUri, port 0
-            DStr host{nullptr, -1}, uri{nullptr, -1};
-            if (f.host)
-                host = format_host(http_str(c, head, f.hs, f.he, scratch + 3 * (int64_t(a) + f.hs)));
-            if (f.uri)
-                uri = format_uri(http_str(c, head, f.us, f.ue, scratch + 3 * (int64_t(a) + f.us)));
-            g = search_for_group(img, host, 0, uri);
+        if (i < n) {
+            if (staged) {
+                StagedCur c{reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (sp.a - a0)};
+                g = http_one(img, c, int(sp.e - sp.a), sp.a, scratch, &kind, abl);
+            } else {
+                HeadCur c{reinterpret_cast<uintptr_t>(blob + sp.a)};
+                g = http_one(img, c, int(sp.e - sp.a), sp.a, scratch, &kind, abl);
+            }
+            out_group[i] = g;
+            if (out_kind) out_kind[i] = kind;
         }
-        out_group[i] = g;
-        if (out_kind) out_kind[i] = kind;
+        if (kStage) wave_done();
     }
 }
 
@@ -163,11 +211,20 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
                                                   c.stream, &slot, &scratch)
                              : hipErrorInvalidValue;
     if (e != hipSuccess) return e;
-    const int64_t want = (n + vcd::kHttpBlock - 1) / vcd::kHttpBlock;
-    const int grid = resident_grid(c, reinterpret_cast<const void*>(vcd::http_hint_kernel),
-                                   vcd::kHttpBlock, 0, want);
-    hipLaunchKernelGGL(vcd::http_hint_kernel, dim3(grid), dim3(vcd::kHttpBlock), 0, c.stream, img,
-                       blob, off, n, scratch, out_group, out_kind);
+    // timing-only ablations (VC_ABL_HTTP): 1 parse only, 2 parse + copies, no search
+    static const int abl = [] {
+        const char* v = std::getenv("VC_ABL_HTTP");
+        return v ? std::atoi(v) : 0;
+    }();
+    const int64_t want = (n + 64 * vcd::kHttpWaves - 1) / (64 * vcd::kHttpWaves);
+    auto go = [&](auto kernel) {
+        const int grid = resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHttpBlock,
+                                       0, want);
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kHttpBlock), 0, c.stream, img, blob, off,
+                           n, scratch, out_group, out_kind, abl);
+    };
+    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0) go(vcd::http_hint_kernel<true>);
+    else go(vcd::http_hint_kernel<false>);
     e = hipGetLastError();
     const hipError_t e2 = c.scratch->release(slot, c.stream);
     return e != hipSuccess ? e : e2;
