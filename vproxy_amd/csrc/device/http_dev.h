@@ -156,6 +156,8 @@ __device__ __forceinline__ int32_t http_one(const HintImage& img, Cur& c, int n,
     if (f.host) host = format_host(http_str(c, f.hs, f.he, scratch + 3 * (int64_t(a) + f.hs)));
     if (f.uri) uri = format_uri(http_str(c, f.us, f.ue, scratch + 3 * (int64_t(a) + f.us)));
     if (abl == 2) return host.n + uri.n;
+    if (abl == 3) return search_for_group(img, host, 0, DStr{nullptr, -1});   // host only
+    if (abl == 4) return search_for_group(img, DStr{nullptr, -1}, 0, uri);    // uri only
     return search_for_group(img, host, 0, uri);
 }
 
@@ -211,7 +213,8 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
                                                   c.stream, &slot, &scratch)
                              : hipErrorInvalidValue;
     if (e != hipSuccess) return e;
-    // timing-only ablations (VC_ABL_HTTP): 1 parse only, 2 parse + copies, no search
+    // timing-only ablations (VC_ABL_HTTP): 1 parse only, 2 parse + copies, no search,
+    // 3 search with the host alone, 4 with the uri alone
     static const int abl = [] {
         const char* v = std::getenv("VC_ABL_HTTP");
         return v ? std::atoi(v) : 0;
