@@ -84,6 +84,12 @@ public final class GpuClassifier {
     public static native void classifyDns(long ctx, ByteBuffer qBlob, ByteBuffer qOff, int n,
                                           ByteBuffer outKind, ByteBuffer outValue) throws IOException;
 
+    /** The first read of each new HTTP/1 connection (blob + n + 1 int offsets): group = handle
+     *  index of HttpContext.connectionHint's Upstream.searchForGroup or -1, kind = VC_HTTP_*
+     *  (0: the hint is null). */
+    public static native void httpHint(long ctx, ByteBuffer heads, ByteBuffer off, int n,
+                                       ByteBuffer outGroup, ByteBuffer outKind) throws IOException;
+
     /** A Switch drain-loop batch: family (4/6), proto, src4, dst4, src6, dst6, dport, host ids. */
     public static native void pipeline(long ctx, ByteBuffer family, ByteBuffer proto, ByteBuffer src4,
                                        ByteBuffer dst4, ByteBuffer src6, ByteBuffer dst6, ByteBuffer dport,

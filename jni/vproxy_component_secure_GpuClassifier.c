@@ -311,6 +311,21 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_classifyDns
     jni_throw(env, vc_dns_classify(CTX(ctx), b, (const uint32_t *) o, n, k, v));
 }
 
+/* HttpContext.connectionHint + Upstream.searchForGroup for the first read
+ * of each new HTTP/1 connection (blob + n + 1 int offsets) */
+JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_httpHint
+  (JNIEnv *env, jclass self, jlong ctx, jobject heads, jobject off, jint n, jobject outGroup,
+   jobject outKind) {
+    int bad = 0;
+    const int32_t *o = offsets(env, off, n, 1, &bad);
+    const uint8_t *b = bad ? NULL : req(env, heads, end_of(o, n), &bad);
+    int32_t *g = buf(env, outGroup, (int64_t) n * 4, &bad);
+    uint8_t *k = buf(env, outKind, n, &bad);
+    (void) self;
+    if (bad) return;
+    jni_throw(env, vc_http_hint(CTX(ctx), b, (const uint32_t *) o, n, g, k));
+}
+
 /* The vswitch drain loop's batch: ACL + route (+ pool group) per packet,
  * IPv4 and IPv6 together (vc_packets / vc_pipeline_out field order) */
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_pipeline

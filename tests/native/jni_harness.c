@@ -98,6 +98,7 @@ void J(switchClassify)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jo
 
 void J(compileCerts)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jint, jint);
 void J(classifyDns)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jobject, jobject);
+void J(httpHint)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jobject, jobject);
 void J(pipelineCompact6)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject,
                         jobject, jint, jobject, jobject, jobject, jint, jint, jobject, jobject,
                         jobject, jobject);
@@ -421,6 +422,30 @@ static void gpu_mode(void) {
         CHECK(memcmp(r1, r2, sizeof r1) == 0 && memcmp(r3, r2, sizeof r2) == 0,
               "hints through the shim (twice) == the C ABI");
         CHECK(r2[0] == 0 && r2[3] == -1, "a.example.com -> group 0, nope.org -> null");
+        {   /* HTTP/1 request heads through the shim == the C ABI (same Upstream) */
+            static const char *heads[4] = {
+                "GET /x HTTP/1.1\r\nHost: a.example.com\r\n\r\n",
+                "GET /y HTTP/1.1\r\nHost: www.a.example.com:80\r\nAccept: x\r\n\r\n",
+                "GET /z HTTP/1.1\r\nhost: nope.org\r\n\r\n", "GET"};
+            static uint8_t hb[256], k1[4], k2[4];
+            static int32_t ho[5], g1[4], g2[4];
+            struct _jobject bhb = B(hb, sizeof hb), bho = B(ho, sizeof ho), bg1 = B(g1, sizeof g1),
+                            bk1 = B(k1, sizeof k1);
+            int q = 0;
+            for (k = 0; k < 4; ++k) {
+                ho[k] = q;
+                memcpy(hb + q, heads[k], strlen(heads[k]));
+                q += (int) strlen(heads[k]);
+            }
+            ho[4] = q;
+            J(httpHint)(env, NULL, h, &bhb, &bho, 4, &bg1, &bk1);
+            CHECK(!n_thrown, "httpHint");
+            CHECK(vc_http_hint(ctx, hb, (const uint32_t *) ho, 4, g2, k2) == VC_OK, "vc_http_hint");
+            CHECK(memcmp(g1, g2, sizeof g1) == 0 && memcmp(k1, k2, sizeof k1) == 0,
+                  "HTTP heads through the shim == the C ABI");
+            CHECK(g2[0] == 0 && g2[2] == -1 && k2[0] == 3 && k2[3] == 0,
+                  "Host a.example.com -> group 0, nope.org -> null, a bare method -> no hint");
+        }
     }
     {   /* source hashing through the shim: compile, health update, select ==
          * the C ABI; a short health buffer is refused */

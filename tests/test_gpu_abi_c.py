@@ -104,7 +104,8 @@ def test_abi_c_sequence_matches_ctypes_and_oracle(tmp_path):
 def test_jni_shim_on_gpu():
     """The JNI shim under a fake JNIEnv (tests/native/jni_harness.c) against
     the C ABI called directly: ACL, routes, per-VNI routes and two
-    compileUpstream calls from one groups buffer give identical results."""
+    compileUpstream calls from one groups buffer, HTTP request heads and
+    source hashing give identical results."""
     import os
     native = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
     exe = os.path.join(native, "build", "jni_harness")

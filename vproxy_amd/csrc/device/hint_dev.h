@@ -536,6 +536,36 @@ VC_HD uint32_t wildcard_pick_or_defer(const HintImage& img, int port, bool* defe
 // '>' scan, Upstream.java:187-198).
 // ---------------------------------------------------------------------------
 
+// The dots of [s, e), right to left, up to eight (d0 the last found, the
+// leftmost; more: the caller scans on left of d0).
+// Probing the k-th suffix of every lane in the same loop trip keeps a
+// wave's lanes together: probing each at its byte position ran one round
+// of dependent table loads per distinct dot position in the wave.
+struct Dots {
+    int d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, d6 = 0, d7 = 0;
+    int n = 0;
+    bool more = false;
+    VC_HD int at(int k) const {
+        return k == 0 ? d0 : k == 1 ? d1 : k == 2 ? d2 : k == 3 ? d3
+             : k == 4 ? d4 : k == 5 ? d5 : k == 6 ? d6 : d7;
+    }
+};
+
+VC_HD Dots find_dots(const uint8_t* p, int s, int e) {
+    Dots x;
+    for (int j = e - 1; j >= s; --j) {
+        if (p[j] != '.') continue;
+        if (x.n == 8) {
+            x.more = true;
+            break;
+        }
+        x.d7 = x.d6; x.d6 = x.d5; x.d5 = x.d4; x.d4 = x.d3;
+        x.d3 = x.d2; x.d2 = x.d1; x.d1 = x.d0; x.d0 = j;
+        ++x.n;
+    }
+    return x;
+}
+
 // Reference-shaped form over a formatted host [s, e) of a plain string: any
 // number of labels, each dot-suffix probed as it is found.  Out of line: the
 // kernels reach it only for names the fast path does not take.
@@ -550,12 +580,23 @@ __host__ __device__ __noinline__ int32_t host_only_seq(const HintImage& img, con
         if (v != VC_NONE) return int32_t(v);
     }
     uint32_t best = VC_NONE;
-    for (int j = e - 1; j >= s; --j) {
-        if (p[j] != '.') continue;
+    const Dots dots = find_dots(p, s, e);
+    for (int k = 0; k < dots.n; ++k) {
+        const int j = dots.at(k);
         slot = host_lookup(t, q, j + 1, e - j - 1, &r);
         if (slot >= 0) {
             const uint32_t v = pick(img, slot, r, port);
             best = v < best ? v : best;
+        }
+    }
+    if (dots.more) {                    // past the eighth dot from the right
+        for (int j = dots.d0 - 1; j >= s; --j) {
+            if (p[j] != '.') continue;
+            slot = host_lookup(t, q, j + 1, e - j - 1, &r);
+            if (slot >= 0) {
+                const uint32_t v = pick(img, slot, r, port);
+                best = v < best ? v : best;
+            }
         }
     }
     if (best != VC_NONE) return int32_t(best);
@@ -791,10 +832,18 @@ __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr
         const HostTable t = host_table(img);
         const PtrSrc q{host.p};
         Rec r;
-        for (int j = host.n - 1; j >= 0; --j) {
-            if (host.p[j] != '.') continue;
+        const Dots dots = find_dots(host.p, 0, host.n);
+        for (int k = 0; k < dots.n; ++k) {
+            const int j = dots.at(k);
             const int slot = host_lookup(t, q, j + 1, host.n - j - 1, &r);
             if (slot >= 0) consider_host_slot(img, slot, host, port, uri, &b);
+        }
+        if (dots.more) {                // past the eighth dot from the right
+            for (int j = dots.d0 - 1; j >= 0; --j) {
+                if (host.p[j] != '.') continue;
+                const int slot = host_lookup(t, q, j + 1, host.n - j - 1, &r);
+                if (slot >= 0) consider_host_slot(img, slot, host, port, uri, &b);
+            }
         }
         const int slot = host_lookup(t, q, 0, host.n, &r);
         if (slot >= 0) consider_host_slot(img, slot, host, port, uri, &b);
