@@ -60,6 +60,69 @@ struct StagedCur {
     __device__ __forceinline__ uint32_t at(int i) { return p[i]; }
 };
 
+// First i' in [i, n) whose byte is x or y (n if none).  The generic form
+// goes byte by byte; a staged head is read a dword at a time from LDS (the
+// aligned dwords around a staged head lie inside the stage and its apron).
+template <class Cur>
+__device__ __forceinline__ int find2(Cur& c, int i, int n, uint32_t x, uint32_t y) {
+    uint32_t b;
+    while (i < n && (b = c.at(i)) != x && b != y) ++i;
+    return i;
+}
+
+__device__ __forceinline__ int find2(StagedCur& c, int i, int n, uint32_t x, uint32_t y) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(c.p);
+    const uint32_t mx = x * 0x01010101u, my = y * 0x01010101u;
+    while (i < n) {
+        const uintptr_t a = base + uintptr_t(i);
+        const uint32_t sh = uint32_t(a & 3);
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(a - sh) >> (8 * sh);
+        // bytes of w equal to x or y: a zero byte of (w ^ mx) or (w ^ my)
+        const uint32_t zx = w ^ mx, zy = w ^ my;
+        const uint32_t hx = (zx - 0x01010101u) & ~zx & 0x80808080u;
+        const uint32_t hy = (zy - 0x01010101u) & ~zy & 0x80808080u;
+        // the shift brought in zero bytes above the 4 - sh valid ones
+        const uint32_t valid = sh ? ((1u << (8 * (4 - sh))) - 1u) : ~0u;
+        const uint32_t hit = (hx | hy) & valid;
+        if (hit) {
+            const int k = __builtin_ctz(hit) >> 3;
+            return i + k < n ? i + k : n;
+        }
+        i += int(4 - sh);
+    }
+    return n;
+}
+
+// No CR and no byte >= 0x80 in [s, e)?  Generic: byte by byte; staged: a
+// dword at a time.
+template <class Cur>
+__device__ __forceinline__ bool plain_span(Cur& c, int s, int e) {
+    bool plain = true;
+    for (int j = s; j < e; ++j) {
+        const uint32_t b = c.at(j);
+        plain = plain && b != '\r' && b < 0x80u;
+    }
+    return plain;
+}
+
+__device__ __forceinline__ bool plain_span(StagedCur& c, int s, int e) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(c.p);
+    uint32_t bad = 0;
+    for (int j = s; j < e;) {
+        const uintptr_t a = base + uintptr_t(j);
+        const uint32_t sh = uint32_t(a & 3);
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(a - sh) >> (8 * sh);
+        const int take = e - j < int(4 - sh) ? e - j : int(4 - sh);
+        const uint32_t keep = take >= 4 ? ~0u : ((1u << (8 * take)) - 1u);
+        const uint32_t z = w ^ 0x0D0D0D0Du;
+        // a CR byte (zero byte of z; the lowest flag is exact and any flag
+        // means one exists) or a high bit, among the kept bytes
+        bad |= (((z - 0x01010101u) & ~z & 0x80808080u) | (w & 0x80808080u)) & keep;
+        j += take;
+    }
+    return bad == 0;
+}
+
 struct HttpFields {
     int us = 0, ue = 0;        // theUri: [us, ue) minus CR
     int hs = 0, he = 0;        // theHostHeader: [hs, he) minus CR (already trimmed)
@@ -73,17 +136,18 @@ template <class Cur>
 __device__ HttpFields http_fields(Cur& c, int n) {
     HttpFields f;
     int i = 0;
-    while (i < n && c.at(i) != ' ') ++i;             // state 1: method
+    i = find2(c, i, n, ' ', ' ');                   // state 1: method
     if (i >= n) return f;
     const int us = ++i;
     uint32_t b = 0;
-    while (i < n && (b = c.at(i)) != ' ' && b != '\n') ++i;   // state 2: uri
+    i = find2(c, i, n, ' ', '\n');                  // state 2: uri
     if (i >= n) return f;
+    b = c.at(i);
     f.uri = true;
     f.us = us;
     f.ue = i;
     if (b == ' ')
-        while (i < n && c.at(i) != '\n') ++i;        // state 3: version
+        i = find2(c, i, n, '\n', '\n');             // state 3: version
     if (i >= n) return f;
     ++i;
     for (;;) {
@@ -91,11 +155,11 @@ __device__ HttpFields http_fields(Cur& c, int n) {
         while (i < n && (b = c.at(i)) == '\r') ++i;
         if (i >= n || b == '\n') return f;
         const int ks = i;
-        while (i < n && c.at(i) != ':') ++i;         // state 5: the key runs to ':'
+        i = find2(c, i, n, ':', ':');                // state 5: the key runs to ':'
         if (i >= n) return f;
         const int ke = i++;
         const int vs = i;
-        while (i < n && c.at(i) != '\n') ++i;        // state 7: value to LF
+        i = find2(c, i, n, '\n', '\n');             // state 7: value to LF
         if (i + 1 >= n) return f;                    // stored on the next byte (state 8)
         const int ve = i++;
         int a = ks, e = ke;                          // key.trim().toLowerCase() == "host"
@@ -121,12 +185,7 @@ __device__ HttpFields http_fields(Cur& c, int n) {
 // hold Java strings in UTF-8 (the DNS path does the same, hint_dev.h).
 template <class Cur>
 __device__ DStr http_str(Cur& c, int s, int e, uint8_t* out) {
-    bool plain = true;
-    for (int j = s; j < e; ++j) {
-        const uint32_t b = c.at(j);
-        plain = plain && b != '\r' && b < 0x80u;
-    }
-    if (plain) return DStr{c.ptr() + s, e - s};
+    if (plain_span(c, s, e)) return DStr{c.ptr() + s, e - s};
     int k = 0;
     for (int j = s; j < e; ++j) {
         const uint32_t b = c.at(j);
