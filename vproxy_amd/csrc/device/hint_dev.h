@@ -825,12 +825,13 @@ VC_HDN void consider_host_slot(const HintImage& img, int slot, DStr host, int po
 // General searchForGroup: every group with a nonzero level has its hint-host
 // equal to / a dot-suffix of / "*" for the host, or its hint-uri a prefix
 // of / "*" for the uri; those candidate lists are scored exactly.
-__host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr host, int port,
-                                                      DStr uri) {
+// q serves host's bytes (a PtrSrc on host.p, or the LDS stage holding them)
+template <class Src>
+__host__ __device__ __noinline__ int32_t hint_general_src(const HintImage& img, DStr host,
+                                                          const Src& q, int port, DStr uri) {
     Best b;
     if (host.n >= 0) {
         const HostTable t = host_table(img);
-        const PtrSrc q{host.p};
         Rec r;
         const Dots dots = find_dots(host.p, 0, host.n);
         for (int k = 0; k < dots.n; ++k) {
@@ -872,6 +873,11 @@ __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr
         }
     }
     return b.idx;
+}
+
+__host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr host, int port,
+                                                      DStr uri) {
+    return hint_general_src(img, host, PtrSrc{host.p}, port, uri);
 }
 
 VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,

@@ -56,6 +56,7 @@ struct HeadCur {
 // A head staged in the wave's LDS copy.
 struct StagedCur {
     const uint8_t* p;
+    const uint32_t* stage;                // the wave's stage (for LdsSrc)
     __device__ __forceinline__ const uint8_t* ptr() const { return p; }
     __device__ __forceinline__ uint32_t at(int i) { return p[i]; }
 };
@@ -201,6 +202,22 @@ __device__ DStr http_str(Cur& c, int s, int e, uint8_t* out) {
     return DStr{out, k};
 }
 
+// Upstream.searchForGroup(hint); a host read in place from the stage is
+// probed through LdsSrc (two dword reads per word instead of four byte reads)
+__device__ __forceinline__ int32_t http_search(const HintImage& img, HeadCur&, DStr host,
+                                               DStr uri) {
+    return search_for_group(img, host, 0, uri);
+}
+
+__device__ __forceinline__ int32_t http_search(const HintImage& img, StagedCur& c, DStr host,
+                                               DStr uri) {
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(c.stage);
+    if (uri.n < 0 || !img.has_uri_keys || host.n < 0 || host.p < base ||
+        host.p >= base + kApron + kHttpStage)
+        return search_for_group(img, host, 0, uri);
+    return hint_general_src(img, host, LdsSrc{c.stage, int(host.p - base)}, 0, uri);
+}
+
 // One head: (group, kind).  Rewritten strings go to the launch's scratch,
 // in the region three times the span's blob offset `a + s`.
 template <class Cur>
@@ -217,7 +234,7 @@ __device__ __forceinline__ int32_t http_one(const HintImage& img, Cur& c, int n,
     if (abl == 2) return host.n + uri.n;
     if (abl == 3) return search_for_group(img, host, 0, DStr{nullptr, -1});   // host only
     if (abl == 4) return search_for_group(img, DStr{nullptr, -1}, 0, uri);    // uri only
-    return search_for_group(img, host, 0, uri);
+    return http_search(img, c, host, uri);
 }
 
 // kStage: each wave takes 64 consecutive heads at a time and copies their
@@ -245,7 +262,8 @@ __global__ __launch_bounds__(kHttpBlock) void http_hint_kernel(
         int32_t g = -1;
         if (i < n) {
             if (staged) {
-                StagedCur c{reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (sp.a - a0)};
+                StagedCur c{reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (sp.a - a0),
+                            stage[w]};
                 g = http_one(img, c, int(sp.e - sp.a), sp.a, scratch, &kind, abl);
             } else {
                 HeadCur c{reinterpret_cast<uintptr_t>(blob + sp.a)};
