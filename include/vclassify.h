@@ -223,6 +223,7 @@ int vc_dns_classify(vc_ctx *ctx, const uint8_t *qblob, const uint32_t *qoff, int
 #define VC_HTTP_URI       1  /* Hint.ofUri(theUri) */
 #define VC_HTTP_HOST      2  /* Hint.ofHost(theHostHeader) */
 #define VC_HTTP_HOST_URI  3  /* Hint.ofHostUri(theHostHeader, theUri) */
+#define VC_HTTP_BAD_SPAN  0xFF  /* _dev only: off[i + 1] > blob_bytes, not classified (group -1) */
 int vc_http_hint_dev(vc_ctx *ctx, const uint8_t *blob, int64_t blob_bytes, const uint32_t *off,
                      int64_t n, int32_t *out_group, uint8_t *out_kind, void *stream);
 int vc_http_hint(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,

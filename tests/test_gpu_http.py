@@ -121,3 +121,23 @@ def test_http_bench_batch_whole(clf):
     np.testing.assert_array_equal(grp.cpu().numpy(), want_g[pidx])
     np.testing.assert_array_equal(kind.cpu().numpy(), want_k[pidx])
     assert (want_g >= 0).mean() > 0.5
+
+
+def test_dev_span_past_blob_bytes(clf):
+    """vc_http_hint_dev with blob_bytes short of off[n]: the heads reaching
+    past it come back VC_HTTP_BAD_SPAN (0xFF, group -1) and nothing is
+    written past the 3 * blob_bytes scratch; the others are classified."""
+    import ctypes as C
+    import torch
+    clf.compile_upstream([({"host": "a.com"}, {})])
+    heads = [b"GET /x HTTP/1.1\r\nHost: a.com\r\n\r\n", b"GET /\xe4 HTTP/1.1\r\nHost: a.com\r\n\r\n"]
+    raw = b"".join(heads)
+    blob = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    off = torch.tensor([0, len(heads[0]), len(raw)], dtype=torch.int32, device="cuda")
+    grp = torch.empty(2, dtype=torch.int32, device="cuda")
+    kind = torch.empty(2, dtype=torch.uint8, device="cuda")
+    V.check(V.lib().vc_http_hint_dev(clf.h, C.c_void_p(blob.data_ptr()), len(heads[0]) + 3,
+                                     C.c_void_p(off.data_ptr()), 2, C.c_void_p(grp.data_ptr()),
+                                     C.c_void_p(kind.data_ptr()), None))
+    torch.cuda.synchronize()
+    assert grp.tolist() == [0, -1] and kind.tolist() == [3, 0xFF]

@@ -222,7 +222,12 @@ __device__ __forceinline__ int32_t http_search(const HintImage& img, StagedCur& 
 // in the region three times the span's blob offset `a + s`.
 template <class Cur>
 __device__ __forceinline__ int32_t http_one(const HintImage& img, Cur& c, int n, uint32_t a,
-                                            uint8_t* scratch, uint8_t* kind_out, int abl) {
+                                            int64_t blob_bytes, uint8_t* scratch,
+                                            uint8_t* kind_out, int abl) {
+    if (int64_t(a) + n > blob_bytes) {         // the scratch covers 3 * blob_bytes only
+        *kind_out = VC_HTTP_BAD_SPAN;
+        return -1;
+    }
     const HttpFields f = http_fields(c, n);
     const uint8_t kind = uint8_t((f.host ? 2 : 0) | (f.uri ? 1 : 0));
     *kind_out = kind;
@@ -246,8 +251,8 @@ __device__ __forceinline__ int32_t http_one(const HintImage& img, Cur& c, int n,
 template <bool kStage>
 __global__ __launch_bounds__(kHttpBlock) void http_hint_kernel(
     HintImage img, const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n,
-    uint8_t* __restrict__ scratch, int32_t* __restrict__ out_group, uint8_t* __restrict__ out_kind,
-    int abl) {
+    int64_t blob_bytes, uint8_t* __restrict__ scratch, int32_t* __restrict__ out_group,
+    uint8_t* __restrict__ out_kind, int abl) {
     __shared__ uint32_t stage[kStage ? kHttpWaves : 1][kStage ? (kHttpStage + 2 * kApron) / 4 : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     const int64_t nchunks = (n + 63) / 64;
@@ -264,10 +269,10 @@ __global__ __launch_bounds__(kHttpBlock) void http_hint_kernel(
             if (staged) {
                 StagedCur c{reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (sp.a - a0),
                             stage[w]};
-                g = http_one(img, c, int(sp.e - sp.a), sp.a, scratch, &kind, abl);
+                g = http_one(img, c, int(sp.e - sp.a), sp.a, blob_bytes, scratch, &kind, abl);
             } else {
                 HeadCur c{reinterpret_cast<uintptr_t>(blob + sp.a)};
-                g = http_one(img, c, int(sp.e - sp.a), sp.a, scratch, &kind, abl);
+                g = http_one(img, c, int(sp.e - sp.a), sp.a, blob_bytes, scratch, &kind, abl);
             }
             out_group[i] = g;
             if (out_kind) out_kind[i] = kind;
@@ -301,7 +306,7 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
         const int grid = resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHttpBlock,
                                        0, want);
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kHttpBlock), 0, c.stream, img, blob, off,
-                           n, scratch, out_group, out_kind, abl);
+                           n, blob_bytes, scratch, out_group, out_kind, abl);
     };
     if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0) go(vcd::http_hint_kernel<true>);
     else go(vcd::http_hint_kernel<false>);
