@@ -141,3 +141,23 @@ def test_dev_span_past_blob_bytes(clf):
                                      C.c_void_p(kind.data_ptr()), None))
     torch.cuda.synchronize()
     assert grp.tolist() == [0, -1] and kind.tolist() == [3, 0xFF]
+
+
+def test_heads_past_the_stage(clf):
+    """Chunks of 64 heads longer than a wave's 10 KiB stage (kilobyte
+    cookies) take the global-memory path inside the staged kernel; mixed
+    with chunks that stage, every result equals the oracle."""
+    rng = np.random.default_rng(91)
+    groups, _, _ = hint_cases_random(rng, 200, 0)
+    base = http_heads_random(rng, 6000, [h for h in _HOSTS if h], ["/", "/a", "/a/b?x", "*"])
+    heads = []
+    for k, h in enumerate(base):
+        if (k // 64) % 3 == 0:                       # every third chunk: big heads
+            cut = h.find(b"\r\n") + 2 if b"\r\n" in h else len(h)
+            h = h[:cut] + b"Cookie: " + b"c" * int(rng.integers(200, 2000)) + b"\r\n" + h[cut:]
+        heads.append(h)
+    clf.compile_upstream(groups)
+    got, kind = clf.http_hint(heads)
+    want, wkind = _oracle(O.Groups(groups), heads)
+    np.testing.assert_array_equal(kind, wkind)
+    np.testing.assert_array_equal(got, want)
