@@ -308,7 +308,12 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kHttpBlock), 0, c.stream, img, blob, off,
                            n, blob_bytes, scratch, out_group, out_kind, abl);
     };
-    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0) go(vcd::http_hint_kernel<true>);
+    // VC_HTTP_NOSTAGE=1 (measurement only): every chunk through the global-memory path
+    static const bool nostage = [] {
+        const char* v = std::getenv("VC_HTTP_NOSTAGE");
+        return v && v[0] == '1';
+    }();
+    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0 && !nostage) go(vcd::http_hint_kernel<true>);
     else go(vcd::http_hint_kernel<false>);
     e = hipGetLastError();
     const hipError_t e2 = c.scratch->release(slot, c.stream);
