@@ -79,6 +79,44 @@ int vc_create(int device, vc_ctx **out);
 void vc_destroy(vc_ctx *ctx);
 
 /* ------------------------------------------------------------------------ */
+/* Snapshot pins (SURVEY.md §8(b) "Threading").  The reference's readers    */
+/* never wait for a writer: SecurityGroup and Upstream swap copy-on-write    */
+/* lists (core/src/main/java/vproxy/component/secure/SecurityGroup.java:     */
+/* 56-103, core/.../svrgroup/Upstream.java:146-157).  Every vc_compile_*    */
+/* (and vc_servers_set_health) publishes an immutable snapshot under a new  */
+/* generation; a caller that maps result indices back to its own lists pins */
+/* the snapshots its lists describe, binds the pin to the thread that runs  */
+/* the batch, and maps through those lists -- no lock across the compile.   */
+/* ------------------------------------------------------------------------ */
+#define VC_SNAP_ACL       0   /* vc_compile_acl (SecurityGroup) */
+#define VC_SNAP_ROUTE     1   /* vc_compile_routes (RouteTable) */
+#define VC_SNAP_UPSTREAM  2   /* vc_compile_upstream (Upstream) */
+#define VC_SNAP_HOSTS     3   /* vc_compile_hosts[_text] (Resolver.getHosts) */
+#define VC_SNAP_SERVERS   4   /* vc_compile_servers / vc_servers_set_health */
+#define VC_SNAP_CERTS     5   /* vc_compile_certs */
+#define VC_SNAP_MIRROR    6   /* vc_compile_mirror */
+#define VC_SNAP_VNI       7   /* vc_compile_vni_routes (Switch.tables) */
+#define VC_SNAP_ALL       0xFF
+typedef struct vc_pin vc_pin;
+/* Pins the snapshots of the kinds in the bit set `kinds` (1 << VC_SNAP_*)
+ * that are current now.  The pin keeps them (and their device tables)
+ * alive until vc_pin_release; it never blocks a compile, and a compile
+ * never waits for it. */
+int vc_pin_acquire(vc_ctx *ctx, uint32_t kinds, vc_pin **out);
+/* Calls on ctx from the calling thread use pin's snapshots for the kinds
+ * it pinned (the current ones for the others) until the next bind; NULL
+ * unbinds.  A pin may be bound on several threads at once. */
+int vc_pin_bind(vc_ctx *ctx, const vc_pin *pin);
+/* The generation of a pinned snapshot: every publish on a context takes
+ * the next number (from 1, shared by all kinds); 0 = nothing compiled. */
+int vc_pin_generation(const vc_pin *pin, int kind, uint64_t *gen);
+/* Unbinds it from the calling thread if bound there (binding a released
+ * pin on another thread is the caller's error). */
+void vc_pin_release(vc_pin *pin);
+/* The generation of the current snapshot of `kind` (0 = none). */
+int vc_generation(vc_ctx *ctx, int kind, uint64_t *gen);
+
+/* ------------------------------------------------------------------------ */
 /* Network value: base/src/main/java/vproxybase/util/Network.java            */
 /* ------------------------------------------------------------------------ */
 typedef struct vc_net {

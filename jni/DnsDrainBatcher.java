@@ -51,9 +51,11 @@ import java.nio.ByteBuffer;
  * Handler's readable becomes {@code batcher.readable(ctx)}; the UDP list of
  * {@code securityGroup}, the rrsets Upstream and the hosts map are compiled
  * into {@code gpu} after each change (GpuContext.compileSecurityGroup /
- * compileUpstream / compileHostsText).  A batch's outputs are acted on
- * inside GpuContext.batch, so the group indices and hosts values it hands
- * to Host.answer belong to the snapshot the call classified against.
+ * compileUpstream / compileHostsText).  Host.answer gets the batch's
+ * GpuContext.View with the indices, so the group indices and hosts values
+ * map through the lists of the snapshot the call classified against; no
+ * lock is held while the batch is acted on (a recompile never waits for
+ * it, and it never waits for a recompile).
  */
 public final class DnsDrainBatcher {
     public static final int ANSWER = 0, RECURSIVE = 1, RESPONSE = 2, REJECTED = 3,
@@ -71,9 +73,9 @@ public final class DnsDrainBatcher {
         /**
          * handleRequest(p, remote) for the datagram's packet with question q already classified:
          * kind[q] = VC_DNS_HOSTS / GROUP / IP_LITERAL / INTERNAL, value[q] its hosts value, group
-         * index (GpuContext.group), IP family or 0.  Server choice and the records stay in Java.
+         * index (view.group), IP family or 0.  Server choice and the records stay in Java.
          */
-        void answer(IPPort remote, ByteArray data, int nq, byte[] kind, int[] value);
+        void answer(IPPort remote, ByteArray data, int nq, byte[] kind, int[] value, GpuContext.View view);
     }
 
     private final GpuContext gpu;
@@ -175,12 +177,12 @@ public final class DnsDrainBatcher {
         final int m = n;
         pack(m);
         // the native call and every group index of this batch resolve against
-        // one snapshot: a recompile waits for the batch (GpuContext.batch)
+        // one snapshot: the view the call ran on (GpuContext.batch)
         return gpu.batch(c -> GpuClassifier.dnsDatagrams(c, blob, off, m, family, remote4, remote6,
-            remotePort, out), ok -> act(m, ok));
+            remotePort, out), (ok, view) -> act(m, ok, view));
     }
 
-    private boolean act(int m, boolean ok) {
+    private boolean act(int m, boolean ok, GpuContext.View view) {
         for (int i = 0; i < m; ++i) {
             head = i + 1;
             if (!ok) {
@@ -211,7 +213,7 @@ public final class DnsDrainBatcher {
                         kind[q] = out[4].get(i * MAXQ + q);
                         value[q] = out[5].getInt(4 * (i * MAXQ + q));
                     }
-                    host.answer(remotes[i], datas[i], nq, kind, value);
+                    host.answer(remotes[i], datas[i], nq, kind, value, view);
                     break;
                 }
                 default:  // HOST

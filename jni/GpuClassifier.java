@@ -45,6 +45,17 @@ public final class GpuClassifier {
 
     public static native long create(int device) throws IOException;
     public static native void destroy(long ctx);
+
+    /** VC_SNAP_* bits of vc_pin_acquire: the snapshots GpuContext maps result indices through. */
+    public static final int SNAP_ACL = 0, SNAP_ROUTE = 1, SNAP_UPSTREAM = 2, SNAP_HOSTS = 3,
+        SNAP_SERVERS = 4, SNAP_CERTS = 5, SNAP_MIRROR = 6, SNAP_VNI = 7, SNAP_ALL = 0xFF;
+    /** Pins the snapshots of {@code kinds} (bit set of SNAP_*) current now; a handle for bindPin / pinRelease. */
+    public static native long pinAcquire(long ctx, int kinds) throws IOException;
+    /** Calls on ctx from this thread use pin's snapshots (0 = the current ones again). */
+    public static native void bindPin(long ctx, long pin) throws IOException;
+    /** The generation of a pinned snapshot (every publish on a context takes the next one; 0 = none). */
+    public static native long pinGeneration(long pin, int kind) throws IOException;
+    public static native void pinRelease(long pin);
     /** Page-lock and map a long-lived direct buffer once: calls on it become zero-copy. */
     public static native void registerBuffer(ByteBuffer buf) throws IOException;
     public static native void unregisterBuffer(ByteBuffer buf) throws IOException;

@@ -16,8 +16,8 @@ import java.nio.ByteOrder;
 import java.nio.charset.StandardCharsets;
 import java.util.ArrayList;
 import java.util.List;
-import java.util.concurrent.locks.ReentrantReadWriteLock;
-import java.util.function.Function;
+import java.util.concurrent.atomic.AtomicInteger;
+import java.util.function.BiFunction;
 
 /**
  * One libvclassify context (one GPU) with the fallback INTEGRATION.md
@@ -40,13 +40,22 @@ import java.util.function.Function;
  * The Java lists stay live and authoritative: the library only holds
  * compiled snapshots of them, so the fallback needs no state transfer.  The
  * compile helpers pack the lists in the vclassify.h layouts and keep the
- * list each index refers to.  A result maps back to the rule object of the
- * snapshot that produced it because publishing is one critical section:
- * compile* hold the write side of {@code snap} across the native compile
- * and the list swap, and {@link #batch} holds the read side across a
- * batch's native call and its index mapping (aclRule / route / group), so
- * no recompile can land between the two.  Batches on different event-loop
- * threads share the read side and never wait for each other.
+ * list each index refers to.
+ *
+ * <p>Readers never wait for a compile, as the reference's copy-on-write
+ * swaps never make them wait (SecurityGroup.java:56-103,
+ * Upstream.java:146-157).  A {@link View} is one published state: a native
+ * pin of the snapshots (vc_pin_acquire) and the Java lists their indices
+ * refer to.  A compile runs the native compile with no lock a batch takes,
+ * pins what it published, and swaps {@link #view} in one volatile write.
+ * {@link #batch} retains the current view (a compare-and-set, retried only
+ * when a swap raced it), binds its pin to the thread for the native call
+ * (vc_pin_bind), and hands the view to {@code map}, which maps indices
+ * through the view's lists -- those of the snapshot the call classified
+ * against -- with nothing held, so {@code map} may do I/O or even compile.
+ * A replaced view's pin is released when its last batch ends.
+ * tests/native/pin_loop.c replays this protocol on the GPU while the
+ * control thread recompiles C3-size route tables.
  */
 public final class GpuContext {
     // include/vclassify.h struct sizes (tests/test_jni_shim.py checks them
@@ -64,19 +73,82 @@ public final class GpuContext {
     private final String name;
     private volatile boolean dead;
 
-    // the lists the compiled snapshots index into
-    private volatile List<SecurityGroupRule> tcpRules = List.of();
-    private volatile List<SecurityGroupRule> udpRules = List.of();
-    private volatile List<RouteTable.RouteRule> routesV4 = List.of();
-    private volatile List<RouteTable.RouteRule> routesV6 = List.of();
-    private volatile List<Upstream.ServerGroupHandle> handles = List.of();
+    // the current view; every compile replaces it (publish)
+    private volatile View view;
+    // serialises compiles (control threads only): batches never take it
+    private final Object compileLock = new Object();
 
-    // write: a compile + list swap; read: a batch's call + index mapping
-    private final ReentrantReadWriteLock snap = new ReentrantReadWriteLock();
-
-    private GpuContext(long ctx, String name) {
+    private GpuContext(long ctx, String name) throws IOException {
         this.ctx = ctx;
         this.name = name;
+        // nothing compiled: every kind pinned empty, so a batch before the
+        // first publish gets VC_ESTATE (the Java path), never a snapshot its
+        // view has no lists for
+        this.view = new View(GpuClassifier.pinAcquire(ctx, GpuClassifier.SNAP_ALL), List.of(), List.of(),
+            List.of(), List.of(), List.of(), null);
+    }
+
+    /**
+     * One published state: the pinned native snapshots and the Java lists
+     * their result indices refer to.  Immutable.  {@code refs} counts the
+     * holders: 1 for being {@link #view}, 1 per batch running on it.
+     */
+    public static final class View {
+        final long pin;
+        public final List<SecurityGroupRule> tcpRules, udpRules;
+        public final List<RouteTable.RouteRule> routesV4, routesV6;
+        public final List<Upstream.ServerGroupHandle> handles;
+        /** What the caller installed with compileHostsText (its line -> IP list for hosts values). */
+        public final Object hosts;
+        private final AtomicInteger refs = new AtomicInteger(1);
+
+        View(long pin, List<SecurityGroupRule> tcpRules, List<SecurityGroupRule> udpRules,
+             List<RouteTable.RouteRule> routesV4, List<RouteTable.RouteRule> routesV6,
+             List<Upstream.ServerGroupHandle> handles, Object hosts) {
+            this.pin = pin;
+            this.tcpRules = tcpRules;
+            this.udpRules = udpRules;
+            this.routesV4 = routesV4;
+            this.routesV6 = routesV6;
+            this.handles = handles;
+            this.hosts = hosts;
+        }
+
+        View withPin(long p) {
+            return new View(p, tcpRules, udpRules, routesV4, routesV6, handles, hosts);
+        }
+
+        /** false once the view was replaced and its last batch ended (its pin is gone). */
+        boolean retain() {
+            while (true) {
+                int r = refs.get();
+                if (r == 0) {
+                    return false;
+                }
+                if (refs.compareAndSet(r, r + 1)) {
+                    return true;
+                }
+            }
+        }
+
+        void release() {
+            if (refs.decrementAndGet() == 0) {
+                GpuClassifier.pinRelease(pin);
+            }
+        }
+
+        // results -> the Java objects of this view's snapshot
+        public SecurityGroupRule aclRule(Protocol p, int idx) {
+            return idx < 0 ? null : (p == Protocol.TCP ? tcpRules : udpRules).get(idx);
+        }
+
+        public RouteTable.RouteRule route(IP dst, int idx) {
+            return idx < 0 ? null : (dst instanceof IPv4 ? routesV4 : routesV6).get(idx);
+        }
+
+        public Upstream.ServerGroupHandle group(int idx) {
+            return idx < 0 ? null : handles.get(idx);
+        }
     }
 
     /**
@@ -124,19 +196,38 @@ public final class GpuContext {
     }
 
     /**
-     * One batch: the native call, then {@code map} with its outcome (true =
-     * the outputs are valid; false = answer the batch with the Java
-     * classifiers), both under the read side of the snapshot lock, so every
-     * aclRule / route / group lookup inside {@code map} sees the lists of
-     * the snapshot the call classified against.
+     * One batch: the native call on the current view's snapshots, then
+     * {@code map} with its outcome (true = the outputs are valid; false =
+     * answer the batch with the Java classifiers) and that view, whose
+     * aclRule / route / group map the outputs to the objects of the
+     * snapshot that produced them.  No lock is held at any point: a
+     * concurrent compile publishes a new view, and this batch keeps its own.
      */
-    public <T> T batch(Call c, Function<Boolean, T> map) {
-        snap.readLock().lock();
+    public <T> T batch(Call c, BiFunction<Boolean, View, T> map) {
+        View v;
+        do {
+            v = view;
+        } while (!v.retain());      // lost a race with a swap and its last release: read again
+        final long pin = v.pin;
+        boolean ok;
         try {
-            return map.apply(call(c));
+            ok = call(h -> {
+                GpuClassifier.bindPin(h, pin);
+                try {
+                    c.run(h);
+                } finally {
+                    GpuClassifier.bindPin(h, 0);
+                }
+            });
         } finally {
-            snap.readLock().unlock();
+            v.release();            // the outputs are in the caller's buffers: the pin may go
         }
+        return map.apply(ok, v);
+    }
+
+    /** The current view (control-plane reads; a batch gets its own from {@link #batch}). */
+    public View view() {
+        return view;
     }
 
     /** A control-plane call (compile, register): false when it failed and the context is not usable for it. */
@@ -144,18 +235,44 @@ public final class GpuContext {
         return call(c);
     }
 
-    /** A compile and the swap of the lists its indices refer to, as one publish (see the class comment). */
-    private boolean publish(Call compile, Runnable swap) {
-        snap.writeLock().lock();
-        try {
-            boolean ok = control(compile);
-            if (ok) {
-                swap.run();
+    /** Builds the next view from the previous one and the pin of what the compile published. */
+    interface Next {
+        View make(long pin, View old);
+    }
+
+    /**
+     * A compile and the view that describes it: the native compile (no
+     * batch waits for it), a pin of the snapshots it published, and the swap.
+     * Compiles are serialised by {@code compileLock}, so the pin holds
+     * exactly this compile's snapshot beside the ones the old view pinned.
+     */
+    private boolean publish(Call compile, Next next) {
+        synchronized (compileLock) {
+            if (!control(compile)) {
+                return false;
             }
-            return ok;
-        } finally {
-            snap.writeLock().unlock();
+            long pin;
+            try {
+                pin = GpuClassifier.pinAcquire(ctx, GpuClassifier.SNAP_ALL);
+            } catch (IOException e) {
+                return control(c -> {
+                    throw e;
+                });
+            }
+            View old = view;
+            view = next.make(pin, old);
+            old.release();
+            return true;
         }
+    }
+
+    /**
+     * Every other call that publishes a snapshot -- compileServers,
+     * setServerHealth, compileCerts, compileMirror, compileVniRoutes -- goes
+     * through here, so the next batch's view pins it.
+     */
+    public boolean publish(Call compile) {
+        return publish(compile, (pin, old) -> old.withPin(pin));
     }
 
     // ------------------------------------------------------------------
@@ -188,10 +305,8 @@ public final class GpuContext {
             (r.protocol == Protocol.TCP ? tcp : udp).add(r);
         }
         ByteBuffer t = packRules(tcp), u = packRules(udp);
-        return publish(c -> GpuClassifier.compileAcl(c, t, tcp.size(), u, udp.size(), sg.defaultAllow), () -> {
-            tcpRules = tcp;
-            udpRules = udp;
-        });
+        return publish(c -> GpuClassifier.compileAcl(c, t, tcp.size(), u, udp.size(), sg.defaultAllow),
+            (pin, old) -> new View(pin, tcp, udp, old.routesV4, old.routesV6, old.handles, old.hosts));
     }
 
     private static ByteBuffer packRules(List<SecurityGroupRule> rules) {
@@ -213,10 +328,8 @@ public final class GpuContext {
             (r.rule.getIp() instanceof IPv4 ? v4 : v6).add(r);
         }
         ByteBuffer a = packNets(v4), b = packNets(v6);
-        return publish(c -> GpuClassifier.compileRoutes(c, a, v4.size(), b, v6.size()), () -> {
-            routesV4 = v4;
-            routesV6 = v6;
-        });
+        return publish(c -> GpuClassifier.compileRoutes(c, a, v4.size(), b, v6.size()),
+            (pin, old) -> new View(pin, old.tcpRules, old.udpRules, v4, v6, old.handles, old.hosts));
     }
 
     private static ByteBuffer packNets(List<RouteTable.RouteRule> rules) {
@@ -237,16 +350,18 @@ public final class GpuContext {
             putAnnos(g, h.group.getAnnotations(), strings);
         }
         ByteBuffer s = strings.toDirect();
-        return publish(c -> GpuClassifier.compileUpstream(c, g, hs.size(), s), () -> handles = hs);
+        return publish(c -> GpuClassifier.compileUpstream(c, g, hs.size(), s),
+            (pin, old) -> new View(pin, old.tcpRules, old.udpRules, old.routesV4, old.routesV6, hs, old.hosts));
     }
 
     /**
      * The hosts map -> compileHostsText (Resolver.getHosts' text); a hosts
-     * value is the index of the file's valid line, so {@code swap} installs
-     * the caller's line -> IP list of the same text under the same publish.
+     * value is the index of the file's valid line, so {@code lines} (the
+     * caller's line -> IP list of the same text) goes into the same view.
      */
-    public boolean compileHostsText(ByteBuffer text, int len, Runnable swap) {
-        return publish(c -> GpuClassifier.compileHostsText(c, text, len), swap);
+    public boolean compileHostsText(ByteBuffer text, int len, Object lines) {
+        return publish(c -> GpuClassifier.compileHostsText(c, text, len),
+            (pin, old) -> new View(pin, old.tcpRules, old.udpRules, old.routesV4, old.routesV6, old.handles, lines));
     }
 
     /** vc_annos with string slots as offsets into `strings` (-1 = null). */
@@ -269,23 +384,8 @@ public final class GpuContext {
         strings.append(u);
     }
 
-    // ------------------------------------------------------------------
-    // results -> the Java objects of the compiled snapshot (call these
-    // inside batch(): the read side pins the lists to the call's snapshot)
-    // ------------------------------------------------------------------
-    public SecurityGroupRule aclRule(Protocol p, int idx) {
-        return idx < 0 ? null : (p == Protocol.TCP ? tcpRules : udpRules).get(idx);
-    }
-
-    public RouteTable.RouteRule route(IP dst, int idx) {
-        return idx < 0 ? null : (dst instanceof IPv4 ? routesV4 : routesV6).get(idx);
-    }
-
-    public Upstream.ServerGroupHandle group(int idx) {
-        return idx < 0 ? null : handles.get(idx);
-    }
-
     public void close() {
+        view.release();
         GpuClassifier.destroy(ctx);
     }
 

@@ -55,8 +55,12 @@ public final class SwitchDrainBatcher {
 
         void handleEncrypted(String uuid, SelectorEventLoop loop, IPPort remote, VProxyEncryptedPacket p);
 
-        /** The bare branch after VXLanPacket.from succeeded (:688-731), then inputVXLan with the route. */
-        void handleBare(String uuid, SelectorEventLoop loop, IPPort remote, ByteArray data, int route);
+        /**
+         * The bare branch after VXLanPacket.from succeeded (:688-731), then inputVXLan with the route:
+         * an index into the VNI table's lists of the snapshot the batch ran on, which {@code view} pins.
+         */
+        void handleBare(String uuid, SelectorEventLoop loop, IPPort remote, ByteArray data, int route,
+                        GpuContext.View view);
 
         /** The reference body: handleNetworkAndGetVXLanPacket + inputVXLan (:760-774). */
         void handleJava(String uuid, SelectorEventLoop loop, IPPort remote, ByteArray data);
@@ -165,19 +169,19 @@ public final class SwitchDrainBatcher {
     private void dispatch(SelectorEventLoop loop, int n, int nb) {
         final int m = nb;
         if (m == 0) {
-            act(loop, n, true);
+            act(loop, n, true, null);
             return;
         }
-        // route indices resolve against the snapshot that produced them: a
-        // recompile waits for this batch (GpuContext.batch)
+        // route indices resolve against the snapshot that produced them: the
+        // view the call ran on (GpuContext.batch), with no lock held
         gpu.batch(c -> GpuClassifier.switchClassify(c, blob, off, m, LAYER_VXLAN, family,
-            remote4, remote6, host.bindPort(), pktOut, outAcl, outAllow, outRoute), ok -> {
-            act(loop, n, ok);
+            remote4, remote6, host.bindPort(), pktOut, outAcl, outAllow, outRoute), (ok, view) -> {
+            act(loop, n, ok, view);
             return null;
         });
     }
 
-    private void act(SelectorEventLoop loop, int n, boolean ok) {
+    private void act(SelectorEventLoop loop, int n, boolean ok, GpuContext.View view) {
         for (int i = 0; i < n; ++i) {
             String uuid = host.newHandlingUUID();
             if (decrypted[i] != null) {
@@ -200,7 +204,7 @@ public final class SwitchDrainBatcher {
             } else if (st != PKT_OK) {
                 assert Logger.lowLevelDebug(uuid + " invalid packet for vxlan, drop it");
             } else {
-                host.handleBare(uuid, loop, remotes[i], datas[i], outRoute.getInt(4 * k));
+                host.handleBare(uuid, loop, remotes[i], datas[i], outRoute.getInt(4 * k), view);
             }
         }
     }

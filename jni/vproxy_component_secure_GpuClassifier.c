@@ -125,6 +125,36 @@ JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_destroy
     vc_destroy(CTX(ctx));
 }
 
+/* Snapshot pins: GpuContext's views (vc_pin_*).  A pin crosses as a jlong
+ * like the context handle. */
+JNIEXPORT jlong JNICALL Java_vproxy_component_secure_GpuClassifier_pinAcquire
+  (JNIEnv *env, jclass self, jlong ctx, jint kinds) {
+    vc_pin *pin = NULL;
+    (void) self;
+    if (jni_throw(env, vc_pin_acquire(CTX(ctx), (uint32_t) kinds, &pin))) return 0;
+    return (jlong) (intptr_t) pin;
+}
+
+JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_bindPin
+  (JNIEnv *env, jclass self, jlong ctx, jlong pin) {
+    (void) self;
+    jni_throw(env, vc_pin_bind(CTX(ctx), (const vc_pin *) (intptr_t) pin));
+}
+
+JNIEXPORT jlong JNICALL Java_vproxy_component_secure_GpuClassifier_pinGeneration
+  (JNIEnv *env, jclass self, jlong pin, jint kind) {
+    uint64_t g = 0;
+    (void) self;
+    if (jni_throw(env, vc_pin_generation((const vc_pin *) (intptr_t) pin, kind, &g))) return 0;
+    return (jlong) g;
+}
+
+JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_pinRelease
+  (JNIEnv *env, jclass self, jlong pin) {
+    (void) env; (void) self;
+    vc_pin_release((vc_pin *) (intptr_t) pin);
+}
+
 JNIEXPORT void JNICALL Java_vproxy_component_secure_GpuClassifier_registerBuffer
   (JNIEnv *env, jclass self, jobject b) {
     (void) self;

@@ -1,0 +1,84 @@
+"""GPU tier: snapshot pins (include/vclassify.h "Snapshot pins").
+
+A pin keeps the snapshots that were current when it was taken; bound to a
+thread it is what that thread's calls classify against, while other threads
+and unbound calls see every later compile -- the copy-on-write behaviour of
+SecurityGroup.java:56-103 / Upstream.java:146-157, where a reader holding
+the old list keeps reading it.  Generations grow by one per publish.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import vproxy_amd as V
+from vproxy_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _acl(clf, allow_first):
+    clf.compile_acl([("10.0.0.0/8", 0, 65535, allow_first), ("0.0.0.0/0", 80, 80, True)],
+                    [("0.0.0.0/0", 0, 65535, False)], False)
+
+
+def test_pin_keeps_its_snapshot():
+    clf = V.Classifier(0)
+    try:
+        with pytest.raises(V.StateError):
+            with clf.pin():                       # nothing compiled: pinned empty
+                clf.acl_v4(np.array([6], np.uint8), np.array([0x0A000001], np.uint32),
+                           np.array([80], np.uint16))
+        _acl(clf, True)
+        g1 = clf.generation(L.SNAP_ACL)
+        p = clf.pin()
+        assert p.generation(L.SNAP_ACL) == g1 > 0
+        assert p.generation(L.SNAP_ROUTE) == 0          # no routes compiled
+        clf.compile_routes(["10.0.0.0/8"])
+        _acl(clf, False)
+        g2 = clf.generation(L.SNAP_ACL)
+        assert g2 > clf.generation(L.SNAP_ROUTE) > g1
+        proto = np.array([6, 6, 17], np.uint8)
+        src = np.array([0x0A000001, 0x0B000001, 0x0A000001], np.uint32)
+        port = np.array([22, 80, 53], np.uint16)
+        idx_new, allow_new = clf.acl_v4(proto, src, port)
+        with p:
+            idx_old, allow_old = clf.acl_v4(proto, src, port)
+            # the pin holds no route snapshot: routes are VC_ESTATE through it
+            with pytest.raises(V.StateError):
+                clf.route_v4(np.array([0x0A000001], np.uint32))
+            seen = {}
+            t = threading.Thread(target=lambda: seen.update(
+                r=clf.acl_v4(proto, src, port)))          # another thread is not bound
+            t.start()
+            t.join()
+        assert list(idx_old) == list(idx_new) == [0, 1, 0]
+        assert list(allow_old) == [1, 1, 0] and list(allow_new) == [0, 1, 0]
+        assert list(seen["r"][1]) == [0, 1, 0]
+        # a pin of only the route kind leaves the ACL current
+        q = clf.pin(1 << L.SNAP_ROUTE)
+        _acl(clf, True)
+        with q:
+            assert list(clf.acl_v4(proto, src, port)[1]) == [1, 1, 0]
+            assert list(clf.route_v4(np.array([0x0A000001, 0x0B000001], np.uint32))) == [0, -1]
+        with pytest.raises(V.IllegalArgumentException):
+            q.generation(L.SNAP_ACL)                      # not pinned
+        p.release()
+        q.release()
+        # bound pins are gone with their release; unbound calls see the current tables
+        assert list(clf.acl_v4(proto, src, port)[1]) == [1, 1, 0]
+    finally:
+        clf.close()
+
+
+def test_pin_of_another_context_is_refused():
+    a, b = V.Classifier(0), V.Classifier(0)
+    try:
+        _acl(a, True)
+        p = a.pin()
+        with pytest.raises(V.IllegalArgumentException):
+            V.check(V.lib().vc_pin_bind(b.h, p.h))
+        p.release()
+    finally:
+        a.close()
+        b.close()

@@ -11,8 +11,10 @@ from ._lib import (AlreadyExistException, DeviceError, IllegalArgumentException,
                    DNSD_ANSWER, DNSD_RECURSIVE, DNSD_RESPONSE, DNSD_REJECTED, DNSD_EMPTY,
                    DNSD_MALFORMED, DNSD_HOST, DNSD_MAXQ,
                    SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6,
-                   LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6, SWITCH_NO_TABLE)
-from .classifier import (Annotations, Classifier, Network, RouteTable, SecurityGroup,  # noqa: F401
+                   LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6, SWITCH_NO_TABLE,
+                   SNAP_ACL, SNAP_ROUTE, SNAP_UPSTREAM, SNAP_HOSTS, SNAP_SERVERS, SNAP_CERTS,
+                   SNAP_MIRROR, SNAP_VNI, SNAP_ALL)
+from .classifier import (Annotations, Classifier, Network, Pin, RouteTable, SecurityGroup,  # noqa: F401
                          acl_rule_array, group_array, net_array, pack_strings, parse_ip,
                          server_array, cn_of_dn, digest_acl, digest_routes, digest_upstream)
 

@@ -23,6 +23,10 @@ DNSD_MAXQ = 4
 SOURCE_ALL, SOURCE_IPV4, SOURCE_IPV6 = 0, 4, 6
 LAYER_VXLAN, LAYER_ETHER, LAYER_IPV4, LAYER_IPV6 = 0, 1, 4, 6
 SWITCH_NO_TABLE = -2           # vc_switch_classify: the packet's VNI has no table
+# snapshot kinds of vc_pin_acquire / vc_generation (VC_SNAP_*)
+(SNAP_ACL, SNAP_ROUTE, SNAP_UPSTREAM, SNAP_HOSTS, SNAP_SERVERS, SNAP_CERTS, SNAP_MIRROR,
+ SNAP_VNI) = range(8)
+SNAP_ALL = 0xFF
 
 
 class VcNet(C.Structure):
@@ -220,6 +224,13 @@ def lib():
         L.vc_counters_add_dev.argtypes = [vp, i32, vp, vp, i32, i64, vp]
         u64p = P(C.c_uint64)
         L.vc_table_digest.argtypes = [vp, i32, u64p]
+        if hasattr(L, "vc_pin_acquire"):       # (A/B runs load older builds without it)
+            L.vc_pin_acquire.argtypes = [vp, C.c_uint32, P(vp)]
+            L.vc_pin_bind.argtypes = [vp, vp]
+            L.vc_pin_generation.argtypes = [vp, i32, u64p]
+            L.vc_pin_release.argtypes = [vp]
+            L.vc_pin_release.restype = None
+            L.vc_generation.argtypes = [vp, i32, u64p]
         L.vc_digest_acl.argtypes = [P(VcAclRule), i32, P(VcAclRule), i32, i32, u64p]
         L.vc_digest_routes.argtypes = [P(VcNet), i32, P(VcNet), i32, u64p]
         L.vc_digest_upstream.argtypes = [P(VcGroupAnnos), i32, u64p]

@@ -350,6 +350,47 @@ def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+class Pin:
+    """vc_pin: the snapshots current when it was taken.  A `with` block
+    binds it to the calling thread (vc_pin_bind), so that thread's calls on
+    the classifier use them; release() drops it."""
+
+    def __init__(self, clf, kinds=None):
+        self.clf = clf
+        self.h = C.c_void_p()
+        check(lib().vc_pin_acquire(clf.h, _lib.SNAP_ALL if kinds is None else int(kinds),
+                                   C.byref(self.h)))
+
+    def generation(self, kind):
+        g = C.c_uint64()
+        check(lib().vc_pin_generation(self.h, int(kind), C.byref(g)))
+        return g.value
+
+    def bind(self):
+        check(lib().vc_pin_bind(self.clf.h, self.h))
+
+    def unbind(self):
+        check(lib().vc_pin_bind(self.clf.h, None))
+
+    def __enter__(self):
+        self.bind()
+        return self
+
+    def __exit__(self, *exc):
+        self.unbind()
+
+    def release(self):
+        if self.h and self.h.value:
+            lib().vc_pin_release(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:       # interpreter shutdown
+            pass
+
+
 class Classifier:
     """One libvclassify context on one GPU.  Raises DeviceError without a
     usable gfx950 device: there is no CPU path."""
@@ -369,6 +410,18 @@ class Classifier:
             self.close()
         except Exception:
             pass
+
+    # ---------------- snapshots ----------------
+    def pin(self, kinds=None):
+        """Pin the current snapshots (vc_pin_acquire; kinds = bit set of
+        1 << SNAP_*, default all).  `with clf.pin() as p:` binds it to this
+        thread for the block's calls."""
+        return Pin(self, kinds)
+
+    def generation(self, kind):
+        g = C.c_uint64()
+        check(lib().vc_generation(self.h, int(kind), C.byref(g)))
+        return g.value
 
     # ---------------- compile ----------------
     def compile_acl(self, tcp_rules, udp_rules, default_allow):

@@ -299,9 +299,60 @@ struct CertSnap;
 struct MirrorSnap;
 struct VniSnap;
 
+// The published snapshot of every table kind, in VC_SNAP_* order.  A
+// context holds the current set; a vc_pin holds a copy of the slots it
+// pinned.
+template <class S> struct snap_kind;
+template <> struct snap_kind<AclSnap> { static constexpr int value = VC_SNAP_ACL; };
+template <> struct snap_kind<RouteSnap> { static constexpr int value = VC_SNAP_ROUTE; };
+template <> struct snap_kind<HintSnap> { static constexpr int value = VC_SNAP_UPSTREAM; };
+template <> struct snap_kind<HostsSnap> { static constexpr int value = VC_SNAP_HOSTS; };
+template <> struct snap_kind<ServerSnap> { static constexpr int value = VC_SNAP_SERVERS; };
+template <> struct snap_kind<CertSnap> { static constexpr int value = VC_SNAP_CERTS; };
+template <> struct snap_kind<MirrorSnap> { static constexpr int value = VC_SNAP_MIRROR; };
+template <> struct snap_kind<VniSnap> { static constexpr int value = VC_SNAP_VNI; };
+
+struct SnapSet {
+    std::shared_ptr<const AclSnap> acl;
+    std::shared_ptr<const RouteSnap> route;
+    std::shared_ptr<const HintSnap> hint;
+    std::shared_ptr<const HostsSnap> hosts;
+    std::shared_ptr<const ServerSnap> servers;
+    std::shared_ptr<const CertSnap> certs;
+    std::shared_ptr<const MirrorSnap> mirror;
+    std::shared_ptr<const VniSnap> vni;      // Switch.tables (vc_compile_vni_routes)
+
+    template <class S> const std::shared_ptr<const S>& slot() const;
+};
+template <> const std::shared_ptr<const AclSnap>& SnapSet::slot<AclSnap>() const { return acl; }
+template <> const std::shared_ptr<const RouteSnap>& SnapSet::slot<RouteSnap>() const { return route; }
+template <> const std::shared_ptr<const HintSnap>& SnapSet::slot<HintSnap>() const { return hint; }
+template <> const std::shared_ptr<const HostsSnap>& SnapSet::slot<HostsSnap>() const { return hosts; }
+template <> const std::shared_ptr<const ServerSnap>& SnapSet::slot<ServerSnap>() const {
+    return servers;
+}
+template <> const std::shared_ptr<const CertSnap>& SnapSet::slot<CertSnap>() const { return certs; }
+template <> const std::shared_ptr<const MirrorSnap>& SnapSet::slot<MirrorSnap>() const {
+    return mirror;
+}
+template <> const std::shared_ptr<const VniSnap>& SnapSet::slot<VniSnap>() const { return vni; }
+
 }  // namespace
 
-struct vc_ctx {
+// A caller's pin (vc_pin_acquire): the snapshots of `kinds` that were
+// current when it was taken.  Bound to a thread (vc_pin_bind), it is what
+// that thread's classify calls on `ctx` use for those kinds.
+struct vc_pin {
+    vc_ctx* ctx = nullptr;
+    uint32_t kinds = 0;
+    SnapSet s;
+};
+
+namespace {
+thread_local const vc_pin* t_pin = nullptr;
+}  // namespace
+
+struct vc_ctx : SnapSet {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
@@ -315,21 +366,26 @@ struct vc_ctx {
     std::shared_ptr<Graveyard> grave = std::make_shared<Graveyard>();
     std::mutex stage_mu;     // idle stagers (one per concurrent host-buffer call)
     std::vector<std::unique_ptr<Stager>> stagers;
-    std::shared_ptr<const AclSnap> acl;
-    std::shared_ptr<const RouteSnap> route;
-    std::shared_ptr<const HintSnap> hint;
-    std::shared_ptr<const HostsSnap> hosts;
-    std::shared_ptr<const ServerSnap> servers;
-    std::shared_ptr<const CertSnap> certs;
-    std::shared_ptr<const MirrorSnap> mirror;
-    std::shared_ptr<const VniSnap> vni;      // Switch.tables (vc_compile_vni_routes)
+    std::atomic<uint64_t> next_gen{1};       // generation of the next publish (any kind)
 
+    // The snapshot a classify call uses: the calling thread's bound pin
+    // when it pinned this kind (vc_pin_bind), else the current one.
     template <class S>
     std::shared_ptr<const S> get(const std::shared_ptr<const S>& p) const {
+        const vc_pin* pin = t_pin;
+        if (pin && pin->ctx == this && (pin->kinds >> snap_kind<S>::value & 1u))
+            return pin->s.slot<S>();
+        return std::atomic_load(&p);
+    }
+    // The current snapshot whatever the thread has bound (compiles).
+    template <class S>
+    std::shared_ptr<const S> current(const std::shared_ptr<const S>& p) const {
         return std::atomic_load(&p);
     }
     template <class S>
-    void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
+    void publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v);
+    template <class S>
+    void publish_raw(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
         std::atomic_store(&slot, std::move(v));
         // the previous tables' buffers, if no call pins them any more
         grave->drain();
@@ -549,6 +605,7 @@ struct Snapshot {
     unsigned long long* counters = nullptr;
     int64_t n_counters = 0;
     uint64_t digest = 0;           // vc::digest of the host-built image (vc_table_digest)
+    mutable uint64_t gen = 0;      // set once by vc_ctx::publish (vc_pin_generation)
 
     void alloc_counters(Upload& up, int64_t n) {
         counters = up.zeros(*this, n);
@@ -606,6 +663,14 @@ struct ServerSnap : Snapshot {
 
 }  // namespace
 
+// Every publish takes the context's next generation, so a pin can report
+// which compile each of its snapshots came from (vc_pin_generation).
+template <class S>
+void vc_ctx::publish(std::shared_ptr<const S>& slot, std::shared_ptr<const S> v) {
+    if (v) v->gen = next_gen.fetch_add(1, std::memory_order_relaxed);
+    publish_raw(slot, std::move(v));
+}
+
 extern "C" {
 
 const char* vc_version(void) { return "vclassify 0.1 (gfx950)"; }
@@ -658,6 +723,7 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->certs.reset();
     ctx->mirror.reset();
     ctx->vni.reset();
+    if (t_pin && t_pin->ctx == ctx) t_pin = nullptr;
     ctx->grave->drain();
     for (auto& st : ctx->stagers) StagerLease::destroy(st.get());
     ctx->stagers.clear();
@@ -666,6 +732,89 @@ void vc_destroy(vc_ctx* ctx) {
     ctx->scratch.destroy();
     ctx->tickets.destroy();
     delete ctx;
+}
+
+// ---------------------------------------------------------------------------
+// Snapshot pins (SURVEY.md §8(b) "Threading")
+// ---------------------------------------------------------------------------
+static const Snapshot* slot_snap(const SnapSet& s, int kind) {
+    switch (kind) {
+    case VC_SNAP_ACL: return s.acl.get();
+    case VC_SNAP_ROUTE: return s.route.get();
+    case VC_SNAP_UPSTREAM: return s.hint.get();
+    case VC_SNAP_HOSTS: return s.hosts.get();
+    case VC_SNAP_SERVERS: return s.servers.get();
+    case VC_SNAP_CERTS: return s.certs.get();
+    case VC_SNAP_MIRROR: return s.mirror.get();
+    case VC_SNAP_VNI: return s.vni.get();
+    default: return nullptr;
+    }
+}
+
+int vc_pin_acquire(vc_ctx* ctx, uint32_t kinds, vc_pin** out) {
+    if (!ctx || !out) return fail(VC_EINVAL, "null argument");
+    *out = nullptr;
+    if (kinds & ~uint32_t(VC_SNAP_ALL)) return fail(VC_EINVAL, "unknown snapshot kind bits");
+    auto* p = new (std::nothrow) vc_pin();
+    if (!p) return fail(VC_ENOMEM, "pin");
+    p->ctx = ctx;
+    p->kinds = kinds;
+    // each slot on its own atomic load: a compile of one kind publishes
+    // one slot, so the set is what the calls of a batch would have seen
+    // had they started now
+    if (kinds >> VC_SNAP_ACL & 1) p->s.acl = ctx->current(ctx->acl);
+    if (kinds >> VC_SNAP_ROUTE & 1) p->s.route = ctx->current(ctx->route);
+    if (kinds >> VC_SNAP_UPSTREAM & 1) p->s.hint = ctx->current(ctx->hint);
+    if (kinds >> VC_SNAP_HOSTS & 1) p->s.hosts = ctx->current(ctx->hosts);
+    if (kinds >> VC_SNAP_SERVERS & 1) p->s.servers = ctx->current(ctx->servers);
+    if (kinds >> VC_SNAP_CERTS & 1) p->s.certs = ctx->current(ctx->certs);
+    if (kinds >> VC_SNAP_MIRROR & 1) p->s.mirror = ctx->current(ctx->mirror);
+    if (kinds >> VC_SNAP_VNI & 1) p->s.vni = ctx->current(ctx->vni);
+    *out = p;
+    return VC_OK;
+}
+
+int vc_pin_bind(vc_ctx* ctx, const vc_pin* pin) {
+    if (!ctx) return fail(VC_EINVAL, "null context");
+    if (pin && pin->ctx != ctx) return fail(VC_EINVAL, "pin belongs to another context");
+    t_pin = pin;
+    return VC_OK;
+}
+
+int vc_pin_generation(const vc_pin* pin, int kind, uint64_t* gen) {
+    if (!pin || !gen) return fail(VC_EINVAL, "null argument");
+    if (kind < 0 || kind > VC_SNAP_VNI) return fail(VC_EINVAL, "bad snapshot kind");
+    if (!(pin->kinds >> kind & 1)) return fail(VC_EINVAL, "kind not pinned");
+    const Snapshot* s = slot_snap(pin->s, kind);
+    *gen = s ? s->gen : 0;
+    return VC_OK;
+}
+
+void vc_pin_release(vc_pin* pin) {
+    if (!pin) return;
+    if (t_pin == pin) t_pin = nullptr;
+    // the last reference to a replaced snapshot sends its buffers to the
+    // graveyard; the next compile frees them
+    delete pin;
+}
+
+int vc_generation(vc_ctx* ctx, int kind, uint64_t* gen) {
+    if (!ctx || !gen) return fail(VC_EINVAL, "null argument");
+    if (kind < 0 || kind > VC_SNAP_VNI) return fail(VC_EINVAL, "bad snapshot kind");
+    SnapSet cur;
+    switch (kind) {
+    case VC_SNAP_ACL: cur.acl = ctx->current(ctx->acl); break;
+    case VC_SNAP_ROUTE: cur.route = ctx->current(ctx->route); break;
+    case VC_SNAP_UPSTREAM: cur.hint = ctx->current(ctx->hint); break;
+    case VC_SNAP_HOSTS: cur.hosts = ctx->current(ctx->hosts); break;
+    case VC_SNAP_SERVERS: cur.servers = ctx->current(ctx->servers); break;
+    case VC_SNAP_CERTS: cur.certs = ctx->current(ctx->certs); break;
+    case VC_SNAP_MIRROR: cur.mirror = ctx->current(ctx->mirror); break;
+    default: cur.vni = ctx->current(ctx->vni); break;
+    }
+    const Snapshot* s = slot_snap(cur, kind);
+    *gen = s ? s->gen : 0;
+    return VC_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1460,7 +1609,7 @@ int vc_servers_set_health(vc_ctx* ctx, const uint8_t* healthy, int64_t n_servers
     int rc = set_dev(ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->compile_mu);
-    auto s = ctx->get(ctx->servers);
+    auto s = ctx->current(ctx->servers);
     if (!s) return fail(VC_ESTATE, "no servers compiled");
     if (n_servers != s->img.n_servers || (n_servers > 0 && !healthy))
         return fail(VC_EINVAL, "health array does not match the compiled servers");
