@@ -477,6 +477,46 @@ def launch_ranks(n, argv, script=None, env=None, poll_s=0.2, grace_s=20.0):
             signal.signal(s, h)
 
 
+def visible_gpus(environ=None, topology="/sys/class/kfd/kfd/topology/nodes", dri="/dev/dri"):
+    """The GPUs this process's ranks could use, counted without any HIP or
+    HSA call (the parent of the ranks must not initialise the GPU: it
+    spawns them, and on ROCm torch.cuda.device_count() falls back to
+    hipGetDeviceCount when its amdsmi count fails): KFD topology nodes with
+    a non-zero gfx_target_version whose render node /dev/dri/renderD<minor>
+    exists (a container sees the host's nodes but only its own devices; the
+    GPU box hides the other nodes' properties), then the ROCR_VISIBLE_DEVICES,
+    HIP_VISIBLE_DEVICES and CUDA_VISIBLE_DEVICES lists in that order, each
+    cut at its first entry that names no device.  0 without KFD."""
+    environ = os.environ if environ is None else environ
+    n = 0
+    try:
+        nodes = sorted(os.listdir(topology))
+    except OSError:
+        nodes = []
+    for d in nodes:
+        try:
+            with open(os.path.join(topology, d, "properties")) as f:
+                props = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("gfx_target_version", "0")) == 0:
+            continue                                    # a CPU node
+        minor = props.get("drm_render_minor")
+        if minor is not None and os.path.exists(os.path.join(dri, "renderD%s" % minor)):
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = environ.get(var)
+        if v is None:
+            continue
+        k = 0
+        for x in (t.strip() for t in v.split(",")):
+            if not ((x.isdigit() and int(x) < n) or x.startswith("GPU-")):
+                break
+            k += 1
+        n = min(n, k)
+    return n
+
+
 def resolve_world(gpus, environ=None, shared=False, device_count=None):
     """What `--gpus N` means for this process: ("run", world) when it is one
     rank of a launched job (WORLD_SIZE set, and equal to N) or N == 1;
@@ -498,7 +538,7 @@ def resolve_world(gpus, environ=None, shared=False, device_count=None):
         return "run", 1
     if not shared:
         if device_count is None:
-            device_count = torch.cuda.device_count()     # counts only: no HIP context
+            device_count = visible_gpus(environ)         # no HIP call in the ranks' parent
         if device_count < gpus:
             print("bench.py: --gpus %d but %d GPU(s) visible" % (gpus, device_count),
                   file=sys.stderr)
@@ -749,7 +789,7 @@ def build_parser():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
-                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "dns", "dnsd", "sni", "http",
+                    choices=["c5", "c1", "c2", "c2host", "c3", "c4", "c4uri", "dns", "dnsd", "sni", "http",
                              "parse", "switch", "source", "mirror", "mix", "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
@@ -1028,6 +1068,55 @@ def c4_workload(dns, n=16 << 20):
         names = W.gen_hostnames(ghosts, 1 << 20, W.SEED + 6)
     pidx = np.random.default_rng(W.SEED + (8 if dns else 7)).integers(0, len(names), n)
     return groups, hosts_text() if dns else None, names, pidx
+
+
+URI_PATHS = ["/", "/api", "/api/v1", "/api/v1/users", "/api/v2", "/static", "/static/img",
+             "/static/img/a.png", "*", "/login", "/a/b/c/d/e/f"]
+URI_TAILS = ["", "/", "/x", "?q=1", "/?q=2", "/users/7"]
+
+
+def c4uri_workload(n=16 << 20, n_groups=100_000, n_names=1 << 20, seed_off=0):
+    """The `c4uri` sub-bench's inputs (also checked whole by
+    tests/test_gpu_c4uri.py): the hint the L7 callers send,
+    Hint.ofHostUri(Host, uri) with port 0 (HttpContext.java:63-69,
+    httpbin/Stream.java:50), scored by the whole Hint.matchLevel
+    (Hint.java:100-160).  The C4 groups with a fifth carrying a hint-uri and
+    200 uri-only groups (the generator of test_hint_uri_levels_at_scale), the
+    n_groups / 20 path-routed groups (an earlier group's hint-host with a
+    hint-uri), the C4 hostnames (n_names distinct, 10 % with ':port'), the
+    66 uris of
+    URI_PATHS x URI_TAILS; n seeded (name, uri) draws, 80 % with a uri.
+    -> groups, names, uris, name index per hint, uri index per hint (-1 =
+    null uri)."""
+    groups, ghosts = W.gen_groups(n_groups, W.SEED + 5 + seed_off)
+    rng = np.random.default_rng(81 + seed_off)
+    for i in np.nonzero(rng.random(len(groups)) < 0.2)[0]:
+        groups[i][1]["uri"] = URI_PATHS[int(rng.integers(0, len(URI_PATHS)))]
+    groups += [({}, {"uri": URI_PATHS[k % len(URI_PATHS)] +
+                     ("/u%d" % k if k > len(URI_PATHS) else "")}) for k in range(200)]
+    # path-routed backends: n_groups / 20 more groups sharing the hint-host
+    # of an earlier group, each with a hint-uri, so that for their hosts the
+    # uri level picks the group
+    for h in rng.integers(0, len(ghosts), n_groups // 20):
+        groups.append(({}, {"host": ghosts[int(h)],
+                            "uri": URI_PATHS[int(rng.integers(0, len(URI_PATHS)))]}))
+    names = W.gen_hostnames(ghosts, n_names, W.SEED + 6 + seed_off)
+    uris = [(p + t).encode() for p in URI_PATHS for t in URI_TAILS]
+    r = np.random.default_rng(W.SEED + 24 + seed_off)
+    nidx = r.integers(0, len(names), n)
+    uidx = np.where(r.random(n) < 0.8, r.integers(0, len(uris), n), -1)
+    return groups, names, uris, nidx, uidx
+
+
+def c4uri_batch(names, uris, nidx, uidx, dev):
+    """The c4uri batch on the device: host blob + offsets, uri blob +
+    offsets and the null-uri flags, in the layout vc_hint_search_dev takes."""
+    nblob, noff = W.pack(names)
+    ublob, uoff = W.pack(uris)
+    hb, ho, hbytes = gather_strings_dev(nblob, noff, nidx, dev)
+    ub, uo, ubytes = gather_strings_dev(ublob, uoff, np.maximum(uidx, 0), dev)
+    un = torch.from_numpy((uidx < 0).astype(np.uint8)).to(dev)
+    return hb, ho, ub, uo, un, hbytes + ubytes
 
 
 def http_workload(n=8 << 20, n_templates=1 << 18):
@@ -1458,6 +1547,34 @@ def sub_bench(args, clf, dev, rank, world):
                 return time.perf_counter() - t0
             cpu = cpu_rates(run, "M items/s", 3.0, "SNIs of the workload, oracle "
                             "SSLContextHolder.choose scan over 100k holders (200k names)", cap=n)
+    elif args.workload == "c4uri":
+        n = 16 << 20
+        groups, names, uris, nidx, uidx = c4uri_workload(n)
+        clf.compile_upstream(groups)
+        hb, ho, ub, uo, un, nbytes = c4uri_batch(names, uris, nidx, uidx, dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        fn = lambda: V.check(V.lib().vc_hint_search_dev(
+            clf.h, C.c_void_p(hb.data_ptr()), C.c_void_p(ho.data_ptr()), None, None,
+            C.c_void_p(ub.data_ptr()), C.c_void_p(uo.data_ptr()), C.c_void_p(un.data_ptr()), n,
+            C.c_void_p(out.data_ptr()), S()))
+        per_unit = nbytes / n + 13
+        unit = "B/hint (host + uri bytes + 2 x 4 offsets + 1 null + 4 out)"
+        kern = "hint_kernel"
+        extra["uri_fraction"] = round(float((uidx >= 0).mean()), 4)
+        if O is not None:
+            og = O.Groups(groups)
+            nblob, noff = W.pack(names)
+            ublob, uoff = W.pack(uris)
+
+            def run(k, threads):
+                sb, so = sample_blob(nblob, noff, nidx[:k])
+                ubs, uos = sample_blob(ublob, uoff, np.maximum(uidx[:k], 0))
+                t0 = time.perf_counter()
+                O.hint_uri_batch_np(og, sb, so, ubs, uos, (uidx[:k] < 0).astype(np.uint8),
+                                    nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = cpu_rates(run, "M items/s", 4.0, "Hint.ofHostUri hints of the workload, oracle "
+                            "searchForGroup scan (whole matchLevel) over 100,200 groups", cap=n)
     elif args.workload == "http":
         n = 8 << 20
         groups, heads, pidx = http_workload(n)

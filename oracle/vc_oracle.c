@@ -826,6 +826,37 @@ void vo_hint_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_
     parallel_for(n, nthreads, hint_range, &c);
 }
 
+/* searchForGroup(Hint.ofHostPortUri(host, port, uri)) per item: the hint
+ * HttpContext.connectionHint builds for an HTTP request (HttpContext.java:
+ * 55-71, Hint.ofHostUri with port 0); uri_null[i] != 0 = a null uri. */
+typedef struct {
+    const vo_group *g; int ng; const uint8_t *hblob; const uint32_t *hoff;
+    const uint8_t *ublob; const uint32_t *uoff; const uint8_t *unull; const uint16_t *port;
+    int32_t *out;
+} hint_uri_ctx;
+
+static void hint_uri_range(void *p, int64_t lo, int64_t hi)
+{
+    hint_uri_ctx *c = (hint_uri_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        const char *s = (const char *)c->hblob + c->hoff[i];
+        const int len = (int)(c->hoff[i + 1] - c->hoff[i]);
+        const int has_uri = !(c->unull && c->unull[i]);
+        const char *u = has_uri ? (const char *)c->ublob + c->uoff[i] : NULL;
+        const int ulen = has_uri ? (int)(c->uoff[i + 1] - c->uoff[i]) : 0;
+        vo_hint h = vo_hint_of(s, len, c->port ? c->port[i] : 0, u, ulen);
+        c->out[i] = vo_search_for_group(c->g, c->ng, &h);
+    }
+}
+
+void vo_hint_uri_batch(const vo_group *g, int ng, const uint8_t *hblob, const uint32_t *hoff,
+                       const uint8_t *ublob, const uint32_t *uoff, const uint8_t *unull,
+                       const uint16_t *port, int64_t n, int32_t *out, int nthreads)
+{
+    hint_uri_ctx c = {g, ng, hblob, hoff, ublob, uoff, unull, port, out};
+    parallel_for(n, nthreads, hint_uri_range, &c);
+}
+
 /* ------------------------------------------------------------------------ */
 /* DNSServer.handleRequest classification -- DNSServer.java:116-166         */
 /* ------------------------------------------------------------------------ */

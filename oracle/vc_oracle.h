@@ -146,6 +146,11 @@ int vo_search_for_group(const vo_group *g, int ng, const vo_hint *h); /* Upstrea
  * over a packed host blob (item i = blob[off[i], off[i+1])) -- CPU baseline. */
 void vo_hint_batch(const vo_group *g, int ng, const uint8_t *blob, const uint32_t *off,
                    const uint16_t *port, int64_t n, int32_t *out, int nthreads);
+/* the same with uris: searchForGroup(Hint.ofHostPortUri(host, port, uri)),
+ * uri i = ublob[uoff[i], uoff[i+1]) unless unull[i] (unull / port may be NULL) */
+void vo_hint_uri_batch(const vo_group *g, int ng, const uint8_t *hblob, const uint32_t *hoff,
+                       const uint8_t *ublob, const uint32_t *uoff, const uint8_t *unull,
+                       const uint16_t *port, int64_t n, int32_t *out, int nthreads);
 
 /* ---- DNSServer classification: core/src/main/java/vproxy/dns/DNSServer.java:116-166 ---- */
 enum { VO_DNS_HOSTS = 1, VO_DNS_GROUP = 2, VO_DNS_IP_LITERAL = 3, VO_DNS_INTERNAL = 4, VO_DNS_RECURSIVE = 5 };

@@ -469,6 +469,70 @@ class HintLevelChecker:
                         take(min(idx), ul)
         return best
 
+    def table(self, names, uris):
+        """searchForGroup(Hint.ofHostUri(name, uri)) -- port 0, what
+        HttpContext.connectionHint sends (HttpContext.java:55-71) -- for
+        every pair: int32 [len(names), len(uris)] (a uri may be None).  With
+        port 0 no hint-port excludes a group, so level(g) = hl(g) << 10 +
+        ul(g) with ul <= 1023: when the name's top host level L is > 0 the
+        winner is among the groups at L -- the largest ul, then the lowest
+        index -- and otherwise it is the uri-only argmax, one per uri.  The
+        per-uri ul of every group is a vector, so a batch of tens of
+        millions of hints is a gather from this table."""
+        ng = len(self.g)
+        assert ng < (1 << 20)
+        furis = [format_uri(u) for u in uris]
+        members = {}
+        for i, (H, P, U) in enumerate(self.g):
+            if U is not None:
+                members.setdefault(U, []).append(i)
+        members = {U: np.array(m, np.int64) for U, m in members.items()}
+        ul = np.zeros((len(uris), ng), np.int64)
+        for k, u in enumerate(furis):
+            if u is None:
+                continue
+            for U, m in members.items():
+                if u == U:
+                    lvl = len(u) + 1
+                elif u.startswith(U):
+                    lvl = len(U) + 1
+                elif U == b"*":
+                    lvl = 1
+                else:
+                    continue
+                ul[k, m] = min(lvl, 1023)
+        uonly = np.where(ul.max(1) > 0, ul.argmax(1), -1)     # argmax: the lowest index of the max
+        starts, flat = [0], []
+        for name in names:
+            assert name.count(b":") <= 1, "table covers names with at most one ':'"
+            host = HintChecker.format_host(name)
+            top = []
+            if host is not None:
+                cand = set(self.by_host.get(host, ()))
+                d = host.find(b".")
+                while d != -1:
+                    cand.update(self.by_host.get(host[d + 1:], ()))
+                    d = host.find(b".", d + 1)
+                cand.update(self.by_host.get(b"*", ()))
+                lv = {i: self.level(i, host, 0, None) >> 10 for i in cand}
+                L = max(lv.values(), default=0)
+                if L > 0:
+                    top = sorted(i for i, v in lv.items() if v == L)
+            flat.extend(top)
+            starts.append(len(flat))
+        flat = np.array(flat, np.int64)
+        starts = np.array(starts, np.int64)
+        has = starts[1:] > starts[:-1]
+        out = np.empty((len(names), len(uris)), np.int32)
+        low = (1 << 20) - 1
+        for k in range(len(uris)):
+            if flat.size:
+                key = (ul[k, flat] << 20) + (low - flat)
+                best = np.maximum.reduceat(key, starts[:-1][has])
+                out[has, k] = low - (best & low)
+            out[~has, k] = uonly[k]
+        return out
+
 
 # ---------------------------------------------------------------------------
 # DNSServer.handleRequest classification

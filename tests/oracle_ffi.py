@@ -116,6 +116,8 @@ def lib():
         L.vo_search_for_group.argtypes = [P(VoGroup), C.c_int, P(VoHint)]
         L.vo_hint_batch.argtypes = [P(VoGroup), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_int64, C.c_void_p, C.c_int]
+        L.vo_hint_uri_batch.argtypes = [P(VoGroup), C.c_int] + [C.c_void_p] * 6 + \
+            [C.c_int64, C.c_void_p, C.c_int]
         L.vo_dns_classify.argtypes = [P(VoHosts), P(VoGroup), C.c_int, C.c_char_p, C.c_int,
                                       P(C.c_int32)]
         L.vo_hosts_parse.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p,
@@ -495,6 +497,20 @@ def hint_batch_np(groups, blob, off, port, nthreads=1):
                         _ptr(np.ascontiguousarray(off, np.uint32)),
                         _ptr(np.ascontiguousarray(port, np.uint16)) if port is not None else None,
                         n, _ptr(out), nthreads)
+    return out
+
+
+def hint_uri_batch_np(groups, hblob, hoff, ublob, uoff, unull=None, port=None, nthreads=1):
+    """searchForGroup(Hint.ofHostPortUri(host, port, uri)) per item (vo_hint_uri_batch)."""
+    g = groups if isinstance(groups, Groups) else Groups(groups)
+    n = len(hoff) - 1
+    out = np.empty(n, np.int32)
+    keep = [np.ascontiguousarray(hblob, np.uint8), np.ascontiguousarray(hoff, np.uint32),
+            np.ascontiguousarray(ublob, np.uint8), np.ascontiguousarray(uoff, np.uint32),
+            None if unull is None else np.ascontiguousarray(unull, np.uint8),
+            None if port is None else np.ascontiguousarray(port, np.uint16)]
+    lib().vo_hint_uri_batch(g.arr, g.n, *[_ptr(k) if k is not None else None for k in keep],
+                            n, _ptr(out), nthreads)
     return out
 
 

@@ -113,3 +113,38 @@ def test_bench_refuses_mismatch(env_ws, gpus):
     assert p.returncode == 2, p.stderr[-2000:]
     assert "--gpus %d" % gpus in p.stderr
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def _node(root, i, gfx, minor=None, readable=True):
+    d = root / "nodes" / str(i)
+    d.mkdir(parents=True)
+    if readable:
+        (d / "properties").write_text("cpu_cores_count 0\ngfx_target_version %d\n%s" % (
+            gfx, "" if minor is None else "drm_render_minor %d\n" % minor))
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path):
+    """bench.visible_gpus counts GPUs with no HIP call: KFD nodes with a
+    gfx target whose render node exists (the GPU box hides the other nodes'
+    properties and render nodes), then the *_VISIBLE_DEVICES lists."""
+    _node(tmp_path, 0, 0)                       # CPU
+    _node(tmp_path, 1, 90500, 128)
+    _node(tmp_path, 2, 90500, 136)
+    _node(tmp_path, 3, 90500, 144)              # render node not in this container
+    _node(tmp_path, 4, 90500, readable=False)   # properties not readable
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for m in (128, 136):
+        (dri / ("renderD%d" % m)).write_text("")
+    V = lambda env: B.visible_gpus(env, str(tmp_path / "nodes"), str(dri))
+    assert V({}) == 2
+    assert V({"HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert V({"ROCR_VISIBLE_DEVICES": "1", "HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert V({"CUDA_VISIBLE_DEVICES": "0,1,2"}) == 2          # 2 names no device: cut there
+    assert V({"HIP_VISIBLE_DEVICES": "-1,0"}) == 0
+    assert V({"HIP_VISIBLE_DEVICES": ""}) == 0
+    assert V({"ROCR_VISIBLE_DEVICES": "GPU-abc,GPU-def"}) == 2
+    assert B.visible_gpus({}, str(tmp_path / "absent"), str(dri)) == 0
+    with pytest.raises(SystemExit) as e:
+        B.resolve_world(2, {"HIP_VISIBLE_DEVICES": "0"}, device_count=V({"HIP_VISIBLE_DEVICES": "0"}))
+    assert e.value.code == 2

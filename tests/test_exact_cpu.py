@@ -306,3 +306,29 @@ def test_source_checker_vs_oracle():
     want = O.source_batch_np(groups, 0, grp, src, nthreads=THREADS)
     np.testing.assert_array_equal(got, want)
     assert (want >= 0).mean() > 0.5 and (want < 0).any()
+
+
+def test_hint_level_table_vs_checker_and_oracle():
+    """HintLevelChecker.table (the whole-batch form the c4uri checks use:
+    port 0, every (name, uri) pair) against the per-item checker on every
+    pair and against vo_hint_uri_batch on a sample: the c4uri generator at
+    3,000 groups (a fifth with hint-uris, 200 uri-only groups) and 2,000
+    names with the 66 uris and a null one."""
+    import bench
+    from exact import HintLevelChecker
+    groups, names, uris, nidx, uidx = bench.c4uri_workload(20000, n_groups=3000, n_names=2000)
+    og = O.Groups(groups)
+    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    cols = uris + [None]
+    tab = chk.table(names, cols)
+    for i, name in enumerate(names[:600]):
+        assert [chk(name, 0, u) for u in cols] == list(tab[i]), name
+    u = np.where(uidx < 0, len(uris), uidx)
+    want = tab[nidx, u]
+    hb, ho = W.pack([names[i] for i in nidx])
+    ub, uo = W.pack([uris[max(j, 0)] for j in uidx])
+    got = O.hint_uri_batch_np(og, hb, ho, ub, uo, (uidx < 0).astype(np.uint8), nthreads=8)
+    np.testing.assert_array_equal(got, want)
+    assert len(np.unique(want)) > 500 and (want >= 0).mean() > 0.5
+    # the uri decides: some names change group with the uri
+    assert (tab[:, :-1] != tab[:, -1:]).any(axis=1).mean() > 0.02

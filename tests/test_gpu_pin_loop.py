@@ -110,10 +110,13 @@ def test_batches_never_wait_for_a_recompile(tables):
     for d in (pins, lock):
         assert d["errors"] == 0 and d["mismatches"] == 0, d
         assert d["table_batches"][0] > 0 and d["table_batches"][1] > 0, d
-        assert d["batches_quiet"] > 100 and d["batches_during"] > 100, d
+        assert d["batches_quiet"] > 100 and d["batches_during"] > 0, d
+    assert pins["batches_during"] > 1000, pins    # the event loops kept going
     assert pins["gen_mismatches"] == 0
     assert pins["views_used"] >= 8, pins          # batches ran on most of the 11 views
     # a compile (~150 ms) never shows in a batch's latency
     assert pins["compile_ms_mean"] > 50, pins
     assert pins["p99_during"] < pins["p99_quiet"] + 10.0, pins
     assert pins["max_during"] < 0.5 * pins["compile_ms_mean"], pins
+    # the round-5 protocol: a batch that meets a recompile waits it out
+    assert lock["max_during"] > 0.5 * lock["compile_ms_mean"], lock

@@ -126,6 +126,14 @@ struct VniImage {
 // ---------------------------------------------------------------------------
 #define VC_REC_INLINE 48           // key bytes held inline in a HostRec
 #define VC_REC_HAS_PM 0x80000000u  // HostRec.len_pm: key has hint-port minima
+// Hint table only (Hint.matchLevel with a uri): some member of the key has a
+// hint-uri; SPLIT: and the key has two or more members, so the uri level can
+// decide among them.  A key without SPLIT answers a port-0 hint with a uri
+// exactly as without one when it is the only key at the hint's top host
+// level (hint_dev.h host_only_fast).
+#define VC_REC_ANYURI 0x40000000u
+#define VC_REC_SPLIT  0x20000000u
+#define VC_REC_LEN    0x1FFFFFFFu  // key length bits of len_pm
 
 struct HostRec {                   // 64 bytes, 64-byte aligned
     uint32_t len_pm;               // key length | VC_REC_HAS_PM

@@ -507,6 +507,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         std::vector<uint32_t> members;
         std::map<int32_t, int32_t> port_min;   // distinct nonzero hint-port -> min index
         int32_t a = -1, b = -1;
+        bool any_uri = false;                  // a member has a hint-uri
     };
     std::map<std::string, KeyAcc> hostk, urik;
     std::vector<std::string> host_order, uri_order;
@@ -539,6 +540,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
             }
             KeyAcc& acc = it->second;
             acc.members.push_back(static_cast<uint32_t>(g));
+            if (U) acc.any_uri = true;
             if (acc.a < 0) acc.a = g;
             if (P == 0 && acc.b < 0) acc.b = g;
             if (P != 0 && !acc.port_min.count(P)) acc.port_min[P] = g;
@@ -557,7 +559,7 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
     }
     KeySlotH empty{0, -1, 0, -1, -1, 0, 0};
     for (auto& k : host_order)
-        if (k.size() > 0x7FFFFFFFu) return VC_EINVAL;
+        if (k.size() > VC_REC_LEN) return VC_EINVAL;     // the record's length bits
     out->host.init(host_order.size());
     out->uri_slots.assign(pow2_cap(uri_order.size()), empty);
     out->uri_tags.assign(out->uri_slots.size(), 0);
@@ -572,6 +574,8 @@ int build_hints(const vc_group_annos* groups, int n, HintBuilt* out) {
         x.pm_off = static_cast<uint32_t>(out->port_mins.size() / 2);
         x.pm_cnt = static_cast<uint32_t>(acc.port_min.size());
         if (!acc.port_min.empty()) out->host.recs[slot].len_pm |= VC_REC_HAS_PM;
+        if (acc.any_uri) out->host.recs[slot].len_pm |= VC_REC_ANYURI;
+        if (acc.any_uri && acc.members.size() > 1) out->host.recs[slot].len_pm |= VC_REC_SPLIT;
         for (auto& pm : acc.port_min) {
             out->port_mins.push_back(pm.first);
             out->port_mins.push_back(pm.second);
@@ -606,6 +610,7 @@ int build_hosts(const char* const* keys, const int32_t* key_lens, const int32_t*
     std::vector<int> order;
     for (int i = 0; i < n; ++i) {
         if (key_lens[i] < 0 || (!keys[i] && key_lens[i] > 0)) return VC_EINVAL;
+        if (uint32_t(key_lens[i]) > VC_REC_LEN) return VC_EINVAL;
         std::string k(keys[i] ? keys[i] : "", key_lens[i]);
         if (seen.count(k)) continue;     // first key wins
         seen.emplace(k, i);
@@ -632,6 +637,7 @@ int build_certs(const char* const* names, const int32_t* name_lens, const int32_
     for (int i = 0; i < n; ++i) {
         if (name_lens[i] < 0 || (!names[i] && name_lens[i] > 0)) return VC_EINVAL;
         if (holder[i] < 0 || holder[i] >= n_holders) return VC_EINVAL;
+        if (uint32_t(name_lens[i]) > VC_REC_LEN) return VC_EINVAL;
         std::string k(names[i] ? names[i] : "", name_lens[i]);
         const bool wild = k.size() >= 2 && k[0] == '*' && k[1] == '.';
         if (wild) k.erase(0, 1);

@@ -286,11 +286,15 @@ __device__ __forceinline__ void chunk_loop(Ch& ch, int w, const uint8_t* blob,
     }
 }
 
-// kDefer (no hint-uri in the batch or the image): host-only levels with no
-// call in the loop -- lanes that need an out-of-line step are written as
-// kDeferred and counted in ticket[1] for hint_defer_kernel, which runs next
-// on the stream.  Otherwise every lane is finished here (the general path).
-template <bool kStage, bool kDefer>
+// kDefer: no call in the loop -- lanes that need an out-of-line step are
+// written as kDeferred and counted in ticket[1] for hint_defer_kernel, which
+// runs next on the stream.  With hint-uris in the batch and the image, a
+// port-0 lane with a uri takes the host fast path too (host_only_fast's
+// `uri`: the uri cannot change the answer unless the top host level has
+// candidates it orders) and defers otherwise; a uri lane with a port or no
+// host always defers.  !kDefer (an unstaged batch): every lane is finished
+// here, uri lanes through the general path.
+template <bool kStage, bool kDefer, bool kUri = false>
 __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
     const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
@@ -300,7 +304,9 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     __shared__ uint32_t stage[kWaves][kStageWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     ChunksT<kPerTicket, kTailChunks, kTailRounds, VC_HINT_STATIC> ch(ticket, (n + 63) / 64);
-    const bool general = !kDefer && uri_blob && img.has_uri_keys;
+    // kUri: the deferring kernel's instance for batches with uris (the
+    // host-only instance, the C5 pool pass's, carries no uri logic)
+    const bool general = (kUri || !kDefer) && uri_blob && img.has_uri_keys;
     // Out-of-line slow paths take the image by address; give them their own
     // copy so the fast path keeps reading the kernel argument (whose table
     // pointers the compiler then knows to be global).
@@ -313,13 +319,17 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             const int p = port ? int(port[i]) : 0;
             const bool has_host = host_blob && !(host_null && host_null[i]);
             const bool has_uri = uri_blob && !(uri_null && uri_null[i]);
-            if (!general || !has_uri) {
-                // uri null (or no hint-uri anywhere): host-only levels
+            const bool lane_uri = general && has_uri;
+            if (kDefer && lane_uri && (p != 0 || !has_host)) {
+                r = kDeferred;                    // the general search decides
+            } else if (kDefer || !lane_uri) {
+                // uri null (or no hint-uri anywhere): host-only levels; a
+                // port-0 uri lane whose answer they already give (kDefer)
                 if (has_host) {
                     if (staged)
                         r = host_only_fast<kDefer>(img, &slow_img,
                                                    LdsSrc{stage[w], int(kApron + (a - a0))},
-                                                   int(e - a), p);
+                                                   int(e - a), p, lane_uri);
                     else if (kDefer)
                         r = kDeferred;
                     else
@@ -343,13 +353,17 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
 }
 
 // The lanes hint_kernel<*, true> deferred, through the reference-shaped
-// host-only search (Hint.formatHost + every dot-suffix probed in turn).
+// host-only search (Hint.formatHost + every dot-suffix probed in turn), or
+// for a lane with a uri (when the image has hint-uris) the general search
+// (the whole Hint.matchLevel over the candidate lists).
 // ctl = the launch's ticket slot: [1] deferred lanes (0: nothing to do),
 // [2] workgroups done; the last workgroup zeroes both for the slot's next
 // launch.  Without a slot every workgroup scans.
 __global__ __launch_bounds__(256) void hint_defer_kernel(
     HintImage img, const uint8_t* __restrict__ host_blob, const uint32_t* __restrict__ host_off,
-    const uint16_t* __restrict__ port, int64_t n, int32_t* __restrict__ out, uint32_t* ctl) {
+    const uint8_t* __restrict__ host_null, const uint16_t* __restrict__ port,
+    const uint8_t* __restrict__ uri_blob, const uint32_t* __restrict__ uri_off,
+    const uint8_t* __restrict__ uri_null, int64_t n, int32_t* __restrict__ out, uint32_t* ctl) {
     __shared__ uint32_t todo;
     if (threadIdx.x == 0) todo = ctl ? __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT)
@@ -359,8 +373,17 @@ __global__ __launch_bounds__(256) void hint_defer_kernel(
         for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
              i += int64_t(gridDim.x) * blockDim.x) {
             if (out[i] != kDeferred) continue;
+            const int p = port ? int(port[i]) : 0;
+            const bool has_host = !(host_null && host_null[i]);
             const uint32_t a = host_off[i], e = host_off[i + 1];
-            out[i] = host_only_slow(img, host_blob + a, int(e - a), port ? int(port[i]) : 0);
+            if (uri_blob && img.has_uri_keys && !(uri_null && uri_null[i])) {
+                const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
+                const DStr h = has_host ? DStr{host_blob + a, int(e - a)} : DStr{nullptr, -1};
+                out[i] = hint_general(img, format_host(h), p,
+                                      format_uri(DStr{uri_blob + ua, int(ue - ua)}));
+            } else {
+                out[i] = host_only_slow(img, host_blob + a, int(e - a), p);
+            }
         }
     }
     if (ctl && threadIdx.x == 0 && atomicAdd(ctl + 2, 1u) == gridDim.x - 1) {
@@ -922,8 +945,9 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kHintBlock - 1) / vcd::kHintBlock;
     const bool stage = host_blob && (reinterpret_cast<uintptr_t>(host_blob) & 3) == 0;
-    // the deferring kernel when no lane takes the general (hint-uri) path
-    const bool defer = VC_HINT_DEFER && stage && !(uri_blob && img.has_uri_keys);
+    // the deferring kernel whenever the names can be staged: uri lanes the
+    // host levels do not decide go to the follow-up's general search
+    const bool defer = VC_HINT_DEFER && stage;
     uint32_t* ticket = VC_HINT_TICKETS && c.tickets ? c.tickets->next(c.stream) : nullptr;
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel,
@@ -932,7 +956,8 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out, ticket);
     };
-    if (defer) go(vcd::hint_kernel<true, true>);
+    if (defer && uri_blob && img.has_uri_keys) go(vcd::hint_kernel<true, true, true>);
+    else if (defer) go(vcd::hint_kernel<true, true>);
     else if (stage) go(vcd::hint_kernel<true, false>);
     else go(vcd::hint_kernel<false, false>);
     hipError_t e = hipGetLastError();
@@ -940,7 +965,8 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
         const int64_t dwant = (n + 255) / 256;
         const int64_t dgrid = dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID;
         hipLaunchKernelGGL(vcd::hint_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
-                           img, host_blob, host_off, port, n, out, ticket);
+                           img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
+                           n, out, ticket);
         e = hipGetLastError();
     }
     if (e != hipSuccess || !counters) return e;

@@ -310,7 +310,7 @@ VC_HD bool rec_eq(const Rec& r, const uint8_t* blob, const Src& q, int st, int n
     // The word masks use rn, the record's length, made opaque after the
     // check: with n the compiler hoists all twelve masks out of the probe
     // loop and computes them per hit; only the key's last word needs one.
-    int rn = int(r.m.x & ~VC_REC_HAS_PM);
+    int rn = int(r.m.x & VC_REC_LEN);
     if (rn != n) return false;
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(rn));
@@ -352,7 +352,7 @@ VC_HD bool rec_match(const HostRec* recs, uint32_t s, const uint8_t* blob, const
     }
 #endif
     const uint4 m = gload(p), k0 = gload(p + 1), k1 = gload(p + 2);
-    int rn = int(m.x & ~VC_REC_HAS_PM);
+    int rn = int(m.x & VC_REC_LEN);
     if (rn != n) return false;
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(rn));
@@ -625,9 +625,21 @@ constexpr int kProbes = kMaxSuffix + 1;      // [0] = the whole host
 // loaded together, and only tag hits touch a record.  Names the scan does
 // not cover (two or more ':' -- a possible IPv6 literal -- or more than
 // kMaxSuffix labels) go to the reference-shaped slow path.
+//
+// uri (kDefer only): the hint also has a uri and port 0 -- Hint.ofHostUri,
+// what HttpContext.connectionHint sends (HttpContext.java:55-71).  Then
+// level(g) = hostLevel(g) << 10 + uriLevel(g) (Hint.java:100-160) with
+// uriLevel <= 1023, so the winner is among the groups at the top host level
+// L, ordered by uriLevel and then index.  When L's groups are one key's
+// members and that key is not VC_REC_SPLIT (one member, or none with a
+// hint-uri), or several keys none of whose members has a hint-uri
+// (VC_REC_ANYURI), every candidate has the same uriLevel and the host-only
+// answer -- the lowest index at L -- is the answer.  Otherwise (and when no
+// host key matches, L = 0: the uri alone decides) the lane is deferred to
+// the general search.
 template <bool kDefer = false, class Src>
 VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
-                             int port) {
+                             int port, bool uri = false) {
 #if defined(VC_ABL_NOSCAN)         // timing ablation only: stage, no scan
     if (n != 0x7FFFFFFF) return int32_t(q.word(0, 0, n) & 1u) - 1;
 #endif
@@ -683,7 +695,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             stp = stp >> 8;
             np -= 1;
         }
-        if (e - int(stp & 0xFF) <= 0) return -1;
+        if (e - int(stp & 0xFF) <= 0) return kDefer && uri ? kDeferred : -1;   // null host
     }
     const HostTable t = host_table(img);
     // hits: bit k = probe k's first group has a tag match or continues;
@@ -709,6 +721,8 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
     VC_PMARK(2);
     uint32_t best = VC_NONE;
     bool defer = false;
+    int nsuf = 0;                     // suffix keys at level 2 (uri lanes)
+    uint32_t uflags = 0;              // their len_pm words, or-ed
     while (hits) {
         const int k = __builtin_ctz(hits);
         hits &= hits - 1;
@@ -722,12 +736,28 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         if (slot < 0) continue;
         const uint32_t v = pick_or_defer<kDefer>(img, slot, r, port, &defer);
         if (k == 0) {
-            if (v != VC_NONE) return int32_t(v);          // exact level wins
+            if (v != VC_NONE) {                            // exact level wins
+                if (kDefer && uri && (r.m.x & VC_REC_SPLIT)) return kDeferred;
+                return kDefer && defer ? kDeferred : int32_t(v);
+            }
         } else {
             best = v < best ? v : best;
+            if (v != VC_NONE) {
+                ++nsuf;
+                uflags |= r.m.x;
+            }
         }
     }
     VC_PMARK(3);
+    if (kDefer && uri) {
+        if (best != VC_NONE) {
+            if (uflags & (nsuf > 1 ? VC_REC_ANYURI : VC_REC_SPLIT)) return kDeferred;
+        } else {
+            best = wildcard_pick_or_defer<kDefer>(img, port, &defer);
+            // "*" at level 1, or no host level at all: the uri decides
+            if (best == VC_NONE || (img.wild_len_pm & VC_REC_SPLIT)) return kDeferred;
+        }
+    }
     if (best == VC_NONE) best = wildcard_pick_or_defer<kDefer>(img, port, &defer);
     if (kDefer && defer) return kDeferred;
     return best != VC_NONE ? int32_t(best) : -1;
