@@ -174,7 +174,20 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
                                  ? hint_general(img, format_host(h), p, format_uri(u))
                                  : hint_host_only(img, format_host(h), p);
         out[i] = want;
-        if (u.n >= 0 && img.has_uri_keys) continue;
+        if (u.n >= 0 && img.has_uri_keys) {
+            // the uri-aware deferring form (hint_kernel<.., .., true>): a
+            // port-0 hint with a host takes the host fast path and gets the
+            // same result there, or kDeferred for the general search
+            if (p != 0 || h.n < 0) { ++g_hint_deferred; continue; }
+            for (int al = 0; al < 4; ++al) {
+                Staged st(h.p, h.n, al);
+                int32_t d = host_only_fast<true>(img, &img, st.src, h.n, 0, true);
+                if (is_uri_slot_code(d)) d = uri_in_slot(img, -2 - d, u.p, u.n);
+                if (d != want && d != kDeferred) return -105;
+                if (al == 0 && d == kDeferred) ++g_hint_deferred;
+            }
+            continue;
+        }
         if (h.n < 0) { if (want != -1) return -100; continue; }
         // the kernels' fused fast path, from a plain pointer and from a
         // staged copy at every word alignment: all must agree

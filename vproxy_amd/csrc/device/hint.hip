@@ -311,6 +311,11 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
     // copy so the fast path keeps reading the kernel argument (whose table
     // pointers the compiler then knows to be global).
     HintImage slow_img = img;
+    // kUri: deferred lanes are common (a few percent), so a wave counts them
+    // over its chunks and adds once at its end -- one same-address atomic
+    // per chunk (C4uri: 262K per launch) serialised at the memory side and
+    // held the kernel at 2.9 ms
+    uint32_t ndef = 0;
     VC_PBEGIN();
     chunk_loop<kStageBytes, true, VC_HINT_PRE, bool(VC_HINT_SWAP)>(ch, w, kStage ? host_blob : nullptr, host_off, n, stage[w],
                                   [&](int64_t i, bool staged, uint32_t a0, uint32_t a, uint32_t e) {
@@ -334,6 +339,11 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
                         r = kDeferred;
                     else
                         r = host_only_slow(slow_img, host_blob + a, int(e - a), p);
+                    // one SPLIT key holds the top host level: its members by uri level
+                    if (kUri && is_uri_slot_code(r)) {
+                        const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
+                        r = uri_in_slot(img, -2 - r, uri_blob + ua, int(ue - ua));
+                    }
                 }
             } else if (!kDefer) {
                 DStr h{nullptr, -1}, u{nullptr, -1};
@@ -346,9 +356,13 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
         }
         if (kDefer && ticket) {
             const uint64_t dm = __ballot(i < n && r == kDeferred);
-            if (dm && lane == 0) atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
+            if constexpr (kUri)
+                ndef += uint32_t(__popcll(dm));
+            else if (dm && lane == 0)
+                atomicAdd(ticket + 1, uint32_t(__popcll(dm)));
         }
     });
+    if (kUri && ticket && ndef && lane == 0) atomicAdd(ticket + 1, ndef);
     VC_PEND();
 }
 
@@ -956,14 +970,21 @@ hipError_t launch_hint(const LaunchCfg& c, const HintImage& img, const uint8_t* 
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out, ticket);
     };
-    if (defer && uri_blob && img.has_uri_keys) go(vcd::hint_kernel<true, true, true>);
+    const bool uri = uri_blob && img.has_uri_keys;
+    if (defer && uri) go(vcd::hint_kernel<true, true, true>);
     else if (defer) go(vcd::hint_kernel<true, true>);
     else if (stage) go(vcd::hint_kernel<true, false>);
     else go(vcd::hint_kernel<false, false>);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && defer) {
         const int64_t dwant = (n + 255) / 256;
-        const int64_t dgrid = dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID;
+        // uri batches defer a few percent of their lanes to the general
+        // search, a chain of dependent loads per lane: a resident grid
+        // (C4uri: 24.8 ms on 128 workgroups)
+        const int64_t dgrid =
+            uri ? resident_grid(c, reinterpret_cast<const void*>(vcd::hint_defer_kernel), 256, 0,
+                                dwant)
+                : (dwant < VC_DEFER_GRID ? dwant : VC_DEFER_GRID);
         hipLaunchKernelGGL(vcd::hint_defer_kernel, dim3(unsigned(dgrid)), dim3(256), 0, c.stream,
                            img, host_blob, host_off, host_null, port, uri_blob, uri_off, uri_null,
                            n, out, ticket);

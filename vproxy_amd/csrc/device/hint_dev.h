@@ -506,11 +506,11 @@ VC_HD uint32_t wildcard_pick(const HintImage& img, int port) {
 // The deferring fast path (kDefer below) leaves a lane that needs an
 // out-of-line step -- the port filter over a key's distinct hint-port
 // minima, a name the word scan does not cover, an unstaged chunk -- marked
-// with kDeferred for the reference-shaped pass that follows the kernel
-// (hint.hip hint_defer_kernel), so the kernel's loop contains no call: a
-// call site inside it makes the compiler keep the loop's state in scratch
-// and spill SGPRs across the call on every chunk.
-constexpr int32_t kDeferred = INT32_MIN;
+// with kDeferred (defined with host_only_fast) for the reference-shaped
+// pass that follows the kernel (hint.hip hint_defer_kernel), so the
+// kernel's loop contains no call: a call site inside it makes the compiler
+// keep the loop's state in scratch and spill SGPRs across the call on every
+// chunk.
 
 template <bool kDefer>
 VC_HD uint32_t pick_or_defer(const HintImage& img, int slot, const Rec& r, int port,
@@ -634,9 +634,18 @@ constexpr int kProbes = kMaxSuffix + 1;      // [0] = the whole host
 // members and that key is not VC_REC_SPLIT (one member, or none with a
 // hint-uri), or several keys none of whose members has a hint-uri
 // (VC_REC_ANYURI), every candidate has the same uriLevel and the host-only
-// answer -- the lowest index at L -- is the answer.  Otherwise (and when no
-// host key matches, L = 0: the uri alone decides) the lane is deferred to
-// the general search.
+// answer -- the lowest index at L -- is the answer.  When they are one
+// SPLIT key's members the result is uri_slot_code(slot): the caller scores
+// that key's members by uriLevel (uri_in_slot).  Otherwise (several keys at
+// L with a hint-uri among them, or no host key at all, L = 0: the uri alone
+// decides) the lane is deferred to the general search.
+constexpr int32_t kDeferred = INT32_MIN;
+
+// host_only_fast's answer for a uri lane whose top host level is one SPLIT
+// key: -2 - slot (below -1, above kDeferred)
+VC_HD int32_t uri_slot_code(int slot) { return -2 - slot; }
+VC_HD bool is_uri_slot_code(int32_t r) { return r < -1 && r != kDeferred; }
+
 template <bool kDefer = false, class Src>
 VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, const Src& q, int n,
                              int port, bool uri = false) {
@@ -723,6 +732,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
     bool defer = false;
     int nsuf = 0;                     // suffix keys at level 2 (uri lanes)
     uint32_t uflags = 0;              // their len_pm words, or-ed
+    int sslot = 0;                    // the (last) one's slot
     while (hits) {
         const int k = __builtin_ctz(hits);
         hits &= hits - 1;
@@ -737,7 +747,7 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
         const uint32_t v = pick_or_defer<kDefer>(img, slot, r, port, &defer);
         if (k == 0) {
             if (v != VC_NONE) {                            // exact level wins
-                if (kDefer && uri && (r.m.x & VC_REC_SPLIT)) return kDeferred;
+                if (kDefer && uri && (r.m.x & VC_REC_SPLIT)) return uri_slot_code(slot);
                 return kDefer && defer ? kDeferred : int32_t(v);
             }
         } else {
@@ -745,22 +755,81 @@ VC_HD int32_t host_only_fast(const HintImage& img, const HintImage* slow_img, co
             if (v != VC_NONE) {
                 ++nsuf;
                 uflags |= r.m.x;
+                sslot = slot;
             }
         }
     }
     VC_PMARK(3);
     if (kDefer && uri) {
         if (best != VC_NONE) {
-            if (uflags & (nsuf > 1 ? VC_REC_ANYURI : VC_REC_SPLIT)) return kDeferred;
+            if (nsuf > 1 && (uflags & VC_REC_ANYURI)) return kDeferred;
+            if (nsuf == 1 && (uflags & VC_REC_SPLIT)) return uri_slot_code(sslot);
         } else {
             best = wildcard_pick_or_defer<kDefer>(img, port, &defer);
-            // "*" at level 1, or no host level at all: the uri decides
-            if (best == VC_NONE || (img.wild_len_pm & VC_REC_SPLIT)) return kDeferred;
+            if (best == VC_NONE) return kDeferred;        // no host level: the uri decides
+            if (img.wild_len_pm & VC_REC_SPLIT) return uri_slot_code(img.wildcard_slot);
         }
     }
     if (best == VC_NONE) best = wildcard_pick_or_defer<kDefer>(img, port, &defer);
     if (kDefer && defer) return kDeferred;
     return best != VC_NONE ? int32_t(best) : -1;
+}
+
+// Hint.formatUri's length (Hint.java:75-90: cut at the first '?'; "/"
+// stays, else one trailing '/' goes) of a uri in global memory.  Up to 60
+// bytes its aligned words are loaded together and searched a word at a time
+// (a byte loop with an exit per byte is one dependent load per byte); an
+// aligned word holding a byte of the uri never crosses a page.
+VC_HD int format_uri_len(const uint8_t* p, int n) {
+    if (n > 60) return format_uri(DStr{p, n}).n;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const int sh = int(a & 3), nw = (sh + n + 3) >> 2;
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = k < nw ? gload(w + k) : 0u;
+    int m = n;
+#pragma unroll
+    for (int k = 15; k >= 0; --k) {              // the first '?' wins: scan down
+        const int b0 = 4 * k - sh;               // uri position of the word's byte 0
+        uint32_t f = vck::byte_eq_flags(x[k], 0x3F3F3F3Fu);
+        f &= lo_mask(b0, 0) & (b0 + 4 <= n ? ~0u : tail_mask(n - b0 > 0 ? n - b0 : 0));
+        if (k < nw && f) m = b0 + (__builtin_ctz(f) >> 3);
+    }
+    if (m == 1 && p[0] == '/') return 1;
+    return m > 0 && p[m - 1] == '/' ? m - 1 : m;
+}
+
+// Upstream.searchForGroup for a port-0 uri hint whose top host level is
+// one key's members (host_only_fast's uri_slot_code): they share the host
+// level, so the highest uriLevel wins and then the lowest index (the list
+// ascends; strict '>'), Hint.java:144-157 -- uriLevel = U.length() + 1 when
+// the uri starts with U (equal included), 1 for "*", capped at 1023.  A
+// member list longer than 32 goes to the general search.
+VC_HD int32_t uri_in_slot(const HintImage& img, int slot, const uint8_t* up, int un) {
+    const HostExt x = gload(img.host_ext + slot);
+    if (x.list_cnt > 32) return kDeferred;
+    const int m = format_uri_len(up, un);
+    int32_t best = int32_t(gload(img.lists + x.list_off));
+    int lvl = 0;
+    for (uint32_t i = 0; i < x.list_cnt; ++i) {
+        const uint32_t g = gload(img.lists + x.list_off + i);
+        // GroupRec: {host_len, host_off, uri_len, uri_off}, {port, any, uri_units, pad}
+        const int4 r = gload(reinterpret_cast<const int4*>(img.groups) + 2 * g);
+        const int4 r2 = gload(reinterpret_cast<const int4*>(img.groups) + 2 * g + 1);
+        const int Un = r.z;
+        if (Un < 0) continue;                                      // no hint-uri: 0
+        const uint8_t* U = img.blob + uint32_t(r.w);
+        int ul = 0;
+        if (Un <= m && bytes_eq(U, up, Un)) ul = r2.z + 1;
+        else if (Un == 1 && U[0] == '*') ul = 1;
+        ul = ul > 1023 ? 1023 : ul;
+        if (ul > lvl) {
+            lvl = ul;
+            best = int32_t(g);
+        }
+    }
+    return best;
 }
 
 // ---------------------------------------------------------------------------
