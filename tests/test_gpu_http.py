@@ -161,3 +161,25 @@ def test_heads_past_the_stage(clf):
     want, wkind = _oracle(O.Groups(groups), heads)
     np.testing.assert_array_equal(kind, wkind)
     np.testing.assert_array_equal(got, want)
+
+
+def test_http_hint_device_argument_checks():
+    """classifier.http_hint refuses device arguments the kernel would
+    misread, before the library is called: an int64 offsets tensor (read as
+    uint32 pairs), a non-uint8 blob (numel() undercounts its bytes), an
+    empty offsets tensor."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        clf.compile_upstream([({}, {"host": "a.com"})])
+        head = b"GET / HTTP/1.1\r\nHost: a.com\r\n\r\n"
+        hb = torch.tensor(list(head), dtype=torch.uint8, device="cuda")
+        ok = torch.tensor([0, len(head)], dtype=torch.int32, device="cuda")
+        g, k = clf.http_hint((hb, ok))
+        assert g.cpu().tolist() == [0] and k.cpu().tolist() == [2]
+        for bad in ((hb, ok.to(torch.int64)), (hb.to(torch.int32), ok),
+                    (hb, torch.empty(0, dtype=torch.int32, device="cuda"))):
+            with pytest.raises(V.IllegalArgumentException):
+                clf.http_hint(bad)
+    finally:
+        clf.close()

@@ -595,6 +595,16 @@ class Classifier:
         if isinstance(heads, tuple) and _is_dev(heads[0]):
             import torch
             hb, ho = heads[0], heads[1]
+            # refused before the kernel sees them: an int64 offsets tensor
+            # would be read as uint32 pairs, a wider blob dtype would make
+            # numel() undercount its bytes
+            if hb.dtype != torch.uint8 or not hb.is_contiguous():
+                raise IllegalArgumentException("http heads: a contiguous uint8 blob expected")
+            if (ho.dtype not in (torch.int32, getattr(torch, "uint32", torch.int32)) or
+                    not ho.is_contiguous() or ho.dim() != 1 or len(ho) < 1 or
+                    ho.device != hb.device):
+                raise IllegalArgumentException(
+                    "http heads: contiguous 32-bit offsets (n + 1) on the blob's device expected")
             n = len(ho) - 1
             grp = torch.empty(n, dtype=torch.int32, device=hb.device)
             kind = torch.empty(n, dtype=torch.uint8, device=hb.device)

@@ -358,6 +358,7 @@ struct vc_ctx : SnapSet {
     hipEvent_t handoff = nullptr;  // vc::Handoff: stream -> count_stream ordering
     std::mutex handoff_mu;
     vc::ScratchRing scratch;       // counter-pass scratch, reused across calls
+    vc::ScratchRing http_scratch;  // vc_http_hint's rewrite space (best-fit, no grow-all)
     vc::TicketRing tickets;        // work counters of the string kernels
     int num_cus = 256;
     bool sync_check = false;       // VC_SYNC_CHECK: synchronise + check after every launch / copy
@@ -408,6 +409,7 @@ struct vc_ctx : SnapSet {
         c.cu_masked = c.num_cus < num_cus;
         c.handoff = vc::Handoff{handoff, const_cast<std::mutex*>(&handoff_mu)};
         c.scratch = const_cast<vc::ScratchRing*>(&scratch);
+        c.http_scratch = const_cast<vc::ScratchRing*>(&http_scratch);
         c.tickets = const_cast<vc::TicketRing*>(&tickets);
         return c;
     }
@@ -698,8 +700,10 @@ int vc_create(int device, vc_ctx** out) {
     if ((e = hipSetDevice(device)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming)) != hipSuccess ||
-        (e = c->scratch.init()) != hipSuccess || (e = c->tickets.init()) != hipSuccess) {
+        (e = c->scratch.init()) != hipSuccess || (e = c->http_scratch.init(false)) != hipSuccess ||
+        (e = c->tickets.init()) != hipSuccess) {
         c->scratch.destroy();
+        c->http_scratch.destroy();
         c->tickets.destroy();
         if (c->handoff) (void)hipEventDestroy(c->handoff);
         if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -730,6 +734,7 @@ void vc_destroy(vc_ctx* ctx) {
     (void)hipStreamDestroy(ctx->stream);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     ctx->scratch.destroy();
+    ctx->http_scratch.destroy();
     ctx->tickets.destroy();
     delete ctx;
 }

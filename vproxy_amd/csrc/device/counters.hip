@@ -564,7 +564,8 @@ void big_hist_begin(uint8_t* scratch, int64_t n, int64_t nval, int nblk, BigHist
     h->tmp = reinterpret_cast<uint16_t*>(p);
 }
 
-hipError_t ScratchRing::init() {
+hipError_t ScratchRing::init(bool grow_all) {
+    grow_all_ = grow_all;
     for (Slot& s : slots_) {
         hipError_t e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
         if (e != hipSuccess) return e;
@@ -589,6 +590,17 @@ hipError_t ScratchRing::acquire(size_t bytes, hipStream_t st, int* slot, uint8_t
                 const int j = (next_ + i) % kSlots;
                 if (!slots_[j].busy) k = j;
             }
+            if (k >= 0 && !grow_all_) {
+                // an idle arena that fits, else the largest idle one
+                int fit = -1, big = k;
+                for (int j = 0; j < kSlots; ++j) {
+                    if (slots_[j].busy) continue;
+                    if (slots_[j].cap >= bytes && (fit < 0 || slots_[j].cap < slots_[fit].cap))
+                        fit = j;
+                    if (slots_[j].cap > slots_[big].cap) big = j;
+                }
+                k = fit >= 0 ? fit : big;
+            }
             if (k >= 0) break;
             cv_.wait(lk);                      // more concurrent calls than arenas
         }
@@ -604,7 +616,7 @@ hipError_t ScratchRing::acquire(size_t bytes, hipStream_t st, int* slot, uint8_t
         // batches as bubbles.
         const size_t cap = up256(bytes + bytes / 4);
         std::vector<int> grow{k};
-        {
+        if (grow_all_) {
             std::lock_guard<std::mutex> lk(mu_);
             for (int j = 0; j < kSlots; ++j)
                 if (j != k && !slots_[j].busy && slots_[j].cap < cap) {

@@ -13,12 +13,15 @@
 // stores a header on the next byte).  Parsing stops at the empty line that
 // ends the headers (state 9); bytes after it are not read.
 //
-// The two strings are then written out for the search -- CR bytes dropped
-// and every byte >= 0x80 as the UTF-8 of the Java char (char) b = U+FF00 | b
-// (EF, BC | b >> 6, 80 | b & 3F), as the compiled annotations hold Java
-// strings in UTF-8 (the DNS path does the same, hint_dev.h) -- into the
-// lane's LDS buffer, or when longer than it into the launch's scratch, in
-// the region three times the span's offset.
+// A string with a CR or a byte >= 0x80 is written out for the search -- CR
+// bytes dropped and every byte >= 0x80 as the UTF-8 of the Java char
+// (char) b = U+FF00 | b (EF, BC | b >> 6, 80 | b & 3F), as the compiled
+// annotations hold Java strings in UTF-8 (the DNS path does the same,
+// hint_dev.h) -- into the launch's rewrite space, in the region three times
+// the span's offset; plain strings (nearly all) are searched in place.  The
+// space comes from the context's own arena ring (capi.cpp http_scratch),
+// which keeps one arena of the largest batch's size instead of growing the
+// counter passes' four.
 // Included once, at the end of hint.hip (hint_dev.h's out-of-line
 // functions belong to that translation unit).
 #pragma once
@@ -292,16 +295,19 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
     if (n <= 0) return hipSuccess;
     int slot = -1;
     uint8_t* scratch = nullptr;
-    hipError_t e = c.scratch ? c.scratch->acquire(size_t(blob_bytes > 0 ? blob_bytes : 1) * 3,
-                                                  c.stream, &slot, &scratch)
-                             : hipErrorInvalidValue;
+    ScratchRing* ring = c.http_scratch ? c.http_scratch : c.scratch;
+    hipError_t e = ring ? ring->acquire(size_t(blob_bytes > 0 ? blob_bytes : 1) * 3, c.stream,
+                                        &slot, &scratch)
+                        : hipErrorInvalidValue;
     if (e != hipSuccess) return e;
-    // timing-only ablations (VC_ABL_HTTP): 1 parse only, 2 parse + copies, no search,
-    // 3 search with the host alone, 4 with the uri alone
-    static const int abl = [] {
-        const char* v = std::getenv("VC_ABL_HTTP");
-        return v ? std::atoi(v) : 0;
-    }();
+    // timing-only ablations, in a build with -DVC_ABL_HTTP=k only: 1 parse
+    // only, 2 parse + copies, no search, 3 search with the host alone, 4 with
+    // the uri alone
+#if defined(VC_ABL_HTTP)
+    const int abl = VC_ABL_HTTP;
+#else
+    const int abl = 0;
+#endif
     const int64_t want = (n + 64 * vcd::kHttpWaves - 1) / (64 * vcd::kHttpWaves);
     auto go = [&](auto kernel) {
         const int grid = resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kHttpBlock,
@@ -309,15 +315,17 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kHttpBlock), 0, c.stream, img, blob, off,
                            n, blob_bytes, scratch, out_group, out_kind, abl);
     };
-    // VC_HTTP_NOSTAGE=1 (measurement only): every chunk through the global-memory path
-    static const bool nostage = [] {
-        const char* v = std::getenv("VC_HTTP_NOSTAGE");
-        return v && v[0] == '1';
-    }();
+    // -DVC_HTTP_NOSTAGE (measurement builds only): every chunk through the
+    // global-memory path
+#if defined(VC_HTTP_NOSTAGE)
+    const bool nostage = true;
+#else
+    const bool nostage = false;
+#endif
     if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0 && !nostage) go(vcd::http_hint_kernel<true>);
     else go(vcd::http_hint_kernel<false>);
     e = hipGetLastError();
-    const hipError_t e2 = c.scratch->release(slot, c.stream);
+    const hipError_t e2 = ring->release(slot, c.stream);
     return e != hipSuccess ? e : e2;
 }
 

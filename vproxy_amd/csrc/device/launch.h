@@ -44,7 +44,11 @@ struct Handoff {
 class ScratchRing {
 public:
     static constexpr int kSlots = 4;
-    hipError_t init();
+    // grow_all (the counter passes): a batch larger than any before grows
+    // every idle arena at once.  Off (the HTTP rewrite space): a call takes
+    // an idle arena that already fits, else grows only the largest idle one,
+    // so a steady stream of calls keeps one large arena, not four.
+    hipError_t init(bool grow_all = true);
     void destroy();           // after the device is idle
     hipError_t acquire(size_t bytes, hipStream_t s, int* slot, uint8_t** base);
     hipError_t release(int slot, hipStream_t s);
@@ -61,6 +65,7 @@ private:
     std::condition_variable cv_;
     Slot slots_[kSlots];
     int next_ = 0;
+    bool grow_all_ = true;
 };
 
 // Work counters of the dynamically scheduled string kernels (hint, DNS,
@@ -123,6 +128,7 @@ struct LaunchCfg {
     hipStream_t stream = nullptr;
     Handoff handoff;
     ScratchRing* scratch = nullptr;   // counter-pass scratch (required by the launchers)
+    ScratchRing* http_scratch = nullptr;   // the HTTP rewrite space (launch_http_hint)
     TicketRing* tickets = nullptr;    // work counters; null: static grid-stride split
 };
 
