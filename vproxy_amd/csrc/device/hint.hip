@@ -571,23 +571,12 @@ __global__ __launch_bounds__(kHintBlock) void cert_kernel(
 constexpr int kDnsdBlock = 128;
 constexpr int kDnsdWaves = kDnsdBlock / 64;
 // LDS per 128-thread workgroup: two 4 KiB stages (64 queries of up to 64 B
-// on average per wave; longer spans are read from global memory) and a
-// per-lane qname buffer -- 25.6 KiB, six workgroups per CU in 1 KiB LDS
-// granules (classify.hip resident_per_cu).  A 16-byte qname apron made it
-// 28.7 KiB and five: 5.28 -> 4.44 ms with the sixth
-// (profiles/r02_ab_dnsd_residency.txt).
+// on average per wave; longer spans are read from global memory).  The
+// deferring kernel classifies each qname in place in the stage (dnsd_one);
+// the others decode it into a per-lane buffer (kNameWords).
 constexpr uint32_t kDnsdStage = 4096;
 constexpr uint32_t kDnsdStageWords = (kDnsdStage + 2 * kApron) / 4;
 constexpr int kNameCap = 128;                 // decoded qname chars classified (contract)
-// The deferring kernel's per-lane buffer holds kFastCap chars; a datagram
-// with a longer qname (up to kNameCap) is left to dnsd_defer_kernel, whose
-// buffers hold kNameCap.  96-char buffers make the workgroup 21.6 KiB, seven
-// per CU instead of six: 3.83 -> 3.51 ms for the bench's 16.7M datagrams
-// (profiles/r05_ab_dnsd_cap96.jsonl); the bench's names are under 60 chars.
-#ifndef VC_DNSD_FAST_CAP
-#define VC_DNSD_FAST_CAP 96
-#endif
-constexpr int kFastCap = VC_DNSD_FAST_CAP;
 // Readable bytes around a qname: LdsSrc reads the aligned word pair that
 // holds [pos, pos + 4) for pos in [-3, len + 3].
 constexpr int kNameApron = 4;
@@ -596,13 +585,16 @@ constexpr int kNameApron = 4;
 // (an even stride of 40 words put them on 8 banks)
 constexpr int name_words(int cap) { return (cap + 2 * kNameApron) / 4 + 1; }
 constexpr int kNameWords = name_words(kNameCap);
-constexpr int kFastWords = name_words(kFastCap);
 static_assert((kNameApron + kNameCap + 3) / 4 + 1 < kNameWords, "qname buffer too short");
-static_assert((kNameApron + kFastCap + 3) / 4 + 1 < kFastWords, "qname buffer too short");
-static_assert(kFastCap <= kNameCap && (kNameWords & 1) && (kFastWords & 1), "odd strides");
+static_assert(kNameWords & 1, "odd stride");
 constexpr int kMaxPtr = 16;
 
 enum : int { kNameOk = 0, kNameBad = 1, kNameHost = 2 };
+
+// parse_name's output for a validation-only pass
+struct NoOut {
+    __device__ void operator()(int) const {}
+};
 
 // Formatter.parseDomainName over the datagram p[0, n): the name at index 0
 // of the view [vs, vs + vlen) (vlen may be <= 0: SubByteArray takes a
@@ -632,6 +624,13 @@ __device__ __forceinline__ int parse_name(const uint8_t* p, int n, int vs, int v
                 i = 0;
                 continue;
             }
+            if constexpr (std::is_same_v<Out, NoOut>) {
+                // validation only: a label's bytes matter only through the
+                // bounds check each read makes, and the next length byte's
+                // check fails whenever one of them would: jump over it
+                i += b + 1;
+                continue;
+            }
             len = b;                                  // any other byte is a label length
         } else {
             out(b);
@@ -643,9 +642,6 @@ __device__ __forceinline__ int parse_name(const uint8_t* p, int n, int vs, int v
     return kNameOk;
 }
 
-struct NoOut {
-    __device__ void operator()(int) const {}
-};
 
 __device__ __forceinline__ int be16(const uint8_t* p, int i) { return (p[i] << 8) | p[i + 1]; }
 
@@ -729,11 +725,22 @@ constexpr uint8_t kDnsdDeferred = 0xFF;
 // kDefer: a question dns_one<true> defers makes the whole datagram
 // kDnsdDeferred (status only); dnsd_defer_kernel redoes it.  Returns the
 // status written.
-template <bool kDefer, int kCap = kDefer ? kFastCap : kNameCap>
+//
+// kDefer also classifies in place: the datagram is this lane's own bytes in
+// the wave's LDS stage (`name` = the stage, p at byte p_off of it).
+// Formatter.parseDomainName's qname is the name's wire bytes after its first
+// length byte with every later length byte and the terminating 0 read as
+// '.' (a '.' after each label), so for a query of one question whose name
+// holds no compression pointer -- a resolver's query -- those bytes are
+// patched to '.' in the stage and the qname is searched where it lies: no
+// byte-by-byte decode into a per-lane buffer, and no such buffer in the
+// kernel's LDS.  Other shapes (several questions, a pointer) are deferred.
+template <bool kDefer, int kCap = kNameCap>
 __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintImage& img,
                                             const HintImage* slow_img, const AclImage& acl,
                                             const DnsdIn& in, const DnsdOut& out, int64_t i,
-                                            const uint8_t* p, int n, uint32_t* name) {
+                                            const uint8_t* p, int n, uint32_t* name,
+                                            int p_off = 0) {
     // securityGroup.allow(Protocol.UDP, remote.getAddress(), remote.getPort())
     const bool six = in.rfam && in.rfam[i] == 6;
     const uint32_t port = in.rport[i];
@@ -803,6 +810,45 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
                 st = VC_DNSD_RECURSIVE;               // runRecursive(p, remote)
             } else if (qd > VC_DNSD_MAXQ) {
                 st = VC_DNSD_HOST;
+            } else if (kDefer) {
+                // one question, its name in place (see above)
+                int j = 12;
+                bool ptr = qd != 1;
+                while (!ptr) {
+                    const int b = p[j];
+                    if ((b & 0xC0) == 0xC0) {
+                        ptr = true;
+                        break;
+                    }
+                    if (j > 12) const_cast<uint8_t*>(p)[j] = '.';
+                    if (b == 0) break;
+                    j += b + 1;
+                }
+                if (ptr) {
+                    st = kDnsdDeferred;
+                } else {
+                    const int len = j - 12;           // the qname's chars, its last '.' included
+                    const int qtype = be16(p, j + 1);
+                    nq = 1;
+                    if (qtype != 1 && qtype != 28 && qtype != 33) {   // not A / AAAA / SRV
+                        put(0, qtype, VC_DNS_RECURSIVE, 0);
+                        st = VC_DNSD_RECURSIVE;
+                    } else if (len > kNameCap) {      // the Java path decides
+                        st = VC_DNSD_HOST;
+                        nq = 0;
+                    } else {
+                        uint8_t kd;
+                        int32_t val;
+                        dns_one<kDefer>(hosts, img, slow_img, LdsSrc{name, p_off + 13}, len, &kd,
+                                        &val);
+                        if (kd == kDnsDeferred) {
+                            st = kDnsdDeferred;
+                        } else {
+                            put(0, qtype, kd, val);
+                            if (kd == VC_DNS_RECURSIVE) st = VC_DNSD_RECURSIVE;
+                        }
+                    }
+                }
             } else {
                 // handleRequest: questions in order until one goes recursive
                 at = 12;
@@ -825,10 +871,6 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
                     if (len > kNameCap) {               // the Java path decides
                         st = VC_DNSD_HOST;
                         nq = 0;
-                        break;
-                    }
-                    if (kDefer && len > kCap) {         // longer than this kernel's buffer
-                        st = kDnsdDeferred;
                         break;
                     }
                     uint8_t kd;
@@ -860,7 +902,8 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
     const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out,
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kDnsdWaves : 1][kStage ? kDnsdStageWords : 1];
-    __shared__ uint32_t names[kDnsdBlock][kDefer ? kFastWords : kNameWords];
+    // kDefer classifies the qname in place in the stage: no per-lane buffer
+    __shared__ uint32_t names[kDefer ? 1 : kDnsdBlock][kDefer ? 1 : kNameWords];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
     HintImage slow_img = img;
     // 64-datagram chunks from the work tickets, or the static grid-stride
@@ -884,9 +927,10 @@ __global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
         uint8_t st = 0;
         if (i < n) {
             if (staged) {
+                const int po = int(kApron + (a - a0));
                 st = dnsd_one<kDefer>(hosts, img, &slow_img, acl, in, out, i,
-                                      reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
-                                      int(e - a), names[threadIdx.x]);
+                                      reinterpret_cast<const uint8_t*>(stage[w]) + po, int(e - a),
+                                      kDefer ? stage[w] : names[threadIdx.x], po);
             } else if (kDefer) {
                 st = kDnsdDeferred;
                 out.status[i] = st;
