@@ -113,7 +113,7 @@ HOT = {   # kernel (mangled-name fragment) -> VGPR ceiling of its launch
 # (VGPR bound, spilled dwords allowed)
 HOT_STRING = {
     "hint_kernelILb1ELb1ELb0E": (72, 0),      # 7 waves per SIMD
-    "hint_kernelILb1ELb1ELb1E": (72, 6),      # the uri-aware instance (c4uri)
+    "hint_kernelILb1ELb1ELb1E": (72, 3),      # the uri-aware instance (c4uri)
     "dns_kernelILb1ELb1E": (80, 0),           # 6
     "dnsd_kernelILb1ELb1E": (128, 0),
 }

@@ -339,11 +339,10 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
                         r = kDeferred;
                     else
                         r = host_only_slow(slow_img, host_blob + a, int(e - a), p);
-                    // one SPLIT key holds the top host level: its members by uri level
-                    if (kUri && is_uri_slot_code(r)) {
-                        const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
-                        r = uri_in_slot(img, -2 - r, uri_blob + ua, int(ue - ua));
-                    }
+                    // (a uri_slot_code -- one SPLIT key holds the top host
+                    // level -- is left to hint_defer_kernel's uri_in_slot:
+                    // scoring the members here made every wave wait on the
+                    // few lanes that need it and spilled the chunk loop)
                 }
             } else if (!kDefer) {
                 DStr h{nullptr, -1}, u{nullptr, -1};
@@ -355,7 +354,7 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
             out[i] = r;
         }
         if (kDefer && ticket) {
-            const uint64_t dm = __ballot(i < n && r == kDeferred);
+            const uint64_t dm = __ballot(i < n && (r == kDeferred || (kUri && is_uri_slot_code(r))));
             if constexpr (kUri)
                 ndef += uint32_t(__popcll(dm));
             else if (dm && lane == 0)
@@ -369,7 +368,8 @@ __global__ __launch_bounds__(kHintBlock, VC_HINT_MINW) void hint_kernel(
 // The lanes hint_kernel<*, true> deferred, through the reference-shaped
 // host-only search (Hint.formatHost + every dot-suffix probed in turn), or
 // for a lane with a uri (when the image has hint-uris) the general search
-// (the whole Hint.matchLevel over the candidate lists).
+// (the whole Hint.matchLevel over the candidate lists); a lane left as a
+// uri_slot_code takes uri_in_slot over that key's members first.
 // ctl = the launch's ticket slot: [1] deferred lanes (0: nothing to do),
 // [2] workgroups done; the last workgroup zeroes both for the slot's next
 // launch.  Without a slot every workgroup scans.
@@ -386,7 +386,13 @@ __global__ __launch_bounds__(256) void hint_defer_kernel(
     if (todo) {
         for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
              i += int64_t(gridDim.x) * blockDim.x) {
-            if (out[i] != kDeferred) continue;
+            const int32_t o = out[i];
+            if (o >= -1) continue;
+            if (is_uri_slot_code(o)) {          // one SPLIT key's members by uri level
+                const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
+                out[i] = uri_in_slot(img, -2 - o, uri_blob + ua, int(ue - ua));
+                if (out[i] != kDeferred) continue;
+            }
             const int p = port ? int(port[i]) : 0;
             const bool has_host = !(host_null && host_null[i]);
             const uint32_t a = host_off[i], e = host_off[i + 1];
