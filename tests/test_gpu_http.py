@@ -176,7 +176,7 @@ def test_http_hint_device_argument_checks():
         hb = torch.tensor(list(head), dtype=torch.uint8, device="cuda")
         ok = torch.tensor([0, len(head)], dtype=torch.int32, device="cuda")
         g, k = clf.http_hint((hb, ok))
-        assert g.cpu().tolist() == [0] and k.cpu().tolist() == [2]
+        assert g.cpu().tolist() == [0] and k.cpu().tolist() == [3]      # Hint.ofHostUri
         for bad in ((hb, ok.to(torch.int64)), (hb.to(torch.int32), ok),
                     (hb, torch.empty(0, dtype=torch.int32, device="cuda"))):
             with pytest.raises(V.IllegalArgumentException):
