@@ -178,6 +178,8 @@ int ic_hint(const vc_group_annos* g, int ng, const uint8_t* hb, const uint32_t* 
             // the uri-aware deferring form (hint_kernel<.., .., true>): a
             // port-0 hint with a host takes the host fast path and gets the
             // same result there, or kDeferred for the general search
+            // the follow-up kernel's level-ordered form for port 0
+            if (p == 0 && hint_port0_uri(img, h, u.p, u.n) != want) return -106;
             if (p != 0 || h.n < 0) { ++g_hint_deferred; continue; }
             for (int al = 0; al < 4; ++al) {
                 Staged st(h.p, h.n, al);

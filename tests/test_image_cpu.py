@@ -410,3 +410,31 @@ def test_hint_bench_names_are_never_deferred():
     blob, off = W.pack(odd)
     IC.hint(arr, ng, (blob, off.astype(np.uint32), None), np.full(len(odd), 80, np.uint16), None)
     assert IC.hint_deferred() >= 3
+
+
+@pytest.mark.parametrize("wildcards", [0.0, 0.02])
+def test_hint_uri_fast_path_on_image(wildcards):
+    """The uri-aware fast path (host_only_fast with `uri`: the host answer,
+    a SPLIT key's slot for uri_in_slot, or deferred) and the follow-up's
+    level-ordered port-0 search (hint_port0_uri) against the general search
+    on every port-0 uri hint (imgcheck ic_hint: -105 / -106 on a mismatch),
+    over groups that share hint-hosts with and without hint-uris, several
+    matching suffix keys, "*" groups, hosts no key lists and uris with '?',
+    '*', '' and over 60 bytes; a sample against the oracle."""
+    import test_gpu_c4uri as T
+    rng = np.random.default_rng(17)
+    hosts = ["a.com", "b.a.com", "c.b.a.com", "x.org", "y.x.org", "z.net", "com", "org"]
+    g = T._split_groups(rng, hosts, 300, wildcards)
+    qh = hosts + ["d.c.b.a.com", "q.z.net", "nope.io", "www.a.com:80", "a.com:8080", ":80",
+                  "m.y.x.org", "[::1]:80"]
+    qu = ["/a/b/c/x", "/a/b", "/a/", "/a?x=1", "/", "/b/q", "/zz", "*", "/a/b/c/d/e/f?g", "*x",
+          "", "?", "/" + "/".join("abcdefghijklmnopqrstuvwxyz0123456")]
+    n = 12000
+    hs = [None if rng.random() < 0.05 else qh[int(rng.integers(0, len(qh)))] for _ in range(n)]
+    us = [qu[int(rng.integers(0, len(qu)))] for _ in range(n)]
+    arr, ng, keep = group_array(g)
+    out = IC.hint(arr, ng, pack_strings(hs), np.zeros(n, np.uint16), pack_strings(us))
+    og = O.Groups(g)
+    s = rng.integers(0, n, 1500)
+    assert [int(out[i]) for i in s] == [O.search_for_group(og, hs[i], 0, us[i]) for i in s]
+    assert 0 < IC.hint_deferred() < n

@@ -399,8 +399,9 @@ __global__ __launch_bounds__(256) void hint_defer_kernel(
             if (uri_blob && img.has_uri_keys && !(uri_null && uri_null[i])) {
                 const uint32_t ua = uri_off[i], ue = uri_off[i + 1];
                 const DStr h = has_host ? DStr{host_blob + a, int(e - a)} : DStr{nullptr, -1};
-                out[i] = hint_general(img, format_host(h), p,
-                                      format_uri(DStr{uri_blob + ua, int(ue - ua)}));
+                out[i] = p == 0 ? hint_port0_uri(img, h, uri_blob + ua, int(ue - ua))
+                                : hint_general(img, format_host(h), p,
+                                               format_uri(DStr{uri_blob + ua, int(ue - ua)}));
             } else {
                 out[i] = host_only_slow(img, host_blob + a, int(e - a), p);
             }

@@ -806,6 +806,30 @@ VC_HD int format_uri_len(const uint8_t* p, int n) {
 // ascends; strict '>'), Hint.java:144-157 -- uriLevel = U.length() + 1 when
 // the uri starts with U (equal included), 1 for "*", capped at 1023.  A
 // member list longer than 32 goes to the general search.
+// Scores host slot `slot`'s members by uriLevel against the formatted uri
+// up[0, m) into (*lvl, *best): a higher level wins, then the lower index.
+VC_HD void score_slot(const HintImage& img, int slot, const uint8_t* up, int m, int* lvl,
+                      int32_t* best) {
+    const HostExt x = gload(img.host_ext + slot);
+    for (uint32_t i = 0; i < x.list_cnt; ++i) {
+        const uint32_t g = gload(img.lists + x.list_off + i);
+        const int4 r = gload(reinterpret_cast<const int4*>(img.groups) + 2 * g);
+        const int4 r2 = gload(reinterpret_cast<const int4*>(img.groups) + 2 * g + 1);
+        const int Un = r.z;
+        int ul = 0;
+        if (Un >= 0) {
+            const uint8_t* U = img.blob + uint32_t(r.w);
+            if (Un <= m && bytes_eq(U, up, Un)) ul = r2.z + 1;
+            else if (Un == 1 && U[0] == '*') ul = 1;
+            ul = ul > 1023 ? 1023 : ul;
+        }
+        if (ul > *lvl || (ul == *lvl && (*best < 0 || int32_t(g) < *best))) {
+            *lvl = ul;
+            *best = int32_t(g);
+        }
+    }
+}
+
 VC_HD int32_t uri_in_slot(const HintImage& img, int slot, const uint8_t* up, int un) {
     const HostExt x = gload(img.host_ext + slot);
     if (x.list_cnt > 32) return kDeferred;
@@ -977,6 +1001,84 @@ __host__ __device__ __noinline__ int32_t hint_general_src(const HintImage& img, 
 __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr host, int port,
                                                       DStr uri) {
     return hint_general_src(img, host, PtrSrc{host.p}, port, uri);
+}
+
+// searchForGroup(Hint.ofHostUri(host, uri)) -- port 0, a non-null uri --
+// by levels (Hint.java:100-160, Upstream.java:187-198), for the lanes the
+// fast path leaves: every group at the top host level L beats every group
+// below it (uriLevel <= 1023), so only L's keys are scored, their members
+// by uriLevel and then index; with no host level (L = 0) the uri alone
+// decides -- the longest hint-uri that prefixes the uri (one level per
+// length; "" and "*" share level 1), its first member.  host / uri raw
+// (formatted here), in global memory.
+__host__ __device__ __noinline__ int32_t hint_port0_uri(const HintImage& img, DStr host_raw,
+                                                        const uint8_t* up, int un) {
+    const int m = format_uri_len(up, un);
+    int lvl = 0;
+    int32_t best = -1;
+    const DStr host = format_host(host_raw);
+    if (host.n >= 0) {
+        const HostTable t = host_table(img);
+        const PtrSrc q{host.p};
+        Rec r;
+        int slot = host_lookup(t, q, 0, host.n, &r);
+        if (slot >= 0) {                                    // level 3: the exact key
+            score_slot(img, slot, up, m, &lvl, &best);
+            return best;
+        }
+        const Dots dots = find_dots(host.p, 0, host.n);
+        bool any = false;
+        for (int k = 0; k < dots.n; ++k) {                  // level 2: every dot-suffix key
+            const int j = dots.at(k);
+            slot = host_lookup(t, q, j + 1, host.n - j - 1, &r);
+            if (slot >= 0) {
+                score_slot(img, slot, up, m, &lvl, &best);
+                any = true;
+            }
+        }
+        if (dots.more)
+            for (int j = dots.d0 - 1; j >= 0; --j) {
+                if (host.p[j] != '.') continue;
+                slot = host_lookup(t, q, j + 1, host.n - j - 1, &r);
+                if (slot >= 0) {
+                    score_slot(img, slot, up, m, &lvl, &best);
+                    any = true;
+                }
+            }
+        if (any) return best;
+        if (img.wildcard_slot >= 0) {                       // level 1: "*"
+            score_slot(img, img.wildcard_slot, up, m, &lvl, &best);
+            return best;
+        }
+    }
+    // level 0: the uri alone (port 0: a key's members share its level, the
+    // first is the lowest index)
+    const uint64_t lens = uint64_t(img.uri_len_hi) << 32 | img.uri_len_lo;
+    uint32_t h = kFnvBasis;
+    KeySlot k;
+    for (int j = 0; j <= m; ++j) {
+        if (((lens >> (j < 63 ? j : 63)) & 1u) && uri_probe(img, h, up, j, &k) >= 0 && k.list_cnt) {
+            const int32_t g = int32_t(img.lists[k.list_off]);
+            const int ul = (j == 0 ? 0 : img.groups[g].uri_units) + 1;
+            const int cl = ul > 1023 ? 1023 : ul;
+            if (cl > lvl || (cl == lvl && g < best)) {
+                lvl = cl;
+                best = g;
+            }
+        }
+        if (j < m) h = fnv_step(h, up[j]);
+    }
+    if (img.uri_star_slot >= 0) {
+        const KeySlot u = load_slot(img.uri_slots, uint32_t(img.uri_star_slot));
+        if (u.list_cnt) {
+            const int32_t g = int32_t(img.lists[u.list_off]);
+            if (1 > lvl || (1 == lvl && g < best)) {
+                lvl = 1;
+                best = g;
+            }
+        }
+    }
+    return best;
 }
 
 VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,
