@@ -903,8 +903,12 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
     return st;
 }
 
+// Minimum waves per SIMD of dnsd_kernel (the register budget it compiles to)
+#ifndef VC_DNSD_MINW
+#define VC_DNSD_MINW 3
+#endif
 template <bool kStage, bool kDefer>
-__global__ __launch_bounds__(kDnsdBlock, 3) void dnsd_kernel(
+__global__ __launch_bounds__(kDnsdBlock, VC_DNSD_MINW) void dnsd_kernel(
     HostsImage hosts, HintImage img, AclImage acl, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, DnsdIn in, DnsdOut out,
     uint32_t* __restrict__ ticket) {

@@ -1011,12 +1011,12 @@ __host__ __device__ __noinline__ int32_t hint_general(const HintImage& img, DStr
 // decides -- the longest hint-uri that prefixes the uri (one level per
 // length; "" and "*" share level 1), its first member.  host / uri raw
 // (formatted here), in global memory.
-__host__ __device__ __noinline__ int32_t hint_port0_uri(const HintImage& img, DStr host_raw,
-                                                        const uint8_t* up, int un) {
-    const int m = format_uri_len(up, un);
+// hint_port0_levels: the same over a formatted host and the formatted uri
+// up[0, m) (formatUri is not idempotent: "/a//" -> "/a/" -> "/a").
+__host__ __device__ __noinline__ int32_t hint_port0_levels(const HintImage& img, DStr host,
+                                                           const uint8_t* up, int m) {
     int lvl = 0;
     int32_t best = -1;
-    const DStr host = format_host(host_raw);
     if (host.n >= 0) {
         const HostTable t = host_table(img);
         const PtrSrc q{host.p};
@@ -1079,6 +1079,11 @@ __host__ __device__ __noinline__ int32_t hint_port0_uri(const HintImage& img, DS
         }
     }
     return best;
+}
+
+__host__ __device__ __noinline__ int32_t hint_port0_uri(const HintImage& img, DStr host_raw,
+                                                        const uint8_t* up, int un) {
+    return hint_port0_levels(img, format_host(host_raw), up, format_uri_len(up, un));
 }
 
 VC_HD int32_t search_for_group(const HintImage& img, DStr host, int port,

@@ -206,20 +206,19 @@ __device__ DStr http_str(Cur& c, int s, int e, uint8_t* out) {
     return DStr{out, k};
 }
 
-// Upstream.searchForGroup(hint); a host read in place from the stage is
-// probed through LdsSrc (two dword reads per word instead of four byte reads)
+// Upstream.searchForGroup(hint), port 0.  With a uri (and hint-uris in the
+// image): by levels (hint_port0_levels, round 6) -- only the top host
+// level's keys are scored, the uri keys probed only without a host level.
 __device__ __forceinline__ int32_t http_search(const HintImage& img, HeadCur&, DStr host,
                                                DStr uri) {
+    if (uri.n >= 0 && img.has_uri_keys) return hint_port0_levels(img, host, uri.p, uri.n);
     return search_for_group(img, host, 0, uri);
 }
 
-__device__ __forceinline__ int32_t http_search(const HintImage& img, StagedCur& c, DStr host,
+__device__ __forceinline__ int32_t http_search(const HintImage& img, StagedCur&, DStr host,
                                                DStr uri) {
-    const uint8_t* base = reinterpret_cast<const uint8_t*>(c.stage);
-    if (uri.n < 0 || !img.has_uri_keys || host.n < 0 || host.p < base ||
-        host.p >= base + kApron + kHttpStage)
-        return search_for_group(img, host, 0, uri);
-    return hint_general_src(img, host, LdsSrc{c.stage, int(host.p - base)}, 0, uri);
+    if (uri.n >= 0 && img.has_uri_keys) return hint_port0_levels(img, host, uri.p, uri.n);
+    return search_for_group(img, host, 0, uri);
 }
 
 // One head: (group, kind).  Rewritten strings go to the launch's scratch,
