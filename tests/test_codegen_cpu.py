@@ -115,7 +115,7 @@ HOT_STRING = {
     "hint_kernelILb1ELb1ELb0E": (72, 0),      # 7 waves per SIMD
     "hint_kernelILb1ELb1ELb1E": (72, 3),      # the uri-aware instance (c4uri)
     "dns_kernelILb1ELb1E": (80, 0),           # 6
-    "dnsd_kernelILb1ELb1E": (128, 0),
+    "dnsd_kernelILb1ELb1E": (96, 0),          # 5 waves per SIMD, in-place qnames
 }
 
 

@@ -903,9 +903,13 @@ __device__ __forceinline__ uint8_t dnsd_one(const HostsImage& hosts, const HintI
     return st;
 }
 
-// Minimum waves per SIMD of dnsd_kernel (the register budget it compiles to)
+// Minimum waves per SIMD of dnsd_kernel (the register budget it compiles
+// to).  5 (96 VGPRs, no spills) since the qname is classified in place and
+// the workgroup's LDS is 8 KiB: 1.55 -> 1.43 ms for the bench's 16.7M
+// datagrams against 3 (98 VGPRs), interleaved on one box
+// (profiles/r06_ab_dnsd_minw.jsonl).
 #ifndef VC_DNSD_MINW
-#define VC_DNSD_MINW 3
+#define VC_DNSD_MINW 5
 #endif
 template <bool kStage, bool kDefer>
 __global__ __launch_bounds__(kDnsdBlock, VC_DNSD_MINW) void dnsd_kernel(
