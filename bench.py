@@ -26,6 +26,7 @@ torch.distributed.run (one rank per GPU, RCCL).
 """
 import argparse
 import ctypes as C
+import functools
 import json
 import os
 import sys
@@ -1378,7 +1379,7 @@ def sub_bench(args, clf, dev, rank, world):
                        "affinity": info["affinity"], "cgroup_cpu_max": info["cgroup_cpu_max"],
                        "quota_cpus": info["quota_cpus"], "cpu_model": info["cpu_model"]}
             else:
-                cpu = cpu_rates(run, "M items/s", 4.0, "first tuples of the C2 batch, oracle "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "first tuples of the C2 batch, oracle "
                                 "first-match scan over 10k rules")
     elif args.workload == "c3":
         n = 256 << 20
@@ -1415,7 +1416,7 @@ def sub_bench(args, clf, dev, rank, world):
                 O.rt_batch_v4_np(v4l, q4h[:k4_], nthreads=threads)
                 O.rt_batch_v6_np(v6l, q6h[:max(1, k - k4_)], nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 4.0, "85/15 v4/v6 lookups of the C3 workload, "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "85/15 v4/v6 lookups of the C3 workload, "
                             "oracle first-match scans over the RouteTable lists")
     elif args.workload in ("c4", "dns"):
         dns = args.workload == "dns"
@@ -1467,10 +1468,10 @@ def sub_bench(args, clf, dev, rank, world):
                     O.hint_batch_np(og, sb, so, None, nthreads=threads)
                 return time.perf_counter() - t0
             if dns:
-                cpu = cpu_rates(run, "M items/s", 4.0, "qnames of the DNS workload, oracle hosts "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "qnames of the DNS workload, oracle hosts "
                                 "lookup (50k entries) + searchForGroup scan over 100k groups", cap=n)
             else:
-                cpu = cpu_rates(run, "M items/s", 4.0, "hostnames of the C4 pool, oracle "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "hostnames of the C4 pool, oracle "
                                 "searchForGroup scan over 100k groups", cap=n)
     elif args.workload == "dnsd":
         # DNSServer's drain loop per datagram: UDP SecurityGroup (10k rules)
@@ -1523,7 +1524,7 @@ def sub_bench(args, clf, dev, rank, world):
                 O.dnsd_batch_np(tcp, udp, True, oh, og, sb, so, None, h4[:k], None, hp[:k],
                                 nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 4.0, "datagrams of the workload, oracle UDP "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "datagrams of the workload, oracle UDP "
                             "SecurityGroup scan (10k rules) + parsePackets + hosts lookup and "
                             "searchForGroup scan over 100k groups", cap=n)
     elif args.workload == "sni":
@@ -1545,7 +1546,7 @@ def sub_bench(args, clf, dev, rank, world):
                 t0 = time.perf_counter()
                 O.cert_batch_np(oc, sb, so, nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 3.0, "SNIs of the workload, oracle "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "SNIs of the workload, oracle "
                             "SSLContextHolder.choose scan over 100k holders (200k names)", cap=n)
     elif args.workload == "c4uri":
         n = 16 << 20
@@ -1573,7 +1574,7 @@ def sub_bench(args, clf, dev, rank, world):
                 O.hint_uri_batch_np(og, sb, so, ubs, uos, (uidx[:k] < 0).astype(np.uint8),
                                     nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 4.0, "Hint.ofHostUri hints of the workload, oracle "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "Hint.ofHostUri hints of the workload, oracle "
                             "searchForGroup scan (whole matchLevel) over 100,200 groups", cap=n)
     elif args.workload == "http":
         n = 8 << 20
@@ -1604,7 +1605,7 @@ def sub_bench(args, clf, dev, rank, world):
                 t0 = time.perf_counter()
                 O.http_batch_np(og, sb, so, nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 4.0, "request heads of the workload, oracle "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "request heads of the workload, oracle "
                             "HttpSubContext state machine + searchForGroup scan over 100k groups",
                             cap=n)
     elif args.workload in ("parse", "mirror", "switch"):
@@ -1629,7 +1630,7 @@ def sub_bench(args, clf, dev, rank, world):
                     t0 = time.perf_counter()
                     O.parse_batch_np(sb, so, 0, nthreads=threads)
                     return time.perf_counter() - t0
-                cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle vpacket "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "frames of the workload, oracle vpacket "
                                 "parse chain (VXLAN -> Ethernet -> IPv4/IPv6 -> TCP/ICMP)", cap=1 << 22)
         elif args.workload == "switch":
             # parse + bare-VXLAN ACL on the sender + inner route, one kernel,
@@ -1659,7 +1660,7 @@ def sub_bench(args, clf, dev, rank, world):
                     O.switch_batch_np(sw_tcp, sw_udp, False, sb, so, r4h[:k], 4789, t.v4_list,
                                       t.v6_list, nthreads=threads)
                     return time.perf_counter() - t0
-                cpu = cpu_rates(run, "M items/s", 4.0, "datagrams of the workload, oracle parse + "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 4.0, "datagrams of the workload, oracle parse + "
                                 "SecurityGroup.allow scan + RouteTable.lookup scan of the inner "
                                 "destination", cap=1 << 20)
         else:
@@ -1683,7 +1684,7 @@ def sub_bench(args, clf, dev, rank, world):
                     O.mirror_switch_batch_np(oarr, len(filters), ids["switch"], sb, so, 0,
                                              nthreads=threads)
                     return time.perf_counter() - t0
-                cpu = cpu_rates(run, "M items/s", 3.0, "frames of the workload, oracle "
+                cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "frames of the workload, oracle "
                                 "Mirror.switchPacket over the 17 filters", cap=1 << 22)
     elif args.workload == "source":
         n = 128 << 20
@@ -1703,12 +1704,17 @@ def sub_bench(args, clf, dev, rank, world):
                 t0 = time.perf_counter()
                 O.source_batch_np(osg, 0, gh[:k], sh[:k], nthreads=threads)
                 return time.perf_counter() - t0
-            cpu = cpu_rates(run, "M items/s", 3.0, "clients of the workload, oracle "
+            cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "clients of the workload, oracle "
                             "sourceHashGet over each group's sourceReset order (built once per "
                             "call for all 10k groups, as Java caches it per group)", cap=1 << 22)
     else:
         return mix_bench(args, clf, dev, rank, O, world)
     el, ms = _time(fn, args.steps, args.warmup)
+    # the CPU baseline after the timed launches: run before them, its seconds
+    # of host work left the GPU idle, and short kernels (SNI: 0.53 ms) timed
+    # up to 2.3x slower right after
+    if callable(cpu):
+        cpu = cpu()
     gbs = per_unit * n / (ms / 1e3) / 1e9
     res = {"workload": args.workload, "items": n, "ms_per_step": round(el / args.steps * 1e3, 3),
            "kernel_ms": round(ms, 4), "M_items_per_s": round(n / (ms / 1e3) / 1e6, 1),
