@@ -93,6 +93,10 @@ void J(compileVniRoutes)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, job
 void J(compileUpstream)(JNIEnv *, jclass, jlong, jobject, jint, jobject);
 void J(searchHints)(JNIEnv *, jclass, jlong, jobject, jobject, jobject, jobject, jobject, jobject,
                     jobject, jint, jobject);
+jlong J(pinAcquire)(JNIEnv *, jclass, jlong, jint);
+void J(bindPin)(JNIEnv *, jclass, jlong, jlong);
+jlong J(pinGeneration)(JNIEnv *, jclass, jlong, jint);
+void J(pinRelease)(JNIEnv *, jclass, jlong);
 void J(switchClassify)(JNIEnv *, jclass, jlong, jobject, jobject, jint, jint, jobject, jobject,
                        jobject, jint, jobjectArray, jobject, jobject, jobject);
 
@@ -167,6 +171,19 @@ static void cpu_mode(void) {
     struct _jobject bg = B(&g, sizeof g), bstr = B(strings, 5);
     (void) J(create)(env, NULL, 0);
     expect_throw("java/io/IOException", "", "create without a GPU throws IOException");
+    /* snapshot pins: a null context or pin is refused, release of 0 is a no-op */
+    {
+        const jlong pin = J(pinAcquire)(env, NULL, 0, 0xFF);
+        expect_throw("java/lang/IllegalArgumentException", "null", "pinAcquire on a null context");
+        CHECK(pin == 0, "pinAcquire on a null context returns 0");
+        J(bindPin)(env, NULL, 0, 0);
+        expect_throw("java/lang/IllegalArgumentException", "null", "bindPin on a null context");
+        const jlong gen = J(pinGeneration)(env, NULL, 0, 1);
+        expect_throw("java/lang/IllegalArgumentException", "null", "pinGeneration of a null pin");
+        CHECK(gen == 0, "pinGeneration of a null pin returns 0");
+    }
+    J(pinRelease)(env, NULL, 0);
+    CHECK(n_thrown == 0, "pinRelease(0) is a no-op");
     /* 8 items need 32 bytes of src4: a 31-byte buffer is refused before any vc_ call */
     J(classifyAclV4)(env, NULL, 0, &bp, &bs, &bq, 8, &bo, NULL);
     expect_throw("java/lang/IllegalArgumentException", "smaller than the batch",

@@ -82,3 +82,41 @@ def test_pin_of_another_context_is_refused():
     finally:
         a.close()
         b.close()
+
+
+def test_pinned_snapshots_are_freed_after_release():
+    """A pin keeps its snapshot's device tables alive across recompiles,
+    and they go once it is released: after ten recompiles of a 200k-rule
+    route table (each image tens of MB) under a pin held all along, the
+    device memory in use comes back to about one table image above the
+    start once the pin is released and the next compile frees the
+    graveyard (capi.cpp: a replaced snapshot's buffers are freed by the
+    control thread, never by the thread that drops the last pin)."""
+    import torch
+    from vproxy_amd import workloads as W
+    net, plen = W.gen_v4_prefixes(200_000, 5)
+    a = [W.v4_nets(net, plen), W.v4_nets(net[::-1].copy(), plen[::-1].copy())]
+    arrs = [W.as_ctypes(x, V._lib.VcNet) for x in a]
+    clf = V.Classifier(0)
+    try:
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        clf.compile_routes_raw(arrs[0][0], arrs[0][1], None, 0)
+        q = np.random.default_rng(6).integers(0, 2**32, 100000, dtype=np.uint64).astype(np.uint32)
+        want = clf.route_v4(q)
+        p = clf.pin(1 << L.SNAP_ROUTE)
+        for k in range(10):
+            clf.compile_routes_raw(arrs[(k + 1) % 2][0], arrs[(k + 1) % 2][1], None, 0)
+        with p:
+            np.testing.assert_array_equal(clf.route_v4(q), want)     # the pinned table
+        assert (clf.route_v4(q) != want).mean() > 0.5               # the current one differs
+        torch.cuda.synchronize()
+        held = free0 - torch.cuda.mem_get_info()[0]
+        p.release()
+        clf.compile_routes_raw(arrs[0][0], arrs[0][1], None, 0)     # frees the graveyard
+        torch.cuda.synchronize()
+        after = free0 - torch.cuda.mem_get_info()[0]
+        assert held > 0 and after < held, (held, after)
+        assert after < 0.75 * held or held - after > (16 << 20), (held, after)
+    finally:
+        clf.close()
