@@ -76,6 +76,32 @@ def test_source_select_vs_oracle(clf):
     np.testing.assert_array_equal(got, _want(sick, grp, src4_bytes, V.SOURCE_ALL))
 
 
+@pytest.mark.parametrize("shape", ["many_groups", "long_list"])
+def test_source_global_lists(clf, shape):
+    """The kernels copy a view's lists (offset, count) into LDS when they fit
+    (select.hip kSelLdsMax, ServerImage.view_pk); past that -- more groups
+    than the LDS copy holds, or a list of 256+ servers the packed form cannot
+    count -- they read the global table.  Both equal the oracle."""
+    rng = np.random.default_rng(23 if shape == "many_groups" else 24)
+    groups = _groups(rng, 12000 if shape == "many_groups" else 300)
+    if shape == "long_list":
+        groups[7] = [(bytes(rng.integers(0, 256, 4).astype(np.uint8)), 80, 1,
+                      bool(rng.random() < 0.7)) for _ in range(300)]
+    clf.compile_servers(groups)
+    n = 12000
+    grp = rng.integers(-1, len(groups) + 2, n).astype(np.int32)
+    if shape == "long_list":
+        grp[::3] = 7
+    src4 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    src4_bytes = src4.astype(">u4").view(np.uint8).reshape(-1, 4)
+    src6 = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    for view in (V.SOURCE_ALL, V.SOURCE_IPV4, V.SOURCE_IPV6):
+        np.testing.assert_array_equal(clf.source_select(grp, src4, view),
+                                      _want(groups, grp, src4_bytes, view))
+        np.testing.assert_array_equal(clf.source_select(grp, src6, view),
+                                      _want(groups, grp, src6, view))
+
+
 def test_source_sticky_like_tcplb(clf):
     """TestTcpLB.proxySource: every connection from 127.0.0.1 reaches svr0,
     the backend that answers "0" (TestTcpLB.java:383-405; kats.json source)."""

@@ -1602,8 +1602,10 @@ int vc_compile_servers(vc_ctx* ctx, const vc_server* servers, const int32_t* gro
     s->img.healthy = up(*s, b.healthy);
     s->img.group_base = up(*s, b.group_base);
     s->img.pick = up(*s, b.pick);
+    s->img.view_pk = up(*s, b.view_pk);
     s->img.n_groups = b.n_groups;
     s->img.n_servers = b.n_servers;
+    s->img.pk_ok = b.pk_ok ? 1 : 0;
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "server upload");
     s->host = std::make_shared<const vc::ServersBuilt>(std::move(b));
     ctx->publish(ctx->servers, std::shared_ptr<const ServerSnap>(std::move(s)));

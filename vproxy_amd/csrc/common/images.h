@@ -266,6 +266,9 @@ struct MirrorImage {
 // there: the first healthy server from that position on, cyclically within
 // the list, as an index within its group (-1: none healthy) -- rebuilt on
 // the host with every health update (compile.cpp source_pick_table).
+// view_pk is view_off packed for the kernels' LDS copy: [view][group] =
+// offset << 8 | count, present (pk_ok) when every offset < 2^24 and every
+// count < 256.
 // ---------------------------------------------------------------------------
 struct ServerImage {
     const uint32_t* view_off;      // 6 words per group
@@ -273,6 +276,8 @@ struct ServerImage {
     const uint8_t* healthy;
     const int32_t* group_base;
     const int32_t* pick;
+    const uint32_t* view_pk;       // 3 * n_groups words, or null
     int32_t n_groups;
     int32_t n_servers;
+    int32_t pk_ok;
 };

@@ -758,6 +758,19 @@ int build_servers(const vc_server* servers, const int32_t* group_off, int n_grou
         }
     }
     out->group_base[n_groups] = total;
+    // the packed form for the kernels' LDS copy (images.h ServerImage.view_pk)
+    out->pk_ok = n_groups > 0;
+    out->view_pk.assign(size_t(n_groups) * 3 + 1, 0);
+    for (int g = 0; g < n_groups && out->pk_ok; ++g)
+        for (int v = 0; v < 3; ++v) {
+            const uint32_t off = out->view_off[size_t(g) * 6 + 2 * v];
+            const uint32_t cnt = out->view_off[size_t(g) * 6 + 2 * v + 1];
+            if (off >= (1u << 24) || cnt >= 256u) {
+                out->pk_ok = false;
+                break;
+            }
+            out->view_pk[size_t(v) * n_groups + g] = off << 8 | cnt;
+        }
     if (out->order.empty()) out->order.push_back(0);
     if (out->view_off.empty()) out->view_off.assign(6, 0);
     source_pick_table(*out, out->healthy.data(), &out->pick);

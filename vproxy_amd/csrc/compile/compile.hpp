@@ -107,6 +107,8 @@ struct ServersBuilt {
     std::vector<uint8_t> healthy;
     std::vector<int32_t> group_base;
     std::vector<int32_t> pick;           // per order[] entry (images.h ServerImage)
+    std::vector<uint32_t> view_pk;       // [view][group] offset << 8 | count (when pk_ok)
+    bool pk_ok = false;
     int32_t n_groups = 0;
     int32_t n_servers = 0;
 };
