@@ -421,3 +421,63 @@ def http_heads_random(rng, n, hosts, uris):
             head += b"x" * int(rng.integers(1, 64))
         out.append(head)
     return out
+
+
+def ip_like_strings(rng, n):
+    """Strings shaped like IP literals and near misses: hex groups, "::",
+    dotted quads (leading zeros, > 255), brackets, stray characters."""
+    out = []
+    hexd = b"0123456789abcdefABCDEF"
+
+    def group():
+        r = rng.random()
+        k = int(rng.integers(1, 5)) if r < 0.9 else int(rng.choice([0, 5]))
+        g = bytes(rng.choice(np.frombuffer(hexd, np.uint8), k))
+        return g + b"g" if rng.random() < 0.02 else g
+
+    def quad():
+        return b".".join(str(int(rng.choice([0, 1, 10, 99, 192, 255, 256]))).encode()
+                         if rng.random() < 0.97 else b"01" for _ in range(4))
+
+    for _ in range(n):
+        if rng.random() < 0.6:                  # address-shaped: 8 groups, or "::" in them
+            tail4 = rng.random() < 0.25
+            want = 6 if tail4 else 8
+            if rng.random() < 0.5:
+                gs = [group() for _ in range(want + int(rng.choice([0, 0, 0, -1, 1])))]
+                s = b":".join(gs)
+            else:
+                k = int(rng.integers(0, want))
+                a = int(rng.integers(0, k + 1))
+                s = b":".join(group() for _ in range(a)) + b"::" + \
+                    b":".join(group() for _ in range(k - a))
+            if tail4:
+                s = s + (b"" if s.endswith(b":") else b":") + quad()
+            if rng.random() < 0.1:
+                s = b"[" + s + b"]"
+            if rng.random() < 0.05:
+                s = s + b":" + str(int(rng.integers(0, 70000))).encode()
+            out.append(s)
+            continue
+        parts = []
+        for _ in range(int(rng.integers(0, 10))):
+            r = rng.random()
+            if r < 0.55:
+                parts.append(bytes(rng.choice(np.frombuffer(hexd, np.uint8), int(rng.integers(0, 6)))))
+            elif r < 0.7:
+                parts.append(b"")
+            elif r < 0.85:
+                parts.append(b".".join(str(int(rng.choice([0, 1, 9, 10, 99, 255, 256, 7]))).encode()
+                                       if rng.random() < 0.9 else b"01"
+                                       for _ in range(int(rng.integers(3, 6)))))
+            else:
+                parts.append(bytes(rng.choice(np.frombuffer(b"gz.%x", np.uint8), int(rng.integers(1, 3)))))
+        s = b":".join(parts)
+        if rng.random() < 0.2:
+            s = s.replace(b":", b"::", 1)
+        if rng.random() < 0.15:
+            s = b"[" + s + b"]"
+        if rng.random() < 0.1:
+            s = s + b":" + str(int(rng.integers(0, 70000))).encode()
+        out.append(s)
+    return out

@@ -49,6 +49,11 @@ kernels or the table compiler.
   116-166) -- a dict restatement of Resolver.getHosts' dual-key map
   (Resolver.java:62-153), then HintChecker on the dot-stripped name, then
   the IP-literal / .vproxy.local / recursive tail.
+- java_is_ipv6 / java_is_ip_literal: IP.isIpv6 / IP.isIpLiteral
+  (IP.java:112-300) as validity predicates over bytes, with the parser's
+  quirks (Utils.split keeps empty pieces; parseIpv6LastBits' `4 +
+  colonPart` counts a failed colon part as 3), so formatHost's IPv6 branch
+  and the DNS IP-literal step need no oracle call.
 """
 import re
 
@@ -273,6 +278,77 @@ def _anno(a, k):
     return a.get("vproxy/hint-" + k, a.get(k))
 
 
+_HEX = frozenset(b"0123456789abcdefABCDEF")
+
+
+def _v4_ok(s, from_idx, cap):
+    """IP.parseIpv4String(s, bytes, fromIdx) succeeds (IP.java:129-155):
+    three dots, four pieces of 1-3 ASCII digits, no leading zero, <= 255,
+    every piece inside the byte array."""
+    if s.count(b".") != 3:
+        return False
+    for i, p in enumerate(s.split(b".")):
+        if from_idx + i >= cap or not 1 <= len(p) <= 3 or not p.isdigit():
+            return False
+        if (p[:1] == b"0" and len(p) > 1) or int(p) > 255:
+            return False
+    return True
+
+
+def _colon_part(s, from_idx):
+    """IP.parseIpv6ColonPart (IP.java:200-248): 2 x its pieces, or -1.
+    None (Java null) and "" consume nothing."""
+    if not s:
+        return 0
+    if from_idx < 0:
+        return -1
+    parts = s.split(b":")
+    for i, f in enumerate(parts):
+        if from_idx + 2 * i >= 16 or not 1 <= len(f) <= 4 or any(c not in _HEX for c in f):
+            return -1
+    return 2 * len(parts)
+
+
+def _last_bits(s):
+    """IP.parseIpv6LastBits (IP.java:251-269): the bytes the part after
+    "::" (or the whole string) consumes, or -1; a dotted tail is an IPv4
+    quad, and `4 + colonPart` turns a failed colon part before it into 3."""
+    dot = s.find(b".")
+    if dot == -1:
+        return _colon_part(s, 16 - 2 * (s.count(b":") + 1))
+    k = s.rfind(b":", 0, dot)
+    if k == -1:
+        return 4 if _v4_ok(s, 12, 16) else -1
+    if not _v4_ok(s[k + 1:], 12, 16):
+        return -1
+    head = s[:k]
+    return 4 + _colon_part(head, 16 - 4 - 2 * (head.count(b":") + 1))
+
+
+def java_is_ipv6(s):
+    """IP.isIpv6 = IP.parseIpv6String(s) != null (IP.java:158-197) on bytes."""
+    if b":" not in s:
+        return False                       # one piece: never 16 bytes
+    if s.startswith(b"[") and s.endswith(b"]"):
+        s = s[1:-1]
+    if s.count(b"::") > 1:
+        return False
+    k = s.find(b"::")
+    head, tail = (None, s) if k == -1 else (s[:k], s[k + 2:])
+    a = _colon_part(head, 0)
+    if a == -1:
+        return False
+    b = _last_bits(tail)
+    if b == -1:
+        return False
+    return a + b < 16 if k != -1 else a + b == 16
+
+
+def java_is_ip_literal(s):
+    """IP.isIpLiteral (IP.java:271-300): an IPv6 string, or an IPv4 quad."""
+    return java_is_ipv6(s) or _v4_ok(s, 0, 4)
+
+
 class HintChecker:
     """searchForGroup for hints built by Hint.ofHost / ofHostPort."""
 
@@ -298,13 +374,12 @@ class HintChecker:
 
     @staticmethod
     def format_host(s):
-        """Hint.formatHost (Hint.java:57-73) for names with at most one ':'
-        (no such string parses as IPv6: without "::" IP.parseIpv6 needs 16
-        bytes of groups, with it two colons)."""
+        """Hint.formatHost (Hint.java:57-73): an IPv6 string or a name
+        without ':' unchanged, else the part before the first ':' without
+        one leading "www." (empty -> null)."""
         c = s.find(b":")
-        if c == -1:
+        if c == -1 or java_is_ipv6(s):
             return s
-        assert s.find(b":", c + 1) == -1, "checker covers names with at most one ':'"
         h = s[:c]
         if h.startswith(b"www."):
             h = h[4:]
@@ -366,12 +441,9 @@ class HintLevelChecker:
       the port filter lets through counts (precomputed per uri and port).
       A group that also matches the host scores >= 1024 on the host side,
       above any uri-only level (<= 1023), so the underestimate never wins.
-    Any other group scores 0.  ASCII strings (UTF-16 length = byte length).
-    `fallback(host, port, uri)` answers names with two or more ':'
-    (IP.isIpv6 in formatHost)."""
+    Any other group scores 0.  ASCII strings (UTF-16 length = byte length)."""
 
-    def __init__(self, groups, fallback=None):
-        self.fallback = fallback
+    def __init__(self, groups):
         self.g = []                 # merged (host, port, uri) per handle
         self.by_host, self.by_uri = {}, {}
         for i, (ha, ga) in enumerate(groups):
@@ -427,8 +499,6 @@ class HintLevelChecker:
 
     def __call__(self, name, port=0, uri=None):
         """Hint.ofHostPortUri(name, port, uri) (name / uri may be None)."""
-        if name is not None and name.count(b":") > 1:
-            return self.fallback(name, port, uri)
         host = None if name is None else HintChecker.format_host(name)
         uri = format_uri(uri)
         best, lv = -1, 0
@@ -504,7 +574,6 @@ class HintLevelChecker:
         uonly = np.where(ul.max(1) > 0, ul.argmax(1), -1)     # argmax: the lowest index of the max
         starts, flat = [0], []
         for name in names:
-            assert name.count(b":") <= 1, "table covers names with at most one ':'"
             host = HintChecker.format_host(name)
             top = []
             if host is not None:
@@ -578,15 +647,12 @@ class DnsChecker:
     trailing dot and Upstream.searchForGroup(Hint.ofHost(domain)) through
     HintChecker, else IP.isIpLiteral -> the literal's family, else
     `.vproxy.local` -> internal, else recursive.  `is_ip`: the IP-literal
-    predicate (IP.java:112-300) -- the oracle's strict parser, consulted only
-    for the few names no hosts entry and no group took; `fallback(name)`
-    answers the rare names HintChecker does not cover (two or more ':')."""
+    predicate (IP.java:112-300), java_is_ip_literal unless given."""
 
-    def __init__(self, hosts_text, groups, is_ip, fallback=None):
-        self.is_ip = is_ip
-        self.hosts = hosts_map(hosts_text, is_ip) if hosts_text else {}
+    def __init__(self, hosts_text, groups, is_ip=None):
+        self.is_ip = is_ip or java_is_ip_literal
+        self.hosts = hosts_map(hosts_text, self.is_ip) if hosts_text else {}
         self.hint = HintChecker(groups)
-        self.fallback = fallback
 
     def __call__(self, q):
         assert max(q, default=0) < 0x80, "checker covers ASCII qnames"
@@ -594,8 +660,6 @@ class DnsChecker:
         if v is not None:
             return DNS_HOSTS, v
         d = q[:-1] if q.endswith(b".") else q
-        if d.count(b":") > 1:
-            return self.fallback(q)
         g = self.hint(d)
         if g >= 0:
             return DNS_GROUP, g

@@ -17,7 +17,7 @@ import oracle_ffi as O
 from exact import AclChecker, HintChecker, RouteChecker
 from vproxy_amd import workloads as W
 
-from cases import hint_cases_random, hint_cases_shapes, rule_row, v6_edge_inputs
+from cases import hint_cases_random, hint_cases_shapes, rule_row, v6_edge_inputs, ip_like_strings
 
 CPU = torch.device("cpu")
 THREADS = 8
@@ -159,20 +159,38 @@ def test_hint_dict_vs_oracle_generated():
 def test_hint_dict_vs_oracle_edge_cases():
     rng = np.random.default_rng(23)
     groups, _, queries = hint_cases_random(rng, 400, 20000)
-    names = [(h, p) for h, p, _ in queries if h is not None and h.count(":") <= 1]
+    names = [(h, p) for h, p, _ in queries if h is not None]
     g2, n2 = hint_cases_shapes(rng, 20000)
     chk, og = HintChecker(groups), O.Groups(groups)
     for h, p in names:
         assert chk(h.encode(), p) == O.search_for_group(og, h, p), (h, p)
     chk, og = HintChecker(g2), O.Groups(g2)
-    keep = [n for n in n2 if n.count(b":") <= 1]
-    blob, off = W.pack(keep)
+    blob, off = W.pack(n2)
     np.testing.assert_array_equal(chk.batch(blob, off), O.hint_batch_np(og, blob, off, None,
                                                                         nthreads=THREADS))
 
 
-def _dns_oracle_fallback(oh, og):
-    return lambda q: O.dns_classify(oh, og, q)
+def test_java_ip_predicates_vs_oracle():
+    """exact.java_is_ipv6 / java_is_ip_literal (IP.isIpv6 / isIpLiteral
+    restated on bytes) against the oracle's parser: the TestIpParser vectors
+    (tests/golden/ip_parser.json) and 200k literal-shaped strings, the
+    parser's quirks included ("::" twice, a bad colon part before a dotted
+    tail, brackets, 1-4 hex digits)."""
+    import json
+    import os
+    from exact import java_is_ip_literal, java_is_ipv6
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ip_parser.json")) as f:
+        d = json.load(f)
+    fixed = [v["s"] for v in d["v4_ok"] + d["v6_ok"]] + d["v4_fail"] + d["bogus"]
+    fixed = [x.encode() for x in fixed] + [b"", b":", b"::", b":::", b"[]", b"[::]", b"::1.2.3.4",
+                                           b"::a:zz:1.2.3.4", b"1::2::3", b"a:b:c:d:e:f:1.2.3.4"]
+    strings = fixed + ip_like_strings(np.random.default_rng(41), 200_000)
+    v6 = [java_is_ipv6(x) for x in strings]
+    assert v6 == [O.parse_ipv6(x) is not None for x in strings]
+    assert [java_is_ip_literal(x) for x in strings] == [O.is_ip_literal(x) for x in strings]
+    assert 0.05 < np.mean(v6) < 0.95
+    for v in d["v6_ok"]:
+        assert java_is_ipv6(v["s"].encode())
 
 
 def test_hosts_map_vs_oracle_parser():
@@ -214,7 +232,7 @@ def test_dns_checker_vs_oracle():
               b"01.2.3.4.", b"", b".", b"..", b"miss.nowhere.", b"www.x:80", b"1.2.3.256."]
     for gs in (groups, [g for g in groups if g[1].get("host") != "*"]):
         oh, og = O.Hosts(O.hosts_parse(hosts)[0]), O.Groups(gs)
-        chk = DnsChecker(hosts, gs, O.is_ip_literal, _dns_oracle_fallback(oh, og))
+        chk = DnsChecker(hosts, gs)
         blob, off = W.pack(names)
         kind, val = chk.batch(blob, off)
         wk, wv = O.dns_batch_np(oh, og, blob, off, nthreads=THREADS)
@@ -233,8 +251,7 @@ def test_hint_level_checker_vs_oracle():
     rng = np.random.default_rng(71)
     groups, _, queries = hint_cases_random(rng, 400, 20000)
     og = O.Groups(groups)
-    fb = lambda h, p, u: O.search_for_group(og, h, p, u)
-    chk = HintLevelChecker(groups, fb)
+    chk = HintLevelChecker(groups)
     enc = lambda x: None if x is None else x.encode()
     for h, p, u in queries:
         assert chk(enc(h), p, enc(u)) == O.search_for_group(og, h, p, u), (h, p, u)
@@ -252,7 +269,7 @@ def test_hint_level_checker_vs_oracle():
                                                       if rng.random() < 0.5 else "")
           for _ in names]
     og2 = O.Groups(g2)
-    chk2 = HintLevelChecker(g2, lambda h, p, u: O.search_for_group(og2, h, p, u))
+    chk2 = HintLevelChecker(g2)
     got = [chk2(n, int(p), enc(u)) for n, p, u in zip(names, qp, qu)]
     want = [O.search_for_group(og2, n, int(p), u) for n, p, u in zip(names, qp, qu)]
     assert got == want
@@ -318,7 +335,7 @@ def test_hint_level_table_vs_checker_and_oracle():
     from exact import HintLevelChecker
     groups, names, uris, nidx, uidx = bench.c4uri_workload(20000, n_groups=3000, n_names=2000)
     og = O.Groups(groups)
-    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    chk = HintLevelChecker(groups)
     cols = uris + [None]
     tab = chk.table(names, cols)
     for i, name in enumerate(names[:600]):

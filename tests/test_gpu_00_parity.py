@@ -501,7 +501,7 @@ def test_hint_uri_levels_at_scale(clf):
             for _ in range(len(names))]
     got = clf.hint_search([n.decode() for n in names], ports, uris)
     og = O.Groups(groups)
-    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    chk = HintLevelChecker(groups)
     enc = lambda x: None if x is None else x.encode()
     want = np.array([chk(n, int(p), enc(u)) for n, p, u in zip(names, ports, uris)], np.int32)
     np.testing.assert_array_equal(got, want)
@@ -637,3 +637,45 @@ def test_hosts_text_kats_on_gpu(clf):
         kind, value = clf.dns_classify([q for q, _, _ in case["queries"]])
         assert list(zip(kind.tolist(), value.tolist())) == \
             [(k, v) for _, k, v in case["queries"]], case["source"]
+
+
+def test_hosts_with_ipv6_literals_at_scale(clf):
+    """formatHost's IPv6 branch (Hint.java:57-73: an IPv6 string is the host
+    as it is, any other name with a ':' is cut at the first one) and the DNS
+    IP-literal step (DNSServer.java:116-166), item by item over 400k names --
+    generated hostnames, IPv6 / IPv4 literals and near misses
+    (cases.ip_like_strings), bracketed, with ports -- against
+    exact.HintChecker and exact.DnsChecker, whose IP predicates restate
+    IP.java (checked against the oracle on the CPU tier)."""
+    from cases import ip_like_strings
+    from exact import DnsChecker, HintChecker
+    rng = np.random.default_rng(47)
+    groups, ghosts = W.gen_groups(5000, 48, port_frac=0.2)
+    groups = [g for g in groups if g[1].get("host") != "*"]    # so misses reach the literal step
+    lits = [b"::1", b"2001:db8::1", b"fe80::1", b"::ffff:1.2.3.4", b"[::1]", b"a::b",
+            b"1:2:3:4:5:6:7:8", b"10.1.2.3"]
+    groups += [({}, {"host": h.decode()}) for h in lits]
+    clf.compile_upstream(groups)
+    names = W.gen_hostnames(ghosts, 200_000, 49, port_frac=0.2)
+    names += ip_like_strings(rng, 200_000)
+    names += lits + [x + b":80" for x in lits] + [b"[" + x + b"]:443" for x in lits]
+    ports = rng.choice(np.array([0, 0, 80, 443, 8080], np.uint16), len(names))
+    chk = HintChecker(groups)
+    blob, off = W.pack(names)
+    for p in (None, ports):
+        got = clf.hint_search(names, p)
+        want = chk.batch(blob, off, p)
+        np.testing.assert_array_equal(got, want)
+    lit_groups = set(range(len(groups) - len(lits), len(groups)))
+    assert len(lit_groups & set(want.tolist())) >= 5
+    # the DNS classification of the same names (as qnames, half with the
+    # trailing dot), over a hosts file with IPv6 and IPv4 entries
+    text = "::1 six.hosts.local\n10.0.0.1 four.hosts.local\n2001:db8::2 v6.hosts.local.\n"
+    clf.compile_hosts_text(text)
+    qn = [x + b"." if i % 2 else x for i, x in enumerate(names)]
+    qn += [b"six.hosts.local", b"v6.hosts.local", b"four.hosts.local."]
+    kind, val = clf.dns_classify(qn)
+    wk, wv = DnsChecker(text, groups).batch(*W.pack(qn))
+    np.testing.assert_array_equal(kind, wk)
+    np.testing.assert_array_equal(val, wv)
+    assert {V.DNS_HOSTS, V.DNS_GROUP, V.DNS_IP_LITERAL} <= set(np.unique(kind).tolist())

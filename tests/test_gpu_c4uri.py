@@ -35,7 +35,7 @@ def test_c4uri_bench_batch_exact():
         hb, ho, ub, uo, un, _ = bench.c4uri_batch(names, uris, nidx, uidx, "cuda")
         n = len(nidx)
         og = O.Groups(groups)
-        chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+        chk = HintLevelChecker(groups)
         tab = chk.table(names, uris + [None])
         want = tab[nidx, np.where(uidx < 0, len(uris), uidx)]
         out = torch.empty(n, dtype=torch.int32, device="cuda")

@@ -378,7 +378,7 @@ def test_generator_device_equals_host(c5):
 def _dns_checker(text, groups):
     oh = O.Hosts(O.hosts_parse(text)[0])
     og = O.Groups(groups)
-    return DnsChecker(text, groups, O.is_ip_literal, lambda q: O.dns_classify(oh, og, q)), oh, og
+    return DnsChecker(text, groups), oh, og
 
 
 def test_dns_c4_scale():

@@ -85,7 +85,7 @@ def test_dns_ragged_sizes(clf):
     clf.compile_hosts_text(text)
     oh = O.Hosts(O.hosts_parse(text)[0])
     og = O.Groups(groups)
-    chk = DnsChecker(text, groups, O.is_ip_literal, lambda q: O.dns_classify(oh, og, q))
+    chk = DnsChecker(text, groups)
     nblob, noff = W.pack(names)
     wk, wv = chk.batch(nblob, noff)
 

@@ -108,7 +108,7 @@ def test_http_bench_batch_whole(clf):
     grp, kind = clf.http_hint((blob, off))
     torch.cuda.synchronize()
     og = O.Groups(groups)
-    chk = HintLevelChecker(groups, lambda h, p, u: O.search_for_group(og, h, p, u))
+    chk = HintLevelChecker(groups)
     want_g = np.empty(len(heads), np.int32)
     want_k = np.empty(len(heads), np.uint8)
     for t, h in enumerate(heads):
