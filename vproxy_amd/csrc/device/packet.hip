@@ -114,9 +114,19 @@ __device__ __forceinline__ const RouteImage* vni_table(const VniImage& vt, uint3
     return glb_ld(vt.vni + lo) == vni ? vt.tables + lo : nullptr;
 }
 
+#ifndef VC_SWITCH_PRELOAD
+#define VC_SWITCH_PRELOAD 1
+#endif
 __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage& rt,
                                            const VniImage& vt, const SwitchIn& in, int64_t i,
                                            const PktOut& o, const SwitchOut& so) {
+    // one table (no VNI map) and an IPv4 inner packet: its route's root
+    // entry is loaded first, so that gather (into a table of up to 64 MB)
+    // is in flight during the ACL's dependent loads instead of after them
+    const bool pre = VC_SWITCH_PRELOAD && vt.n == 0 && o.status == VC_PKT_OK && o.l3 == VC_L3_IPV4;
+    const uint32_t k4 = bswap32(o.dst[0]);
+    uint32_t e0 = 0;
+    if (pre) e0 = glb_ld(rt.fam[0].nodes + (k4 >> (32 - rt.fam[0].root_bits)));
     // SecurityGroup.allow(Protocol.UDP, remote, port): the UDP list
     const bool six = in.rfam && in.rfam[i] == 6;
     uint32_t v;
@@ -149,8 +159,10 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
         }
         if (!have) {
             r = VC_SWITCH_NO_TABLE;                   // inputVXLan: vni not defined, drop
+        } else if (pre) {
+            r = out_index(trie_v4_from(t4.nodes, t4.root_bits, k4, e0));
         } else if (o.l3 == VC_L3_IPV4) {
-            r = out_index(trie_v4(t4.nodes, t4.root_bits, bswap32(o.dst[0])));
+            r = out_index(trie_v4(t4.nodes, t4.root_bits, k4));
         } else if (o.l3 == VC_L3_IPV6) {
             uint64_t hi, lo;
             v6_key(*reinterpret_cast<const uint4*>(o.dst), &hi, &lo);

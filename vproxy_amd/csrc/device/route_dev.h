@@ -38,8 +38,9 @@ VC_HD uint32_t v4_sub(uint32_t key, int bits, int s) {
     return (key >> (32 - bits - s)) & ((1u << s) - 1u);
 }
 
-VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
-    uint32_t e = nodes[key >> (32 - rb)];
+// The walk from the root entry e = nodes[key >> (32 - rb)], which a caller
+// may load ahead of time (its latency then overlaps other work).
+VC_HD uint32_t trie_v4_from(const uint32_t* nodes, int rb, uint32_t key, uint32_t e) {
     int bits = rb;
     const uint32_t root = 1u << rb;
     while (e & VC_PTR) {
@@ -48,6 +49,10 @@ VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
         bits += s;
     }
     return e;
+}
+
+VC_HD uint32_t trie_v4(const uint32_t* nodes, int rb, uint32_t key) {
+    return trie_v4_from(nodes, rb, key, nodes[key >> (32 - rb)]);
 }
 
 VC_HD uint32_t v6_sub(uint64_t hi, uint64_t lo, int bits, int s) {
