@@ -29,6 +29,8 @@ def lib():
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
         L.ic_mirror.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
         L.ic_mirror_switch.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp]
+        L.ic_mirror_switch_sw.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp,
+                                          vp]
         L.ic_net_match.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
         L.ic_packets.argtypes = [vp, vp, C.c_int64, C.c_int, vp, vp]
         L.ic_is_ipv6.argtypes = [C.c_char_p, C.c_int]
@@ -171,3 +173,18 @@ def mirror_switch(filter_arr, nf, origin, frames, layer):
                                 len(frames), layer, P(out))
     assert rc == 0, rc
     return out
+
+
+def mirror_switch_sw(filter_arr, nf, origin, frames, layer):
+    """switchPacket through the origin's bit-set image on the host ->
+    (results, (nb4, nb6)), or None when the origin has no such image."""
+    lens = np.array([len(f) for f in frames], np.int64)
+    off = np.zeros(len(frames) + 1, np.uint32)
+    off[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(frames) or b"\0", np.uint8).copy()
+    out = np.empty(len(frames), np.uint64)
+    nb = np.zeros(2, np.int32)
+    rc = lib().ic_mirror_switch_sw(C.cast(filter_arr, C.c_void_p), nf, origin, P(blob), P(off),
+                                   len(frames), layer, P(out), P(nb))
+    assert rc in (0, 1), rc
+    return None if rc == 1 else (out, tuple(int(x) for x in nb))

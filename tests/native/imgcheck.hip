@@ -302,6 +302,29 @@ int ic_mirror_switch(const vc_mirror_filter* f, int nf, int32_t origin, const ui
     return 0;
 }
 
+// switchPacket through the origin's bit-set image (mirror_dev.h
+// mirror_switch_sw over compile.cpp build_mirror_switch); returns 1, with
+// nothing written, when the origin has no such image
+int ic_mirror_switch_sw(const vc_mirror_filter* f, int nf, int32_t origin, const uint8_t* blob,
+                        const uint32_t* off, int64_t n, int layer, uint64_t* out, int32_t* nb) {
+    std::vector<MirrorRec> recs;
+    int rc = vc::build_mirror(f, nf, &recs);
+    if (rc) return rc;
+    vc::MirrorSwBuilt b;
+    if (!vc::build_mirror_switch(recs, origin, &b)) return 1;
+    b.img.macs = b.macs.data();
+    b.img.mirs = b.mirs.data();
+    b.img.b4 = b.b4.data();
+    b.img.p4 = b.p4.data();
+    b.img.b6 = b.b6.data();
+    b.img.p6 = b.p6.data();
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = mirror_switch_sw(b.img, blob + off[i], int(off[i + 1] - off[i]), layer);
+    nb[0] = b.img.nb4;
+    nb[1] = b.img.nb6;
+    return 0;
+}
+
 // the mirror filters' compiled Network.contains (common/netmatch.h NetMatch)
 int ic_net_match(const uint8_t* in, int inlen, const uint8_t* rule, int rlen, const uint8_t* mask,
                  int mlen) {

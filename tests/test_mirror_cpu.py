@@ -122,3 +122,86 @@ def test_switch_vs_oracle(layer):
     want = np.array([O.mirror_switch(oarr, nf, oid, f, layer) for f in frames], np.uint64)
     np.testing.assert_array_equal(got, want)
     assert (want != 0).mean() > 0.2
+
+
+def _v6_frames(rng, n):
+    """IPv6 VXLAN frames whose addresses come from the mirror pools'
+    families: ::ffff:a.b.c.d and ::a.b.c.d forms (matchIp's lowBitsV6V4
+    case of IPv4 filter networks), fd00:: addresses and random ones."""
+    out = []
+    for _ in range(n):
+        addr = []
+        for _s in range(2):
+            r = rng.random()
+            v4 = bytes([10, int(rng.integers(0, 3)), 2, int(rng.integers(0, 5))])
+            if r < 0.3:
+                a = bytes(10) + b"\xff\xff" + v4
+            elif r < 0.5:
+                a = bytes(12) + v4
+            elif r < 0.6:
+                a = bytes(10) + bytes([0xff, 0]) + v4            # not lowBitsV6V4
+            elif r < 0.8:
+                a = bytes([0xfd, 0, 0, int(rng.integers(0, 2))]) + rng.bytes(12)
+            else:
+                a = rng.bytes(16)
+            addr.append(a)
+        l4 = rng.bytes(12) + bytes([5 << 4, 0x18]) + rng.bytes(6)
+        ip = bytes([0x60, 0, 0, 0, 0, len(l4), 6, 64]) + addr[0] + addr[1]
+        eth = parse_mac(A) + parse_mac(B)
+        out.append(bytes([8, 0, 0, 0, 0, 0, 1, 0]) + eth + b"\x86\xdd" + ip + l4)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_switch_bitsets_vs_oracle(seed):
+    """switchPacket through the per-origin bit-set image (MirrorSwImage:
+    interval masks of netX / netY per address family, MAC filters, mirror
+    bits) against the oracle, on random filter lists over the mirror
+    network pools (IPv4, IPv6, v4-mapped and v4-compatible forms) and
+    random, mirror-pool and IPv6 frames, for every origin."""
+    rng = np.random.default_rng(70 + seed)
+    nf = [3, 17, 40, 64, 90, 130][seed]
+    origins = ("switch", "other") if nf < 130 else ("switch", "other", "a", "b")
+    filters, _ = gen_mirror_case(rng, nf, 0, origins=origins)
+    if nf == 130:                       # one origin over 64 filters: per-filter path
+        filters += [{"origin": "big", "mirror": k % 5, "network": "10.%d.0.0/16" % k}
+                    for k in range(65)]
+        origins += ("big",)
+    frames = mirror_frames(rng, 3000) + _v6_frames(rng, 1500)
+    mf = MirrorFilters()
+    arr, nf = mf.build(filters)
+    oarr = O.mirror_filters(filters, {})
+    built = 0
+    for origin in origins:
+        oid = mf.id_of(origin, create=False)
+        r = I.mirror_switch_sw(arr, nf, oid, frames, 0)
+        count = sum(f["origin"] == origin for f in filters)
+        if count == 0 or count > 64:
+            assert r is None, (origin, count)
+            continue
+        assert r is not None, (origin, count)
+        built += 1
+        got, (nb4, nb6) = r
+        want = np.array([O.mirror_switch(oarr, nf, oid, f, 0) for f in frames], np.uint64)
+        np.testing.assert_array_equal(got, want, err_msg=origin)
+        assert nb4 >= 1 and nb6 >= 1
+        if nf >= 17:
+            assert (want != 0).mean() > 0.1
+    assert built >= 1
+
+
+def test_switch_bitsets_bench_filters():
+    """The mirror sub-bench's 17 filters (bench.MIRROR_FILTERS): the
+    bit-set image exists, and equals the oracle on the bench's frame
+    templates."""
+    import bench as Bn
+    from vproxy_amd import workloads as W
+    frames = W.gen_vxlan_frames(4000, W.SEED + 12)
+    mf = MirrorFilters()
+    arr, nf = mf.build(Bn.MIRROR_FILTERS)
+    oarr = O.mirror_filters(Bn.MIRROR_FILTERS, {})
+    oid = mf.id_of("switch", create=False)
+    got, (nb4, nb6) = I.mirror_switch_sw(arr, nf, oid, frames, 0)
+    want = np.array([O.mirror_switch(oarr, nf, oid, f, 0) for f in frames], np.uint64)
+    np.testing.assert_array_equal(got, want)
+    assert nb4 <= 2 * 32 + 1 and nb6 >= 1

@@ -11,6 +11,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -651,6 +652,7 @@ struct CertSnap : Snapshot {
 };
 struct MirrorSnap : Snapshot {
     MirrorImage img{};
+    std::map<int32_t, MirrorSwImage> sw;   // per origin: switchPacket's bit-set image
 };
 struct ServerSnap : Snapshot {
     ServerImage img{};
@@ -1498,6 +1500,31 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
     Upload up(ctx);
     s->img.f = up(*s, recs);
     s->img.n = n;
+    // switchPacket's bit-set image of every origin that has one (compile.hpp
+    // build_mirror_switch); VC_MIRROR_SW=0 keeps every origin on the
+    // per-filter kernel (an A/B switch: both forms give the same answers)
+    const char* env = std::getenv("VC_MIRROR_SW");
+    std::vector<vc::MirrorSwBuilt> built;
+    if (!(env && env[0] == '0')) {
+        std::set<int32_t> origins;
+        for (const MirrorRec& r : recs) origins.insert(r.origin);
+        built.reserve(origins.size());
+        for (const int32_t o : origins) {
+            built.emplace_back();
+            vc::MirrorSwBuilt& b = built.back();
+            if (!vc::build_mirror_switch(recs, o, &b)) {
+                built.pop_back();
+                continue;
+            }
+            b.img.macs = up(*s, b.macs);
+            b.img.mirs = up(*s, b.mirs);
+            b.img.b4 = up(*s, b.b4);
+            b.img.p4 = up(*s, b.p4);
+            b.img.b6 = up(*s, b.b6);
+            b.img.p6 = up(*s, b.p6);
+            s->sw[o] = b.img;
+        }
+    }
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "mirror filter upload");
     ctx->publish(ctx->mirror, std::shared_ptr<const MirrorSnap>(std::move(s)));
     return VC_OK;
@@ -1559,8 +1586,10 @@ int vc_mirror_switch_dev(vc_ctx* ctx, int32_t origin, const uint8_t* blob, const
         return fail(VC_EINVAL, "switchPacket takes VXLAN or Ethernet frames");
     auto s = ctx->get(ctx->mirror);
     if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
-    hipError_t e = vc::launch_mirror_switch(ctx->cfg(stream), s->img, origin, blob, off, n, layer,
-                                            out_mirrors);
+    const auto sw = s->sw.find(origin);
+    hipError_t e = vc::launch_mirror_switch(ctx->cfg(stream), s->img,
+                                            sw == s->sw.end() ? nullptr : &sw->second, origin,
+                                            blob, off, n, layer, out_mirrors);
     return launched(ctx, e, stream, "mirror switch launch");
 }
 

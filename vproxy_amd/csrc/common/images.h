@@ -255,6 +255,40 @@ struct MirrorImage {
     int32_t n;
 };
 
+// Mirror.switchPacket's filter step for one origin as bit sets (built at
+// compile time for every origin with 1..64 filters whose networks compile
+// to prefix ranges).  switchPacket reaches only matchEthernet and matchIp
+// (Mirror.java:73-87), and every Network.contains projection onto one input
+// family is a union of at most two key ranges (common/netmatch.h cases 1-5;
+// case 4's lowBitsV6V4 gives ::a.b.c.d and ::ffff:a.b.c.d).  So the
+// elementary intervals of all ranges of the origin's filters carry, per
+// interval, the filters whose netX / netY contain it: one interval search
+// per address, then the match of every filter at once in 64-bit masks.
+// Keys: IPv4 as the big-endian u32; IPv6 as (hi, lo) big-endian u64 halves.
+struct MirrorSwMac {               // a filter with a MAC (matchEthernet)
+    uint64_t bit;                  // 1 << filter's position in the origin
+    uint64_t mac_x, mac_y;
+    uint32_t has_y, pad;
+};
+
+struct MirrorSwMir {               // filters whose FilterConfig.mirror is `bit`
+    uint64_t filters;
+    uint32_t bit, pad;
+};
+
+struct MirrorSwImage {
+    uint64_t all;                  // the origin's filters
+    uint64_t has_x, has_y;         // NET_X / NET_Y
+    uint64_t mac;                  // filters with a MAC_X
+    int32_t n_mac, n_mir, nb4, nb6;
+    const MirrorSwMac* macs;
+    const MirrorSwMir* mirs;
+    const uint32_t* b4;            // nb4 ascending interval starts, b4[0] = 0
+    const uint64_t* p4;            // per interval: (xmask, ymask)
+    const uint64_t* b6;            // nb6 ascending interval starts as (hi, lo), b6[0] = (0, 0)
+    const uint64_t* p6;            // per interval: (xmask, ymask)
+};
+
 // ---------------------------------------------------------------------------
 // ServerGroup source hashing (method == source): per group, three lists of
 // server indices (all / IPv4 / IPv6 servers with weight > 0, in

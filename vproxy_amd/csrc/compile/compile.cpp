@@ -702,6 +702,113 @@ int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out) 
     return VC_OK;
 }
 
+namespace {
+uint32_t be32(uint32_t w) { return __builtin_bswap32(w); }
+
+// the key of left-aligned bytes held as little-endian words (netmatch.h)
+u128 be128(const uint32_t w[4]) {
+    return (u128(be32(w[0])) << 96) | (u128(be32(w[1])) << 64) | (u128(be32(w[2])) << 32) |
+           u128(be32(w[3]));
+}
+
+// (k & m) == r as the range [r, r | ~m] when m is a run of high ones;
+// false when m is not (the per-filter path keeps such a network)
+template <class T>
+bool prefix_range(T m, T r, std::vector<std::pair<T, T>>* out) {
+    const T inv = T(~m);
+    if (inv & T(inv + 1)) return false;                    // not a prefix mask
+    if ((r & inv) == 0) out->push_back({r, T(r | inv)});   // else: matches nothing
+    return true;
+}
+
+// Network.contains projected onto 4- and 16-byte inputs (netmatch.h
+// NetMatch) as key ranges
+bool net_ranges(const MirrorNet& n, std::vector<std::pair<uint32_t, uint32_t>>* r4,
+                std::vector<std::pair<u128, u128>>* r6) {
+    if (!prefix_range<uint32_t>(be32(n.m4), be32(n.r4), r4)) return false;
+    const u128 m = be128(n.m6), r = be128(n.r6);
+    if (!n.low6) return prefix_range<u128>(m, r, r6);
+    // lowBitsV6V4(input): bytes 0-9 zero, bytes 10-11 both 0x00 or both 0xFF
+    const u128 top = ~u128(0) << 32;
+    if (r & ~m) return true;                                // matches nothing
+    for (const u128 v : {u128(0), u128(0xFFFF) << 32}) {
+        if ((r ^ v) & m & top) continue;                    // this form contradicts the rule
+        if (!prefix_range<u128>(m | top, (r & ~top) | v, r6)) return false;
+    }
+    return true;
+}
+
+// elementary intervals of the ranges, each with the (x, y) filter masks of
+// the ranges covering it; equal neighbours merged
+template <class T>
+void intervals(const std::vector<std::pair<T, T>>& rg, const std::vector<uint64_t>& bit,
+               const std::vector<int>& side, std::vector<T>* starts,
+               std::vector<std::pair<uint64_t, uint64_t>>* masks) {
+    std::vector<T> b{T(0)};
+    for (const auto& p : rg) {
+        b.push_back(p.first);
+        if (p.second != T(~T(0))) b.push_back(T(p.second + 1));
+    }
+    std::sort(b.begin(), b.end());
+    b.erase(std::unique(b.begin(), b.end()), b.end());
+    starts->clear();
+    masks->clear();
+    for (const T s : b) {
+        uint64_t x = 0, y = 0;
+        for (size_t k = 0; k < rg.size(); ++k)
+            if (rg[k].first <= s && s <= rg[k].second) (side[k] ? y : x) |= bit[k];
+        if (!masks->empty() && masks->back() == std::make_pair(x, y)) continue;
+        starts->push_back(s);
+        masks->push_back({x, y});
+    }
+}
+}  // namespace
+
+bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, MirrorSwBuilt* out) {
+    *out = MirrorSwBuilt{};
+    std::vector<std::pair<uint32_t, uint32_t>> r4;
+    std::vector<std::pair<u128, u128>> r6;
+    std::vector<uint64_t> bit4, bit6;
+    std::vector<int> side4, side6;
+    std::map<int32_t, uint64_t> mirs;
+    MirrorSwImage& s = out->img;
+    int j = 0;
+    for (const MirrorRec& f : recs) {
+        if (f.origin != origin) continue;
+        if (j == 64) return false;
+        const uint64_t b = uint64_t(1) << j++;
+        s.all |= b;
+        mirs[f.mirror] |= b;
+        if (f.flags & VC_MF_MAC_X) {
+            s.mac |= b;
+            out->macs.push_back({b, f.mac_x, f.mac_y, (f.flags & VC_MF_MAC_Y) ? 1u : 0u, 0});
+        }
+        for (int y = 0; y < 2; ++y) {
+            if (!(f.flags & (y ? VC_MF_NET_Y : VC_MF_NET_X))) continue;
+            (y ? s.has_y : s.has_x) |= b;
+            if (!net_ranges(y ? f.net_y : f.net_x, &r4, &r6)) return false;
+            bit4.resize(r4.size(), b);
+            side4.resize(r4.size(), y);
+            bit6.resize(r6.size(), b);
+            side6.resize(r6.size(), y);
+        }
+    }
+    if (!j) return false;
+    for (const auto& m : mirs) out->mirs.push_back({m.second, uint32_t(m.first), 0});
+    std::vector<std::pair<uint64_t, uint64_t>> m4, m6;
+    intervals<uint32_t>(r4, bit4, side4, &out->b4, &m4);
+    std::vector<u128> b6;
+    intervals<u128>(r6, bit6, side6, &b6, &m6);
+    for (const auto& m : m4) out->p4.insert(out->p4.end(), {m.first, m.second});
+    for (const u128 v : b6) out->b6.insert(out->b6.end(), {uint64_t(v >> 64), uint64_t(v)});
+    for (const auto& m : m6) out->p6.insert(out->p6.end(), {m.first, m.second});
+    s.n_mac = int32_t(out->macs.size());
+    s.n_mir = int32_t(out->mirs.size());
+    s.nb4 = int32_t(out->b4.size());
+    s.nb6 = int32_t(b6.size());
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // ServerGroup source hashing
 // ---------------------------------------------------------------------------

@@ -100,6 +100,20 @@ int build_certs(const char* const* names, const int32_t* name_lens, const int32_
 // Mirror FilterConfig list -> MirrorRec records (images.h).
 int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out);
 
+// One origin's filters as MirrorSwImage bit sets (images.h); the image's
+// pointers are left for the upload.  Returns false (nothing built) when the
+// origin has no filter or more than 64, or when a network's projection is
+// not a union of prefix ranges (a non-contiguous mask): switchPacket then
+// takes the per-filter path.
+struct MirrorSwBuilt {
+    MirrorSwImage img{};
+    std::vector<MirrorSwMac> macs;
+    std::vector<MirrorSwMir> mirs;
+    std::vector<uint32_t> b4;
+    std::vector<uint64_t> p4, b6, p6;
+};
+bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, MirrorSwBuilt* out);
+
 // ServerGroup source-hash lists (ServerGroup.java:620-664), see ServerImage.
 struct ServersBuilt {
     std::vector<uint32_t> view_off;      // 6 words per group

@@ -27,9 +27,11 @@ constexpr int kMirrorWaves = kMirrorBlock / 64;
 constexpr uint32_t kMirrorStage = 7168;      // as packet.hip kPktStage: 5 blocks per CU
 constexpr uint32_t kMirrorStageWords = (kMirrorStage + 2 * kApron) / 4;
 
-template <bool kStage>
+// kSw: the origin's filters as bit sets (MirrorSwImage, mirror_switch_sw);
+// otherwise every filter of the list in turn (mirror_switch_one).
+template <bool kStage, bool kSw>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
-    MirrorImage img, int32_t origin, const uint8_t* __restrict__ blob,
+    MirrorImage img, MirrorSwImage sw, int32_t origin, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, int layer, uint64_t* __restrict__ out,
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kMirrorWaves : 1][kStage ? kMirrorStageWords : 1];
@@ -48,14 +50,10 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
         if (nx < ch.nchunks) cur = lane_span(off, nx * 64, n);             // next chunk's
         const bool staged = kStage && stage_wave<kMirrorStage>(blob, o0, o1, stage[w], &a0);
         if (i < n) {
-            uint64_t m;
-            if (staged)
-                m = mirror_switch_one(
-                    fi, origin, reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0),
-                    int(e - a), layer);
-            else
-                m = mirror_switch_one(fi, origin, blob + a, int(e - a), layer);
-            out[i] = m;
+            const uint8_t* fp =
+                staged ? reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0) : blob + a;
+            out[i] = kSw ? mirror_switch_sw(sw, fp, int(e - a), layer)
+                         : mirror_switch_one(fi, origin, fp, int(e - a), layer);
         }
         if (kStage) wave_done();
         c = nx;
@@ -82,20 +80,28 @@ hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32
     return hipGetLastError();
 }
 
-hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
-                                const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
-                                uint64_t* out) {
+namespace {
+template <bool kStage, bool kSw>
+void mirror_switch_go(const LaunchCfg& c, const MirrorImage& img, const MirrorSwImage& sw,
+                      int32_t origin, const uint8_t* blob, const uint32_t* off, int64_t n,
+                      int layer, uint64_t* out) {
+    const auto k = vcd::mirror_switch_kernel<kStage, kSw>;
+    hipLaunchKernelGGL(k, dim3(mirror_grid(c, k, n)), dim3(vcd::kMirrorBlock), 0, c.stream, img,
+                       sw, origin, blob, off, n, layer, out, launch_ticket(c));
+}
+}  // namespace
+
+// sw: the origin's bit-set image, or null for the per-filter kernel
+hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img,
+                                const MirrorSwImage* sw, int32_t origin, const uint8_t* blob,
+                                const uint32_t* off, int64_t n, int layer, uint64_t* out) {
     if (n <= 0) return hipSuccess;
-    if ((reinterpret_cast<uintptr_t>(blob) & 3) == 0)
-        hipLaunchKernelGGL(vcd::mirror_switch_kernel<true>,
-                           dim3(mirror_grid(c, vcd::mirror_switch_kernel<true>, n)),
-                           dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
-                           out, launch_ticket(c));
-    else
-        hipLaunchKernelGGL(vcd::mirror_switch_kernel<false>,
-                           dim3(mirror_grid(c, vcd::mirror_switch_kernel<false>, n)),
-                           dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, blob, off, n, layer,
-                           out, launch_ticket(c));
+    const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
+    const MirrorSwImage none{};
+    if (sw && stage) mirror_switch_go<true, true>(c, img, *sw, origin, blob, off, n, layer, out);
+    else if (sw) mirror_switch_go<false, true>(c, img, *sw, origin, blob, off, n, layer, out);
+    else if (stage) mirror_switch_go<true, false>(c, img, none, origin, blob, off, n, layer, out);
+    else mirror_switch_go<false, false>(c, img, none, origin, blob, off, n, layer, out);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #pragma once
 
 #include "../common/netmatch.h"
+#include "acl_dev.h"
 #include "dev_common.h"
 #include "packet_dev.h"
 
@@ -162,6 +163,65 @@ VC_HD uint64_t mirror_switch_one(const MirrorImage& img, int32_t origin, const u
         lvl = kLvlIp;
     }
     return mirror_eval(img, origin, it, lvl);
+}
+
+// A uniform record through the scalar cache (as load_filter).
+template <class T>
+VC_HD T load_uniform(const T* p, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) T* CP;
+    return ((CP)(p))[k];
+#else
+    return p[k];
+#endif
+}
+
+// The (xmask, ymask) pair of interval j
+VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
+    return glb_ld(reinterpret_cast<const ulonglong2*>(p) + j);
+}
+
+// Mirror.switchPacket through the origin's bit-set image (images.h
+// MirrorSwImage): the same answer as mirror_switch_one over the origin's
+// filters.  matchEthernet (FilterConfig.java:27-38) for every MAC filter,
+// then for an IPv4 / IPv6 packet matchIp's network part (:40-55) for all
+// filters at once from the interval masks of the two addresses:
+//   no netX -> true; netX and netY -> (xs && yd) || (ys && xd); netX only
+//   -> xs || xd.
+VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint8_t* p, int len, int layer) {
+    PktOut o;
+    parse_packet(p, len, layer, &o);
+    if (o.status != VC_PKT_OK) return 0;
+    const uint8_t* eth = layer == VC_LAYER_VXLAN ? p + 8 : p;
+    const uint64_t dst = mac48(eth), src = mac48(eth + 6);
+    uint64_t hit = s.all & ~s.mac;
+    for (int k = 0; k < s.n_mac; ++k) {
+        const MirrorSwMac f = load_uniform(s.macs, k);
+        const bool ok = f.has_y ? (f.mac_x == src && f.mac_y == dst) || (f.mac_y == src && f.mac_x == dst)
+                                : f.mac_x == src || f.mac_x == dst;
+        if (ok) hit |= f.bit;
+    }
+    if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
+        ulonglong2 ms, md;
+        if (o.l3 == VC_L3_IPV4) {
+            ms = sw_masks(s.p4, bsearch_u32(s.b4, s.nb4, bswap32(o.src[0])));
+            md = sw_masks(s.p4, bsearch_u32(s.b4, s.nb4, bswap32(o.dst[0])));
+        } else {
+            uint64_t sh, sl, dh, dl;
+            v6_key(*reinterpret_cast<const uint4*>(o.src), &sh, &sl);
+            v6_key(*reinterpret_cast<const uint4*>(o.dst), &dh, &dl);
+            ms = sw_masks(s.p6, bsearch_u128(s.b6, s.nb6, sh, sl));
+            md = sw_masks(s.p6, bsearch_u128(s.b6, s.nb6, dh, dl));
+        }
+        const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
+        hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
+    }
+    uint64_t m = 0;
+    for (int k = 0; k < s.n_mir; ++k) {
+        const MirrorSwMir r = load_uniform(s.mirs, k);
+        if (hit & r.filters) m |= uint64_t(1) << r.bit;
+    }
+    return m;
 }
 
 }  // namespace vcd
