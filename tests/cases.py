@@ -363,6 +363,34 @@ def mirror_frames(rng, n):
     return frames
 
 
+def mirror_v6_frames(rng, n):
+    """IPv6 VXLAN frames whose addresses come from the mirror pools'
+    families: ::ffff:a.b.c.d and ::a.b.c.d forms (matchIp's lowBitsV6V4
+    case of IPv4 filter networks), fd00:: addresses and random ones."""
+    out = []
+    for _ in range(n):
+        addr = []
+        for _s in range(2):
+            r = rng.random()
+            v4 = bytes([10, int(rng.integers(0, 3)), 2, int(rng.integers(0, 5))])
+            if r < 0.3:
+                a = bytes(10) + b"\xff\xff" + v4
+            elif r < 0.5:
+                a = bytes(12) + v4
+            elif r < 0.6:
+                a = bytes(10) + bytes([0xff, 0]) + v4            # not lowBitsV6V4
+            elif r < 0.8:
+                a = bytes([0xfd, 0, 0, int(rng.integers(0, 2))]) + rng.bytes(12)
+            else:
+                a = rng.bytes(16)
+            addr.append(a)
+        l4 = rng.bytes(12) + bytes([5 << 4, 0x18]) + rng.bytes(6)
+        ip = bytes([0x60, 0, 0, 0, 0, len(l4), 6, 64]) + addr[0] + addr[1]
+        eth = bytes([10, 0, 0x27, 0, 0, 0, 10, 0, 0x27, 0, 0, 1])
+        out.append(bytes([8, 0, 0, 0, 0, 0, 1, 0]) + eth + b"\x86\xdd" + ip + l4)
+    return out
+
+
 def http_heads_random(rng, n, hosts, uris):
     """HTTP/1 request heads (bytes) for HttpContext.connectionHint: request
     lines with and without a version, bare-LF lines, Host headers in any

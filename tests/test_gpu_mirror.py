@@ -8,7 +8,7 @@ import pytest
 
 import oracle_ffi as O
 import vproxy_amd as V
-from cases import gen_mirror_case, mirror_columns, mirror_frames
+from cases import gen_mirror_case, mirror_columns, mirror_frames, mirror_v6_frames
 from vproxy_amd.mirror import parse_mac
 
 pytestmark = pytest.mark.gpu
@@ -54,12 +54,16 @@ def test_items_defaults(clf):
     np.testing.assert_array_equal(got, np.full(5, 0b011, np.uint64))
 
 
+# sw "1": switchPacket through the per-origin bit-set image (the default);
+# "0": the per-filter kernel (VC_MIRROR_SW=0 at compile)
+@pytest.mark.parametrize("sw", ["1", "0"])
 @pytest.mark.parametrize("layer", [0, 1])
-def test_switch_vs_oracle(clf, layer):
+def test_switch_vs_oracle(clf, layer, sw, monkeypatch):
     import torch
     rng = np.random.default_rng(50 + layer)
     filters, _ = gen_mirror_case(rng, 60, 0, origins=("switch", "other"))
-    frames = [f if layer == 0 else f[8:] for f in mirror_frames(rng, 30000)]
+    frames = [f if layer == 0 else f[8:] for f in mirror_frames(rng, 30000) + mirror_v6_frames(rng, 8000)]
+    monkeypatch.setenv("VC_MIRROR_SW", sw)
     mf = clf.compile_mirror(filters)
     oarr = O.mirror_filters(filters, {})
     oid = mf.id_of("switch", create=False)
@@ -77,6 +81,24 @@ def test_switch_vs_oracle(clf, layer):
     assert (want != 0).mean() > 0.2
 
 
+def test_switch_origin_over_64_filters(clf):
+    """An origin with 65 filters has no bit-set image (64-bit masks): its
+    frames take the per-filter kernel; the other origin's take the image."""
+    rng = np.random.default_rng(61)
+    filters = [{"origin": "big", "mirror": k % 7, "network": "10.%d.0.0/16" % (k % 3),
+                "mac": "0a:00:27:00:00:%02x" % (k % 4)} for k in range(65)]
+    filters += gen_mirror_case(rng, 20, 0, origins=("switch",))[0]
+    frames = mirror_frames(rng, 20000)
+    mf = clf.compile_mirror(filters)
+    oarr = O.mirror_filters(filters, {})
+    for origin in ("big", "switch"):
+        oid = mf.id_of(origin, create=False)
+        want = np.array([O.mirror_switch(oarr, len(filters), oid, f, 0) for f in frames],
+                        np.uint64)
+        np.testing.assert_array_equal(clf.mirror_switch(origin, frames, 0), want, err_msg=origin)
+        assert (want != 0).mean() > 0.05
+
+
 def test_errors(clf):
     for bad in ({"origin": "o", "mirror": 64}, {"origin": "o", "mirror": 0, "port": [5, 4]},
                 {"origin": "o", "mirror": 0, "port": [1, 2], "port2": [9, 3]}):
@@ -87,13 +109,15 @@ def test_errors(clf):
         clf.mirror_switch("switch", [b"\0" * 20], layer=4)
 
 
+@pytest.mark.parametrize("sw", ["1", "0"])
 @pytest.mark.parametrize("shift,pad", [(1, 0), (0, 1400)])
-def test_switch_unstaged(clf, shift, pad):
+def test_switch_unstaged(clf, shift, pad, sw, monkeypatch):
     import torch
     rng = np.random.default_rng(80 + shift)
     filters, _ = gen_mirror_case(rng, 30, 0, origins=("switch",))
     frames = [f + bytes(int(rng.integers(0, pad + 1))) if pad else f
               for f in mirror_frames(rng, 5000)]
+    monkeypatch.setenv("VC_MIRROR_SW", sw)
     mf = clf.compile_mirror(filters)
     oarr = O.mirror_filters(filters, {})
     oid = mf.id_of("switch", create=False)

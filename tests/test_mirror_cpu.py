@@ -12,7 +12,7 @@ import pytest
 import imgcheck_ffi as I
 import oracle_ffi as O
 import vproxy_amd as V
-from cases import gen_mirror_case, mirror_columns, mirror_frames
+from cases import gen_mirror_case, mirror_columns, mirror_frames, mirror_v6_frames
 from vproxy_amd.mirror import MirrorFilters, items_struct, parse_mac
 
 A, B, C_, D = ("0a:00:27:00:00:%02x" % i for i in range(4))
@@ -124,34 +124,6 @@ def test_switch_vs_oracle(layer):
     assert (want != 0).mean() > 0.2
 
 
-def _v6_frames(rng, n):
-    """IPv6 VXLAN frames whose addresses come from the mirror pools'
-    families: ::ffff:a.b.c.d and ::a.b.c.d forms (matchIp's lowBitsV6V4
-    case of IPv4 filter networks), fd00:: addresses and random ones."""
-    out = []
-    for _ in range(n):
-        addr = []
-        for _s in range(2):
-            r = rng.random()
-            v4 = bytes([10, int(rng.integers(0, 3)), 2, int(rng.integers(0, 5))])
-            if r < 0.3:
-                a = bytes(10) + b"\xff\xff" + v4
-            elif r < 0.5:
-                a = bytes(12) + v4
-            elif r < 0.6:
-                a = bytes(10) + bytes([0xff, 0]) + v4            # not lowBitsV6V4
-            elif r < 0.8:
-                a = bytes([0xfd, 0, 0, int(rng.integers(0, 2))]) + rng.bytes(12)
-            else:
-                a = rng.bytes(16)
-            addr.append(a)
-        l4 = rng.bytes(12) + bytes([5 << 4, 0x18]) + rng.bytes(6)
-        ip = bytes([0x60, 0, 0, 0, 0, len(l4), 6, 64]) + addr[0] + addr[1]
-        eth = parse_mac(A) + parse_mac(B)
-        out.append(bytes([8, 0, 0, 0, 0, 0, 1, 0]) + eth + b"\x86\xdd" + ip + l4)
-    return out
-
-
 @pytest.mark.parametrize("seed", range(6))
 def test_switch_bitsets_vs_oracle(seed):
     """switchPacket through the per-origin bit-set image (MirrorSwImage:
@@ -167,7 +139,7 @@ def test_switch_bitsets_vs_oracle(seed):
         filters += [{"origin": "big", "mirror": k % 5, "network": "10.%d.0.0/16" % k}
                     for k in range(65)]
         origins += ("big",)
-    frames = mirror_frames(rng, 3000) + _v6_frames(rng, 1500)
+    frames = mirror_frames(rng, 3000) + mirror_v6_frames(rng, 1500)
     mf = MirrorFilters()
     arr, nf = mf.build(filters)
     oarr = O.mirror_filters(filters, {})
