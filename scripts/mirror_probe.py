@@ -53,7 +53,7 @@ def main():
     }
     for name, filters in variants.items():
         res = {}
-        for sw in ("0", "1"):                      # per-filter kernel / bit-set image
+        for sw in ("0", "1", "2"):     # per-filter kernel / bit-set image / + IPv4 table in LDS
             os.environ["VC_MIRROR_SW"] = sw
             mf = clf.compile_mirror(filters)
             oid = mf.id_of("switch", create=False)
@@ -63,9 +63,10 @@ def main():
             ms = timed(fn)
             res[sw] = out.clone()
             print(json.dumps({"variant": name, "filters": len(filters),
-                              "path": "bitsets" if sw == "1" else "per_filter",
+                              "path": {"0": "per_filter", "1": "bitsets_global",
+                                       "2": "bitsets_lds4"}[sw],
                               "ms": round(ms, 4)}), flush=True)
-        assert torch.equal(res["0"], res["1"]), name
+        assert torch.equal(res["0"], res["1"]) and torch.equal(res["0"], res["2"]), name
         del res
     os.environ.pop("VC_MIRROR_SW")
     res = {k: torch.empty((n, w) if w > 1 else (n,), dtype={"u8": torch.uint8,

@@ -54,9 +54,10 @@ def test_items_defaults(clf):
     np.testing.assert_array_equal(got, np.full(5, 0b011, np.uint64))
 
 
-# sw "1": switchPacket through the per-origin bit-set image (the default);
-# "0": the per-filter kernel (VC_MIRROR_SW=0 at compile)
-@pytest.mark.parametrize("sw", ["1", "0"])
+# switchPacket's three kernels, chosen at compile by VC_MIRROR_SW: "2" (the
+# default) the per-origin bit-set image with its IPv4 intervals in LDS, "1"
+# the same read from the global table, "0" the per-filter kernel
+@pytest.mark.parametrize("sw", ["2", "1", "0"])
 @pytest.mark.parametrize("layer", [0, 1])
 def test_switch_vs_oracle(clf, layer, sw, monkeypatch):
     import torch
@@ -109,7 +110,7 @@ def test_errors(clf):
         clf.mirror_switch("switch", [b"\0" * 20], layer=4)
 
 
-@pytest.mark.parametrize("sw", ["1", "0"])
+@pytest.mark.parametrize("sw", ["2", "1", "0"])
 @pytest.mark.parametrize("shift,pad", [(1, 0), (0, 1400)])
 def test_switch_unstaged(clf, shift, pad, sw, monkeypatch):
     import torch

@@ -176,9 +176,10 @@ VC_HD T load_uniform(const T* p, int k) {
 #endif
 }
 
-// The (xmask, ymask) pair of interval j
+// The (xmask, ymask) pair of interval j (kL: the table is staged in LDS)
+template <bool kL = false>
 VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
-    return glb_ld(reinterpret_cast<const ulonglong2*>(p) + j);
+    return tbl_ld<kL>(reinterpret_cast<const ulonglong2*>(p) + j);
 }
 
 // Mirror.switchPacket through the origin's bit-set image (images.h
@@ -188,7 +189,10 @@ VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
 // filters at once from the interval masks of the two addresses:
 //   no netX -> true; netX and netY -> (xs && yd) || (ys && xd); netX only
 //   -> xs || xd.
-VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint8_t* p, int len, int layer) {
+// b4 / p4: the IPv4 interval table, from the image or its LDS copy (kL4).
+template <bool kL4 = false>
+VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint32_t* b4, const uint64_t* p4,
+                                const uint8_t* p, int len, int layer) {
     PktOut o;
     parse_packet(p, len, layer, &o);
     if (o.status != VC_PKT_OK) return 0;
@@ -204,8 +208,8 @@ VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint8_t* p, int le
     if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
         ulonglong2 ms, md;
         if (o.l3 == VC_L3_IPV4) {
-            ms = sw_masks(s.p4, bsearch_u32(s.b4, s.nb4, bswap32(o.src[0])));
-            md = sw_masks(s.p4, bsearch_u32(s.b4, s.nb4, bswap32(o.dst[0])));
+            ms = sw_masks<kL4>(p4, bsearch_u32<kL4>(b4, s.nb4, bswap32(o.src[0])));
+            md = sw_masks<kL4>(p4, bsearch_u32<kL4>(b4, s.nb4, bswap32(o.dst[0])));
         } else {
             uint64_t sh, sl, dh, dl;
             v6_key(*reinterpret_cast<const uint4*>(o.src), &sh, &sl);
