@@ -48,6 +48,8 @@ def main():
         "one_mac": [{"origin": "switch", "mirror": 9, "mac": "0a:00:27:00:00:01"}],
         "skip16_plus_mac": other + [{"origin": "switch", "mirror": 9,
                                      "mac": "0a:00:27:00:00:01"}],
+        "four_nets": [{"origin": "switch", "mirror": i, "network": "%d.0.0.0/8" % (i + 1)}
+                      for i in range(4)],
         "net_x_only16": [{"origin": "switch", "mirror": i % 8, "network": "%d.0.0.0/8" % (i + 1)}
                          for i in range(16)],
     }

@@ -319,8 +319,8 @@ int ic_mirror_switch_sw(const vc_mirror_filter* f, int nf, int32_t origin, const
     b.img.b6 = b.b6.data();
     b.img.p6 = b.p6.data();
     for (int64_t i = 0; i < n; ++i)
-        out[i] = mirror_switch_sw(b.img, b.img.b4, b.img.p4, blob + off[i],
-                                  int(off[i + 1] - off[i]), layer);
+        out[i] = mirror_switch_sw(b.img, SwTables{b.img.b4, b.img.p4, b.img.b6, b.img.p6},
+                                  blob + off[i], int(off[i + 1] - off[i]), layer);
     nb[0] = b.img.nb4;
     nb[1] = b.img.nb6;
     return 0;

@@ -1501,10 +1501,10 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
     s->img.f = up(*s, recs);
     s->img.n = n;
     // switchPacket's bit-set image of every origin that has one (compile.hpp
-    // build_mirror_switch), its IPv4 intervals copied into LDS by the kernel.
+    // build_mirror_switch), its interval tables copied into LDS by the kernel.
     // A/B switches (every form gives the same answers): VC_MIRROR_SW=0 keeps
-    // every origin on the per-filter kernel, =1 reads the IPv4 intervals from
-    // the global table.
+    // every origin on the per-filter kernel, =1 reads the interval tables
+    // from global memory.
     const char* env = std::getenv("VC_MIRROR_SW");
     std::vector<vc::MirrorSwBuilt> built;
     if (!(env && env[0] == '0')) {
@@ -1524,7 +1524,7 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
             b.img.p4 = up(*s, b.p4);
             b.img.b6 = up(*s, b.b6);
             b.img.p6 = up(*s, b.p6);
-            b.img.lds4 = !(env && env[0] == '1');
+            b.img.lds = !(env && env[0] == '1');
             s->sw[o] = b.img;
         }
     }

@@ -281,7 +281,7 @@ struct MirrorSwImage {
     uint64_t has_x, has_y;         // NET_X / NET_Y
     uint64_t mac;                  // filters with a MAC_X
     int32_t n_mac, n_mir, nb4, nb6;
-    int32_t lds4, pad;             // the kernel copies b4 / p4 into LDS (nb4 <= 64)
+    int32_t lds, pad;              // the kernel copies the tables into LDS (both nb <= 48)
     const MirrorSwMac* macs;
     const MirrorSwMir* mirs;
     const uint32_t* b4;            // nb4 ascending interval starts, b4[0] = 0

@@ -28,28 +28,36 @@ constexpr uint32_t kMirrorStage = 7168;      // as packet.hip kPktStage: 5 block
 constexpr uint32_t kMirrorStageWords = (kMirrorStage + 2 * kApron) / 4;
 
 // kSw: the origin's filters as bit sets (MirrorSwImage, mirror_switch_sw);
-// otherwise every filter of the list in turn (mirror_switch_one).  kL4: the
-// IPv4 interval table (at most kMirrorL4 intervals) copied into LDS first.
-constexpr int kMirrorL4 = 64;
-template <bool kStage, bool kSw, bool kL4>
+// otherwise every filter of the list in turn (mirror_switch_one).  kL: the
+// interval tables (at most kMirrorL intervals per family) copied into LDS
+// first -- with 48 + 48 the kernel keeps its 5 workgroups per CU.
+constexpr int kMirrorL = 48;
+static_assert(kMirrorL <= kMirrorBlock, "one copy pass per workgroup");
+template <bool kStage, bool kSw, bool kL>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     MirrorImage img, MirrorSwImage sw, int32_t origin, const uint8_t* __restrict__ blob,
     const uint32_t* __restrict__ off, int64_t n, int layer, uint64_t* __restrict__ out,
     uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kMirrorWaves : 1][kStage ? kMirrorStageWords : 1];
-    __shared__ uint32_t l4b[kL4 ? kMirrorL4 : 1];
-    __shared__ ulonglong2 l4p[kL4 ? kMirrorL4 : 1];
+    __shared__ uint32_t l4b[kL ? kMirrorL : 1];
+    __shared__ ulonglong2 l4p[kL ? kMirrorL : 1], l6b[kL ? kMirrorL : 1], l6p[kL ? kMirrorL : 1];
     const MirrorImage& fi = img;
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    if (kL4) {
-        for (int t = int(threadIdx.x); t < sw.nb4; t += kMirrorBlock) {
+    SwTables tb{sw.b4, sw.p4, sw.b6, sw.p6};
+    if (kL) {
+        const int t = int(threadIdx.x);
+        if (t < sw.nb4) {
             l4b[t] = glb_ld(sw.b4 + t);
             l4p[t] = glb_ld(reinterpret_cast<const ulonglong2*>(sw.p4) + t);
         }
+        if (t < sw.nb6) {
+            l6b[t] = glb_ld(reinterpret_cast<const ulonglong2*>(sw.b6) + t);
+            l6p[t] = glb_ld(reinterpret_cast<const ulonglong2*>(sw.p6) + t);
+        }
         __syncthreads();
+        tb = SwTables{l4b, reinterpret_cast<const uint64_t*>(l4p),
+                      reinterpret_cast<const uint64_t*>(l6b), reinterpret_cast<const uint64_t*>(l6p)};
     }
-    const uint32_t* b4 = kL4 ? l4b : sw.b4;
-    const uint64_t* p4 = kL4 ? reinterpret_cast<const uint64_t*>(l4p) : sw.p4;
     ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);   // chunks.h
     int64_t c = ch.first(w);
     LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
@@ -65,7 +73,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
         if (i < n) {
             const uint8_t* fp =
                 staged ? reinterpret_cast<const uint8_t*>(stage[w]) + kApron + (a - a0) : blob + a;
-            out[i] = kSw ? mirror_switch_sw<kL4>(sw, b4, p4, fp, int(e - a), layer)
+            out[i] = kSw ? mirror_switch_sw<kL>(sw, tb, fp, int(e - a), layer)
                          : mirror_switch_one(fi, origin, fp, int(e - a), layer);
         }
         if (kStage) wave_done();
@@ -94,11 +102,11 @@ hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32
 }
 
 namespace {
-template <bool kStage, bool kSw, bool kL4 = false>
+template <bool kStage, bool kSw, bool kL = false>
 void mirror_switch_go(const LaunchCfg& c, const MirrorImage& img, const MirrorSwImage& sw,
                       int32_t origin, const uint8_t* blob, const uint32_t* off, int64_t n,
                       int layer, uint64_t* out) {
-    const auto k = vcd::mirror_switch_kernel<kStage, kSw, kL4>;
+    const auto k = vcd::mirror_switch_kernel<kStage, kSw, kL>;
     hipLaunchKernelGGL(k, dim3(mirror_grid(c, k, n)), dim3(vcd::kMirrorBlock), 0, c.stream, img,
                        sw, origin, blob, off, n, layer, out, launch_ticket(c));
 }
@@ -111,7 +119,7 @@ hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img,
     if (n <= 0) return hipSuccess;
     const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
     const MirrorSwImage none{};
-    if (sw && stage && sw->lds4 && sw->nb4 <= vcd::kMirrorL4)
+    if (sw && stage && sw->lds && sw->nb4 <= vcd::kMirrorL && sw->nb6 <= vcd::kMirrorL)
         mirror_switch_go<true, true, true>(c, img, *sw, origin, blob, off, n, layer, out);
     else if (sw && stage) mirror_switch_go<true, true>(c, img, *sw, origin, blob, off, n, layer, out);
     else if (sw) mirror_switch_go<false, true>(c, img, *sw, origin, blob, off, n, layer, out);

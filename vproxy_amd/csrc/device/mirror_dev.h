@@ -189,10 +189,16 @@ VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
 // filters at once from the interval masks of the two addresses:
 //   no netX -> true; netX and netY -> (xs && yd) || (ys && xd); netX only
 //   -> xs || xd.
-// b4 / p4: the IPv4 interval table, from the image or its LDS copy (kL4).
-template <bool kL4 = false>
-VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint32_t* b4, const uint64_t* p4,
-                                const uint8_t* p, int len, int layer) {
+// The interval tables are read from the image, or from the kernel's LDS
+// copy of them (kL: t carries the LDS pointers).
+struct SwTables {
+    const uint32_t* b4;
+    const uint64_t *p4, *b6, *p6;
+};
+
+template <bool kL = false>
+VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const SwTables& t, const uint8_t* p,
+                                int len, int layer) {
     PktOut o;
     parse_packet(p, len, layer, &o);
     if (o.status != VC_PKT_OK) return 0;
@@ -208,14 +214,14 @@ VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const uint32_t* b4, cons
     if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
         ulonglong2 ms, md;
         if (o.l3 == VC_L3_IPV4) {
-            ms = sw_masks<kL4>(p4, bsearch_u32<kL4>(b4, s.nb4, bswap32(o.src[0])));
-            md = sw_masks<kL4>(p4, bsearch_u32<kL4>(b4, s.nb4, bswap32(o.dst[0])));
+            ms = sw_masks<kL>(t.p4, bsearch_u32<kL>(t.b4, s.nb4, bswap32(o.src[0])));
+            md = sw_masks<kL>(t.p4, bsearch_u32<kL>(t.b4, s.nb4, bswap32(o.dst[0])));
         } else {
             uint64_t sh, sl, dh, dl;
             v6_key(*reinterpret_cast<const uint4*>(o.src), &sh, &sl);
             v6_key(*reinterpret_cast<const uint4*>(o.dst), &dh, &dl);
-            ms = sw_masks(s.p6, bsearch_u128(s.b6, s.nb6, sh, sl));
-            md = sw_masks(s.p6, bsearch_u128(s.b6, s.nb6, dh, dl));
+            ms = sw_masks<kL>(t.p6, bsearch_u128<kL>(t.b6, s.nb6, sh, sl));
+            md = sw_masks<kL>(t.p6, bsearch_u128<kL>(t.b6, s.nb6, dh, dl));
         }
         const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
         hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
