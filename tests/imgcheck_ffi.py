@@ -22,6 +22,7 @@ def lib():
         vp = C.c_void_p
         L.ic_acl.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp,
                              vp, vp]
+        L.ic_acl_port.argtypes = [vp, C.c_int, C.c_uint32, vp, C.c_int64, vp]
         L.ic_route.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64, vp, vp, C.c_int]
         L.ic_hint.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp]
         L.ic_hint_deferred.restype = C.c_int64
@@ -56,6 +57,17 @@ def acl(tcp, udp, dflt, family, proto, src, port):
                       P(src), P(port), n, P(out), P(allow), P(stats))
     assert rc == 0, rc
     return out, allow, stats
+
+
+def acl_port(udp, port, keys):
+    """the UDP list's IPv4 image at `port` (build_acl_port) against the
+    general image at every interval edge and at `keys` -> (rule index per
+    key, -1 = none; port table size)"""
+    keys = np.ascontiguousarray(keys, np.uint32)
+    out = np.empty(len(keys), np.int32)
+    rc = lib().ic_acl_port(P(udp), len(udp), port, P(keys), len(keys), P(out))
+    assert rc > 0, rc
+    return out, rc
 
 
 def route(rules, family, keys, root_bits=0):

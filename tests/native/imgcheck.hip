@@ -277,6 +277,34 @@ int ic_certs(const char* const* names, const int32_t* lens, const int32_t* holde
     return 0;
 }
 
+// The UDP list's IPv4 image at a fixed port (compile.cpp build_acl_port,
+// the switch kernel's LDS table): for every key, the rule the general image
+// gives at that port.  Keys: the given ones plus every interval start of the
+// general image and the key below it.  Returns the port table's size.
+int ic_acl_port(const vc_acl_rule* udp, int nu, uint32_t port, const uint32_t* keys, int64_t n,
+                int32_t* out) {
+    vc::AclBuilt b;
+    int rc = vc::build_acl(nullptr, 0, udp, nu, 0, &b);
+    if (rc) return rc;
+    std::vector<uint32_t> pb, pv;
+    vc::build_acl_port(b.fam[1][0], port, &pb, &pv);
+    const AclFamilyImage f = fam_img(b.fam[1][0]);
+    auto check = [&](uint32_t key) {
+        const uint32_t g = acl_value(f.rec, f.pieces, acl4_interval(f, key), port);
+        const uint32_t v = pv[size_t(bsearch_u32(pb.data(), int(pb.size()), key))];
+        return g == v ? int32_t(g == VC_NONE ? -1 : int32_t(g)) : -1000;
+    };
+    for (int32_t j = 0; j < f.nb; ++j) {
+        if (check(f.bounds4[j]) == -1000) return -300;
+        if (f.bounds4[j] && check(f.bounds4[j] - 1) == -1000) return -301;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        out[i] = check(keys[i]);
+        if (out[i] == -1000) return -302;
+    }
+    return int(pb.size());
+}
+
 // Mirror filters: the kernels' item loading + mirror_eval, and switchPacket.
 int ic_mirror(const vc_mirror_filter* f, int nf, int32_t origin, const vc_mirror_items* items,
               int64_t n, uint64_t* out) {

@@ -240,3 +240,48 @@ def test_switch_per_vni_tables():
             clf.compile_vni_routes([(7, tables[7][0], tables[7][1])] * 2)
     finally:
         clf.close()
+
+
+@pytest.mark.parametrize("env", ["1", "0"])
+def test_switch_bind_port_images(env, monkeypatch):
+    """The UDP list's IPv4 image at the bind port (images.h AclPortImage: the
+    switch kernel's LDS table; built on the first call with a port, kept with
+    the snapshot, and built ahead by every later compile): the sender's rule
+    and verdict for three ports in turn, on two lists (a recompile between),
+    against the oracle's SecurityGroup.allow(UDP, remote, port) scan.
+    VC_ACL_PORT=0 at compile keeps the general image (the A/B)."""
+    import torch
+    monkeypatch.setenv("VC_ACL_PORT", env)
+    rng = np.random.default_rng(23)
+    clf = V.Classifier(0)
+    try:
+        nets4, nets6 = _nets(rng, 500, 100)
+        ra, rn, rk = W.as_ctypes(nets4, V._lib.VcNet)
+        rb, rbn, rbk = W.as_ctypes(nets6, V._lib.VcNet)
+        clf.compile_routes_raw(ra, rn, rb, rbn)
+        frames = gen_frames(rng, 20000)
+        n = len(frames)
+        fam, r4, r6 = _remotes(rng, n)
+        blob, off = W.pack(frames)
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        tcp0, udp0 = _rules(rng)
+        from cases import rule_row
+        lists = [udp0, np.concatenate([udp0[::-1], rule_row("10.0.0.0/9", 53, 53, False)])]
+        for udp in lists:
+            a, na, ka = W.as_ctypes(tcp0, V._lib.VcAclRule)
+            b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
+            V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
+            for port in (BIND_PORT, 53, 4500, BIND_PORT):
+                _, acl, allow, _ = clf.switch_classify(
+                    (T(blob), T(off.astype(np.int32))), T(r4.view(np.int32)), port,
+                    remote6=T(r6), remote_family=T(fam))
+                torch.cuda.synchronize()
+                proto = np.full(n, 17, np.uint8)
+                ports = np.full(n, port, np.uint16)
+                w4, a4 = O.sg_batch_v4_np(tcp0, udp, False, proto, r4, ports)
+                w6, a6 = O.sg_batch_v6_np(tcp0, udp, False, proto, np.ascontiguousarray(r6), ports)
+                six = fam == 6
+                np.testing.assert_array_equal(acl.cpu().numpy(), np.where(six, w6, w4), err_msg=str(port))
+                np.testing.assert_array_equal(allow.cpu().numpy(), np.where(six, a6, a4))
+    finally:
+        clf.close()

@@ -45,6 +45,28 @@ def test_acl_v4_directory_and_records_large(n_rules):
     np.testing.assert_array_equal(allow, wv)
 
 
+@pytest.mark.parametrize("n_rules,p_range,seed", [(64, 0.5, 11), (10000, 0.3, 12), (3000, 0.95, 13)])
+def test_acl_port_image(n_rules, p_range, seed):
+    """The UDP list's IPv4 image at one bind port (build_acl_port: the switch
+    kernel's LDS table, Switch.java:679 allow(UDP, remote, bind port)) equals
+    the general image at that port at every interval edge, and the oracle's
+    SecurityGroup.allow scan on sample keys; C5's list (10k rules) at the
+    VXLAN port stays within the kernel's 256-interval LDS copy."""
+    tcp, udp = W.gen_sg_rules(n_rules, seed, p_range=p_range, weighted=True)
+    rng = np.random.default_rng(seed)
+    nets = W.rule_v4_fields(udp)[0] if len(udp) else np.zeros(1, np.uint32)
+    keys = np.concatenate([rng.integers(0, 2**32, 3000, dtype=np.uint64).astype(np.uint32),
+                           nets[rng.integers(0, len(nets), 3000)]])
+    for port in (4789, 53, 0, 65535, int(udp["min_port"][0])):
+        got, nb = IC.acl_port(udp, port, keys)
+        proto = np.full(len(keys), 17, np.uint8)
+        pr = np.full(len(keys), port, np.uint16)
+        want, _ = O.sg_batch_v4_np(tcp, udp, False, proto, keys, pr, nthreads=4)
+        np.testing.assert_array_equal(got, want)
+        if n_rules == 10000 and port == 4789:
+            assert nb <= 256, nb
+
+
 def test_acl_edges_v4_v6():
     tcp, udp = acl_edge_rules()
     rng = np.random.default_rng(7)

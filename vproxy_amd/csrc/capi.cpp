@@ -369,6 +369,8 @@ struct vc_ctx : SnapSet {
     std::mutex stage_mu;     // idle stagers (one per concurrent host-buffer call)
     std::vector<std::unique_ptr<Stager>> stagers;
     std::atomic<uint64_t> next_gen{1};       // generation of the next publish (any kind)
+    std::mutex port_seen_mu;
+    std::set<int32_t> acl_ports_seen;        // bind ports of switch calls (AclSnap::ports)
 
     // The snapshot a classify call uses: the calling thread's bound pin
     // when it pinned this kind (vc_pin_bind), else the current one.
@@ -631,8 +633,21 @@ void* Upload::dev(Snapshot& s, size_t bytes) {
     return p;
 }
 
+// intervals of an AclPortImage the switch kernel copies into LDS
+// (packet.hip kSwitchPortMax)
+constexpr int kAclPortMax = 256;
+
 struct AclSnap : Snapshot {
     AclImage img{};
+    // The UDP list's IPv4 image at the Switch's VXLAN bind port
+    // (images.h AclPortImage): built by a compile for every bind port a
+    // switch call has used on this context, and on the first call with a new
+    // one (acl_port_image); kept with the snapshot.
+    std::shared_ptr<const vc::AclBuilt> host;
+    bool port_images = true;       // VC_ACL_PORT=0 at compile: general image only (A/B)
+    mutable std::mutex port_mu;
+    mutable std::map<int32_t, AclPortImage> ports;
+    mutable std::vector<std::unique_ptr<DevBuf>> port_bufs;
 };
 struct RouteSnap : Snapshot {
     RouteImage img{};
@@ -886,7 +901,28 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
     s->img.default_allow = b.default_allow;
     s->digest = vc::digest(b);
     s->alloc_counters(up, int64_t(n_tcp) + n_udp + 2);
+    const char* env = std::getenv("VC_ACL_PORT");
+    s->port_images = !(env && env[0] == '0');
+    if (s->port_images) {
+        std::set<int32_t> seen;
+        {
+            std::lock_guard<std::mutex> lk(ctx->port_seen_mu);
+            seen = ctx->acl_ports_seen;
+        }
+        for (const int32_t port : seen) {
+            std::vector<uint32_t> pb, pv;
+            vc::build_acl_port(b.fam[1][0], uint32_t(port), &pb, &pv);
+            AclPortImage im{nullptr, nullptr, 0, port};
+            if (pb.size() <= size_t(kAclPortMax)) {
+                im.bounds = up(*s, pb);
+                im.value = up(*s, pv);
+                im.nb = int32_t(pb.size());
+            }
+            s->ports[port] = im;
+        }
+    }
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "ACL upload");
+    s->host = std::make_shared<const vc::AclBuilt>(std::move(b));
     ctx->publish(ctx->acl, std::shared_ptr<const AclSnap>(std::move(s)));
     return VC_OK;
 }
@@ -1827,6 +1863,41 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
     return st.finish();
 }
 
+// The UDP v4 image of `s` at `port` (the Switch's VXLAN bind port): from
+// the snapshot when its compile built it, else built now and kept with the
+// snapshot (the first switch call with a new port on each snapshot pays one
+// small host build and copy).  nb == 0: the general image (too many
+// intervals for the kernel's LDS copy, VC_ACL_PORT=0, or a failed copy).
+static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) {
+    AclPortImage im{nullptr, nullptr, 0, port};
+    if (!s.port_images || !s.host || port < 0 || port > 65535) return im;
+    {
+        std::lock_guard<std::mutex> lk(ctx->port_seen_mu);
+        ctx->acl_ports_seen.insert(port);
+    }
+    std::lock_guard<std::mutex> lk(s.port_mu);
+    const auto it = s.ports.find(port);
+    if (it != s.ports.end()) return it->second;
+    std::vector<uint32_t> pb, pv;
+    vc::build_acl_port(s.host->fam[1][0], uint32_t(port), &pb, &pv);
+    if (pb.size() <= size_t(kAclPortMax)) {
+        auto d = std::make_unique<DevBuf>();
+        d->n = pb.size() * 8;
+        d->grave = ctx->grave;
+        pb.insert(pb.end(), pv.begin(), pv.end());
+        if (hipMalloc(&d->p, d->n) != hipSuccess) {
+            d->p = nullptr;
+        } else if (hipMemcpy(d->p, pb.data(), d->n, hipMemcpyHostToDevice) == hipSuccess) {
+            im.bounds = static_cast<const uint32_t*>(d->p);
+            im.value = im.bounds + pv.size();
+            im.nb = int32_t(pv.size());
+        }
+        if (d->p) s.port_bufs.push_back(std::move(d));
+    }
+    s.ports[port] = im;
+    return im;
+}
+
 int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int64_t n,
                            int layer, const uint8_t* remote_family, const uint32_t* remote4,
                            const uint8_t* remote6, int bind_port, const vc_pkt_out* out,
@@ -1850,9 +1921,10 @@ int vc_switch_classify_dev(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off
     auto vt = ctx->get(ctx->vni);
     if (!a || (!r && !vt))
         return fail(VC_ESTATE, "SecurityGroup and RouteTable (or per-VNI tables) must be compiled");
+    const AclPortImage ap = acl_port_image(ctx, *a, bind_port);
     hipError_t e = vc::launch_switch(ctx->cfg(stream), a->img, r ? r->img : RouteImage{},
                                      vt ? vt->img : VniImage{}, blob, off, n, layer, o,
-                                     remote_family, remote4, remote6, bind_port, out_acl,
+                                     remote_family, remote4, remote6, bind_port, ap, out_acl,
                                      out_allow, out_route);
     return launched(ctx, e, stream, "switch launch");
 }

@@ -50,6 +50,17 @@ struct AclFamilyImage {
     int32_t v4_only;
 };
 
+// SecurityGroup.allow(UDP, IPv4 key, port) for one fixed port (the Switch's
+// VXLAN bind port, Switch.java:679): the UDP v4 image's intervals with the
+// port function evaluated at that port, equal neighbours merged, so a
+// lookup is one search of a table small enough for LDS.  nb == 0: none.
+struct AclPortImage {
+    const uint32_t* bounds;       // nb ascending interval starts, bounds[0] == 0
+    const uint32_t* value;        // per interval: the UDP rule index or VC_NONE
+    int32_t nb;
+    int32_t port;
+};
+
 struct AclImage {
     AclFamilyImage fam[2][2];     // [0 = tcp list, 1 = udp list][0 = v4 input, 1 = v6 input]
     const uint8_t* allow;         // rule allow bits: tcp rules then udp rules

@@ -659,6 +659,30 @@ int build_certs(const char* const* names, const int32_t* name_lens, const int32_
     return VC_OK;
 }
 
+void build_acl_port(const AclFamilyBuilt& f, uint32_t port, std::vector<uint32_t>* bounds,
+                    std::vector<uint32_t>* value) {
+    bounds->clear();
+    value->clear();
+    for (int32_t j = 0; j < f.nb; ++j) {
+        // desc (x, y): y == 0 -> x; else pieces[x .. x + y) as (port_start,
+        // value), ascending, the first starting at port 0
+        const uint32_t x = f.desc[2 * size_t(j)], y = f.desc[2 * size_t(j) + 1];
+        uint32_t v = x;
+        if (y) {
+            v = f.pieces[2 * size_t(x) + 1];
+            for (uint32_t k = 1; k < y && f.pieces[2 * size_t(x + k)] <= port; ++k)
+                v = f.pieces[2 * size_t(x + k) + 1];
+        }
+        if (!value->empty() && value->back() == v) continue;
+        bounds->push_back(f.bounds4[size_t(j)]);
+        value->push_back(v);
+    }
+    if (bounds->empty()) {                  // no interval at all: one of no rule
+        bounds->push_back(0);
+        value->push_back(VC_NONE);
+    }
+}
+
 // Mirror filters.  Java rejects min > max while parsing the config
 // (Mirror.java:581-582, 590-591); mirror indices are bits of the result.
 int build_mirror(const vc_mirror_filter* f, int n, std::vector<MirrorRec>* out) {

@@ -34,6 +34,11 @@ struct AclBuilt {
 int build_acl(const vc_acl_rule* tcp, int n_tcp, const vc_acl_rule* udp, int n_udp,
               int default_allow, AclBuilt* out);
 
+// One list's IPv4 image at a fixed port (images.h AclPortImage): interval
+// starts and the rule index (or VC_NONE) of each, equal neighbours merged.
+void build_acl_port(const AclFamilyBuilt& f, uint32_t port, std::vector<uint32_t>* bounds,
+                    std::vector<uint32_t>* value);
+
 struct TrieBuilt {
     std::vector<uint32_t> nodes;     // root, 256-entry nodes, then one-prefix records
     int32_t root_bits = 16;

@@ -247,8 +247,8 @@ hipError_t launch_dns_datagrams(const LaunchCfg& c, const HostsImage& hosts,
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
                          const VniImage& vt, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
-                         const uint8_t* r6, int bind_port, int32_t* out_acl, uint8_t* out_allow,
-                         int32_t* out_route);
+                         const uint8_t* r6, int bind_port, const AclPortImage& ap,
+                         int32_t* out_acl, uint8_t* out_allow, int32_t* out_route);
 
 // Large counter spaces (counters.hip): bucket partition + per-bucket LDS
 // histograms, split so a producer kernel (the pipeline) can supply the

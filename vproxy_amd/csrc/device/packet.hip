@@ -117,9 +117,12 @@ __device__ __forceinline__ const RouteImage* vni_table(const VniImage& vt, uint3
 #ifndef VC_SWITCH_PRELOAD
 #define VC_SWITCH_PRELOAD 1
 #endif
+// pb / pv / pnb: the UDP list's IPv4 image at the bind port, staged in LDS
+// (images.h AclPortImage), or pnb == 0 for the general image.
 __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage& rt,
                                            const VniImage& vt, const SwitchIn& in, int64_t i,
-                                           const PktOut& o, const SwitchOut& so) {
+                                           const PktOut& o, const SwitchOut& so,
+                                           const uint32_t* pb, const uint32_t* pv, int pnb) {
     // one table (no VNI map) and an IPv4 inner packet: its route's root
     // entry is loaded first, so that gather (into a table of up to 64 MB)
     // is in flight during the ACL's dependent loads instead of after them
@@ -134,6 +137,8 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
         uint64_t hi, lo;
         v6_key(reinterpret_cast<const uint4*>(in.r6)[i], &hi, &lo);
         v = acl6_global(acl.fam[1][1], acl.fam[1][0], hi, lo, in.bind_port);
+    } else if (pnb) {
+        v = lds_ld(pv + bsearch_u32<true>(pb, pnb, in.r4[i]));
     } else {
         const AclFamilyImage& f = acl.fam[1][0];
         v = acl_value(f.rec, f.pieces, acl4_interval(f, in.r4[i]), in.bind_port);
@@ -172,13 +177,24 @@ __device__ __forceinline__ void switch_one(const AclImage& acl, const RouteImage
     so.route[i] = r;
 }
 
-template <bool kStage>
+// kPort: the bind port's AclPortImage (at most kSwitchPortMax intervals)
+// copied into LDS first; the sender's UDP rule is then one LDS search.
+constexpr int kSwitchPortMax = 256;
+template <bool kStage, bool kPort>
 __global__ __launch_bounds__(kPktBlock) void switch_kernel(
     const uint8_t* __restrict__ blob, const uint32_t* __restrict__ off, int64_t n, int layer,
     vc_pkt_out out, AclImage acl, RouteImage rt, VniImage vt, SwitchIn in, SwitchOut so,
-    uint32_t* __restrict__ ticket) {
+    AclPortImage ap, uint32_t* __restrict__ ticket) {
     __shared__ uint32_t stage[kStage ? kPktWaves : 1][kStage ? kPktStageWords : 1];
+    __shared__ uint32_t pb[kPort ? kSwitchPortMax : 1], pv[kPort ? kSwitchPortMax : 1];
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
+    if (kPort) {
+        for (int t = int(threadIdx.x); t < ap.nb; t += kPktBlock) {
+            pb[t] = glb_ld(ap.bounds + t);
+            pv[t] = glb_ld(ap.value + t);
+        }
+        __syncthreads();
+    }
     Chunks ch(ticket, (n + 63) / 64);              // chunks.h: work tickets or static
     int64_t c = ch.first(w);
     LaneSpan cur = c < ch.nchunks ? lane_span(off, c * 64, n) : LaneSpan{0, 0};
@@ -200,7 +216,7 @@ __global__ __launch_bounds__(kPktBlock) void switch_kernel(
                 parse_packet(blob + a, int(e - a), layer, &o);
             }
             store_pkt(out, i, o);
-            switch_one(acl, rt, vt, in, i, o, so);
+            switch_one(acl, rt, vt, in, i, o, so, pb, pv, kPort ? ap.nb : 0);
         }
         if (kStage) wave_done();
         c = nx;
@@ -218,23 +234,24 @@ namespace vc {
 hipError_t launch_switch(const LaunchCfg& c, const AclImage& acl, const RouteImage& rt,
                          const VniImage& vt, const uint8_t* blob, const uint32_t* off, int64_t n, int layer,
                          const vc_pkt_out& out, const uint8_t* rfam, const uint32_t* r4,
-                         const uint8_t* r6, int bind_port, int32_t* out_acl, uint8_t* out_allow,
-                         int32_t* out_route) {
+                         const uint8_t* r6, int bind_port, const AclPortImage& ap,
+                         int32_t* out_acl, uint8_t* out_allow, int32_t* out_route) {
     if (n <= 0) return hipSuccess;
     const int64_t want = (n + vcd::kPktBlock - 1) / vcd::kPktBlock;
     const bool stage = (reinterpret_cast<uintptr_t>(blob) & 3) == 0;
-    const void* k = stage ? reinterpret_cast<const void*>(vcd::switch_kernel<true>)
-                          : reinterpret_cast<const void*>(vcd::switch_kernel<false>);
-    const int grid = resident_grid(c, k, vcd::kPktBlock, 0, want);
+    const bool port = stage && ap.nb > 0 && ap.nb <= vcd::kSwitchPortMax &&
+                      ap.port == bind_port;
     const vcd::SwitchIn in{rfam, r4, r6, uint32_t(bind_port)};
     const vcd::SwitchOut so{out_acl, out_allow, out_route};
-    if (stage)
-        hipLaunchKernelGGL(vcd::switch_kernel<true>, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream,
-                           blob, off, n, layer, out, acl, rt, vt, in, so, nullptr);
-    else
-        hipLaunchKernelGGL(vcd::switch_kernel<false>, dim3(grid), dim3(vcd::kPktBlock), 0,
-                           c.stream, blob, off, n, layer, out, acl, rt, vt, in, so,
-                           nullptr);
+    auto go = [&](auto kernel) {
+        const int grid = resident_grid(c, reinterpret_cast<const void*>(kernel), vcd::kPktBlock,
+                                       0, want);
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(vcd::kPktBlock), 0, c.stream, blob, off, n,
+                           layer, out, acl, rt, vt, in, so, ap, nullptr);
+    };
+    if (port) go(vcd::switch_kernel<true, true>);
+    else if (stage) go(vcd::switch_kernel<true, false>);
+    else go(vcd::switch_kernel<false, false>);
     return hipGetLastError();
 }
 
