@@ -547,7 +547,12 @@ int vc_parse_packets(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int6
  * checks, synthetic IPs, hop limit) stay with the caller.  remote_family:
  * 4/6 per datagram (NULL = all IPv4); remote4 / remote6 (16-byte aligned)
  * as in vc_packets.  Any vc_pkt_out pointer and out_acl / out_allow may be
- * NULL; out_route is required.  Device pointers. */
+ * NULL; out_route is required.  Device pointers.
+ * bind_port is constant for a switch, so the library keeps the UDP list's
+ * IPv4 rules at that port as a small merged table: the first call with a
+ * new bind_port on a compiled SecurityGroup builds it (a host build and a
+ * small synchronous copy on the calling thread), and every later
+ * vc_compile_acl builds it ahead for each bind_port used so far. */
 int vc_switch_classify_dev(vc_ctx *ctx, const uint8_t *blob, const uint32_t *off, int64_t n,
                            int layer, const uint8_t *remote_family, const uint32_t *remote4,
                            const uint8_t *remote6, int bind_port, const vc_pkt_out *out,
