@@ -1866,8 +1866,9 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
 // The UDP v4 image of `s` at `port` (the Switch's VXLAN bind port): from
 // the snapshot when its compile built it, else built now and kept with the
 // snapshot (the first switch call with a new port on each snapshot pays one
-// small host build and copy).  nb == 0: the general image (too many
-// intervals for the kernel's LDS copy, VC_ACL_PORT=0, or a failed copy).
+// small host build and a synchronous upload).  nb == 0: the general image
+// (too many intervals for the kernel's LDS copy, VC_ACL_PORT=0, or a failed
+// upload).
 static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) {
     AclPortImage im{nullptr, nullptr, 0, port};
     if (!s.port_images || !s.host || port < 0 || port > 65535) return im;
@@ -1881,18 +1882,17 @@ static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) 
     std::vector<uint32_t> pb, pv;
     vc::build_acl_port(s.host->fam[1][0], uint32_t(port), &pb, &pv);
     if (pb.size() <= size_t(kAclPortMax)) {
-        auto d = std::make_unique<DevBuf>();
-        d->n = pb.size() * 8;
-        d->grave = ctx->grave;
-        pb.insert(pb.end(), pv.begin(), pv.end());
-        if (hipMalloc(&d->p, d->n) != hipSuccess) {
-            d->p = nullptr;
-        } else if (hipMemcpy(d->p, pb.data(), d->n, hipMemcpyHostToDevice) == hipSuccess) {
-            im.bounds = static_cast<const uint32_t*>(d->p);
-            im.value = im.bounds + pv.size();
-            im.nb = int32_t(pv.size());
+        // through a stager's page-locked bounce buffer, as every upload
+        Snapshot own;
+        Upload up(ctx);
+        const uint32_t* b = up(own, pb);
+        const uint32_t* v = up(own, pv);
+        if (up.done() == hipSuccess && b && v) {
+            im.bounds = b;
+            im.value = v;
+            im.nb = int32_t(pb.size());
         }
-        if (d->p) s.port_bufs.push_back(std::move(d));
+        for (auto& d : own.bufs) s.port_bufs.push_back(std::move(d));
     }
     s.ports[port] = im;
     return im;
