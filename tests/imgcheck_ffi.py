@@ -30,6 +30,7 @@ def lib():
         L.ic_certs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp]
         L.ic_mirror.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
         L.ic_mirror_switch.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp]
+        L.ic_mirror_sw.argtypes = [vp, C.c_int, C.c_int32, vp, C.c_int64, vp]
         L.ic_mirror_switch_sw.argtypes = [vp, C.c_int, C.c_int32, vp, vp, C.c_int64, C.c_int, vp,
                                           vp]
         L.ic_net_match.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
@@ -173,6 +174,16 @@ def mirror(filter_arr, nf, origin, items, n):
                          C.c_void_p), n, P(out))
     assert rc == 0, rc
     return out
+
+
+def mirror_sw(filter_arr, nf, origin, items, n):
+    """Mirror.mirror through the origin's bit-set image on the host; None
+    when the origin has no such image"""
+    out = np.empty(n, np.uint64)
+    rc = lib().ic_mirror_sw(C.cast(filter_arr, C.c_void_p), nf, origin,
+                            C.cast(C.pointer(items), C.c_void_p), n, P(out))
+    assert rc in (0, 1), rc
+    return None if rc == 1 else out
 
 
 def mirror_switch(filter_arr, nf, origin, frames, layer):

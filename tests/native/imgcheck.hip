@@ -330,6 +330,33 @@ int ic_mirror_switch(const vc_mirror_filter* f, int nf, int32_t origin, const ui
     return 0;
 }
 
+// Mirror.mirror over MirrorData items through the origin's bit-set image
+// (mirror_dev.h mirror_match_sw); returns 1, with nothing written, when the
+// origin has no such image
+int ic_mirror_sw(const vc_mirror_filter* f, int nf, int32_t origin, const vc_mirror_items* items,
+                 int64_t n, uint64_t* out) {
+    std::vector<MirrorRec> recs;
+    int rc = vc::build_mirror(f, nf, &recs);
+    if (rc) return rc;
+    vc::MirrorSwBuilt b;
+    if (!vc::build_mirror_switch(recs, origin, &b)) return 1;
+    b.img.macs = b.macs.data();
+    b.img.mirs = b.mirs.data();
+    b.img.b4 = b.b4.data();
+    b.img.p4 = b.p4.data();
+    b.img.b6 = b.b6.data();
+    b.img.p6 = b.p6.data();
+    b.img.tids = b.tids.data();
+    b.img.aids = b.aids.data();
+    b.img.bp = b.bp.data();
+    b.img.pp = b.pp.data();
+    for (int64_t i = 0; i < n; ++i) {
+        const MirrorItem it = mirror_item(*items, i);
+        out[i] = mirror_match_sw(b.img, sw_tables(b.img), it, mirror_level(it));
+    }
+    return 0;
+}
+
 // switchPacket through the origin's bit-set image (mirror_dev.h
 // mirror_switch_sw over compile.cpp build_mirror_switch); returns 1, with
 // nothing written, when the origin has no such image
@@ -346,9 +373,13 @@ int ic_mirror_switch_sw(const vc_mirror_filter* f, int nf, int32_t origin, const
     b.img.p4 = b.p4.data();
     b.img.b6 = b.b6.data();
     b.img.p6 = b.p6.data();
+    b.img.tids = b.tids.data();
+    b.img.aids = b.aids.data();
+    b.img.bp = b.bp.data();
+    b.img.pp = b.pp.data();
     for (int64_t i = 0; i < n; ++i)
-        out[i] = mirror_switch_sw(b.img, SwTables{b.img.b4, b.img.p4, b.img.b6, b.img.p6},
-                                  blob + off[i], int(off[i + 1] - off[i]), layer);
+        out[i] = mirror_switch_sw(b.img, sw_tables(b.img), blob + off[i],
+                                  int(off[i + 1] - off[i]), layer);
     nb[0] = b.img.nb4;
     nb[1] = b.img.nb6;
     return 0;

@@ -21,9 +21,11 @@ def clf():
     c.close()
 
 
-def test_items_vs_oracle(clf):
+@pytest.mark.parametrize("sw", ["2", "0"])      # bit-set images / per-filter kernel
+def test_items_vs_oracle(clf, sw, monkeypatch):
     import torch
     filters, items = gen_mirror_case(np.random.default_rng(7), 50, 20000)
+    monkeypatch.setenv("VC_MIRROR_SW", sw)
     mf = clf.compile_mirror(filters)
     ids = {}
     oarr = O.mirror_filters(filters, ids)

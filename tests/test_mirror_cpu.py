@@ -109,6 +109,49 @@ def test_items_vs_oracle(seed, nf):
     _device_vs_oracle(filters, items)
 
 
+@pytest.mark.parametrize("seed,nf", [(5, 1), (6, 9), (7, 40), (8, 150), (9, 200)])
+def test_items_bitsets_vs_oracle(seed, nf):
+    """Mirror.mirror over MirrorData items through the per-origin bit-set
+    image (mirror_match_sw: nets per family, MAC filters, transport / app
+    ids, port ranges of both sides) against the oracle at every level, for
+    every origin; origins over 64 filters have no image.  Ports include
+    values outside 0-65535 and negative ones (Java ints)."""
+    rng = np.random.default_rng(seed)
+    filters, items = gen_mirror_case(rng, nf, 4000)
+    for f in filters[::7]:
+        if "port" in f:
+            f["port"] = [-5, f["port"][1]] if rng.random() < 0.5 else [f["port"][0], 70000]
+    for i in items[::11]:
+        i["port_src"] = int(rng.choice([-1, -70000, 65535, 65536, 2**31 - 1, -2**31]))
+    mf = MirrorFilters()
+    arr, n = mf.build(filters)
+    ids = {}
+    oarr = O.mirror_filters(filters, ids)
+    cols = mirror_columns(items, lambda s: mf.id_of(s, create=False), V.parse_ip)
+    it = items_struct(cols)
+    built = 0
+    for origin in sorted(set(f["origin"] for f in filters)) + ["nobody"]:
+        oid = mf.id_of(origin, create=False)
+        got = I.mirror_sw(arr, n, oid, it, len(items))
+        count = sum(f["origin"] == origin for f in filters)
+        if count == 0 or count > 64:
+            assert got is None, (origin, count)
+            continue
+        built += 1
+        want = I.mirror(arr, n, oid, it, len(items))      # per-filter path, == oracle above
+        np.testing.assert_array_equal(got, want, err_msg=origin)
+        o2 = np.array([O.mirror_match(oarr, len(filters), ids.get(origin, -2),
+                                      parse_mac(i["mac_src"]), parse_mac(i["mac_dst"]),
+                                      None if i["ip_src"] is None else O.parse_ip(i["ip_src"]),
+                                      None if i["ip_dst"] is None else O.parse_ip(i["ip_dst"]),
+                                      ids.get(i["transport"], -2) if i["transport"] else -1,
+                                      i["port_src"], i["port_dst"],
+                                      ids.get(i["app"], -2) if i["app"] else -1)
+                       for i in items[:800]], np.uint64)
+        np.testing.assert_array_equal(got[:800], o2, err_msg=origin)
+    assert built >= 1 or nf > 64 * 3
+
+
 @pytest.mark.parametrize("layer", [0, 1])
 def test_switch_vs_oracle(layer):
     rng = np.random.default_rng(40 + layer)

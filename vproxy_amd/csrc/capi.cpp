@@ -1560,6 +1560,10 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
             b.img.p4 = up(*s, b.p4);
             b.img.b6 = up(*s, b.b6);
             b.img.p6 = up(*s, b.p6);
+            b.img.tids = up(*s, b.tids);
+            b.img.aids = up(*s, b.aids);
+            b.img.bp = up(*s, b.bp);
+            b.img.pp = up(*s, b.pp);
             b.img.lds = !(env && env[0] == '1');
             s->sw[o] = b.img;
         }
@@ -1581,7 +1585,10 @@ int vc_mirror_match_dev(vc_ctx* ctx, int32_t origin, const vc_mirror_items* item
         return fail(VC_EINVAL, "ip_src / ip_dst must be 16-byte aligned");
     auto s = ctx->get(ctx->mirror);
     if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
-    hipError_t e = vc::launch_mirror_match(ctx->cfg(stream), s->img, origin, *items, n, out_mirrors);
+    const auto sw = s->sw.find(origin);
+    hipError_t e = vc::launch_mirror_match(ctx->cfg(stream), s->img,
+                                           sw == s->sw.end() ? nullptr : &sw->second, origin,
+                                           *items, n, out_mirrors);
     return launched(ctx, e, stream, "mirror launch");
 }
 

@@ -287,6 +287,11 @@ struct MirrorSwMir {               // filters whose FilterConfig.mirror is `bit`
     uint32_t bit, pad;
 };
 
+struct MirrorSwId {                // filters whose transport / app id is `id`
+    uint64_t filters;
+    int32_t id, pad;
+};
+
 struct MirrorSwImage {
     uint64_t all;                  // the origin's filters
     uint64_t has_x, has_y;         // NET_X / NET_Y
@@ -299,6 +304,16 @@ struct MirrorSwImage {
     const uint64_t* p4;            // per interval: (xmask, ymask)
     const uint64_t* b6;            // nb6 ascending interval starts as (hi, lo), b6[0] = (0, 0)
     const uint64_t* p6;            // per interval: (xmask, ymask)
+    // Mirror.mirror's transport and application levels (MirrorData items,
+    // FilterConfig.java:57-94): protocol ids as sets, port ranges as
+    // intervals over the key uint32(port) ^ 0x80000000 (Java's int order)
+    uint64_t has_px, has_py;       // PORT_X / PORT_Y
+    uint64_t any_t, any_a;         // transport / app -1: any
+    int32_t n_t, n_a, nbp, pad2;
+    const MirrorSwId* tids;
+    const MirrorSwId* aids;
+    const uint32_t* bp;            // nbp ascending port interval starts, bp[0] = 0
+    const uint64_t* pp;            // per port interval: (xmask, ymask)
 };
 
 // ---------------------------------------------------------------------------

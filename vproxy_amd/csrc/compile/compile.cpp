@@ -794,7 +794,11 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
     std::vector<std::pair<u128, u128>> r6;
     std::vector<uint64_t> bit4, bit6;
     std::vector<int> side4, side6;
-    std::map<int32_t, uint64_t> mirs;
+    std::map<int32_t, uint64_t> mirs, tmap, amap;
+    std::vector<std::pair<uint32_t, uint32_t>> rp;           // port ranges, x and y
+    std::vector<uint64_t> bitp;
+    std::vector<int> sidep;
+    auto pkey = [](int32_t p) { return uint32_t(p) ^ 0x80000000u; };
     MirrorSwImage& s = out->img;
     int j = 0;
     for (const MirrorRec& f : recs) {
@@ -816,6 +820,22 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
             bit6.resize(r6.size(), b);
             side6.resize(r6.size(), y);
         }
+        if (f.flags & VC_MF_PORT_X) {
+            s.has_px |= b;
+            rp.push_back({pkey(f.port_x0), pkey(f.port_x1)});
+            bitp.push_back(b);
+            sidep.push_back(0);
+        }
+        if (f.flags & VC_MF_PORT_Y) {
+            s.has_py |= b;
+            rp.push_back({pkey(f.port_y0), pkey(f.port_y1)});
+            bitp.push_back(b);
+            sidep.push_back(1);
+        }
+        if (f.transport == -1) s.any_t |= b;
+        else tmap[f.transport] |= b;
+        if (f.app == -1) s.any_a |= b;
+        else amap[f.app] |= b;
     }
     if (!j) return false;
     for (const auto& m : mirs) out->mirs.push_back({m.second, uint32_t(m.first), 0});
@@ -826,6 +846,14 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
     for (const auto& m : m4) out->p4.insert(out->p4.end(), {m.first, m.second});
     for (const u128 v : b6) out->b6.insert(out->b6.end(), {uint64_t(v >> 64), uint64_t(v)});
     for (const auto& m : m6) out->p6.insert(out->p6.end(), {m.first, m.second});
+    std::vector<std::pair<uint64_t, uint64_t>> mp;
+    intervals<uint32_t>(rp, bitp, sidep, &out->bp, &mp);
+    for (const auto& m : mp) out->pp.insert(out->pp.end(), {m.first, m.second});
+    for (const auto& m : tmap) out->tids.push_back({m.second, m.first, 0});
+    for (const auto& m : amap) out->aids.push_back({m.second, m.first, 0});
+    s.n_t = int32_t(out->tids.size());
+    s.n_a = int32_t(out->aids.size());
+    s.nbp = int32_t(out->bp.size());
     s.n_mac = int32_t(out->macs.size());
     s.n_mir = int32_t(out->mirs.size());
     s.nb4 = int32_t(out->b4.size());

@@ -114,8 +114,9 @@ struct MirrorSwBuilt {
     MirrorSwImage img{};
     std::vector<MirrorSwMac> macs;
     std::vector<MirrorSwMir> mirs;
-    std::vector<uint32_t> b4;
-    std::vector<uint64_t> p4, b6, p6;
+    std::vector<uint32_t> b4, bp;
+    std::vector<uint64_t> p4, b6, p6, pp;
+    std::vector<MirrorSwId> tids, aids;
 };
 bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, MirrorSwBuilt* out);
 

@@ -185,8 +185,9 @@ hipError_t launch_http_hint(const LaunchCfg& c, const HintImage& img, const uint
 hipError_t launch_certs(const LaunchCfg& c, const CertImage& certs, const uint8_t* blob,
                         const uint32_t* off, const uint8_t* null, int64_t n, int32_t* out);
 // Mirror filters (mirror.hip)
-hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
-                               const vc_mirror_items& in, int64_t n, uint64_t* out);
+hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img,
+                               const MirrorSwImage* sw, int32_t origin, const vc_mirror_items& in,
+                               int64_t n, uint64_t* out);
 hipError_t launch_mirror_switch(const LaunchCfg& c, const MirrorImage& img,
                                 const MirrorSwImage* sw, int32_t origin, const uint8_t* blob,
                                 const uint32_t* off, int64_t n, int layer, uint64_t* out);

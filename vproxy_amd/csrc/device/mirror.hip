@@ -12,13 +12,19 @@
 namespace vcd {
 
 constexpr int kMirrorBlock = 256;
+// kSw: the origin's bit-set image (mirror_match_sw), else every filter in
+// turn (mirror_eval)
+template <bool kSw>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
-    MirrorImage img, int32_t origin, vc_mirror_items in, int64_t n, uint64_t* __restrict__ out) {
+    MirrorImage img, MirrorSwImage sw, int32_t origin, vc_mirror_items in, int64_t n,
+    uint64_t* __restrict__ out) {
     const MirrorImage& fi = img;
+    const SwTables tb = sw_tables(sw);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const MirrorItem it = mirror_item(in, i);
-        out[i] = mirror_eval(fi, origin, it, mirror_level(it));
+        out[i] = kSw ? mirror_match_sw(sw, tb, it, mirror_level(it))
+                     : mirror_eval(fi, origin, it, mirror_level(it));
     }
 }
 
@@ -43,7 +49,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
     __shared__ ulonglong2 l4p[kL ? kMirrorL : 1], l6b[kL ? kMirrorL : 1], l6p[kL ? kMirrorL : 1];
     const MirrorImage& fi = img;
     const int lane = int(threadIdx.x & 63), w = int(threadIdx.x >> 6);
-    SwTables tb{sw.b4, sw.p4, sw.b6, sw.p6};
+    SwTables tb = sw_tables(sw);
     if (kL) {
         const int t = int(threadIdx.x);
         if (t < sw.nb4) {
@@ -56,7 +62,8 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
         }
         __syncthreads();
         tb = SwTables{l4b, reinterpret_cast<const uint64_t*>(l4p),
-                      reinterpret_cast<const uint64_t*>(l6b), reinterpret_cast<const uint64_t*>(l6p)};
+                      reinterpret_cast<const uint64_t*>(l6b), reinterpret_cast<const uint64_t*>(l6p),
+                      sw.bp, sw.pp};
     }
     ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);   // chunks.h
     int64_t c = ch.first(w);
@@ -93,11 +100,17 @@ int mirror_grid(const LaunchCfg& c, K kernel, int64_t n) {
 }
 }  // namespace
 
-hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img, int32_t origin,
-                               const vc_mirror_items& in, int64_t n, uint64_t* out) {
+hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img,
+                               const MirrorSwImage* sw, int32_t origin, const vc_mirror_items& in,
+                               int64_t n, uint64_t* out) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vcd::mirror_match_kernel, dim3(mirror_grid(c, vcd::mirror_match_kernel, n)),
-                       dim3(vcd::kMirrorBlock), 0, c.stream, img, origin, in, n, out);
+    const MirrorSwImage none{};
+    auto go = [&](auto kernel, const MirrorSwImage& s) {
+        hipLaunchKernelGGL(kernel, dim3(mirror_grid(c, kernel, n)), dim3(vcd::kMirrorBlock), 0,
+                           c.stream, img, s, origin, in, n, out);
+    };
+    if (sw) go(vcd::mirror_match_kernel<true>, *sw);
+    else go(vcd::mirror_match_kernel<false>, none);
     return hipGetLastError();
 }
 

@@ -194,7 +194,13 @@ VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
 struct SwTables {
     const uint32_t* b4;
     const uint64_t *p4, *b6, *p6;
+    const uint32_t* bp;            // port intervals (Mirror.mirror's items)
+    const uint64_t* pp;
 };
+
+VC_HD SwTables sw_tables(const MirrorSwImage& s) {
+    return SwTables{s.b4, s.p4, s.b6, s.p6, s.bp, s.pp};
+}
 
 template <bool kL = false>
 VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const SwTables& t, const uint8_t* p,
@@ -226,6 +232,65 @@ VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const SwTables& t, const
         const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
         hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
     }
+    uint64_t m = 0;
+    for (int k = 0; k < s.n_mir; ++k) {
+        const MirrorSwMir r = load_uniform(s.mirs, k);
+        if (hit & r.filters) m |= uint64_t(1) << r.bit;
+    }
+    return m;
+}
+
+// The (xmask, ymask) of one address of a MirrorData item (4 or 16 bytes)
+template <bool kL = false>
+VC_HD ulonglong2 sw_addr_masks(const MirrorSwImage& s, const SwTables& t, const vcn::Addr& a) {
+    if (a.len == 4) return sw_masks<kL>(t.p4, bsearch_u32<kL>(t.b4, s.nb4, bswap32(a.w[0])));
+    uint64_t h, l;
+    v6_key(make_uint4(a.w[0], a.w[1], a.w[2], a.w[3]), &h, &l);
+    return sw_masks<kL>(t.p6, bsearch_u128<kL>(t.b6, s.nb6, h, l));
+}
+
+// Filters of a uniform id list whose id is `id`, plus `any`
+VC_HD uint64_t sw_ids(const MirrorSwId* ids, int n, uint64_t any, int32_t id) {
+    for (int k = 0; k < n; ++k) {
+        const MirrorSwId r = load_uniform(ids, k);
+        if (r.id == id) any |= r.filters;
+    }
+    return any;
+}
+
+// Mirror.mirror's filter step for one MirrorData item through the origin's
+// bit-set image: mirror_eval's answer at the item's level (Mirror.java
+// :104-117), with matchTransport's protocol and port part (:57-80) and
+// matchApplication's protocol (:82-94) as sets too:
+//   transport -1 or equal; no portX -> true; portX and portY ->
+//   (pxs && pyd) || (pys && pxd); portX only -> pxs || pxd.
+template <bool kL = false>
+VC_HD uint64_t mirror_match_sw(const MirrorSwImage& s, const SwTables& t, const MirrorItem& it,
+                               int lvl) {
+    uint64_t hit = s.all & ~s.mac;
+    for (int k = 0; k < s.n_mac; ++k) {
+        const MirrorSwMac f = load_uniform(s.macs, k);
+        const bool ok = f.has_y ? (f.mac_x == it.mac_src && f.mac_y == it.mac_dst) ||
+                                      (f.mac_y == it.mac_src && f.mac_x == it.mac_dst)
+                                : f.mac_x == it.mac_src || f.mac_x == it.mac_dst;
+        if (ok) hit |= f.bit;
+    }
+    if (lvl >= kLvlIp) {
+        const ulonglong2 ms = sw_addr_masks<kL>(s, t, it.ip_src);
+        const ulonglong2 md = sw_addr_masks<kL>(s, t, it.ip_dst);
+        const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
+        hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
+    }
+    if (lvl >= kLvlTransport) {
+        const uint64_t tm = sw_ids(s.tids, s.n_t, s.any_t, it.transport);
+        const ulonglong2 ps =
+            sw_masks<kL>(t.pp, bsearch_u32<kL>(t.bp, s.nbp, uint32_t(it.port_src) ^ 0x80000000u));
+        const ulonglong2 pd =
+            sw_masks<kL>(t.pp, bsearch_u32<kL>(t.bp, s.nbp, uint32_t(it.port_dst) ^ 0x80000000u));
+        const uint64_t both = s.has_px & s.has_py, xonly = s.has_px & ~s.has_py;
+        hit &= tm & (~s.has_px | (both & ((ps.x & pd.y) | (ps.y & pd.x))) | (xonly & (ps.x | pd.x)));
+    }
+    if (lvl == kLvlApp) hit &= sw_ids(s.aids, s.n_a, s.any_a, it.app);
     uint64_t m = 0;
     for (int k = 0; k < s.n_mir; ++k) {
         const MirrorSwMir r = load_uniform(s.mirs, k);
