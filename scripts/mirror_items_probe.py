@@ -26,7 +26,7 @@ def main():
     filters, items = gen_mirror_case(rng, 40, 1 << 16, origins=("switch",))
     clf = V.Classifier(0)
     res = {}
-    for sw in ("0", "2"):
+    for sw in ("0", "1", "2"):
         os.environ["VC_MIRROR_SW"] = sw
         mf = clf.compile_mirror(filters)
         if sw == "0":
@@ -48,9 +48,10 @@ def main():
         ms = timed(fn)
         res[sw] = out.clone()
         print(json.dumps({"workload": "mirror items", "items": n, "filters": len(filters),
-                          "path": "bitsets" if sw == "2" else "per_filter", "ms": round(ms, 4)}),
+                          "path": {"0": "per_filter", "1": "bitsets_global",
+                                   "2": "bitsets_lds"}[sw], "ms": round(ms, 4)}),
               flush=True)
-    assert torch.equal(res["0"], res["2"])
+    assert torch.equal(res["0"], res["1"]) and torch.equal(res["0"], res["2"])
     clf.close()
 
 

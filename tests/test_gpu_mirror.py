@@ -21,7 +21,7 @@ def clf():
     c.close()
 
 
-@pytest.mark.parametrize("sw", ["2", "0"])      # bit-set images / per-filter kernel
+@pytest.mark.parametrize("sw", ["2", "1", "0"])   # bit sets from LDS / global / per filter
 def test_items_vs_oracle(clf, sw, monkeypatch):
     import torch
     filters, items = gen_mirror_case(np.random.default_rng(7), 50, 20000)

@@ -13,20 +13,46 @@ namespace vcd {
 
 constexpr int kMirrorBlock = 256;
 // kSw: the origin's bit-set image (mirror_match_sw), else every filter in
-// turn (mirror_eval)
-template <bool kSw>
+// turn (mirror_eval).  kL: its three interval tables (at most kMatchL
+// intervals each) copied into LDS first.
+constexpr int kMatchL = 128;
+template <bool kSw, bool kL>
 __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
     MirrorImage img, MirrorSwImage sw, int32_t origin, vc_mirror_items in, int64_t n,
     uint64_t* __restrict__ out) {
+    __shared__ uint32_t l4b[kL ? kMatchL : 1], lpb[kL ? kMatchL : 1];
+    __shared__ ulonglong2 l4p[kL ? kMatchL : 1], l6b[kL ? kMatchL : 1], l6p[kL ? kMatchL : 1],
+        lpp[kL ? kMatchL : 1];
     const MirrorImage& fi = img;
-    const SwTables tb = sw_tables(sw);
+    SwTables tb = sw_tables(sw);
+    if (kL) {
+        const int t = int(threadIdx.x);
+        typedef const ulonglong2* P2;
+        if (t < sw.nb4) {
+            l4b[t] = glb_ld(sw.b4 + t);
+            l4p[t] = glb_ld(reinterpret_cast<P2>(sw.p4) + t);
+        }
+        if (t < sw.nb6) {
+            l6b[t] = glb_ld(reinterpret_cast<P2>(sw.b6) + t);
+            l6p[t] = glb_ld(reinterpret_cast<P2>(sw.p6) + t);
+        }
+        if (t < sw.nbp) {
+            lpb[t] = glb_ld(sw.bp + t);
+            lpp[t] = glb_ld(reinterpret_cast<P2>(sw.pp) + t);
+        }
+        __syncthreads();
+        typedef const uint64_t* P1;
+        tb = SwTables{l4b, reinterpret_cast<P1>(l4p), reinterpret_cast<P1>(l6b),
+                      reinterpret_cast<P1>(l6p), lpb, reinterpret_cast<P1>(lpp)};
+    }
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const MirrorItem it = mirror_item(in, i);
-        out[i] = kSw ? mirror_match_sw(sw, tb, it, mirror_level(it))
+        out[i] = kSw ? mirror_match_sw<kL>(sw, tb, it, mirror_level(it))
                      : mirror_eval(fi, origin, it, mirror_level(it));
     }
 }
+static_assert(kMatchL <= kMirrorBlock, "one copy pass per workgroup");
 
 // Frames staged per wave in LDS as in packet.hip (kStage), parsed from there.
 constexpr int kMirrorWaves = kMirrorBlock / 64;
@@ -109,8 +135,11 @@ hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img,
         hipLaunchKernelGGL(kernel, dim3(mirror_grid(c, kernel, n)), dim3(vcd::kMirrorBlock), 0,
                            c.stream, img, s, origin, in, n, out);
     };
-    if (sw) go(vcd::mirror_match_kernel<true>, *sw);
-    else go(vcd::mirror_match_kernel<false>, none);
+    if (sw && sw->lds && sw->nb4 <= vcd::kMatchL && sw->nb6 <= vcd::kMatchL &&
+        sw->nbp <= vcd::kMatchL)
+        go(vcd::mirror_match_kernel<true, true>, *sw);
+    else if (sw) go(vcd::mirror_match_kernel<true, false>, *sw);
+    else go(vcd::mirror_match_kernel<false, false>, none);
     return hipGetLastError();
 }
 
