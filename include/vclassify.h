@@ -601,7 +601,9 @@ typedef struct vc_mirror_items {
 /* Mirror.mirror(MirrorData) filter step (Mirror.java:89-118): per item the
  * set of mirrors (bit m = MirrorConfig m) whose filters of `origin` match,
  * at the level the item's null fields select (ether / ip / transport /
- * application).  Device pointers (every array in `items` and out). */
+ * application).  Device pointers (every array in `items` and out); ip_src /
+ * ip_dst 16-byte aligned, mac_src / mac_dst 2-byte aligned (VC_EINVAL
+ * otherwise; the host form stages any alignment). */
 int vc_mirror_match_dev(vc_ctx *ctx, int32_t origin, const vc_mirror_items *items, int64_t n,
                         uint64_t *out_mirrors, void *stream);
 int vc_mirror_match(vc_ctx *ctx, int32_t origin, const vc_mirror_items *items, int64_t n,

@@ -156,3 +156,17 @@ def test_reference_configs(clf, k):
         dev = clf.mirror_match(c["origin"], dcols, len(items))
         torch.cuda.synchronize()
         np.testing.assert_array_equal(dev.cpu().numpy().view(np.uint64), want)
+
+
+def test_items_mac_alignment(clf):
+    """vc_mirror_match_dev reads the 6-byte MAC columns with 16-bit loads:
+    an odd device address is refused (VC_EINVAL), an even one is read."""
+    import torch
+    clf.compile_mirror([{"origin": "o", "mirror": 3, "mac": "0a:00:27:00:00:01"}])
+    raw = torch.zeros(6 * 4 + 2, dtype=torch.uint8, device="cuda")
+    raw[2:8] = torch.tensor([10, 0, 0x27, 0, 0, 1], dtype=torch.uint8)
+    with pytest.raises(V.IllegalArgumentException):
+        clf.mirror_match("o", {"mac_src": raw[1:25]}, 4)
+    got = clf.mirror_match("o", {"mac_src": raw[2:26]}, 4)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), [1 << 3, 0, 0, 0])

@@ -1583,6 +1583,8 @@ int vc_mirror_match_dev(vc_ctx* ctx, int32_t origin, const vc_mirror_items* item
     if (n == 0) return VC_OK;
     if ((items->ip_src && !al16(items->ip_src)) || (items->ip_dst && !al16(items->ip_dst)))
         return fail(VC_EINVAL, "ip_src / ip_dst must be 16-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(items->mac_src) | reinterpret_cast<uintptr_t>(items->mac_dst)) & 1)
+        return fail(VC_EINVAL, "mac_src / mac_dst must be 2-byte aligned");
     auto s = ctx->get(ctx->mirror);
     if (!s) return fail(VC_ESTATE, "no mirror filters compiled");
     const auto sw = s->sw.find(origin);

@@ -115,6 +115,13 @@ VC_HD uint64_t mac48(const uint8_t* p) {
     return v;
 }
 
+// MAC i of a 6-byte-per-item column: three 16-bit loads (6 * i is even;
+// the column is at least 2-byte aligned, vc_mirror_match_dev checks)
+VC_HD uint64_t mac48_col(const uint8_t* col, int64_t i) {
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(col) + 3 * i;
+    return uint64_t(h[0]) | (uint64_t(h[1]) << 16) | (uint64_t(h[2]) << 32);
+}
+
 VC_HD vcn::Addr item_addr(const uint8_t* base, int64_t i, int len) {
     if (!base || (len != 4 && len != 16)) return vcn::Addr{{0, 0, 0, 0}, 0};
     const uint4 w = reinterpret_cast<const uint4*>(base)[i];       // 16-byte aligned rows
@@ -126,8 +133,8 @@ VC_HD vcn::Addr item_addr(const uint8_t* base, int64_t i, int len) {
 // or null.  A length other than 4 / 16 reads as a null IP.
 VC_HD MirrorItem mirror_item(const vc_mirror_items& in, int64_t i) {
     MirrorItem it;
-    it.mac_src = in.mac_src ? mac48(in.mac_src + 6 * i) : 0;
-    it.mac_dst = in.mac_dst ? mac48(in.mac_dst + 6 * i) : 0xFFFFFFFFFFFFull;
+    it.mac_src = in.mac_src ? mac48_col(in.mac_src, i) : 0;
+    it.mac_dst = in.mac_dst ? mac48_col(in.mac_dst, i) : 0xFFFFFFFFFFFFull;
     it.ip_src = item_addr(in.ip_src, i, in.ip_src_len ? in.ip_src_len[i] : 0);
     it.ip_dst = item_addr(in.ip_dst, i, in.ip_dst_len ? in.ip_dst_len[i] : 0);
     it.transport = in.transport ? in.transport[i] : -1;
