@@ -1881,13 +1881,14 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
 static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) {
     AclPortImage im{nullptr, nullptr, 0, port};
     if (!s.port_images || !s.host || port < 0 || port > 65535) return im;
-    {
-        std::lock_guard<std::mutex> lk(ctx->port_seen_mu);
-        ctx->acl_ports_seen.insert(port);
-    }
     std::lock_guard<std::mutex> lk(s.port_mu);
     const auto it = s.ports.find(port);
     if (it != s.ports.end()) return it->second;
+    {
+        // later compiles build this port's image ahead
+        std::lock_guard<std::mutex> seen(ctx->port_seen_mu);
+        ctx->acl_ports_seen.insert(port);
+    }
     std::vector<uint32_t> pb, pv;
     vc::build_acl_port(s.host->fam[1][0], uint32_t(port), &pb, &pv);
     if (pb.size() <= size_t(kAclPortMax)) {
