@@ -791,7 +791,8 @@ def build_parser():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c5",
                     choices=["c5", "c1", "c2", "c2host", "c3", "c4", "c4uri", "dns", "dnsd", "sni", "http",
-                             "parse", "switch", "source", "mirror", "mix", "mixhost"])
+                             "parse", "switch", "source", "mirror", "mirroritems", "mix",
+                             "mixhost"])
     ap.add_argument("--packets", type=int, default=125_000_000, help="per GPU per step (c5)")
     ap.add_argument("--pool", type=int, default=16 << 20, help="hostname pool (c5/c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1179,6 +1180,88 @@ def compile_switch_acl(clf, t):
     b, nb, kb = W.as_ctypes(udp, V._lib.VcAclRule)
     V.check(V.lib().vc_compile_acl(clf.h, a, na, b, nb, 0))
     return t.tcp, udp
+
+
+def mirror_items_workload(n, dev, mf_of):
+    """The `mirroritems` sub-bench (Mirror.mirror over MirrorData items):
+    40 seeded filters of one origin ("tcp-lb": MACs, IPv4 / IPv6 / mapped
+    networks, transport and application protocols, port ranges) and n items
+    drawn on the device from 64K seeded templates at every null level.
+    mf_of(filters) compiles the filters and returns the MirrorFilters
+    interning.  Returns (filters, mf, numpy template columns, device
+    columns of the batch, template index per item)."""
+    rng = np.random.default_rng(W.SEED + 41)
+    pick = lambda xs: xs[int(rng.integers(0, len(xs)))]
+    macs = ["0a:00:27:00:00:%02x" % i for i in range(6)]
+    nets = ["10.0.0.0/8", "10.1.0.0/16", "192.168.0.0/24", "172.16.0.0/12", "fd00::/8",
+            "fd00:1::/32", "::ffff:10.0.0.0/104", "2001:db8::/32", "100.64.0.0/10"]
+    filters = []
+    for k in range(40):
+        f = {"origin": "tcp-lb", "mirror": k % 12}
+        if rng.random() < 0.3:
+            f["mac"] = pick(macs)
+        if rng.random() < 0.8:
+            f["network"] = pick(nets)
+            if rng.random() < 0.4:
+                f["network2"] = pick(nets)
+        if rng.random() < 0.6:
+            f["transportLayerProtocol"] = pick(["tcp", "udp"])
+        if rng.random() < 0.6:
+            a = int(rng.integers(0, 60000))
+            f["port"] = [a, a + int(rng.integers(0, 2000))]
+            if rng.random() < 0.3:
+                b = int(rng.integers(0, 60000))
+                f["port2"] = [b, b + int(rng.integers(0, 2000))]
+        if rng.random() < 0.3:
+            f["applicationLayerProtocol"] = pick(["http", "dns", "h2"])
+        filters.append(f)
+    mf = mf_of(filters)
+    t = 1 << 16
+    ips4 = np.concatenate([np.array([[10, 0, 0, 0], [10, 1, 0, 0], [192, 168, 0, 0], [172, 16, 0, 0],
+                                     [100, 64, 0, 0], [8, 8, 0, 0]], np.uint8)[rng.integers(0, 6, t)]])
+    ips4[:, 2:] = rng.integers(0, 256, (t, 2))
+    cols = {"mac_src": np.array([[0x0a, 0, 0x27, 0, 0, int(x)] for x in rng.integers(0, 8, t)],
+                                np.uint8).reshape(-1),
+            "mac_dst": np.array([[0x0a, 0, 0x27, 0, 0, int(x)] for x in rng.integers(0, 8, t)],
+                                np.uint8).reshape(-1)}
+    for side, sh in (("src", 0), ("dst", 1)):
+        ln = np.where(rng.random(t) < 0.7, 4, 16).astype(np.uint8)
+        ip = np.zeros((t, 16), np.uint8)
+        ip[:, :4] = np.roll(ips4, sh, axis=0)
+        v6 = ln == 16
+        kind = rng.integers(0, 3, t)
+        ip[v6] = 0
+        m = v6 & (kind == 0)                        # ::ffff:a.b.c.d
+        ip[m, 10:12] = 0xFF
+        ip[m, 12:] = np.roll(ips4, sh, axis=0)[m]
+        m = v6 & (kind == 1)                        # fd00:: / fd00:1::
+        ip[m, 0] = 0xFD
+        ip[m, 3] = rng.integers(0, 2, int(m.sum()))
+        ip[m, 8:] = rng.integers(0, 256, (int(m.sum()), 8))
+        m = v6 & (kind == 2)                        # 2001:db8::
+        ip[m, :4] = [0x20, 0x01, 0x0D, 0xB8]
+        ip[m, 8:] = rng.integers(0, 256, (int(m.sum()), 8))
+        ln[rng.random(t) < 0.05] = 0                # null IP: the Ethernet level
+        cols["ip_%s_len" % side] = ln
+        cols["ip_" + side] = ip
+    tid = lambda s: mf.id_of(s, create=False)
+    r = rng.random(t)
+    cols["transport"] = np.where(r < 0.2, -1, np.where(rng.random(t) < 0.6, tid("tcp"),
+                                                      tid("udp"))).astype(np.int32)
+    cols["app"] = np.where((r < 0.5) | (cols["transport"] == -1), -1,
+                           np.array([tid(x) for x in ("http", "dns", "h2")], np.int32)[
+                               rng.integers(0, 3, t)]).astype(np.int32)
+    cols["port_src"] = rng.integers(0, 65536, t).astype(np.int32)
+    cols["port_dst"] = rng.integers(0, 65536, t).astype(np.int32)
+    idx = torch.from_numpy(np.random.default_rng(W.SEED + 42).integers(0, t, n)).to(dev)
+    dcols = {}
+    for k, v in cols.items():
+        d = torch.from_numpy(v).to(dev)
+        if k.startswith("mac"):
+            dcols[k] = d.view(-1, 6)[idx].contiguous().view(-1)
+        else:
+            dcols[k] = d[idx].contiguous()
+    return filters, mf, cols, dcols, idx
 
 
 # the `mirror` sub-bench's 17 filters (Mirror.switchPacket over the switch origin)
@@ -1686,6 +1769,36 @@ def sub_bench(args, clf, dev, rank, world):
                     return time.perf_counter() - t0
                 cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "frames of the workload, oracle "
                                 "Mirror.switchPacket over the 17 filters", cap=1 << 22)
+    elif args.workload == "mirroritems":
+        n = 32 << 20
+        from vproxy_amd.mirror import items_struct
+        filters, mf, tcols, dcols, tidx = mirror_items_workload(n, dev, clf.compile_mirror)
+        it = items_struct(dcols)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        oid = mf.id_of("tcp-lb", create=False)
+        fn = lambda: V.check(V.lib().vc_mirror_match_dev(
+            clf.h, oid, C.byref(it), n, C.c_void_p(out.data_ptr()), S()))
+        per_unit = 6 + 6 + 1 + 1 + 16 + 16 + 4 * 4 + 8
+        unit = ("B/item (MACs 6 + 6, IP lengths 1 + 1, IP rows 16 + 16, transport, ports, app "
+                "4 each in; 8 B mirror set out), 40 filters")
+        kern = "mirror_match_kernel"
+        if O is not None:
+            ids = {}
+            oarr = O.mirror_filters(filters, ids)
+            assert ids == mf.ids
+            ti = tidx[:1 << 22].cpu().numpy()
+            scols = {}
+            for k, v in tcols.items():
+                scols[k] = (v.reshape(-1, 6)[ti].reshape(-1) if k.startswith("mac") else v[ti])
+
+            def run(k, threads):
+                c = {key: (v[:6 * k] if key.startswith("mac") else v[:k])
+                     for key, v in scols.items()}
+                t0 = time.perf_counter()
+                O.mirror_match_batch_np(oarr, len(filters), ids["tcp-lb"], c, nthreads=threads)
+                return time.perf_counter() - t0
+            cpu = functools.partial(cpu_rates, run, "M items/s", 3.0, "items of the workload, "
+                                    "oracle Mirror.mirror over the 40 filters", cap=1 << 22)
     elif args.workload == "source":
         n = 128 << 20
         groups, grp, src = source_workload(n, dev)

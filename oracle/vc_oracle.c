@@ -1515,6 +1515,38 @@ void vo_mirror_switch_batch(const vo_mirror_filter *f, int nf, int origin, const
 }
 
 typedef struct {
+    const vo_mirror_filter *f; int nf, origin;
+    const uint8_t *mac_src, *mac_dst, *src_len, *dst_len, *ip_src, *ip_dst;
+    const int32_t *transport, *port_src, *port_dst, *app;
+    uint64_t *out;
+} mirror_items_ctx;
+
+static void mirror_items_range(void *p, int64_t lo, int64_t hi)
+{
+    mirror_items_ctx *c = (mirror_items_ctx *)p;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int ls = c->src_len[i], ld = c->dst_len[i];
+        c->out[i] = vo_mirror_match(c->f, c->nf, c->origin, c->mac_src + 6 * i, c->mac_dst + 6 * i,
+                                    c->ip_src + 16 * i, ls == 4 || ls == 16 ? ls : 0,
+                                    c->ip_dst + 16 * i, ld == 4 || ld == 16 ? ld : 0,
+                                    c->transport[i], c->port_src[i], c->port_dst[i], c->app[i]);
+    }
+}
+
+/* vo_mirror_match over SoA columns laid out as vc_mirror_items (MACs 6 B,
+ * IP rows 16 B, lengths 0 / 4 / 16), every column present */
+void vo_mirror_match_batch(const vo_mirror_filter *f, int nf, int origin, const uint8_t *mac_src,
+                           const uint8_t *mac_dst, const uint8_t *src_len, const uint8_t *dst_len,
+                           const uint8_t *ip_src, const uint8_t *ip_dst, const int32_t *transport,
+                           const int32_t *port_src, const int32_t *port_dst, const int32_t *app,
+                           int64_t n, uint64_t *out, int nthreads)
+{
+    mirror_items_ctx c = {f, nf, origin, mac_src, mac_dst, src_len, dst_len, ip_src, ip_dst,
+                          transport, port_src, port_dst, app, out};
+    parallel_for(n, nthreads, mirror_items_range, &c);
+}
+
+typedef struct {
     const vo_server *servers; const int32_t *goff; const int32_t *order; const int32_t *size;
     const int32_t *grp; const uint32_t *src4; int32_t *out;
 } source_batch_ctx;

@@ -269,6 +269,11 @@ void vo_switch_batch(const vo_sg_rule *tcp, int ntcp, const vo_sg_rule *udp, int
 void vo_cert_batch(const char *const *names, const int32_t *name_lens, const int32_t *holder,
                    int n_names, int n_holders, const uint8_t *blob, const uint32_t *off,
                    const uint8_t *sni_null, int64_t n, int32_t *out, int nthreads);
+void vo_mirror_match_batch(const vo_mirror_filter *f, int nf, int origin, const uint8_t *mac_src,
+                           const uint8_t *mac_dst, const uint8_t *src_len, const uint8_t *dst_len,
+                           const uint8_t *ip_src, const uint8_t *ip_dst, const int32_t *transport,
+                           const int32_t *port_src, const int32_t *port_dst, const int32_t *app,
+                           int64_t n, uint64_t *out, int nthreads);
 void vo_mirror_switch_batch(const vo_mirror_filter *f, int nf, int origin, const uint8_t *blob,
                             const uint32_t *off, int64_t n, int layer, uint64_t *out,
                             int nthreads);

@@ -147,6 +147,8 @@ def lib():
                                     vp, C.c_int]
         L.vo_mirror_switch_batch.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int, vp, vp, i64,
                                              C.c_int, vp, C.c_int]
+        L.vo_mirror_match_batch.argtypes = [P(VoMirrorFilter), C.c_int, C.c_int] + [vp] * 10 + \
+            [i64, vp, C.c_int]
         L.vo_source_batch.argtypes = [P(VoServer), vp, C.c_int, C.c_int, vp, vp, i64, vp, C.c_int]
         L.vo_dns_datagram.argtypes = [P(VoSgRule), C.c_int, P(VoSgRule), C.c_int, C.c_int,
                                       P(VoHosts), P(VoGroup), C.c_int, vp, C.c_int, vp, C.c_int,
@@ -708,6 +710,20 @@ def mirror_switch_batch_np(arr, nf, origin, blob, off, layer, nthreads=1):
     out = np.empty(n, np.uint64)
     lib().vo_mirror_switch_batch(arr, nf, origin, _ptr(np.ascontiguousarray(blob, np.uint8)),
                                  _ptr(_u32a(off)), n, layer, _ptr(out), nthreads)
+    return out
+
+
+def mirror_match_batch_np(arr, nf, origin, cols, nthreads=1):
+    """vo_mirror_match over vc_mirror_items-shaped numpy columns (every
+    column present: mac_src / mac_dst 6 B per item, ip_*_len, ip_* 16 B rows,
+    transport / port_src / port_dst / app int32)."""
+    n = len(cols["ip_src_len"])
+    c = {k: np.ascontiguousarray(v) for k, v in cols.items()}
+    out = np.empty(n, np.uint64)
+    lib().vo_mirror_match_batch(arr, nf, origin, _ptr(c["mac_src"]), _ptr(c["mac_dst"]),
+                                _ptr(c["ip_src_len"]), _ptr(c["ip_dst_len"]), _ptr(c["ip_src"]),
+                                _ptr(c["ip_dst"]), _ptr(c["transport"]), _ptr(c["port_src"]),
+                                _ptr(c["port_dst"]), _ptr(c["app"]), n, _ptr(out), nthreads)
     return out
 
 

@@ -170,3 +170,31 @@ def test_items_mac_alignment(clf):
     got = clf.mirror_match("o", {"mac_src": raw[2:26]}, 4)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), [1 << 3, 0, 0, 0])
+
+
+def test_mirroritems_bench_batch(clf):
+    """The `mirroritems` sub-bench's whole batch (bench.mirror_items_workload:
+    32M items, 40 filters) through vc_mirror_match_dev, every result equal to
+    the oracle's Mirror.mirror (vo_mirror_match_batch)."""
+    import ctypes as C
+    import os
+    import torch
+    import bench as B
+    from vproxy_amd.mirror import items_struct
+    n = 32 << 20
+    filters, mf, tcols, dcols, idx = B.mirror_items_workload(n, torch.device("cuda"),
+                                                             clf.compile_mirror)
+    out = torch.empty(n, dtype=torch.int64, device="cuda")
+    oid = mf.id_of("tcp-lb", create=False)
+    it = items_struct(dcols)
+    V.check(V.lib().vc_mirror_match_dev(clf.h, oid, C.byref(it), n, C.c_void_p(out.data_ptr()),
+                                        C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    ids = {}
+    oarr = O.mirror_filters(filters, ids)
+    # the oracle on the 64K templates, gathered per item (items are copies of them)
+    want_t = O.mirror_match_batch_np(oarr, len(filters), ids["tcp-lb"], tcols,
+                                     nthreads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(got, want_t[idx.cpu().numpy()])
+    assert (got != 0).mean() > 0.2

@@ -99,3 +99,29 @@ def test_cert_and_mirror_and_source_batches():
     for i in range(len(grp)):
         b = int(src[i]).to_bytes(4, "big")
         assert out[i] == O.source_select(groups[grp[i]], 0, b), i
+
+
+def test_mirror_match_batch_equals_single():
+    """vo_mirror_match_batch (the mirroritems bench's CPU leg) over
+    vc_mirror_items-shaped columns equals vo_mirror_match per item."""
+    from cases import gen_mirror_case, mirror_columns
+    import vproxy_amd as V
+    from vproxy_amd.mirror import MirrorFilters, parse_mac
+    rng = np.random.default_rng(33)
+    filters, items = gen_mirror_case(rng, 30, 3000)
+    mf = MirrorFilters()
+    mf.build(filters)
+    ids = {}
+    arr = O.mirror_filters(filters, ids)
+    cols = mirror_columns(items, lambda s: mf.id_of(s, create=False), V.parse_ip)
+    for origin in ("switch", "tcp-lb"):
+        oid = ids.get(origin, -2)
+        got = O.mirror_match_batch_np(arr, len(filters), oid, cols, nthreads=4)
+        want = [O.mirror_match(arr, len(filters), oid, parse_mac(i["mac_src"]),
+                               parse_mac(i["mac_dst"]),
+                               None if i["ip_src"] is None else O.parse_ip(i["ip_src"]),
+                               None if i["ip_dst"] is None else O.parse_ip(i["ip_dst"]),
+                               ids.get(i["transport"], -2) if i["transport"] else -1,
+                               i["port_src"], i["port_dst"],
+                               ids.get(i["app"], -2) if i["app"] else -1) for i in items]
+        assert [int(x) for x in got] == want, origin
