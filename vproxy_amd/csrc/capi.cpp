@@ -643,7 +643,7 @@ struct AclSnap : Snapshot {
     // (images.h AclPortImage): built by a compile for every bind port a
     // switch call has used on this context, and on the first call with a new
     // one (acl_port_image); kept with the snapshot.
-    std::shared_ptr<const vc::AclBuilt> host;
+    std::shared_ptr<const vc::AclFamilyBuilt> udp4;   // the UDP list's IPv4 image, host side
     bool port_images = true;       // VC_ACL_PORT=0 at compile: general image only (A/B)
     mutable std::mutex port_mu;
     mutable std::map<int32_t, AclPortImage> ports;
@@ -922,7 +922,7 @@ int vc_compile_acl(vc_ctx* ctx, const vc_acl_rule* tcp, int n_tcp, const vc_acl_
         }
     }
     if (const hipError_t e = up.done(); e != hipSuccess) return hip_fail(e, "ACL upload");
-    s->host = std::make_shared<const vc::AclBuilt>(std::move(b));
+    if (s->port_images) s->udp4 = std::make_shared<const vc::AclFamilyBuilt>(std::move(b.fam[1][0]));
     ctx->publish(ctx->acl, std::shared_ptr<const AclSnap>(std::move(s)));
     return VC_OK;
 }
@@ -1880,7 +1880,7 @@ int vc_dns_datagrams(vc_ctx* ctx, const uint8_t* blob, const uint32_t* off, int6
 // upload).
 static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) {
     AclPortImage im{nullptr, nullptr, 0, port};
-    if (!s.port_images || !s.host || port < 0 || port > 65535) return im;
+    if (!s.port_images || !s.udp4 || port < 0 || port > 65535) return im;
     std::lock_guard<std::mutex> lk(s.port_mu);
     const auto it = s.ports.find(port);
     if (it != s.ports.end()) return it->second;
@@ -1890,7 +1890,7 @@ static AclPortImage acl_port_image(vc_ctx* ctx, const AclSnap& s, int32_t port) 
         ctx->acl_ports_seen.insert(port);
     }
     std::vector<uint32_t> pb, pv;
-    vc::build_acl_port(s.host->fam[1][0], uint32_t(port), &pb, &pv);
+    vc::build_acl_port(*s.udp4, uint32_t(port), &pb, &pv);
     if (pb.size() <= size_t(kAclPortMax)) {
         // through a stager's page-locked bounce buffer, as every upload
         Snapshot own;
