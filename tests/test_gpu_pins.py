@@ -120,3 +120,39 @@ def test_pinned_snapshots_are_freed_after_release():
         assert after < 0.75 * held or held - after > (16 << 20), (held, after)
     finally:
         clf.close()
+
+
+def test_switch_port_image_on_a_pinned_snapshot():
+    """The bind-port ACL image (AclPortImage) is built on the first switch
+    call with a port for the snapshot the call uses: through a pin of an old
+    SecurityGroup, a new port builds that old list's image (and the current
+    snapshot gets its own), each call answering by its own list."""
+    import torch
+    clf = V.Classifier(0)
+    try:
+        clf.compile_routes(["10.0.0.0/8", "0.0.0.0/0"])
+        clf.compile_acl([], [("10.0.0.0/8", 4789, 4789, True), ("0.0.0.0/0", 0, 65535, False)],
+                        False)
+        p = clf.pin()
+        clf.compile_acl([], [("10.0.0.0/8", 53, 53, True), ("0.0.0.0/0", 4789, 4789, True)],
+                        False)
+        # one IPv4/UDP VXLAN datagram, senders 10.0.0.1 and 11.0.0.1
+        inner = bytes([0x45, 0, 0, 28, 0, 0, 0, 0, 64, 17, 0, 0, 10, 0, 0, 2, 10, 0, 0, 3]) + \
+            bytes([0, 1, 0, 2, 0, 8, 0, 0])
+        frame = bytes([8, 0, 0, 0, 0, 0, 1, 0]) + bytes(12) + b"\x08\x00" + inner
+        blob = torch.tensor(list(frame * 2), dtype=torch.uint8, device="cuda")
+        off = torch.tensor([0, len(frame), 2 * len(frame)], dtype=torch.int32, device="cuda")
+        r4 = torch.tensor([0x0A000001, 0x0B000001], dtype=torch.int32, device="cuda")
+
+        def verdicts(port):
+            _, acl, allow, _ = clf.switch_classify((blob, off), r4, port)
+            torch.cuda.synchronize()
+            return acl.cpu().tolist(), allow.cpu().tolist()
+        for port in (4789, 53, 4789):
+            with p:                                    # the old list
+                assert verdicts(port) == ({4789: ([0, 1], [1, 0]), 53: ([1, 1], [0, 0])}[port])
+            # the current list
+            assert verdicts(port) == ({4789: ([1, 1], [1, 1]), 53: ([0, -1], [1, 0])}[port])
+        p.release()
+    finally:
+        clf.close()
