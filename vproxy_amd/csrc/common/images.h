@@ -236,7 +236,9 @@ struct CertImage {
 
 // ---------------------------------------------------------------------------
 // Mirror filters (vmirror/FilterConfig.java): one 160-byte record per
-// FilterConfig in list order, staged in LDS and read by all lanes at once.
+// FilterConfig in list order, read by all lanes of a wave at once through
+// the scalar cache (the per-filter kernels; MirrorSwImage below for the
+// bit-set ones).
 // Each network is compiled to its per-input-family masked compare
 // (common/netmatch.h NetMatch); MACs as the low 48 bits of a u64.
 // ---------------------------------------------------------------------------

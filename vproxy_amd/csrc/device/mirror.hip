@@ -1,9 +1,12 @@
 // mirror.hip -- traffic-mirror filter kernels (see mirror_dev.h).
 //
-// One lane per item.  The filter list is small and read by every lane of a
-// wave at the same address (uniform loop): it is read through the scalar
-// cache into SGPRs (mirror_dev.h load_filter), so the per-filter branches
-// are scalar and the compares take SGPR operands.
+// One lane per item.  An origin with 1..64 filters is matched through its
+// bit-set image (images.h MirrorSwImage): one interval
+// search per address (and per port) gives every filter's network (port)
+// match at once, the MAC and protocol lists are uniform loops through the
+// scalar cache.  Other origins take the per-filter loop: the list is read by
+// every lane of a wave at the same address, through the scalar cache into
+// SGPRs (mirror_dev.h load_filter), so its branches are scalar.
 #include "launch.h"
 #include "mirror_dev.h"
 #include "chunks.h"
