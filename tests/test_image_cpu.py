@@ -33,7 +33,7 @@ def test_acl_v4_random(n_rules, p_range, weighted, seed):
 @pytest.mark.parametrize("n_rules", [25000, 70000])
 def test_acl_v4_directory_and_records_large(n_rules):
     """Lists of ~25k and ~70k intervals: the bucket directory (images.h
-    dir4, built for 17-65535 intervals: here 12-bit buckets holding ~6 or
+    dir4, built for 17-65535 intervals: here 16-bit buckets holding ~0.4 or
     none) and the 16-byte interval records; the harness checks every lookup
     against a whole binary search and the (x, y) + pieces form, and the
     results against the oracle on a sample."""

@@ -13,6 +13,13 @@
 #include "../common/netmatch.h"
 #include "../host/net.hpp"
 
+#ifndef VC_ACL_DIR_MAX
+#define VC_ACL_DIR_MAX 16
+#endif
+#ifndef VC_ACL_DIR_EXTRA
+#define VC_ACL_DIR_EXTRA 2
+#endif
+
 namespace vc {
 
 using u128 = unsigned __int128;
@@ -235,9 +242,14 @@ void build_acl_family(const vc_acl_rule* rules, int n, int family, AclFamilyBuil
     }
     if (family == 0 && out->nb > 16 && out->nb < 65536) {
         // bucket directory over the key's top D bits: entry t = s(t) |
-        // (s(t + 1) - s(t)) << 16, s(t) = last j with bounds4[j] <= t << (32 - D)
+        // (s(t + 1) - s(t)) << 16, s(t) = last j with bounds4[j] <= t << (32 - D).
+        // D: 2^D >= 4 nb (VC_ACL_DIR_EXTRA = 2), at most 16 bits (256 KB), so
+        // most buckets hold no boundary and a lookup is the directory load and
+        // the record load (12 bits, 1.2 boundaries per bucket at 5k intervals,
+        // left one or two boundary loads between them)
         int d = 4;
-        while ((1 << d) < out->nb && d < 12) ++d;
+        while ((1 << d) < out->nb && d < VC_ACL_DIR_MAX) ++d;
+        d = std::min(d + VC_ACL_DIR_EXTRA, VC_ACL_DIR_MAX);
         const auto& b = out->bounds4;
         auto s = [&](uint64_t key) {
             return uint32_t(std::upper_bound(b.begin(), b.end(), key,
