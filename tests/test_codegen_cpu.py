@@ -119,9 +119,27 @@ HOT_STRING = {
 }
 
 
+# frame and mirror kernels of round 6 (bind-port ACL image, bit-set mirrors)
+HOT_FRAME = {
+    "switch_kernelILb1ELb1EE": 128,
+    "switch_kernelILb1ELb0EE": 128,
+    "mirror_switch_kernelILb1ELb1ELb1EE": 128,
+    "mirror_match_kernelILb1ELb1EE": 128,
+}
+
+
 def test_hot_kernels_use_no_scratch(tmp_path):
     k = _kernels(_code_object("classify", tmp_path))
     k.update(_kernels(_code_object("counters", tmp_path)))
+    f = _kernels(_code_object("packet", tmp_path))
+    f.update(_kernels(_code_object("mirror", tmp_path)))
+    for part, vmax in HOT_FRAME.items():
+        m = f[_one(f, part)]
+        assert m["private_segment_fixed_size"] == 0, (part, m)
+        assert m["vgpr_spill_count"] == 0, (part, m)
+        assert m["vgpr_count"] <= vmax, (part, m)
+        # LDS within the 5 workgroups per CU these latency-bound kernels keep
+        assert m["group_segment_fixed_size"] <= 160 * 1024 // 5, (part, m)
     for part, vmax in HOT.items():
         name = _one(k, part)
         m = k[name]
