@@ -220,3 +220,26 @@ def test_switch_bitsets_bench_filters():
     want = np.array([O.mirror_switch(oarr, nf, oid, f, 0) for f in frames], np.uint64)
     np.testing.assert_array_equal(got, want)
     assert nb4 <= 2 * 32 + 1 and nb6 >= 1
+
+
+def test_bitsets_refuse_a_non_prefix_mask():
+    """A network whose mask is not a run of high ones (possible only through
+    the C ABI: FilterConfig parses masks from prefix lengths) cannot be an
+    interval: its origin has no bit-set image and keeps the per-filter loop,
+    whose answer still equals the oracle."""
+    filters = [{"origin": "switch", "mirror": 1, "network": "10.0.0.0/8"},
+               {"origin": "switch", "mirror": 2, "network": "10.0.0.0/16"},
+               {"origin": "other", "mirror": 3, "network": "10.0.0.0/8"}]
+    mf = MirrorFilters()
+    arr, nf = mf.build(filters)
+    arr[1].net_x.mask[1] = 0x0F                 # 255.15.0.0: not a prefix
+    oarr = O.mirror_filters(filters, {})
+    oarr[1].net_x.mask[1] = 0x0F
+    frames = mirror_frames(np.random.default_rng(3), 2000)
+    oid = mf.id_of("switch", create=False)
+    assert I.mirror_switch_sw(arr, nf, oid, frames, 0) is None
+    assert I.mirror_switch_sw(arr, nf, mf.id_of("other", create=False), frames, 0) is not None
+    got = I.mirror_switch(arr, nf, oid, frames, 0)
+    want = np.array([O.mirror_switch(oarr, nf, oid, f, 0) for f in frames], np.uint64)
+    np.testing.assert_array_equal(got, want)
+    assert ((want >> 2) & 1).any()              # the odd mask matches some frames
