@@ -350,6 +350,8 @@ int ic_mirror_sw(const vc_mirror_filter* f, int nf, int32_t origin, const vc_mir
     b.img.aids = b.aids.data();
     b.img.bp = b.bp.data();
     b.img.pp = b.pp.data();
+    b.img.bm = b.bm.data();
+    b.img.pm = b.pm.data();
     for (int64_t i = 0; i < n; ++i) {
         const MirrorItem it = mirror_item(*items, i);
         out[i] = mirror_match_sw(b.img, sw_tables(b.img), it, mirror_level(it));
@@ -377,6 +379,8 @@ int ic_mirror_switch_sw(const vc_mirror_filter* f, int nf, int32_t origin, const
     b.img.aids = b.aids.data();
     b.img.bp = b.bp.data();
     b.img.pp = b.pp.data();
+    b.img.bm = b.bm.data();
+    b.img.pm = b.pm.data();
     for (int64_t i = 0; i < n; ++i)
         out[i] = mirror_switch_sw(b.img, sw_tables(b.img), blob + off[i],
                                   int(off[i + 1] - off[i]), layer);

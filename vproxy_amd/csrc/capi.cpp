@@ -1564,6 +1564,8 @@ int vc_compile_mirror(vc_ctx* ctx, const vc_mirror_filter* filters, int n) {
             b.img.aids = up(*s, b.aids);
             b.img.bp = up(*s, b.bp);
             b.img.pp = up(*s, b.pp);
+            b.img.bm = up(*s, b.bm);
+            b.img.pm = up(*s, b.pm);
             b.img.lds = !(env && env[0] == '1');
             s->sw[o] = b.img;
         }

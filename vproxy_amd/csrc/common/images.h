@@ -316,6 +316,13 @@ struct MirrorSwImage {
     const MirrorSwId* aids;
     const uint32_t* bp;            // nbp ascending port interval starts, bp[0] = 0
     const uint64_t* pp;            // per port interval: (xmask, ymask)
+    // matchEthernet as sets (the items kernel): the distinct MACs of the
+    // origin's filters, ascending, each with the filters whose macX / macY
+    // it is
+    uint64_t mac_both, mac_xonly;  // MAC_X with MAC_Y / MAC_X alone
+    int32_t nbm, pad3;
+    const uint64_t* bm;            // nbm ascending MACs (low 48 bits)
+    const uint64_t* pm;            // per MAC: (xmask, ymask)
 };
 
 // ---------------------------------------------------------------------------

@@ -807,6 +807,7 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
     std::vector<uint64_t> bit4, bit6;
     std::vector<int> side4, side6;
     std::map<int32_t, uint64_t> mirs, tmap, amap;
+    std::map<uint64_t, std::pair<uint64_t, uint64_t>> macm;  // MAC -> (macX of, macY of)
     std::vector<std::pair<uint32_t, uint32_t>> rp;           // port ranges, x and y
     std::vector<uint64_t> bitp;
     std::vector<int> sidep;
@@ -822,6 +823,13 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
         if (f.flags & VC_MF_MAC_X) {
             s.mac |= b;
             out->macs.push_back({b, f.mac_x, f.mac_y, (f.flags & VC_MF_MAC_Y) ? 1u : 0u, 0});
+            macm[f.mac_x].first |= b;
+            if (f.flags & VC_MF_MAC_Y) {
+                macm[f.mac_y].second |= b;
+                s.mac_both |= b;
+            } else {
+                s.mac_xonly |= b;
+            }
         }
         for (int y = 0; y < 2; ++y) {
             if (!(f.flags & (y ? VC_MF_NET_Y : VC_MF_NET_X))) continue;
@@ -863,6 +871,11 @@ bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, Mir
     for (const auto& m : mp) out->pp.insert(out->pp.end(), {m.first, m.second});
     for (const auto& m : tmap) out->tids.push_back({m.second, m.first, 0});
     for (const auto& m : amap) out->aids.push_back({m.second, m.first, 0});
+    for (const auto& m : macm) {
+        out->bm.push_back(m.first);
+        out->pm.insert(out->pm.end(), {m.second.first, m.second.second});
+    }
+    s.nbm = int32_t(out->bm.size());
     s.n_t = int32_t(out->tids.size());
     s.n_a = int32_t(out->aids.size());
     s.nbp = int32_t(out->bp.size());

@@ -115,7 +115,7 @@ struct MirrorSwBuilt {
     std::vector<MirrorSwMac> macs;
     std::vector<MirrorSwMir> mirs;
     std::vector<uint32_t> b4, bp;
-    std::vector<uint64_t> p4, b6, p6, pp;
+    std::vector<uint64_t> p4, b6, p6, pp, bm, pm;
     std::vector<MirrorSwId> tids, aids;
 };
 bool build_mirror_switch(const std::vector<MirrorRec>& recs, int32_t origin, MirrorSwBuilt* out);

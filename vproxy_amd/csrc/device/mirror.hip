@@ -25,7 +25,8 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
     uint64_t* __restrict__ out) {
     __shared__ uint32_t l4b[kL ? kMatchL : 1], lpb[kL ? kMatchL : 1];
     __shared__ ulonglong2 l4p[kL ? kMatchL : 1], l6b[kL ? kMatchL : 1], l6p[kL ? kMatchL : 1],
-        lpp[kL ? kMatchL : 1];
+        lpp[kL ? kMatchL : 1], lmp[kL ? kMatchL : 1];
+    __shared__ uint64_t lmb[kL ? kMatchL : 1];
     const MirrorImage& fi = img;
     SwTables tb = sw_tables(sw);
     if (kL) {
@@ -43,10 +44,15 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_match_kernel(
             lpb[t] = glb_ld(sw.bp + t);
             lpp[t] = glb_ld(reinterpret_cast<P2>(sw.pp) + t);
         }
+        if (t < sw.nbm) {
+            lmb[t] = glb_ld(sw.bm + t);
+            lmp[t] = glb_ld(reinterpret_cast<P2>(sw.pm) + t);
+        }
         __syncthreads();
         typedef const uint64_t* P1;
         tb = SwTables{l4b, reinterpret_cast<P1>(l4p), reinterpret_cast<P1>(l6b),
-                      reinterpret_cast<P1>(l6p), lpb, reinterpret_cast<P1>(lpp)};
+                      reinterpret_cast<P1>(l6p), lpb, reinterpret_cast<P1>(lpp), lmb,
+                      reinterpret_cast<P1>(lmp)};
     }
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(kMirrorBlock) void mirror_switch_kernel(
         __syncthreads();
         tb = SwTables{l4b, reinterpret_cast<const uint64_t*>(l4p),
                       reinterpret_cast<const uint64_t*>(l6b), reinterpret_cast<const uint64_t*>(l6p),
-                      sw.bp, sw.pp};
+                      sw.bp, sw.pp, sw.bm, sw.pm};
     }
     ChunksT<kPerTicket, kTailChunks, kTailRounds, 25> ch(ticket, (n + 63) / 64);   // chunks.h
     int64_t c = ch.first(w);
@@ -139,7 +145,7 @@ hipError_t launch_mirror_match(const LaunchCfg& c, const MirrorImage& img,
                            c.stream, img, s, origin, in, n, out);
     };
     if (sw && sw->lds && sw->nb4 <= vcd::kMatchL && sw->nb6 <= vcd::kMatchL &&
-        sw->nbp <= vcd::kMatchL)
+        sw->nbp <= vcd::kMatchL && sw->nbm <= vcd::kMatchL)
         go(vcd::mirror_match_kernel<true, true>, *sw);
     else if (sw) go(vcd::mirror_match_kernel<true, false>, *sw);
     else go(vcd::mirror_match_kernel<false, false>, none);

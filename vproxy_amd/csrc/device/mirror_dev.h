@@ -203,10 +203,25 @@ struct SwTables {
     const uint64_t *p4, *b6, *p6;
     const uint32_t* bp;            // port intervals (Mirror.mirror's items)
     const uint64_t* pp;
+    const uint64_t* bm;            // the origin's MACs (Mirror.mirror's items)
+    const uint64_t* pm;
 };
 
 VC_HD SwTables sw_tables(const MirrorSwImage& s) {
-    return SwTables{s.b4, s.p4, s.b6, s.p6, s.bp, s.pp};
+    return SwTables{s.b4, s.p4, s.b6, s.p6, s.bp, s.pp, s.bm, s.pm};
+}
+
+// (macX of, macY of) for one MAC: its entry in the origin's MAC list, or 0s
+template <bool kL = false>
+VC_HD ulonglong2 sw_mac_masks(const SwTables& t, int nbm, uint64_t mac) {
+    int lo = 0, len = nbm;
+    while (len > 1) {
+        const int half = len >> 1;
+        lo = tbl_ld<kL>(t.bm + lo + half) <= mac ? lo + half : lo;
+        len -= half;
+    }
+    if (tbl_ld<kL>(t.bm + lo) != mac) return make_ulonglong2(0, 0);
+    return sw_masks<kL>(t.pm, lo);
 }
 
 template <bool kL = false>
@@ -274,13 +289,13 @@ VC_HD uint64_t sw_ids(const MirrorSwId* ids, int n, uint64_t any, int32_t id) {
 template <bool kL = false>
 VC_HD uint64_t mirror_match_sw(const MirrorSwImage& s, const SwTables& t, const MirrorItem& it,
                                int lvl) {
+    // matchEthernet: the two MACs looked up in the origin's MAC list;
+    // macX and macY -> (xs && yd) || (ys && xd); macX only -> xs || xd
     uint64_t hit = s.all & ~s.mac;
-    for (int k = 0; k < s.n_mac; ++k) {
-        const MirrorSwMac f = load_uniform(s.macs, k);
-        const bool ok = f.has_y ? (f.mac_x == it.mac_src && f.mac_y == it.mac_dst) ||
-                                      (f.mac_y == it.mac_src && f.mac_x == it.mac_dst)
-                                : f.mac_x == it.mac_src || f.mac_x == it.mac_dst;
-        if (ok) hit |= f.bit;
+    if (s.nbm) {
+        const ulonglong2 ms = sw_mac_masks<kL>(t, s.nbm, it.mac_src);
+        const ulonglong2 md = sw_mac_masks<kL>(t, s.nbm, it.mac_dst);
+        hit |= (s.mac_both & ((ms.x & md.y) | (ms.y & md.x))) | (s.mac_xonly & (ms.x | md.x));
     }
     if (lvl >= kLvlIp) {
         const ulonglong2 ms = sw_addr_masks<kL>(s, t, it.ip_src);
