@@ -189,6 +189,39 @@ VC_HD ulonglong2 sw_masks(const uint64_t* p, int j) {
     return tbl_ld<kL>(reinterpret_cast<const ulonglong2*>(p) + j);
 }
 
+// The intervals of two keys (an item's source and destination) in one
+// loop: the trip count depends on nb only, so the two LDS reads of a step go
+// out together (the C2 ACL kernel's lockstep form, classify.hip acl_v4_four)
+template <bool kL, class T>
+VC_HD void bsearch2(const T* b, int nb, T k0, T k1, int* j0, int* j1) {
+    int lo0 = 0, lo1 = 0, len = nb;
+    while (len > 1) {
+        const int half = len >> 1;
+        const T x0 = tbl_ld<kL>(b + lo0 + half), x1 = tbl_ld<kL>(b + lo1 + half);
+        lo0 = x0 <= k0 ? lo0 + half : lo0;
+        lo1 = x1 <= k1 ? lo1 + half : lo1;
+        len -= half;
+    }
+    *j0 = lo0;
+    *j1 = lo1;
+}
+
+template <bool kL>
+VC_HD void bsearch2_u128(const uint64_t* b, int nb, uint64_t h0, uint64_t l0, uint64_t h1,
+                         uint64_t l1, int* j0, int* j1) {
+    int lo0 = 0, lo1 = 0, len = nb;
+    while (len > 1) {
+        const int half = len >> 1;
+        const ulonglong2 x0 = tbl_ld<kL>(reinterpret_cast<const ulonglong2*>(b) + lo0 + half);
+        const ulonglong2 x1 = tbl_ld<kL>(reinterpret_cast<const ulonglong2*>(b) + lo1 + half);
+        lo0 = le128(x0.x, x0.y, h0, l0) ? lo0 + half : lo0;
+        lo1 = le128(x1.x, x1.y, h1, l1) ? lo1 + half : lo1;
+        len -= half;
+    }
+    *j0 = lo0;
+    *j1 = lo1;
+}
+
 // Mirror.switchPacket through the origin's bit-set image (images.h
 // MirrorSwImage): the same answer as mirror_switch_one over the origin's
 // filters.  matchEthernet (FilterConfig.java:27-38) for every MAC filter,
@@ -211,17 +244,12 @@ VC_HD SwTables sw_tables(const MirrorSwImage& s) {
     return SwTables{s.b4, s.p4, s.b6, s.p6, s.bp, s.pp, s.bm, s.pm};
 }
 
-// (macX of, macY of) for one MAC: its entry in the origin's MAC list, or 0s
+// (macX of, macY of) for a MAC at entry j of the origin's MAC list, or 0s
+// when the entry is not that MAC
 template <bool kL = false>
-VC_HD ulonglong2 sw_mac_masks(const SwTables& t, int nbm, uint64_t mac) {
-    int lo = 0, len = nbm;
-    while (len > 1) {
-        const int half = len >> 1;
-        lo = tbl_ld<kL>(t.bm + lo + half) <= mac ? lo + half : lo;
-        len -= half;
-    }
-    if (tbl_ld<kL>(t.bm + lo) != mac) return make_ulonglong2(0, 0);
-    return sw_masks<kL>(t.pm, lo);
+VC_HD ulonglong2 sw_mac_at(const SwTables& t, int j, uint64_t mac) {
+    if (tbl_ld<kL>(t.bm + j) != mac) return make_ulonglong2(0, 0);
+    return sw_masks<kL>(t.pm, j);
 }
 
 template <bool kL = false>
@@ -242,14 +270,18 @@ VC_HD uint64_t mirror_switch_sw(const MirrorSwImage& s, const SwTables& t, const
     if (o.l3 == VC_L3_IPV4 || o.l3 == VC_L3_IPV6) {
         ulonglong2 ms, md;
         if (o.l3 == VC_L3_IPV4) {
-            ms = sw_masks<kL>(t.p4, bsearch_u32<kL>(t.b4, s.nb4, bswap32(o.src[0])));
-            md = sw_masks<kL>(t.p4, bsearch_u32<kL>(t.b4, s.nb4, bswap32(o.dst[0])));
+            int js, jd;
+            bsearch2<kL>(t.b4, s.nb4, bswap32(o.src[0]), bswap32(o.dst[0]), &js, &jd);
+            ms = sw_masks<kL>(t.p4, js);
+            md = sw_masks<kL>(t.p4, jd);
         } else {
             uint64_t sh, sl, dh, dl;
             v6_key(*reinterpret_cast<const uint4*>(o.src), &sh, &sl);
             v6_key(*reinterpret_cast<const uint4*>(o.dst), &dh, &dl);
-            ms = sw_masks<kL>(t.p6, bsearch_u128<kL>(t.b6, s.nb6, sh, sl));
-            md = sw_masks<kL>(t.p6, bsearch_u128<kL>(t.b6, s.nb6, dh, dl));
+            int js, jd;
+            bsearch2_u128<kL>(t.b6, s.nb6, sh, sl, dh, dl, &js, &jd);
+            ms = sw_masks<kL>(t.p6, js);
+            md = sw_masks<kL>(t.p6, jd);
         }
         const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
         hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
@@ -293,22 +325,33 @@ VC_HD uint64_t mirror_match_sw(const MirrorSwImage& s, const SwTables& t, const 
     // macX and macY -> (xs && yd) || (ys && xd); macX only -> xs || xd
     uint64_t hit = s.all & ~s.mac;
     if (s.nbm) {
-        const ulonglong2 ms = sw_mac_masks<kL>(t, s.nbm, it.mac_src);
-        const ulonglong2 md = sw_mac_masks<kL>(t, s.nbm, it.mac_dst);
+        int js, jd;
+        bsearch2<kL>(t.bm, s.nbm, it.mac_src, it.mac_dst, &js, &jd);
+        const ulonglong2 ms = sw_mac_at<kL>(t, js, it.mac_src);
+        const ulonglong2 md = sw_mac_at<kL>(t, jd, it.mac_dst);
         hit |= (s.mac_both & ((ms.x & md.y) | (ms.y & md.x))) | (s.mac_xonly & (ms.x | md.x));
     }
     if (lvl >= kLvlIp) {
-        const ulonglong2 ms = sw_addr_masks<kL>(s, t, it.ip_src);
-        const ulonglong2 md = sw_addr_masks<kL>(s, t, it.ip_dst);
+        ulonglong2 ms, md;
+        if (it.ip_src.len == 4 && it.ip_dst.len == 4) {
+            int js, jd;
+            bsearch2<kL>(t.b4, s.nb4, bswap32(it.ip_src.w[0]), bswap32(it.ip_dst.w[0]), &js, &jd);
+            ms = sw_masks<kL>(t.p4, js);
+            md = sw_masks<kL>(t.p4, jd);
+        } else {
+            ms = sw_addr_masks<kL>(s, t, it.ip_src);
+            md = sw_addr_masks<kL>(s, t, it.ip_dst);
+        }
         const uint64_t both = s.has_x & s.has_y, xonly = s.has_x & ~s.has_y;
         hit &= ~s.has_x | (both & ((ms.x & md.y) | (ms.y & md.x))) | (xonly & (ms.x | md.x));
     }
     if (lvl >= kLvlTransport) {
         const uint64_t tm = sw_ids(s.tids, s.n_t, s.any_t, it.transport);
-        const ulonglong2 ps =
-            sw_masks<kL>(t.pp, bsearch_u32<kL>(t.bp, s.nbp, uint32_t(it.port_src) ^ 0x80000000u));
-        const ulonglong2 pd =
-            sw_masks<kL>(t.pp, bsearch_u32<kL>(t.bp, s.nbp, uint32_t(it.port_dst) ^ 0x80000000u));
+        int js, jd;
+        bsearch2<kL>(t.bp, s.nbp, uint32_t(it.port_src) ^ 0x80000000u,
+                     uint32_t(it.port_dst) ^ 0x80000000u, &js, &jd);
+        const ulonglong2 ps = sw_masks<kL>(t.pp, js);
+        const ulonglong2 pd = sw_masks<kL>(t.pp, jd);
         const uint64_t both = s.has_px & s.has_py, xonly = s.has_px & ~s.has_py;
         hit &= tm & (~s.has_px | (both & ((ps.x & pd.y) | (ps.y & pd.x))) | (xonly & (ps.x | pd.x)));
     }
